@@ -1,0 +1,224 @@
+"""Benchmark: generated motion frames/s of the gesture-diffusion sampler (BASELINE.json metric).
+
+One "step" = one full sampling pass over one batch of synthetic BEAT-shaped clips:
+speech encoding (once per clip) + all T = 1000 DDPM denoise steps (hipGraph replay of
+the fused decoder + update chain) + the all-gather of the final poses.  Workload
+(config C2, BASELINE.json configs[1]): beat-ours, 32 clips per GPU, L = 40 frames,
+123 pose channels, 32,000-sample wav windows, bf16 decoder, random-init weights.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
+
+Prints ONE JSON line on rank 0.  ``roofline`` is measured live: hipEvents around every
+launch of the dominant kernel (the LN3 + FFN-up + ReLU^2 GEMM) inside the timed region.
+``cpu_baseline`` times the CPU oracle (a faithful fp32 restatement that recomputes the
+speech encoder every step, as models/model.py:95-96 does) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch as th
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+F32_PEAK_TFLOPS = 157.3
+
+
+ENCODER_FLOP_PER_CLIP = 4.764e9   # SURVEY.md 8d, Tw = 32,000 (computed once per clip)
+
+
+def clip_step_flops(L, Tm, d, C, layers):
+    """Algorithmic FLOPs of one decoder forward for one clip with the step-invariant memory
+    K/V cached (314.3 MFLOP at L=40, Tm=32): GEMMs 2*M*K*N, attention
+    4*Lq*Lk*d, depthwise conv 6 FLOP per output (Q/K/V self, Q cross)."""
+    gemm = 2 * L * (C * d + layers * (3 * d * d + d * d + d * d + d * d + 2 * 4 * d * d) + d * C)
+    attn = layers * 4 * L * (L + Tm) * d
+    conv = layers * 6 * L * d * 4
+    return gemm + attn + conv
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--config", default=os.path.join(ROOT, "configs", "beat-ours.json"))
+    p.add_argument("--batch-per-gpu", type=int, default=32)
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    p.add_argument("--alg", default="ddpm", choices=["ddpm", "ddim"])
+    p.add_argument("--respacing", default="")
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-profile", action="store_true", help="skip the in-loop kernel events")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-steps", type=int, default=3)
+    return p.parse_args()
+
+
+def cpu_baseline(pkg, cfg, sd, arch, B, L, T, n_steps):
+    """Oracle on the host cores: faithful per-step encoder, n_steps denoise steps, extrapolated x T."""
+    from oracle import ref_denoiser, ref_diffusion
+    cores = len(os.sched_getaffinity(0))
+    th.set_num_threads(cores)
+    ocfg = {k: arch[k] for k in ("type", "d_model", "decoder", "heads", "n_layers")}
+    om = ref_denoiser.OracleModel(sd, ocfg, cache_speech=False)
+    g = th.Generator().manual_seed(1)
+    wav = th.randn(B, 32000, generator=g) * 0.1
+    sch = ref_diffusion.make_schedule("linear", T, "")
+    noise = ref_diffusion.TorchNoise(2)
+    ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, "ddpm", n_steps=1)
+    t0 = time.perf_counter()
+    ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, "ddpm", n_steps=n_steps)
+    dt = time.perf_counter() - t0
+    per_step = dt / n_steps
+    model_name = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model_name = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:
+        pass
+    return {
+        "value": B * L / (per_step * T),
+        "unit": "frames/s",
+        "cores": th.get_num_threads(),
+        "kind": "port",
+        "sample": (f"{n_steps} DDPM denoise steps of B={B} clips (per-step speech encoder, fp32 oracle) "
+                   f"after 1 warm-up, measured {dt:.2f} s = {per_step * 1e3:.0f} ms/step, extrapolated x{T} steps; "
+                   f"CPU: {model_name}"),
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and "RANK" in os.environ:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    if world > 1 and "RANK" not in os.environ:
+        raise SystemExit("multi-GPU runs are launched with torch.distributed.run (one rank per GPU)")
+    dev = th.device("cuda", local)
+    th.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    sharding = __import__(ge.PKG_NAME + ".sharding", fromlist=["x"])
+    cfg = pkg.load_config(args.config)
+    d_pose = int(cfg.Data.get("d_pose", 123)) if "Data" in cfg else 123
+    L = int(cfg.Data.pose_window_len)
+    wav_len = int(cfg.Data.wav_sr * L / cfg.Data.pose_fps)
+    model, diffusion, _, _, _ = pkg.create_model(d_pose, cfg.Model, dtype=args.dtype, device=dev)
+    if args.respacing:
+        diffusion = pkg.create_diffusion(dict(cfg.Model.Diffusion, timestep_respacing=args.respacing), False)
+    arch = model.arch
+    sd = pkg.init_state_dict(arch, seed=0)
+    model.load_state_dict(sd)
+    B = args.batch_per_gpu
+    n_total = B * world
+    T = diffusion.num_timesteps
+    loop = diffusion.p_sample_loop if args.alg == "ddpm" else diffusion.ddim_sample_loop
+
+    # distinct synthetic wav batches per step, resident in HBM before the timed region
+    g = th.Generator(device=dev).manual_seed(1234)
+    n_batches = args.warmup + args.steps
+    wavs = [th.randn(n_total, wav_len, device=dev, generator=g) * 0.1 for _ in range(n_batches)]
+    start, stop = sharding.shard_range(n_total, rank, world)
+
+    def one_pass(wav_all, seed):
+        def fn(wav_local, offset):
+            out = loop(model, (wav_local.shape[0], d_pose, L), model_kwargs={"wav": wav_local}, seed=seed,
+                       clip_offset=offset, use_graph=not args.no_graph, extras=False)
+            return out["sample"]
+        return sharding.sample_sharded(fn, wav_all, n_total, rank, world, dev)
+
+    # warm-up (graph capture, encoder kernels, allocator); profiling state is part of the
+    # captured graph, so it is set before the warm-up
+    enc = __import__(ge.PKG_NAME + ".encoder", fromlist=["x"])
+    ctx = model.context(L, enc.speech_len(arch["type"], wav_len), B)
+    lib = ctx.lib
+    prof = not args.no_profile
+    lib.ggd_set_profiling(ctx.h, 1 if prof else 0)
+    for w in range(args.warmup):
+        one_pass(wavs[w], seed=w)
+    if dist is not None:
+        dist.barrier()
+    th.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    prof_us, prof_n = [], 0
+    import ctypes
+    for k in range(args.steps):
+        out = one_pass(wavs[args.warmup + k], seed=100 + k)
+        if prof:
+            avg = ctypes.c_double()
+            cnt = ctypes.c_int64()
+            lib.ggd_kernel_time(ctx.h, 0, ctypes.byref(avg), ctypes.byref(cnt))
+            prof_us.append(avg.value * cnt.value)
+            prof_n += cnt.value
+    th.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = th.tensor([elapsed], device=dev, dtype=th.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    lib.ggd_set_profiling(ctx.h, 0)
+    assert out.shape == (n_total, d_pose, L) and bool(th.isfinite(out).all())
+
+    frames = args.steps * n_total * L
+    value = frames / elapsed
+    # algorithmic FLOPs: FFN-up per launch = 2 * (B*L) * d * 4d
+    d = arch["d_model"]
+    ffn_flop = 2.0 * B * L * d * 4 * d
+    peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
+    roof = None
+    if prof and prof_n:
+        avg_us = sum(prof_us) / prof_n
+        ach = ffn_flop / (avg_us * 1e-6) / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 5), "traffic": None,
+                "kernel": "gemm_kernel<bf16,MT=64,PRO_LN,EPI_RELU2> (LN3+FFN-up+ReLU^2)",
+                "flop_per_launch": ffn_flop, "avg_launch_us": round(avg_us, 3), "launches": prof_n}
+    Tm = 1 + int(ctx.desc.speech_len)
+    clip_step = clip_step_flops(L, Tm, d, d_pose, arch["n_layers"])
+    frame_flop = (T * clip_step + ENCODER_FLOP_PER_CLIP) / L
+    res = {
+        "metric": "generated motion frames/sec (whole node), T=1000 BEAT clips, 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (random-init weights of the beat-ours architecture, N(0,0.1^2) wav, counter-stream noise)",
+        "config": {"workload": f"beat-ours C2: {B} clips/GPU x L={L} x C={d_pose}, wav {wav_len}, "
+                               f"{args.alg.upper()} T'={T}, {args.dtype} decoder",
+                   "global_batch": n_total, "seq_len": L, "parallelism": f"dp{world}",
+                   "diffusion_steps": T},
+        "roofline": roof,
+        "whole_job": {"gflop_per_frame": round(frame_flop / 1e9, 4), "clip_step_mflop": round(clip_step / 1e6, 2),
+                      "achieved_tflops_per_gpu": round(value * frame_flop / world / 1e12, 3),
+                      "frac_of_peak": round(value * frame_flop / world / 1e12 / peak, 5)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(pkg, cfg, sd, arch, B, L, T, args.cpu_steps)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,156 @@
+/*
+ * ggd.h -- C ABI of the MI355X-native gesture-diffusion sampler (libggd.so).
+ *
+ * The reference is pure Python; its drop-in boundary for the hot path is the
+ * model protocol and the sampler/generator API:
+ *
+ *   eps = model(x_t (N,C,L) f32, t (N,) i64, wav=...)        models/model.py:12-15
+ *   diffusion.p_sample_loop / ddim_sample_loop(...)           models/modules/gaussian_diffusion.py:331-529
+ *   Generator.generate_sample(shape, wavs, noise, inpaint..)  models/generator.py:218-296
+ *
+ * Each entry point below names the reference interface it replaces.  Plain
+ * pointers and sizes only.  Device pointers are HIP device addresses owned by
+ * the caller (e.g. the PyTorch caching allocator); `stream` is a hipStream_t
+ * (0 = legacy default stream).  The context owns weights, workspaces and
+ * captured hipGraphs; nothing is allocated inside the step loop.
+ *
+ * Error convention: every call returns 0 (GGD_OK) or a negative ggd_status;
+ * ggd_last_error(ctx) returns a message for the last failure on ctx.  The
+ * Python host layer maps these to the reference's exception types
+ * (ValueError for unsupported options, AssertionError for shape checks,
+ * RuntimeError for HIP failures) -- SURVEY.md section 8b "Error conventions".
+ *
+ * Threading: one ctx per (process, device); a ctx is not thread-safe.
+ */
+#ifndef GGD_H
+#define GGD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ggd_ctx ggd_ctx;
+
+enum ggd_status {
+  GGD_OK = 0,
+  GGD_IGNORED = 1,          /* ggd_load_weight: name belongs to the speech encoder */
+  GGD_ERR_ARG = -1,         /* bad argument / shape (Python: AssertionError / ValueError) */
+  GGD_ERR_UNSUPPORTED = -2, /* option not supported (Python: ValueError) */
+  GGD_ERR_HIP = -3,         /* HIP runtime failure (Python: RuntimeError) */
+  GGD_ERR_STATE = -4,       /* call out of order, e.g. sample before weights */
+  GGD_ERR_NAME = -5         /* unknown or mis-shaped state_dict entry */
+};
+
+/* models/model_creation.py:133-161 -- Model.type */
+enum ggd_model_type { GGD_MODEL_S2G_V2 = 0, GGD_MODEL_DEFAULT = 1 };
+/* models/model_creation.py:72-93 -- Decoder.type */
+enum ggd_decoder_type { GGD_DEC_ONEWAY = 0, GGD_DEC_TWOWAY = 1 };
+/* compute dtype of the decoder GEMM operands (accumulation is always f32) */
+enum ggd_dtype { GGD_F32 = 0, GGD_BF16 = 1 };
+/* models/generator.py:34-45 -- sample_alg */
+enum ggd_alg { GGD_DDPM = 0, GGD_DDIM = 1 };
+
+typedef struct ggd_desc {
+  int32_t model_type;    /* ggd_model_type */
+  int32_t decoder_type;  /* ggd_decoder_type */
+  int32_t d_model;       /* Model.d_model (256 beat, 512 tedexp) */
+  int32_t heads;         /* Decoder.heads */
+  int32_t n_layers;      /* Decoder.n_layers */
+  int32_t d_pose;        /* C: pose channels (123 beat) */
+  int32_t seq_len;       /* L: pose window frames (40 beat) */
+  int32_t speech_len;    /* Ts: speech memory tokens (31 beat); memory = 1 + Ts */
+  int32_t max_batch;     /* largest N any call will use (workspaces sized once) */
+  int32_t dtype;         /* ggd_dtype */
+  int32_t diffusion_steps; /* Diffusion.diffusion_steps: range of original t */
+} ggd_desc;
+
+/* Create a context on `device` (hip device ordinal).
+ * Replaces: create_model(...) model construction, models/model_creation.py:51-161. */
+int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out);
+
+/* Destroy a context and every resource it owns. */
+int ggd_destroy(ggd_ctx* ctx);
+
+/* Message describing the last failure on ctx (never NULL). */
+const char* ggd_last_error(const ggd_ctx* ctx);
+
+/* Stage one host f32 tensor keyed by its reference state_dict name, e.g.
+ * "pose_decoder.layers.0.self_attn.query.0.linear.weight".  Names under
+ * "speech_encoder." return GGD_IGNORED.
+ * Replaces: model.load_state_dict(chkpt["model_state_dict"]), main.py:113-115. */
+int ggd_load_weight(ggd_ctx* ctx, const char* name, const float* host_data, int64_t numel);
+
+/* Check that every decoder weight is present, upload them in the compute
+ * dtype and precompute the step-token tables for all original t. */
+int ggd_finalize_weights(ggd_ctx* ctx);
+
+/* Install a diffusion schedule: the respaced betas (fp64, length T) and the
+ * respaced->original timestep map.  Coefficient tables are derived in fp64 and
+ * rounded to f32 exactly as _extract_into_tensor does.
+ * Replaces: GaussianSpacedDiffusion.__init__, respace.py:80-93 +
+ *           GaussianDiffusion.__init__, gaussian_diffusion.py:87-143. */
+int ggd_set_schedule(ggd_ctx* ctx, const double* betas, int32_t T, const int64_t* timestep_map);
+
+/* Install the step-invariant speech memory of N clips: device f32
+ * (N, Ts, dz) with dz = 3*d_model (s2g_v2: the left-zero-padded concat of
+ * z_low|z_mid|z_high; the blend layer runs here) or dz = d_model (default:
+ * tokens already concatenated on time).  Computes emb_mem + PE and the
+ * cross-attention K/V projections once per clip.
+ * Replaces: Speech2GestureModelV2.myforward memory assembly, models/model.py:93-112
+ * (there recomputed on every denoise step). */
+int ggd_set_memory(ggd_ctx* ctx, const float* speech_tokens, int32_t n, int32_t ts, int32_t dz,
+                   void* stream);
+
+/* Model protocol: eps = model(x_t, t).  x_t, eps: device f32 (N, C, L);
+ * t: device int32 (N,) ORIGINAL timesteps; N = the batch given to ggd_set_memory.
+ * Replaces: Speech2GestureModelBase.forward, models/model.py:12-15. */
+int ggd_denoise(ggd_ctx* ctx, const float* x_t, const int32_t* t, float* eps, int32_t n, void* stream);
+
+/* One reverse-diffusion update without the model call, for a caller-supplied
+ * denoise_fn: given eps and the (possibly replaced) x0 of respaced step i,
+ * writes x_{i-1}.  If x0 == NULL it is predicted from eps.  All (N,C,L) f32.
+ * Replaces: p_sample :300-329 / ddim_sample :443-484 after p_mean_variance. */
+int ggd_posterior_step(ggd_ctx* ctx, int32_t alg, float eta, int32_t i, const float* x,
+                       const float* eps, const float* x0, const float* noise, float* x_out,
+                       float* x0_out, int32_t n, void* stream);
+
+typedef struct ggd_sample_args {
+  int32_t alg;            /* ggd_alg */
+  float eta;              /* DDIM eta (0 in the reference) */
+  int32_t n;              /* clips in this call (<= max_batch) */
+  const float* x_T;       /* device (N,C,L) initial noise; NULL = draw from the counter stream */
+  const float* noise;     /* device (T',N,C,L) per-step noise in loop order; NULL = counter stream */
+  uint64_t seed;          /* counter-stream key */
+  int64_t clip_offset;    /* global id of clip 0 (rank sharding keeps streams GPU-count invariant) */
+  const float* inpaint_poses; /* device (N,L,C) or NULL  -- generator.py:249-281 */
+  const float* inpaint_masks; /* device (N,L) or NULL */
+  const float* trans;     /* device (L,) ramp or NULL (= trans_factor None -> 0) */
+  float* out;             /* device (N,C,L): final sample */
+  float* extras;          /* device (6,N,C,L) or NULL: last step's mean, variance, log_variance,
+                             eps, pred_x_start, raw_x_start (gaussian_diffusion.py:278-285) */
+  int32_t n_steps;        /* run only the first n_steps iterations (<=0: all T') */
+  int32_t use_graph;      /* 1: replay a captured hipGraph per step */
+} ggd_sample_args;
+
+/* Full reverse loop, i = T'-1 ... 0, one fused model+update per step.
+ * Replaces: GaussianDiffusion.p_sample_loop / ddim_sample_loop
+ * (gaussian_diffusion.py:331-529) as driven by Generator.generate_sample
+ * (generator.py:283-294). */
+int ggd_sample(ggd_ctx* ctx, const ggd_sample_args* args, void* stream);
+
+/* Timing of the dominant kernel over the last ggd_sample (hipEvents on the ctx
+ * stream): average microseconds of one launch of `which` (0 = the FFN-up GEMM),
+ * and the number of launches averaged.  Needs ggd_set_profiling(ctx, 1). */
+int ggd_set_profiling(ggd_ctx* ctx, int32_t on);
+int ggd_kernel_time(ggd_ctx* ctx, int32_t which, double* avg_us, int64_t* launches);
+
+/* Library version string. */
+const char* ggd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GGD_H */

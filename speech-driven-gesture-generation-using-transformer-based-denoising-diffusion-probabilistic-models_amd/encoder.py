@@ -1,0 +1,128 @@
+"""HA2G speech encoder on the GPU (PyTorch-ROCm ops), run ONCE per clip.
+
+The reference recomputes this encoder inside every denoise step
+(models/model.py:95-96 via gaussian_diffusion.py:256) although its input never
+changes over the reverse loop; in eval mode (BN running statistics, per-instance
+InstanceNorm, dropout 0) hoisting it out of the loop is exact.  It is 4.76 GFLOP
+per clip against 0.35 GFLOP per clip-step for the decoder.
+
+Pipeline (ha2g/speech_encoder.py:37-61): pre-emphasis (utils.py:22-38) ->
+power mel spectrogram (torchaudio MelSpectrogram(16000, n_fft=1024, hop=512,
+n_mels=128): Hann window, centre reflect padding, |STFT|^2, HTK filterbank) ->
++1e-6 -> InstanceNorm1d(128) -> SE-ResNet34 (ResNetSE34V2.py:118-188) -> three
+temporal heads -> shared Linear(32 -> d_model).
+
+MI355X mapping: the STFT is a real-DFT GEMM against a cached [cos | sin] basis
+(1024 x 1026) and the mel projection a second GEMM; the convolutions go to
+MIOpen.  A HIP implicit-GEMM port is the next scope row.
+"""
+import math
+
+import torch as th
+import torch.nn.functional as F
+
+
+class SpeechEncoder:
+    def __init__(self, sd, device, n_fft=1024, hop=512):
+        p = "speech_encoder."
+        self.device = th.device(device)
+        self.w = {k[len(p):]: v.to(self.device, th.float32)
+                  for k, v in sd.items() if k.startswith(p) and v.is_floating_point()}
+        self.n_fft, self.hop = n_fft, hop
+        win = self.w["wav2spec.1.spectrogram.window"]
+        k = th.arange(n_fft, dtype=th.float64, device=self.device)
+        f = th.arange(n_fft // 2 + 1, dtype=th.float64, device=self.device)
+        ang = 2 * math.pi * k[:, None] * f[None, :] / n_fft
+        basis = th.cat([th.cos(ang), -th.sin(ang)], dim=1)          # (n_fft, 2F)
+        self.basis = (basis * win.double()[:, None]).float()          # window folded in
+        self.fb = self.w["wav2spec.1.mel_scale.fb"]
+        self.coef = -float(self.w["wav2spec.0.flipped_filter"].flatten()[0])
+
+    def _bn(self, name, x):
+        w = self.w
+        return F.batch_norm(x, w[name + ".running_mean"], w[name + ".running_var"],
+                            w[name + ".weight"], w[name + ".bias"], False, 0.0, 1e-5)
+
+    def _conv(self, name, x, stride=1, padding=0):
+        return F.conv2d(x, self.w[name + ".weight"], self.w.get(name + ".bias"), stride=stride, padding=padding)
+
+    def mel(self, wav):
+        """(N, T) -> (N, 128, frames) power mel spectrogram of the pre-emphasised signal."""
+        x = th.cat([wav[:, :1] - self.coef * wav[:, 1:2], wav[:, 1:] - self.coef * wav[:, :-1]], dim=1)
+        x = F.pad(x[:, None, :], (self.n_fft // 2, self.n_fft // 2), mode="reflect")[:, 0]
+        frames = x.unfold(1, self.n_fft, self.hop)                  # (N, frames, n_fft)
+        spec = frames @ self.basis                                   # (N, frames, 2F)
+        nf = self.n_fft // 2 + 1
+        power = spec[..., :nf] ** 2 + spec[..., nf:] ** 2
+        return (power @ self.fb).transpose(1, 2)
+
+    def _block(self, q, x, stride):
+        out = self._bn(q + "bn1", F.relu(self._conv(q + "conv1", x, stride, 1)))
+        out = self._bn(q + "bn2", self._conv(q + "conv2", out, 1, 1))
+        y = out.mean(dim=(2, 3))
+        y = F.relu(F.linear(y, self.w[q + "se.fc.0.weight"], self.w[q + "se.fc.0.bias"]))
+        y = th.sigmoid(F.linear(y, self.w[q + "se.fc.2.weight"], self.w[q + "se.fc.2.bias"]))
+        out = out * y[:, :, None, None]
+        if (q + "downsample.0.weight") in self.w:
+            x = self._bn(q + "downsample.1", self._conv(q + "downsample.0", x, stride))
+        return F.relu(out + x)
+
+    def _head(self, feat, conv, bn, fc, shuffle):
+        if shuffle > 1:
+            feat = F.pixel_shuffle(feat, shuffle)
+        feat = self._bn(bn, F.relu(self._conv(conv, feat)))
+        n, c, h, w = feat.shape
+        feat = feat.reshape(n, c * h, w).transpose(1, 2)
+        return F.linear(feat, self.w[fc + ".weight"], self.w[fc + ".bias"])
+
+    @th.no_grad()
+    def __call__(self, wav):
+        """wav (N, T) f32 -> (z_low, z_mid, z_high), each (N, T_i, d_model)."""
+        wav = wav.to(self.device, th.float32)
+        x = self.mel(wav) + 1e-6
+        x = F.instance_norm(x, eps=1e-5)
+        r = "wav_encoder.feat_extractor."
+        x = self._bn(r + "bn1", F.relu(self._conv(r + "conv1", x[:, None], 1, 1)))
+        feats = []
+        for li, (nblk, stride) in enumerate(zip((3, 4, 6, 3), (1, 2, 2, 2))):
+            for bi in range(nblk):
+                x = self._block(r + f"layer{li + 1}.{bi}.", x, stride if bi == 0 else 1)
+            feats.append(x)
+        z = (self._head(feats[1], r + "conv_low", r + "bn_low", r + "fc_low", 1),
+             self._head(feats[2], r + "conv_mid", r + "bn_mid", r + "fc_mid", 2),
+             self._head(feats[3], r + "conv_high", r + "bn_high", r + "fc_high", 4))
+        pw, pb = self.w["wav_proj_layer.weight"], self.w["wav_proj_layer.bias"]
+        return tuple(F.linear(a, pw, pb) for a in z)
+
+
+def speech_tokens(model_type, z):
+    """Step-invariant speech memory input for ggd_set_memory.
+
+    s2g_v2 (models/model.py:97-104): left zero-pad each level to the longest and concat
+    on features -> (N, Ts, 3d); the blend Linear runs in HIP.  default (model.py:55-68):
+    concat on time -> (N, Ts, d).
+    """
+    if model_type == "s2g_v2":
+        longest = max(a.shape[1] for a in z)
+        return th.cat([F.pad(a, (0, 0, longest - a.shape[1], 0)) for a in z], dim=-1).contiguous()
+    if model_type == "default":
+        return th.cat(list(z), dim=1).contiguous()
+    raise ValueError(f"Unsupported model_type {model_type}")
+
+
+def speech_len(model_type, n_wav, n_fft=1024, hop=512):
+    """Speech-memory token count for a wav window (structural; see SURVEY.md 8c KATs)."""
+    frames = 1 + n_wav // hop                                   # centre padding
+    h = 128
+    w = frames
+    # layer2..4 halve (ceil) both axes: conv stride 2, padding 1, kernel 3
+    dims = []
+    for _ in range(3):
+        h, w = (h + 1) // 2, (w + 1) // 2
+        dims.append((h, w))
+    low = dims[0][1] - 1                                        # conv 2x2, no padding
+    mid = dims[1][1] * 2 - 2                                    # pixel shuffle x2, conv 3x3
+    high = dims[2][1] * 4 - 2                                   # pixel shuffle x4, conv 3x3
+    if model_type == "s2g_v2":
+        return max(low, mid, high)
+    return low + mid + high

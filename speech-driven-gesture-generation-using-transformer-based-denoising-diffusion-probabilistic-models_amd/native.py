@@ -1,0 +1,125 @@
+"""ctypes binding of libggd.so -- the C ABI in include/ggd.h.
+
+The library is built in-tree (``build()``; ``__graft_entry__.build()`` calls it) so
+the ``.so`` travels with the repository snapshot to the GPU box.  There is no
+fallback: if the library is missing, ``load()`` raises.
+"""
+import ctypes
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libggd.so")
+SOURCES = ["ggd_kernels.hip", "ggd_api.hip"]
+HEADERS = ["ggd_kernels.h", os.path.join("..", "..", "include", "ggd.h")]
+
+GGD_OK, GGD_IGNORED = 0, 1
+GGD_ERR_ARG, GGD_ERR_UNSUPPORTED, GGD_ERR_HIP, GGD_ERR_STATE, GGD_ERR_NAME = -1, -2, -3, -4, -5
+MODEL_S2G_V2, MODEL_DEFAULT = 0, 1
+DEC_ONEWAY, DEC_TWOWAY = 0, 1
+F32, BF16 = 0, 1
+DDPM, DDIM = 0, 1
+
+EXPORTS = [
+    "ggd_create", "ggd_destroy", "ggd_last_error", "ggd_load_weight", "ggd_finalize_weights",
+    "ggd_set_schedule", "ggd_set_memory", "ggd_denoise", "ggd_posterior_step", "ggd_sample",
+    "ggd_set_profiling", "ggd_kernel_time", "ggd_version",
+]
+
+
+class Desc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "model_type", "decoder_type", "d_model", "heads", "n_layers", "d_pose", "seq_len",
+        "speech_len", "max_batch", "dtype", "diffusion_steps")]
+
+
+class SampleArgs(ctypes.Structure):
+    _fields_ = [
+        ("alg", ctypes.c_int32), ("eta", ctypes.c_float), ("n", ctypes.c_int32),
+        ("x_T", ctypes.c_void_p), ("noise", ctypes.c_void_p), ("seed", ctypes.c_uint64),
+        ("clip_offset", ctypes.c_int64), ("inpaint_poses", ctypes.c_void_p),
+        ("inpaint_masks", ctypes.c_void_p), ("trans", ctypes.c_void_p), ("out", ctypes.c_void_p),
+        ("extras", ctypes.c_void_p), ("n_steps", ctypes.c_int32), ("use_graph", ctypes.c_int32),
+    ]
+
+
+def _sources():
+    return [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
+
+
+def is_stale():
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(p) > t for p in _sources())
+
+
+def build(force=False, verbose=False):
+    """Compile libggd.so for gfx950 with hipcc (cross-compiles without a GPU)."""
+    if not force and not is_stale():
+        return LIB_PATH
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+           "-Wno-unused-value", "-Wno-unused-result"] + \
+          [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB_PATH + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True, cwd=CSRC)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def load():
+    """Load libggd.so (after torch, so both share torch's HIP runtime)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  -- torch's libamdhip64 must be the one the library binds to
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libggd.so not built at {LIB_PATH}; run __graft_entry__.build() "
+                          "(the HIP path has no fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    P, I32, I64, F, VP = ctypes.POINTER, ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+    CTX = ctypes.c_void_p
+    sig = {
+        "ggd_create": (ctypes.c_int, [ctypes.c_int, P(Desc), P(CTX)]),
+        "ggd_destroy": (ctypes.c_int, [CTX]),
+        "ggd_last_error": (ctypes.c_char_p, [CTX]),
+        "ggd_load_weight": (ctypes.c_int, [CTX, ctypes.c_char_p, VP, I64]),
+        "ggd_finalize_weights": (ctypes.c_int, [CTX]),
+        "ggd_set_schedule": (ctypes.c_int, [CTX, VP, I32, VP]),
+        "ggd_set_memory": (ctypes.c_int, [CTX, VP, I32, I32, I32, VP]),
+        "ggd_denoise": (ctypes.c_int, [CTX, VP, VP, VP, I32, VP]),
+        "ggd_posterior_step": (ctypes.c_int, [CTX, I32, F, I32, VP, VP, VP, VP, VP, VP, I32, VP]),
+        "ggd_sample": (ctypes.c_int, [CTX, P(SampleArgs), VP]),
+        "ggd_set_profiling": (ctypes.c_int, [CTX, I32]),
+        "ggd_kernel_time": (ctypes.c_int, [CTX, I32, P(ctypes.c_double), P(I64)]),
+        "ggd_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class GgdError(RuntimeError):
+    pass
+
+
+def check(ctx, code, what):
+    """Map a ggd_status to the reference's exception types."""
+    if code >= 0:
+        return code
+    msg = load().ggd_last_error(ctx)
+    msg = msg.decode() if msg else ""
+    text = f"{what}: {msg}"
+    if code == GGD_ERR_UNSUPPORTED:
+        raise ValueError(text)
+    if code in (GGD_ERR_ARG, GGD_ERR_NAME):
+        raise AssertionError(text)
+    raise GgdError(text)

@@ -1,0 +1,37 @@
+"""Batch-sharded sampling over ranks (one process per GPU, torch.distributed over RCCL).
+
+Clips are independent units (no cross-batch op in eval: BN uses running stats,
+InstanceNorm and attention are per clip), so rank r of G samples clips
+[r*N/G, (r+1)*N/G) with zero per-step communication; the counter-based noise is
+keyed by GLOBAL clip id, so 1/2/4/8-GPU outputs are bit-identical.  The only
+collective is one all-gather of the final poses.  The
+reference's only distributed code is training DDP (utils/pytorch_ddp.py:18,
+models/trainer.py:83); this replaces it in kind for inference.
+"""
+import torch as th
+import torch.distributed as dist
+
+
+def shard_range(n_total, rank, world):
+    """Contiguous, balanced [start, stop) of the clips owned by ``rank``."""
+    base, extra = divmod(n_total, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def sample_sharded(sample_fn, wavs, n_total, rank, world, device):
+    """Run ``sample_fn(wav_shard, clip_offset) -> (n_local, ...)`` on this rank's clips and
+    all-gather the results in global clip order on every rank."""
+    start, stop = shard_range(n_total, rank, world)
+    local = sample_fn(wavs[start:stop], start).contiguous()
+    if world == 1:
+        return local
+    counts = [shard_range(n_total, r, world) for r in range(world)]
+    sizes = [b - a for a, b in counts]
+    maxn = max(sizes)
+    pad = th.zeros((maxn,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    gathered = th.empty((world * maxn,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(gathered, pad)
+    parts = [gathered[r * maxn: r * maxn + sizes[r]] for r in range(world)]
+    return th.cat(parts, dim=0)
