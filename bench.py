@@ -59,11 +59,21 @@ def parse():
     return p.parse_args()
 
 
+def log(*a):
+    print("[bench %.1fs]" % (time.perf_counter() - T_START), *a, file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
+
+
 def cpu_baseline(pkg, cfg, sd, arch, B, L, T, n_steps):
     """Oracle on the host cores: faithful per-step encoder, n_steps denoise steps, extrapolated x T."""
     from oracle import ref_denoiser, ref_diffusion
     cores = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS"):
+        cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))  # the box's CPU share
     th.set_num_threads(cores)
+    log(f"cpu baseline: {cores} threads, B={B}, {n_steps} steps")
     ocfg = {k: arch[k] for k in ("type", "d_model", "decoder", "heads", "n_layers")}
     om = ref_denoiser.OracleModel(sd, ocfg, cache_speech=False)
     g = th.Generator().manual_seed(1)
@@ -71,6 +81,7 @@ def cpu_baseline(pkg, cfg, sd, arch, B, L, T, n_steps):
     sch = ref_diffusion.make_schedule("linear", T, "")
     noise = ref_diffusion.TorchNoise(2)
     ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, "ddpm", n_steps=1)
+    log("cpu baseline warm-up step done")
     t0 = time.perf_counter()
     ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, "ddpm", n_steps=n_steps)
     dt = time.perf_counter() - t0
@@ -147,7 +158,10 @@ def main():
     prof = not args.no_profile
     lib.ggd_set_profiling(ctx.h, 1 if prof else 0)
     for w in range(args.warmup):
+        log(f"warm-up pass {w}")
         one_pass(wavs[w], seed=w)
+        th.cuda.synchronize(dev)
+    log("timed region")
     if dist is not None:
         dist.barrier()
     th.cuda.synchronize(dev)
@@ -156,6 +170,7 @@ def main():
     import ctypes
     for k in range(args.steps):
         out = one_pass(wavs[args.warmup + k], seed=100 + k)
+        log(f"pass {k} issued")
         if prof:
             avg = ctypes.c_double()
             cnt = ctypes.c_int64()
@@ -171,6 +186,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     lib.ggd_set_profiling(ctx.h, 0)
+    log(f"timed region done: {elapsed:.3f} s")
     assert out.shape == (n_total, d_pose, L) and bool(th.isfinite(out).all())
 
     frames = args.steps * n_total * L

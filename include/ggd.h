@@ -146,6 +146,16 @@ int ggd_sample(ggd_ctx* ctx, const ggd_sample_args* args, void* stream);
 int ggd_set_profiling(ggd_ctx* ctx, int32_t on);
 int ggd_kernel_time(ggd_ctx* ctx, int32_t which, double* avg_us, int64_t* launches);
 
+/* Diagnostics (not part of the reference surface): launch one kernel configuration `iters`
+ * times back to back on the ctx stream and return the average microseconds per launch
+ * (hipEvents).  what = 0: GEMM, p = {pro, epi, M, N, K, force_mt, no_xcd_remap};
+ * what = 1: attention, p = {cross, n}; what = 2: one full denoise step (eager launches),
+ * p = {n}; what = 3: the same step as one hipGraph replay, p = {n}; what = 4: one fused kernel,
+ * p = {0 KA | 1 KB | 2 KC | 3 KE, n}; what = 5: calibration micro-kernels, p = {mode, arg, blocks,
+ * buffer MiB} with mode 0 empty launch, 1 dependent-load chase (arg loads), 2 shader clock
+ * (returns GHz instead of microseconds), 3 / 4 bulk 64 KiB / 16 KiB load per block. */
+int ggd_diag(ggd_ctx* ctx, int32_t what, const int32_t* p, int32_t np, int32_t iters, double* avg_us);
+
 /* Library version string. */
 const char* ggd_version(void);
 

@@ -34,10 +34,16 @@ struct Conv3 {          // depthwise 3-tap: f32 [dk][3] + [dk]
   float* b = nullptr;
 };
 
+struct FLin {           // MFMA B-fragment packed Linear: T [tiles][k steps][64 lanes][16 B], f32 bias
+  void* w = nullptr;
+  float* b = nullptr;
+};
+
 struct Layer {
   float *ln1_g, *ln1_b, *ln2_g, *ln2_b, *ln3_g, *ln3_b;
   Lin qkv, o_sa, q_ca, kv_ca, o_ca, ff1, ff2;
   Conv3 sa_q, sa_k, sa_v, ca_q, ca_k, ca_v;
+  FLin f_qkv, f_o_sa, f_q_ca, f_o_ca, f_ff1;  // fused-path copies
 };
 
 struct ProfEvents {
@@ -62,6 +68,8 @@ struct ggd_ctx {
 
   // weights
   Lin emb_x, emb_mem, out_lin, step0, step2, blend;
+  FLin f_emb, f_out;
+  bool fused = false;        // per-clip fused kernels (L <= 64, d_model 256, 8 heads)
   float *out_ln_g = nullptr, *out_ln_b = nullptr;
   std::vector<Layer> layers;
   float* pe = nullptr;       // [pe_len][d]
@@ -82,7 +90,7 @@ struct ggd_ctx {
   int mem_n = -1;
 
   // workspaces
-  float *x = nullptr, *h = nullptr, *eps = nullptr;
+  float *x = nullptr, *h = nullptr, *h2 = nullptr, *eps = nullptr;
   void *qkv = nullptr, *att = nullptr, *q = nullptr, *ffn = nullptr;
   int* d_counter = nullptr;  // iteration counter k
   int* d_t = nullptr;        // per-clip t (denoise path)
@@ -157,7 +165,7 @@ int pack_lin(ggd_ctx* c, Lin& L, const std::vector<std::string>& prefixes, int n
   L.n = n;
   L.k = k;
   L.npad = round_up(n, 64);
-  L.kpad = round_up(k, 128);
+  L.kpad = round_up(k, 256);
   std::vector<float> w((size_t)L.npad * L.kpad, 0.f), b(L.npad, 0.f);
   for (size_t p = 0; p < prefixes.size(); ++p) {
     const auto* W = get(c, prefixes[p] + ".weight", (size_t)n_each * k);
@@ -193,6 +201,63 @@ int pack_conv(ggd_ctx* c, Conv3& cv, const std::string& prefix, int dk) {
   int r = upload_vec(c, &cv.w, prefix + ".conv.weight", (size_t)dk * 3);
   if (r) return r;
   return upload_vec(c, &cv.b, prefix + ".conv.bias", (size_t)dk);
+}
+
+// Pack the rows `perm` of a row-major f32 matrix W (k columns) into MFMA B fragments:
+// fragment (tile nt, k step kf), lane l, element e holds W[perm[nt*16 + (l & 15)]][kf*KF + (l >> 4)*EPL + e]
+// with KF = 64 / sizeof(T) and EPL = 16 / sizeof(T); out-of-range rows / columns are zero.
+int pack_frag(ggd_ctx* c, FLin& F, const std::vector<const float*>& rows_w, const std::vector<float>& bias, int k) {
+  const int n = (int)rows_w.size();
+  const int tsz = (int)c->tsize, KF = 64 / tsz, EPL = 16 / tsz;
+  const int ntiles = (n + 15) / 16, kpad = round_up(k, KF), KT = kpad / KF;
+  std::vector<float> buf((size_t)ntiles * KT * 64 * EPL, 0.f), b((size_t)ntiles * 16, 0.f);
+  for (int nt = 0; nt < ntiles; ++nt)
+    for (int kf = 0; kf < KT; ++kf)
+      for (int l = 0; l < 64; ++l)
+        for (int e = 0; e < EPL; ++e) {
+          const int row = nt * 16 + (l & 15), kk = kf * KF + (l >> 4) * EPL + e;
+          if (row < n && kk < k)
+            buf[(((size_t)nt * KT + kf) * 64 + l) * EPL + e] = rows_w[row][kk];
+        }
+  for (int r = 0; r < n; ++r) b[r] = bias[r];
+  HIP_TRY(c, dalloc(c, &F.b, sizeof(float) * b.size()));
+  HIP_TRY(c, hipMemcpy(F.b, b.data(), sizeof(float) * b.size(), hipMemcpyHostToDevice));
+  HIP_TRY(c, dalloc(c, &F.w, c->tsize * buf.size()));
+  if (c->desc.dtype == GGD_F32) {
+    HIP_TRY(c, hipMemcpy(F.w, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice));
+  } else {
+    std::vector<uint16_t> wb(buf.size());
+    for (size_t i = 0; i < buf.size(); ++i) wb[i] = f2bf_host(buf[i]);
+    HIP_TRY(c, hipMemcpy(F.w, wb.data(), 2 * wb.size(), hipMemcpyHostToDevice));
+  }
+  return GGD_OK;
+}
+
+// rows of the named Linear(s) in the given order; `order` indexes the concatenated rows
+int frag_from(ggd_ctx* c, FLin& F, const std::vector<std::string>& prefixes, int n_each, int k,
+              const std::vector<int>& order) {
+  std::vector<const float*> rw;
+  std::vector<float> bias;
+  std::vector<const std::vector<float>*> W, B;
+  for (const auto& p : prefixes) {
+    const auto* w = get(c, p + ".weight", (size_t)n_each * k);
+    const auto* b = get(c, p + ".bias", (size_t)n_each);
+    if (!w || !b) return GGD_ERR_NAME;
+    W.push_back(w);
+    B.push_back(b);
+  }
+  for (int r : order) {
+    const int p = r / n_each, i = r % n_each;
+    rw.push_back(W[p]->data() + (size_t)i * k);
+    bias.push_back((*B[p])[i]);
+  }
+  return pack_frag(c, F, rw, bias, k);
+}
+
+std::vector<int> iota_n(int n) {
+  std::vector<int> v(n);
+  for (int i = 0; i < n; ++i) v[i] = i;
+  return v;
 }
 
 GemmArgs gemm_args(const Lin& L, int M, const void* A, int lda, void* out, int ldo) {
@@ -279,11 +344,82 @@ int prof_mark(ggd_ctx* c, hipStream_t s, int which) {
   return GGD_OK;
 }
 
+FinalArgs final_args(ggd_ctx* c, int n) {
+  FinalArgs f{};
+  f.n = n;
+  f.L = c->desc.seq_len;
+  f.C = c->desc.d_pose;
+  f.h = c->h;
+  f.ln_g = c->out_ln_g;
+  f.ln_b = c->out_ln_b;
+  f.w_out = c->f_out.w;
+  f.b_out = c->f_out.b;
+  f.w_emb = c->f_emb.w;
+  f.b_emb = c->f_emb.b;
+  f.pe = c->pe;
+  f.x = c->x;
+  f.steps = c->d_steps;
+  f.step_counter = c->d_counter;
+  return f;
+}
+
+// Fused decoder layers (ggd_fused.hip) on h (= emb_x(x) + PE, already in c->h): per layer
+// KA, KB, KC and the FFN-down GEMM.  Residual rows ping-pong h -> h2 -> h so that no
+// workgroup overwrites rows a sibling workgroup of the same clip still reads.
+int launch_fused_layers(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
+  const ggd_desc& D = c->desc;
+  const int L = D.seq_len, d = D.d_model, M = n * L;
+  hipStream_t s = c->stream;
+  for (int li = 0; li < D.n_layers; ++li) {
+    const Layer& Ly = c->layers[li];
+    FusedArgs f{};
+    FusedLayer& w = f.w;
+    w.qkv = Ly.f_qkv.w; w.qkv_b = Ly.f_qkv.b;
+    w.o_sa = Ly.f_o_sa.w; w.o_sa_b = Ly.f_o_sa.b;
+    w.q_ca = Ly.f_q_ca.w; w.q_ca_b = Ly.f_q_ca.b;
+    w.o_ca = Ly.f_o_ca.w; w.o_ca_b = Ly.f_o_ca.b;
+    w.ff1 = Ly.f_ff1.w; w.ff1_b = Ly.f_ff1.b;
+    w.ln1_g = Ly.ln1_g; w.ln1_b = Ly.ln1_b; w.ln2_g = Ly.ln2_g; w.ln2_b = Ly.ln2_b;
+    w.ln3_g = Ly.ln3_g; w.ln3_b = Ly.ln3_b;
+    w.sa_qw = Ly.sa_q.w; w.sa_qb = Ly.sa_q.b; w.sa_kw = Ly.sa_k.w; w.sa_kb = Ly.sa_k.b;
+    w.sa_vw = Ly.sa_v.w; w.sa_vb = Ly.sa_v.b;
+    w.ca_qw = Ly.ca_q.w; w.ca_qb = Ly.ca_q.b; w.ca_kw = Ly.ca_k.w; w.ca_kb = Ly.ca_k.b;
+    w.ca_vw = Ly.ca_v.w; w.ca_vb = Ly.ca_v.b;
+    w.kv_mem = c->kv_mem + (size_t)li * D.max_batch * D.speech_len * 2 * d;
+    w.kv_step = c->kv_step + (size_t)li * D.diffusion_steps * 2 * d;
+    f.L = L;
+    f.Ts = D.speech_len;
+    f.o_sa = c->att;
+    f.o_ca = c->q;
+    f.hid = c->ffn;
+    f.t_clip = t_clip;
+    f.steps = c->d_steps;
+    f.step_counter = c->d_counter;
+    f.scale = 1.0f / std::sqrt((float)(d / D.heads));
+    f.h = c->h;
+    f.h_out = c->h2;
+    f.bump_counter = sampling && li == 0;
+    HIP_TRY(c, launch_fused(0, D.dtype, f, n, s));     // KA: LN1 + QKV + conv + self-attention
+    f.bump_counter = 0;
+    HIP_TRY(c, launch_fused(1, D.dtype, f, n, s));     // KB: out-proj + LN2 + Q + cross-attention
+    f.h = c->h2;
+    f.h_out = c->h;
+    const bool prof = c->profiling && sampling;
+    if (prof) { int r = prof_mark(c, s, 0); if (r) return r; }
+    HIP_TRY(c, launch_fused(2, D.dtype, f, n, s));     // KC: out-proj + LN3 + FFN-up + ReLU^2
+    if (prof) { int r = prof_mark(c, s, 1); if (r) return r; }
+    GemmArgs g = gemm_args(Ly.ff2, M, c->ffn, 4 * d, c->h, d);
+    GEMM(c, PRO_T, EPI_RESID, g, s);                   // KD: FFN-down + residual
+  }
+  return GGD_OK;
+}
+
 // The decoder forward on the internal x state (M = n*L rows) ending in eps [M][cpad].
 // In sampling mode (`sampling`), the first GEMM advances the iteration counter and the
 // cross-attention reads t from the step records.
 int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
   const ggd_desc& D = c->desc;
+  if (c->fused) return launch_fused_layers(c, n, sampling, t_clip);
   const int L = D.seq_len, d = D.d_model, M = n * L, dk = d / D.heads;
   hipStream_t s = c->stream;
 
@@ -371,6 +507,22 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
 int launch_step(ggd_ctx* c, const ggd_sample_args& a, float* extras, int fixed_k) {
   int r = launch_decoder(c, a.n, true, nullptr);
   if (r) return r;
+  if (c->fused) {  // KE: LN_out + out-proj + update + the next step's emb_x + PE
+    FinalArgs f = final_args(c, a.n);
+    f.alg = a.alg;
+    f.noise = a.noise;
+    f.seed = a.seed;
+    f.clip_offset = a.clip_offset;
+    f.inp_pose = a.inpaint_masks ? a.inpaint_poses : nullptr;
+    f.inp_mask = a.inpaint_masks;
+    f.trans = a.trans;
+    f.extras = extras;
+    f.do_out = 1;
+    f.do_update = 1;
+    f.do_emb = 1;
+    HIP_TRY(c, launch_final(c->desc.dtype, f, c->stream));
+    return GGD_OK;
+  }
   UpdArgs u{};
   u.n = a.n;
   u.C = c->desc.d_pose;
@@ -474,8 +626,8 @@ int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out) {
     return GGD_ERR_UNSUPPORTED;
   }
   const int dk = D.d_model / D.heads;
-  if ((dk != 32 && dk != 64) || D.d_model % 128 || D.seq_len > 192 || D.speech_len + 1 > 192) {
-    c->err = "unsupported shape (need d_model % 128 == 0, d_k in {32,64}, L <= 192, memory <= 192)";
+  if ((dk != 32 && dk != 64) || D.d_model != 256 || D.seq_len > 192 || D.speech_len + 1 > 192) {
+    c->err = "unsupported shape (need d_model == 256, d_k in {32,64}, L <= 192, memory <= 192)";
     *out = c;
     return GGD_ERR_UNSUPPORTED;
   }
@@ -495,6 +647,7 @@ int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out) {
   c->cpad = round_up(D.d_pose, 64);
   HIP_TRY(c, dalloc(c, &c->x, sizeof(float) * M * D.d_pose));
   HIP_TRY(c, dalloc(c, &c->h, sizeof(float) * M * d));
+  HIP_TRY(c, dalloc(c, &c->h2, sizeof(float) * M * d));
   HIP_TRY(c, dalloc(c, &c->eps, sizeof(float) * M * c->cpad));
   HIP_TRY(c, dalloc(c, &c->qkv, c->tsize * M * 3 * d));
   HIP_TRY(c, dalloc(c, &c->att, c->tsize * M * d));
@@ -584,6 +737,27 @@ int ggd_finalize_weights(ggd_ctx* c) {
     TRY(pack_lin(c, Ly.ff1, {q + "feed_forward.layer1"}, 4 * d, d));
     TRY(pack_lin(c, Ly.ff2, {q + "feed_forward.layer2"}, d, 4 * d));
   }
+  c->fused = D.d_model == 256 && D.heads == 8 && D.seq_len <= 64 &&
+             fused_lds_max(D.dtype, D.seq_len, D.speech_len) <= 160 * 1024;
+  if (c->fused) {
+    TRY(frag_from(c, c->f_emb, {P + "emb_x"}, d, C, iota_n(d)));
+    TRY(frag_from(c, c->f_out, {P + "out_layers.1"}, C, d, iota_n(C)));
+    std::vector<int> head_major;  // per head h: q rows h*32.., k rows 256 + h*32.., v rows 512 + h*32..
+    for (int h = 0; h < D.heads; ++h)
+      for (int part = 0; part < 3; ++part)
+        for (int i = 0; i < dk; ++i) head_major.push_back(part * d + h * dk + i);
+    for (int l = 0; l < D.n_layers; ++l) {
+      Layer& Ly = c->layers[l];
+      const std::string q = P + "layers." + std::to_string(l) + ".";
+      const std::string sa = q + "self_attn.", ca = q + "cross_attn.";
+      TRY(frag_from(c, Ly.f_qkv, {sa + "query.0.linear", sa + "key.0.linear", sa + "value.0.linear"}, d, d,
+                    head_major));
+      TRY(frag_from(c, Ly.f_o_sa, {sa + "output"}, d, d, iota_n(d)));
+      TRY(frag_from(c, Ly.f_q_ca, {ca + "query.0.linear"}, d, d, iota_n(d)));
+      TRY(frag_from(c, Ly.f_o_ca, {ca + "output"}, d, d, iota_n(d)));
+      TRY(frag_from(c, Ly.f_ff1, {q + "feed_forward.layer1"}, 4 * d, d, iota_n(4 * d)));
+    }
+  }
   TRY(build_step_tables(c));
 #undef TRY
   c->staged.clear();
@@ -657,9 +831,21 @@ int ggd_denoise(ggd_ctx* c, const float* x_t, const int32_t* t, float* eps, int3
   HIP_TRY(c, hipEventRecord(c->ev_in, (hipStream_t)stream));
   HIP_TRY(c, hipStreamWaitEvent(s, c->ev_in, 0));
   HIP_TRY(c, launch_init_state(c->x, x_t, 0, 0, n, D.d_pose, D.seq_len, s));
-  int r = launch_decoder(c, n, false, t);
-  if (r) return r;
-  HIP_TRY(c, launch_nlc_to_ncl(eps, c->eps, n, D.d_pose, D.seq_len, c->cpad, s));
+  if (c->fused) {
+    FinalArgs f = final_args(c, n);
+    f.do_emb = 1;  // emb_x + PE of x_t into h
+    HIP_TRY(c, launch_final(D.dtype, f, s));
+    int r = launch_decoder(c, n, false, t);
+    if (r) return r;
+    f.do_emb = 0;
+    f.do_out = 1;  // LN_out + out-proj -> eps in (N, C, L)
+    f.eps_out = eps;
+    HIP_TRY(c, launch_final(D.dtype, f, s));
+  } else {
+    int r = launch_decoder(c, n, false, t);
+    if (r) return r;
+    HIP_TRY(c, launch_nlc_to_ncl(eps, c->eps, n, D.d_pose, D.seq_len, c->cpad, s));
+  }
   HIP_TRY(c, hipEventRecord(c->ev_out, s));
   HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
   return GGD_OK;
@@ -705,6 +891,207 @@ int ggd_kernel_time(ggd_ctx* c, int32_t which, double* avg_us, int64_t* launches
   return GGD_OK;
 }
 
+int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t iters, double* avg_us) {
+  if (!c || !p || !avg_us || iters <= 0) return fail(c, GGD_ERR_ARG, "bad argument");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const ggd_desc& D = c->desc;
+  const int d = D.d_model;
+  hipEvent_t e0, e1;
+  HIP_TRY(c, hipEventCreate(&e0));
+  HIP_TRY(c, hipEventCreate(&e1));
+  std::vector<void*> tmp;
+  auto talloc = [&](size_t bytes) -> void* {
+    void* v = nullptr;
+    if (hipMalloc(&v, bytes) != hipSuccess) return nullptr;
+    (void)hipMemset(v, 0x3c, bytes);  // small finite values in f32 and bf16
+    tmp.push_back(v);
+    return v;
+  };
+  int rc = GGD_OK;
+  float ms = 0.f;
+  if (what == 0 && np >= 7) {
+    GemmArgs g{};
+    const int pro = p[0], epi = p[1];
+    g.M = p[2]; g.N = p[3]; g.K = p[4]; g.force_mt = p[5]; g.no_xcd_remap = p[6];
+    g.k_valid = g.K;
+    const size_t asz = (pro == PRO_T ? c->tsize : 4) * (size_t)g.M * g.K;
+    g.A = talloc(asz);
+    g.lda = g.K;
+    g.W = talloc(c->tsize * (size_t)g.N * g.K);
+    g.bias = (float*)talloc(4 * (size_t)g.N);
+    g.ln_g = (float*)talloc(4 * (size_t)g.K);
+    g.ln_b = (float*)talloc(4 * (size_t)g.K);
+    g.out = talloc(4 * (size_t)g.M * g.N);
+    g.ldo = g.N;
+    g.n_valid = g.N;
+    g.pe = c->pe;
+    g.pe_period = 1;
+    if (!g.A || !g.W || !g.out) rc = fail(c, GGD_ERR_HIP, "diag alloc");
+    for (int it = 0; rc == GGD_OK && it < iters + 1; ++it) {
+      if (it == 1) HIP_TRY(c, hipEventRecord(e0, s));
+      GEMM(c, pro, epi, g, s);
+    }
+  } else if (what == 1 && np >= 2) {
+    const int n = p[1];
+    if (n > D.max_batch) rc = fail(c, GGD_ERR_ARG, "n > max_batch");
+    AttnArgs at{};
+    const Layer& Ly = c->layers[0];
+    at.cross = p[0];
+    at.q = c->qkv; at.ldq = 3 * d;
+    at.k = (const char*)c->qkv + c->tsize * d;
+    at.v = (const char*)c->qkv + c->tsize * 2 * d;
+    at.ldkv = 3 * d;
+    at.kv_mem = c->kv_mem;
+    at.kv_step = c->kv_step;
+    at.t_clip = c->d_t;
+    at.cw_q = Ly.sa_q.w; at.cb_q = Ly.sa_q.b;
+    at.cw_k = Ly.sa_k.w; at.cb_k = Ly.sa_k.b;
+    at.cw_v = Ly.sa_v.w; at.cb_v = Ly.sa_v.b;
+    at.out = c->att; at.ldo = d;
+    at.Lq = D.seq_len;
+    at.Lk = at.cross ? 1 + D.speech_len : D.seq_len;
+    at.dk = d / D.heads; at.heads = D.heads; at.d = d;
+    at.scale = 1.0f / std::sqrt((float)at.dk);
+    for (int it = 0; rc == GGD_OK && it < iters + 1; ++it) {
+      if (it == 1) HIP_TRY(c, hipEventRecord(e0, s));
+      HIP_TRY(c, launch_attention(D.dtype, at, n, s));
+    }
+  } else if ((what == 2 || what == 3) && np >= 1) {
+    const int n = p[0];
+    if (n > D.max_batch || c->betas.empty()) rc = fail(c, GGD_ERR_STATE, "need schedule and n <= max_batch");
+    ggd_sample_args sa{};
+    sa.alg = GGD_DDPM;
+    sa.n = n;
+    std::vector<StepRec> recs;
+    if (rc == GGD_OK) {
+      make_records(c, GGD_DDPM, 0.f, recs);
+      HIP_TRY(c, hipMemcpyAsync(c->d_steps, recs.data(), sizeof(StepRec) * recs.size(), hipMemcpyHostToDevice, s));
+      HIP_TRY(c, launch_init_state(c->x, nullptr, 1, 0, n, D.d_pose, D.seq_len, s));
+      if (c->fused) {
+        FinalArgs f = final_args(c, n);
+        f.do_emb = 1;
+        HIP_TRY(c, launch_final(D.dtype, f, s));
+      }
+    }
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    if (rc == GGD_OK && what == 3) {
+      HIP_TRY(c, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      rc = launch_step(c, sa, nullptr, -1);
+      hipError_t e = hipStreamEndCapture(s, &g);
+      if (rc == GGD_OK && e != hipSuccess) rc = fail(c, GGD_ERR_HIP, "capture");
+      if (rc == GGD_OK) HIP_TRY(c, hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    }
+    const int T = (int)recs.size();
+    for (int it = 0; rc == GGD_OK && it < iters + 1; ++it) {
+      if (it % T == 0) HIP_TRY(c, launch_set_int(c->d_counter, -1, s));
+      if (it == 1) HIP_TRY(c, hipEventRecord(e0, s));
+      if (what == 3)
+        HIP_TRY(c, hipGraphLaunch(ge, s));
+      else
+        rc = launch_step(c, sa, nullptr, -1);
+    }
+    if (ge) (void)hipGraphExecDestroy(ge);
+    if (g) (void)hipGraphDestroy(g);
+  } else if ((what == 4 || what == 6) && np >= 2 && c->fused) {
+    const int which = p[0], n = p[1];
+    unsigned long long* st = what == 6 ? (unsigned long long*)talloc(64 * 8) : nullptr;
+    if (what == 6) iters = 1;
+    if (n > D.max_batch || c->betas.empty()) rc = fail(c, GGD_ERR_STATE, "need schedule and n <= max_batch");
+    std::vector<StepRec> recs;
+    if (rc == GGD_OK) {
+      make_records(c, GGD_DDPM, 0.f, recs);
+      HIP_TRY(c, hipMemcpyAsync(c->d_steps, recs.data(), sizeof(StepRec) * recs.size(), hipMemcpyHostToDevice, s));
+      HIP_TRY(c, launch_set_int(c->d_counter, 0, s));
+    }
+    for (int it = 0; rc == GGD_OK && it < iters + 1; ++it) {
+      if (it == 1) HIP_TRY(c, hipEventRecord(e0, s));
+      if (which < 3) {
+        // the layer-0 arguments of launch_fused_layers
+        const Layer& Ly = c->layers[0];
+        FusedArgs f{};
+        FusedLayer& w = f.w;
+        w.qkv = Ly.f_qkv.w; w.qkv_b = Ly.f_qkv.b; w.o_sa = Ly.f_o_sa.w; w.o_sa_b = Ly.f_o_sa.b;
+        w.q_ca = Ly.f_q_ca.w; w.q_ca_b = Ly.f_q_ca.b; w.o_ca = Ly.f_o_ca.w; w.o_ca_b = Ly.f_o_ca.b;
+        w.ff1 = Ly.f_ff1.w; w.ff1_b = Ly.f_ff1.b;
+        w.ln1_g = Ly.ln1_g; w.ln1_b = Ly.ln1_b; w.ln2_g = Ly.ln2_g; w.ln2_b = Ly.ln2_b;
+        w.ln3_g = Ly.ln3_g; w.ln3_b = Ly.ln3_b;
+        w.sa_qw = Ly.sa_q.w; w.sa_qb = Ly.sa_q.b; w.sa_kw = Ly.sa_k.w; w.sa_kb = Ly.sa_k.b;
+        w.sa_vw = Ly.sa_v.w; w.sa_vb = Ly.sa_v.b; w.ca_qw = Ly.ca_q.w; w.ca_qb = Ly.ca_q.b;
+        w.ca_kw = Ly.ca_k.w; w.ca_kb = Ly.ca_k.b; w.ca_vw = Ly.ca_v.w; w.ca_vb = Ly.ca_v.b;
+        w.kv_mem = c->kv_mem;
+        w.kv_step = c->kv_step;
+        f.L = D.seq_len; f.Ts = D.speech_len;
+        f.o_sa = c->att; f.o_ca = c->q; f.hid = c->ffn;
+        f.steps = c->d_steps; f.step_counter = c->d_counter;
+        f.scale = 1.0f / std::sqrt((float)(d / D.heads));
+        f.h = c->h; f.h_out = c->h2;
+        f.stamps = it == iters ? st : nullptr;
+        HIP_TRY(c, launch_fused(which, D.dtype, f, n, s));
+      } else {
+        FinalArgs f = final_args(c, n);
+        f.do_out = 1; f.do_update = 1; f.do_emb = 1;
+        f.stamps = it == iters ? st : nullptr;
+        HIP_TRY(c, launch_final(D.dtype, f, s));
+      }
+    }
+    if (rc == GGD_OK && what == 6) {  // avg_us -> 8 phase deltas in microseconds (2.4 GHz-independent: s_memtime ticks / 2400)
+      (void)hipMemset(st, 0, 0);
+      HIP_TRY(c, hipStreamSynchronize(s));
+      unsigned long long h_st[16];
+      HIP_TRY(c, hipMemcpy(h_st, st, sizeof h_st, hipMemcpyDeviceToHost));
+      for (int i = 0; i < 8; ++i) avg_us[i] = (h_st[i + 1] > h_st[0] && h_st[i + 1] < h_st[0] + 100000000ull) ? (h_st[i + 1] - h_st[0]) / 2400.0 : -1.0;
+      for (void* v : tmp) (void)hipFree(v);
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      return GGD_OK;
+    }
+  } else if (what == 5 && np >= 4) {
+    // calibration micro-kernels: p = {mode, arg, blocks, buffer MiB}
+    const int mode = p[0], arg = p[1], blocks = p[2];
+    const size_t bytes = (size_t)p[3] << 20;
+    void* buf = talloc(bytes);
+    if (!buf) rc = fail(c, GGD_ERR_HIP, "diag alloc");
+    if (rc == GGD_OK && mode == 1) {  // chase ring: jump ~1 MiB + 64 B per step through the buffer
+      const size_t n = bytes / 4 - 16;
+      std::vector<int> nx(n);
+      const size_t stride = (size_t)(1 << 18) + 16;
+      for (size_t i = 0; i < n; ++i) nx[i] = (int)((i + stride) % n);
+      HIP_TRY(c, hipMemcpy(buf, nx.data(), 4 * n, hipMemcpyHostToDevice));
+    }
+    for (int it = 0; rc == GGD_OK && it < iters + 1; ++it) {
+      if (it == 1) HIP_TRY(c, hipEventRecord(e0, s));
+      HIP_TRY(c, launch_mb(mode, buf, bytes, arg, blocks, s));
+    }
+    if (rc == GGD_OK && mode == 2) {
+      HIP_TRY(c, hipEventRecord(e1, s));
+      HIP_TRY(c, hipEventSynchronize(e1));
+      unsigned long long st[3];
+      HIP_TRY(c, hipMemcpy(st, buf, sizeof st, hipMemcpyDeviceToHost));
+      *avg_us = st[1] ? (double)st[0] / ((double)st[1] / 100.0) / 1000.0 : 0.0;  // GHz
+      (void)hipStreamSynchronize(s);
+      for (void* v : tmp) (void)hipFree(v);
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      return GGD_OK;
+    }
+  } else {
+    rc = fail(c, GGD_ERR_ARG, "unknown diagnostic");
+  }
+  if (rc == GGD_OK) {
+    HIP_TRY(c, hipEventRecord(e1, s));
+    HIP_TRY(c, hipEventSynchronize(e1));
+    HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
+    *avg_us = ms * 1000.0 / iters;
+  }
+  (void)hipStreamSynchronize(s);
+  for (void* v : tmp) (void)hipFree(v);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return rc;
+}
+
 int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   if (!c || !a || !a->out) return fail(c, GGD_ERR_ARG, "null argument");
   if (!c->finalized) return fail(c, GGD_ERR_STATE, "weights not finalized");
@@ -726,6 +1113,11 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   HIP_TRY(c, hipStreamWaitEvent(s, c->ev_in, 0));
   HIP_TRY(c, hipMemcpyAsync(c->d_steps, recs.data(), sizeof(StepRec) * T, hipMemcpyHostToDevice, s));
   HIP_TRY(c, launch_init_state(c->x, a->x_T, a->seed, a->clip_offset, a->n, D.d_pose, D.seq_len, s));
+  if (c->fused) {  // emb_x + PE of x_T; every later step's embedding is computed by that step's KE
+    FinalArgs f = final_args(c, a->n);
+    f.do_emb = 1;
+    HIP_TRY(c, launch_final(D.dtype, f, s));
+  }
   HIP_TRY(c, launch_set_int(c->d_counter, -1, s));
 
   const int graph_steps = a->extras ? nsteps - 1 : nsteps;

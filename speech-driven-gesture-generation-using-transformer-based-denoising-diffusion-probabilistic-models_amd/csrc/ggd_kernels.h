@@ -38,6 +38,8 @@ struct GemmArgs {
   void* out; int ldo; int n_valid;
   const float* pe; int pe_period; int pe_offset;  // EPI_PE, pe table [max_len][N]
   int* step_counter;     // if non-null, block 0 thread 0 increments it (one step begins)
+  int no_xcd_remap;      // diagnostics: 1 = plain blockIdx tile order
+  int force_mt;          // diagnostics: 0 = automatic tile height, else 32 or 64
 };
 
 // Per-iteration diffusion coefficients, f32, computed on the host from fp64
@@ -95,7 +97,48 @@ struct PostArgs {
   float* x_out; float* x0_out;
 };
 
+// Fused per-clip decoder (ggd_fused.hip): fragment-packed weights of one layer.
+struct FusedLayer {
+  const void *qkv, *o_sa, *q_ca, *o_ca, *ff1;  // T fragments [tile][k step][64 lanes][16 B]
+  const float *qkv_b, *o_sa_b, *q_ca_b, *o_ca_b, *ff1_b;
+  const float *ln1_g, *ln1_b, *ln2_g, *ln2_b, *ln3_g, *ln3_b;
+  const float *sa_qw, *sa_qb, *sa_kw, *sa_kb, *sa_vw, *sa_vb;
+  const float *ca_qw, *ca_qb, *ca_kw, *ca_kb, *ca_vw, *ca_vb;
+  const float *kv_mem, *kv_step;
+};
+
+struct FusedArgs {
+  FusedLayer w;
+  int L, Ts;
+  float* h;          // residual rows read (f32 [N*L][256])
+  float* h_out;      // KB / KC: updated residual rows written (ping-pong buffer)
+  void *o_sa, *o_ca, *hid;
+  const int* t_clip; const StepRec* steps; int* step_counter; int bump_counter;
+  float scale;
+  unsigned long long* stamps;  // diagnostics: block (0,0) writes s_memtime at phase boundaries
+};
+
+struct FinalArgs {
+  int n, L, C, alg;
+  float* h; const float *ln_g, *ln_b;
+  const void* w_out; const float* b_out;   // packed out_layers.1 (8 tiles, K 256)
+  const void* w_emb; const float* b_emb;   // packed emb_x (16 tiles, K 128)
+  const float* pe;
+  float* x;                // state (N, L, C)
+  float* eps_out;          // model-protocol mode: (N, C, L)
+  const StepRec* steps; int* step_counter;
+  const float* noise; uint64_t seed; int64_t clip_offset;
+  const float *inp_pose, *inp_mask, *trans;
+  float* extras;
+  int do_out, do_update, do_emb;
+  unsigned long long* stamps;  // diagnostics
+};
+
 // launchers (return hipError_t of the launch)
+hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s);  // 0 KA, 1 KB, 2 KC
+hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s);
+size_t fused_lds_max(int dtype, int L, int Ts);
+hipError_t launch_mb(int mode, void* buf, size_t buf_bytes, int arg, int blocks, hipStream_t s);  // ggd_diag.hip
 hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);

@@ -9,100 +9,173 @@
 //                   Q/K/V fused on load, QK^T, 64-lane wavefront softmax, PV.
 //   update_kernel   fused DDPM / DDIM posterior update with inpaint x0-replacement and
 //                   counter-based (Philox4x32-10 + Box-Muller) noise.
-#include "ggd_kernels.h"
+#include "ggd_common.h"
 
 namespace ggd {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-
-constexpr int KC = 128;          // K chunk staged in LDS per iteration
-constexpr int NT = 64;           // output columns per workgroup
-constexpr int NTHREADS = 256;    // 4 waves
-
-__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
-__device__ __forceinline__ float bf2f(bf16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
-
-template <typename T> __device__ __forceinline__ T from_f32(float v);
-template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
-template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float v) { return f2bf(v); }
-template <typename T> __device__ __forceinline__ float to_f32(T v);
-template <> __device__ __forceinline__ float to_f32<float>(float v) { return v; }
-template <> __device__ __forceinline__ float to_f32<bf16_t>(bf16_t v) { return bf2f(v); }
-
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
-}
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
 // ---------------------------------------------------------------------------
-// GEMM
+// GEMM:  out[M][N] = epi( pro(A)[M][K] . W[N][K]^T + b )
+//
+// One 256-thread workgroup per MT x 64 output tile; K is staged through LDS in 256-wide
+// chunks.  Every global load of a chunk (A rows and W rows) is issued back to back into
+// registers before any of them is consumed, and chunk c+1 is prefetched into registers
+// while the MFMAs of chunk c run -- these small, latency-bound GEMMs are paced by memory
+// round trips, not by MFMA throughput.  PRO_LN keeps the tile's f32 rows in registers,
+// reduces the row statistics there (4 lanes per row, fixed, so results do not depend on
+// the tile height) and normalises on the way into LDS.
 // ---------------------------------------------------------------------------
 template <typename T> struct Tile;
 template <> struct Tile<bf16_t> { static constexpr int PAD = 8; static constexpr int VE = 8; };
 template <> struct Tile<float>  { static constexpr int PAD = 4; static constexpr int VE = 4; };
 
+template <typename T, int MT, int PRO> struct ARegs;
+template <typename T, int MT> struct ARegs<T, MT, PRO_T> {          // T rows, 16-byte vectors
+  static constexpr int VPR = KC / Tile<T>::VE;                      // vectors per row
+  static constexpr int N = MT * VPR / NTHREADS;
+  uint4 v[N];
+};
+template <typename T, int MT> struct ARegs<T, MT, PRO_LN> {         // f32 rows, 4 lanes per row
+  static constexpr int N = KC / 16;                                 // float4 per lane
+  float4 v[N];
+  float mu, rs;
+};
+template <typename T, int MT> struct ARegs<T, MT, PRO_F32> {        // f32, arbitrary lda, k < k_valid
+  static constexpr int N = MT * KC / NTHREADS;
+  float v[N];
+};
+
 template <typename T, int MT, int PRO>
-__device__ __forceinline__ void stage_a(const GemmArgs& a, T* As, int m0, int kc0,
-                                        const float* s_mean, const float* s_rstd) {
-  constexpr int STR = KC + Tile<T>::PAD;
+__device__ __forceinline__ void load_a(ARegs<T, MT, PRO>& R, const GemmArgs& a, int m0, int kc0) {
+  constexpr int N = ARegs<T, MT, PRO>::N;
   const int tid = threadIdx.x;
   if constexpr (PRO == PRO_T) {
-    constexpr int VE = Tile<T>::VE;
-    constexpr int VPR = KC / VE;
+    constexpr int VPR = ARegs<T, MT, PRO>::VPR, VE = Tile<T>::VE;
     const T* A = (const T*)a.A;
-    for (int v = tid; v < MT * VPR; v += NTHREADS) {
-      const int r = v / VPR, cv = v % VPR, m = m0 + r;
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (m < a.M) val = *(const uint4*)(A + (size_t)m * a.lda + kc0 + cv * VE);
-      *(uint4*)(As + r * STR + cv * VE) = val;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int v = tid + i * NTHREADS, r = v / VPR, cv = v % VPR, m = m0 + r;
+      R.v[i] = m < a.M ? *(const uint4*)(A + (size_t)m * a.lda + kc0 + cv * VE) : make_uint4(0, 0, 0, 0);
     }
   } else if constexpr (PRO == PRO_LN) {
-    constexpr int VPR = KC / 4;
+    const int r = tid >> 2, j = tid & 3, m = m0 + r;
+    const bool ok = tid < MT * 4 && m < a.M;
+    const float* row = (const float*)a.A + (size_t)m * a.lda + kc0;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      R.v[i] = ok ? *(const float4*)(row + (j + 4 * i) * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  } else {
     const float* A = (const float*)a.A;
-    for (int v = tid; v < MT * VPR; v += NTHREADS) {
-      const int r = v / VPR, cv = v % VPR, m = m0 + r, k = kc0 + cv * 4;
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (m < a.M) {
-        x = *(const float4*)(A + (size_t)m * a.lda + k);
-        const float mu = s_mean[r], rs = s_rstd[r];
-        const float4 g = *(const float4*)(a.ln_g + k);
-        const float4 bb = *(const float4*)(a.ln_b + k);
-        x.x = (x.x - mu) * rs * g.x + bb.x;
-        x.y = (x.y - mu) * rs * g.y + bb.y;
-        x.z = (x.z - mu) * rs * g.z + bb.z;
-        x.w = (x.w - mu) * rs * g.w + bb.w;
-      }
-      T* dst = As + r * STR + cv * 4;
-      dst[0] = from_f32<T>(x.x); dst[1] = from_f32<T>(x.y);
-      dst[2] = from_f32<T>(x.z); dst[3] = from_f32<T>(x.w);
-    }
-  } else {  // PRO_F32: f32 rows with only k_valid columns, arbitrary lda
-    const float* A = (const float*)a.A;
-    for (int v = tid; v < MT * KC; v += NTHREADS) {
-      const int r = v / KC, c = v % KC, m = m0 + r, k = kc0 + c;
-      float x = 0.f;
-      if (m < a.M && k < a.k_valid) x = A[(size_t)m * a.lda + k];
-      As[r * STR + c] = from_f32<T>(x);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int v = tid + i * NTHREADS, r = v / KC, c = v % KC, m = m0 + r, k = kc0 + c;
+      R.v[i] = (m < a.M && k < a.k_valid) ? A[(size_t)m * a.lda + k] : 0.f;
     }
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void stage_w(const GemmArgs& a, T* Ws, int n0, int kc0) {
+// LayerNorm statistics of the registers' rows (two-pass: mean, then centred sum of squares).
+template <typename T, int MT>
+__device__ __forceinline__ void ln_stats(ARegs<T, MT, PRO_LN>& R, int K) {
+  constexpr int N = ARegs<T, MT, PRO_LN>::N;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < N; ++i) s += (R.v[i].x + R.v[i].y) + (R.v[i].z + R.v[i].w);
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  const float mu = s / (float)K;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float d0 = R.v[i].x - mu, d1 = R.v[i].y - mu, d2 = R.v[i].z - mu, d3 = R.v[i].w - mu;
+    q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+  }
+  q += __shfl_xor(q, 1);
+  q += __shfl_xor(q, 2);
+  R.mu = mu;
+  R.rs = 1.0f / sqrtf(q / (float)K + 1e-5f);
+}
+
+template <typename T, int MT, int PRO>
+__device__ __forceinline__ void store_a(const ARegs<T, MT, PRO>& R, const GemmArgs& a, T* As, int kc0) {
   constexpr int STR = KC + Tile<T>::PAD;
-  constexpr int VE = Tile<T>::VE;
-  constexpr int VPR = KC / VE;
+  constexpr int N = ARegs<T, MT, PRO>::N;
+  const int tid = threadIdx.x;
+  if constexpr (PRO == PRO_T) {
+    constexpr int VPR = ARegs<T, MT, PRO>::VPR, VE = Tile<T>::VE;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int v = tid + i * NTHREADS, r = v / VPR, cv = v % VPR;
+      *(uint4*)(As + r * STR + cv * VE) = R.v[i];
+    }
+  } else if constexpr (PRO == PRO_LN) {
+    if (tid >= MT * 4) return;
+    const int r = tid >> 2, j = tid & 3;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int k = (j + 4 * i) * 4;
+      const float4 g = *(const float4*)(a.ln_g + kc0 + k);
+      const float4 b = *(const float4*)(a.ln_b + kc0 + k);
+      const float4 x = R.v[i];
+      T* dst = As + r * STR + k;
+      dst[0] = from_f32<T>((x.x - R.mu) * R.rs * g.x + b.x);
+      dst[1] = from_f32<T>((x.y - R.mu) * R.rs * g.y + b.y);
+      dst[2] = from_f32<T>((x.z - R.mu) * R.rs * g.z + b.z);
+      dst[3] = from_f32<T>((x.w - R.mu) * R.rs * g.w + b.w);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int v = tid + i * NTHREADS, r = v / KC, c = v % KC;
+      As[r * STR + c] = from_f32<T>(R.v[i]);
+    }
+  }
+}
+
+// rows [r0, r0 + ROWS) x columns [kc0, kc0 + KC) of a row-major T matrix -> LDS tile
+// (rows >= nrows read as zero).  All loads of the tile are independent and issue together.
+template <typename T, int ROWS>
+__device__ __forceinline__ void copy_tile(T* dst, const T* src, int ld, int r0, int nrows, int kc0) {
+  constexpr int STR = KC + Tile<T>::PAD, VE = Tile<T>::VE, VPR = KC / VE, N = ROWS * VPR / NTHREADS;
+  uint4 v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int e = threadIdx.x + i * NTHREADS, r = e / VPR, cv = e % VPR;
+    v[i] = r0 + r < nrows ? *(const uint4*)(src + (size_t)(r0 + r) * ld + kc0 + cv * VE) : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int e = threadIdx.x + i * NTHREADS, r = e / VPR, cv = e % VPR;
+    *(uint4*)(dst + r * STR + cv * VE) = v[i];
+  }
+}
+
+template <typename T> struct WRegs {
+  static constexpr int VPR = KC / Tile<T>::VE;
+  static constexpr int N = NT * VPR / NTHREADS;
+  uint4 v[N];
+};
+
+template <typename T>
+__device__ __forceinline__ void load_w(WRegs<T>& R, const GemmArgs& a, int n0, int kc0) {
+  constexpr int N = WRegs<T>::N;
+  constexpr int VPR = WRegs<T>::VPR, VE = Tile<T>::VE;
   const T* W = (const T*)a.W;
-  for (int v = threadIdx.x; v < NT * VPR; v += NTHREADS) {
-    const int r = v / VPR, cv = v % VPR;
-    *(uint4*)(Ws + r * STR + cv * VE) = *(const uint4*)(W + (size_t)(n0 + r) * a.K + kc0 + cv * VE);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int v = threadIdx.x + i * NTHREADS, r = v / VPR, cv = v % VPR;
+    R.v[i] = *(const uint4*)(W + (size_t)(n0 + r) * a.K + kc0 + cv * VE);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_w(const WRegs<T>& R, T* Ws) {
+  constexpr int N = WRegs<T>::N;
+  constexpr int STR = KC + Tile<T>::PAD;
+  constexpr int VPR = WRegs<T>::VPR, VE = Tile<T>::VE;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int v = threadIdx.x + i * NTHREADS, r = v / VPR, cv = v % VPR;
+    *(uint4*)(Ws + r * STR + cv * VE) = R.v[i];
   }
 }
 
@@ -128,9 +201,9 @@ __device__ __forceinline__ void mma_chunk(const T* As, const T* Ws, int arow0, i
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bw[j], acc[i][j], 0, 0, 0);
     }
   } else {
-    // f32 operands: each lane reads 4 consecutive k; MFMA step s pairs k = 16*kk' + 4*g + s
-    // identically for A and W, so every k is used once (k-permuted f32 fma chain).
-#pragma unroll 2
+    // f32 operands: each lane reads 4 consecutive k; MFMA step s pairs k = kk + 4*g + s
+    // identically for A and W, so every k is used once (a k-permuted f32 fma chain).
+#pragma unroll 4
     for (int kk = 0; kk < KC; kk += 16) {
       f32x4 af[TM], bw[TN];
 #pragma unroll
@@ -150,53 +223,27 @@ __device__ __forceinline__ void mma_chunk(const T* As, const T* Ws, int arow0, i
   }
 }
 
-template <typename T, int MT, int PRO, int EPI>
+template <typename T, int MT, int PRO, int EPI, int NCH>
 __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
   constexpr int STR = KC + Tile<T>::PAD;
-  constexpr int WM = MT / 2, WN = NT / 2;     // 2x2 waves
+  constexpr int WM = MT / 2, WN = NT / 2;     // 2 x 2 waves
   constexpr int TM = WM / 16, TN = WN / 16;
   __shared__ __attribute__((aligned(16))) T As[MT * STR];
   __shared__ __attribute__((aligned(16))) T Ws[NT * STR];
-  __shared__ float s_mean[MT], s_rstd[MT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int n0 = blockIdx.x * NT, m0 = blockIdx.y * MT;
+  // XCD-aware tile order (T1): workgroups are dealt round-robin over the 8 XCDs; remap so each
+  // XCD gets a contiguous run of row-major tiles, i.e. whole row blocks share one L2 and the
+  // A rows are fetched once per XCD instead of once per column tile.  Speed only.
+  int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  if (!a.no_xcd_remap) {
+    const int nwg = gridDim.x * gridDim.y, q = nwg / 8, rem = nwg % 8, x = tile % 8, slot = tile / 8;
+    tile = (x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q) + slot;
+  }
+  const int n0 = (tile % gridDim.x) * NT, m0 = (tile / gridDim.x) * MT;
 
   if (a.step_counter && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) atomicAdd(a.step_counter, 1);
-
-  if constexpr (PRO == PRO_LN) {
-    // row statistics over the full K (LayerNorm width), two-pass, 4 threads per row whatever the
-    // tile height, so a row's LN result does not depend on the batch size (shard invariance)
-    constexpr int TPR = 4;
-    if (tid < MT * TPR) {
-      const int r = tid / TPR, j = tid % TPR, m = m0 + r;
-      const float* row = (const float*)a.A + (size_t)m * a.lda;
-      float s = 0.f;
-      if (m < a.M)
-        for (int k = j * 4; k < a.K; k += TPR * 4) {
-          const float4 v = *(const float4*)(row + k);
-          s += (v.x + v.y) + (v.z + v.w);
-        }
-      s += __shfl_xor(s, 1);
-      s += __shfl_xor(s, 2);
-      const float mu = s / (float)a.K;
-      float q = 0.f;
-      if (m < a.M)
-        for (int k = j * 4; k < a.K; k += TPR * 4) {
-          const float4 v = *(const float4*)(row + k);
-          const float d0 = v.x - mu, d1 = v.y - mu, d2 = v.z - mu, d3 = v.w - mu;
-          q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-        }
-      q += __shfl_xor(q, 1);
-      q += __shfl_xor(q, 2);
-      if (j == 0) {
-        s_mean[r] = mu;
-        s_rstd[r] = 1.0f / sqrtf(q / (float)a.K + 1e-5f);
-      }
-    }
-    __syncthreads();
-  }
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -204,16 +251,40 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int kc0 = 0; kc0 < a.K; kc0 += KC) {
-    stage_a<T, MT, PRO>(a, As, m0, kc0, s_mean, s_rstd);
-    stage_w<T>(a, Ws, n0, kc0);
+  // NCH = K / 256 is a template constant.  Each chunk's loads are issued together (one
+  // memory round trip) and written to LDS; plain T operands and the weights are copied
+  // global -> LDS directly (no register array survives a chunk: a loop-carried staging
+  // array is demoted to scratch by the compiler).
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (c > 0) __syncthreads();  // previous chunk's MFMAs are done with the LDS tiles
+    if constexpr (PRO == PRO_T) {
+      copy_tile<T, MT>(As, (const T*)a.A, a.lda, m0, a.M, c * KC);
+    } else {
+      ARegs<T, MT, PRO> ra;
+      load_a<T, MT, PRO>(ra, a, m0, c * KC);
+      if constexpr (PRO == PRO_LN) ln_stats<T, MT>(ra, a.K);
+      store_a<T, MT, PRO>(ra, a, As, c * KC);
+    }
+    copy_tile<T, NT>(Ws, (const T*)a.W, a.K, n0, 1 << 30, c * KC);
     __syncthreads();
     mma_chunk<T, TM, TN>(As, Ws, wr * WM, wc * WN, lane, acc);
-    __syncthreads();
   }
 
-  // epilogue: C/D map of 16x16 MFMA: col = lane & 15, row = 4 * (lane >> 4) + r
+  // epilogue: C/D map of the 16x16 MFMA: col = lane & 15, row = 4 * (lane >> 4) + r
   const int g = lane >> 4, c16 = lane & 15;
+  float res[TM][TN][4];
+  if constexpr (EPI == EPI_RESID) {  // read every residual first: one round trip, not one per store
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wr * WM + i * 16 + g * 4 + r, n = n0 + wc * WN + j * 16 + c16;
+          res[i][j][r] = m < a.M ? ((const float*)a.out)[(size_t)m * a.ldo + n] : 0.f;
+        }
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -235,8 +306,7 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
         } else if constexpr (EPI == EPI_SILU) {
           ((float*)a.out)[(size_t)m * a.ldo + n] = v / (1.0f + expf(-v));
         } else if constexpr (EPI == EPI_RESID) {
-          float* o = (float*)a.out + (size_t)m * a.ldo + n;
-          *o = *o + v;
+          ((float*)a.out)[(size_t)m * a.ldo + n] = res[i][j][r] + v;
         } else {  // EPI_PE
           const int pos = (m % a.pe_period) + a.pe_offset;
           ((float*)a.out)[(size_t)m * a.ldo + n] = v + a.pe[(size_t)pos * a.N + n];
@@ -248,7 +318,16 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
 template <typename T, int MT, int PRO, int EPI>
 static hipError_t gemm_go(const GemmArgs& a, hipStream_t s) {
   dim3 grid(a.N / NT, (a.M + MT - 1) / MT);
-  hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI>), grid, dim3(NTHREADS), 0, s, a);
+  switch (a.K / KC) {
+    case 1: hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 1>), grid, dim3(NTHREADS), 0, s, a); break;
+    case 3:
+      if constexpr (PRO != PRO_LN) hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 3>), grid, dim3(NTHREADS), 0, s, a);
+      break;
+    case 4:
+      if constexpr (PRO != PRO_LN) hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 4>), grid, dim3(NTHREADS), 0, s, a);
+      break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -256,7 +335,7 @@ template <typename T, int PRO, int EPI>
 static hipError_t gemm_mt(const GemmArgs& a, hipStream_t s) {
   // 64-row tiles when that still gives >= ~200 workgroups, else 32-row tiles.
   const long tiles64 = (long)(a.N / NT) * ((a.M + 63) / 64);
-  if (tiles64 >= 200) return gemm_go<T, 64, PRO, EPI>(a, s);
+  if (a.force_mt == 64 || (a.force_mt == 0 && tiles64 >= 200)) return gemm_go<T, 64, PRO, EPI>(a, s);
   return gemm_go<T, 32, PRO, EPI>(a, s);
 }
 
@@ -285,126 +364,90 @@ static hipError_t gemm_pro(int pro, int epi, const GemmArgs& a, hipStream_t s) {
 
 hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream_t s) {
   if (a.N % NT != 0 || a.K % KC != 0 || a.M <= 0) return hipErrorInvalidValue;
+  if (a.K != KC && a.K != 3 * KC && a.K != 4 * KC) return hipErrorInvalidValue;
+  if (pro == PRO_LN && a.K != KC) return hipErrorInvalidValue;  // LayerNorm width = one chunk
   if (dtype == 0) return gemm_pro<float>(pro, epi, a, s);
   return gemm_pro<bf16_t>(pro, epi, a, s);
 }
 
 // ---------------------------------------------------------------------------
 // attention with fused depthwise sequence conv (transformer.py:28-44, 88-118)
+//
+// One workgroup per (head, clip).  The head's raw Q / K / V rows are staged into LDS (f32,
+// zero halo rows) and the Primer-EZ 3-tap conv writes MFMA-ready operands: Q and K row-major,
+// V transposed (so P.V's B operand is a contiguous 16-byte read).  Each wave owns 16-row
+// query tiles: S = Q K^T on MFMA (16 x Lk_pad accumulators in registers), softmax on the
+// accumulator layout (row reductions over the 16 lanes sharing a row: xor 1, 2, 4, 8),
+// P to a per-wave LDS tile, O = P V on MFMA.  bf16: v_mfma_f32_16x16x32_bf16; f32 parity
+// mode: v_mfma_f32_16x16x4_f32.
 // ---------------------------------------------------------------------------
-constexpr int ATT_LMAX = 192;  // keys per query row handled as 3 x 64 lanes
-
-template <typename T>
-__device__ __forceinline__ float ld_any(const void* p, size_t idx) {
-  return to_f32<T>(((const T*)p)[idx]);
-}
-
 template <typename T>
 __global__ void __launch_bounds__(NTHREADS) attn_kernel(AttnArgs a) {
-  extern __shared__ float sm[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int h = blockIdx.x, b = blockIdx.y;
-  const int dk = a.dk, S = dk + 1, Lq = a.Lq, Lk = a.Lk;
-  float* Qs = sm;
-  float* Ks = Qs + Lq * S;
-  float* Vs = Ks + Lk * S;
+  const int dk = a.dk, Lq = a.Lq, Lk = a.Lk;
+  const AttGeom G = att_geom<T>(Lq, Lk, dk);
+  T* Qm = (T*)(smem + G.off_q);
+  T* Km = (T*)(smem + G.off_k);
+  T* Vt = (T*)(smem + G.off_v);
+  T* Pw = (T*)(smem + G.off_p);
+  float* raw = (float*)(smem + G.off_raw);
   const int tid = threadIdx.x;
 
-  int t = 0;
-  if (a.cross) t = a.t_clip ? a.t_clip[b] : a.steps[*a.step_counter].t_orig;
-
-  // Q: 3-tap conv over the query sequence, zero padded
-  for (int idx = tid; idx < Lq * dk; idx += NTHREADS) {
-    const int i = idx / dk, c = idx % dk;
-    const size_t col = (size_t)h * dk + c;
-    const float r0 = i > 0 ? ld_any<T>(a.q, (size_t)(b * Lq + i - 1) * a.ldq + col) : 0.f;
-    const float r1 = ld_any<T>(a.q, (size_t)(b * Lq + i) * a.ldq + col);
-    const float r2 = i + 1 < Lq ? ld_any<T>(a.q, (size_t)(b * Lq + i + 1) * a.ldq + col) : 0.f;
-    Qs[i * S + c] = a.cb_q[c] + a.cw_q[c * 3 + 0] * r0 + a.cw_q[c * 3 + 1] * r1 + a.cw_q[c * 3 + 2] * r2;
+  // zero the padded operand images (rows >= Lq / Lk must be finite zeros)
+  {
+    uint4* z = (uint4*)smem;
+    const int n16 = (int)(G.off_p / 16);
+    for (int i = tid; i < n16; i += NTHREADS) z[i] = make_uint4(0, 0, 0, 0);
   }
-  // K, V
-  for (int idx = tid; idx < Lk * dk; idx += NTHREADS) {
-    const int j = idx / dk, c = idx % dk;
-    float k3[3], v3[3];
-#pragma unroll
-    for (int o = 0; o < 3; ++o) {
-      const int jj = j + o - 1;
-      float kv = 0.f, vv = 0.f;
-      if (jj >= 0 && jj < Lk) {
-        if (!a.cross) {
-          const size_t base = (size_t)(b * Lk + jj) * a.ldkv + (size_t)h * dk + c;
-          kv = ld_any<T>(a.k, base);
-          vv = ld_any<T>(a.v, base);
-        } else {
-          const float* row = jj == 0 ? a.kv_step + (size_t)t * 2 * a.d
-                                     : a.kv_mem + (size_t)(b * (Lk - 1) + jj - 1) * 2 * a.d;
-          kv = row[h * dk + c];
-          vv = row[a.d + h * dk + c];
-        }
+  att_stage_rows<T>(raw, a.q, (size_t)b * Lq, a.ldq, h * dk, Lq, dk);
+  __syncthreads();
+  att_conv<T, false>(Qm, G.SQ, raw, Lq, dk, a.cw_q, a.cb_q);
+  __syncthreads();
+  if (!a.cross) {
+    att_stage_rows<T>(raw, a.k, (size_t)b * Lk, a.ldkv, h * dk, Lk, dk);
+    __syncthreads();
+    att_conv<T, false>(Km, G.SQ, raw, Lk, dk, a.cw_k, a.cb_k);
+    __syncthreads();
+    att_stage_rows<T>(raw, a.v, (size_t)b * Lk, a.ldkv, h * dk, Lk, dk);
+    __syncthreads();
+    att_conv<T, true>(Vt, G.SV, raw, Lk, dk, a.cw_v, a.cb_v);
+  } else {
+    // memory row 0 = the diffusion-step token of this clip's t; rows 1.. = cached speech K|V
+    const int t = a.t_clip ? a.t_clip[b] : a.steps[*a.step_counter].t_orig;
+    const float* r0 = a.kv_step + (size_t)t * 2 * a.d;
+    for (int half = 0; half < 2; ++half) {
+      const int col = half * a.d + h * dk;
+      att_stage_rows<float>(raw + dk, a.kv_mem, (size_t)b * (Lk - 1), 2 * a.d, col, Lk - 1, dk);
+      for (int c = tid; c < dk; c += NTHREADS) {
+        raw[c] = 0.f;
+        raw[dk + c] = r0[col + c];
       }
-      k3[o] = kv;
-      v3[o] = vv;
+      __syncthreads();
+      if (half == 0)
+        att_conv<T, false>(Km, G.SQ, raw, Lk, dk, a.cw_k, a.cb_k);
+      else
+        att_conv<T, true>(Vt, G.SV, raw, Lk, dk, a.cw_v, a.cb_v);
+      __syncthreads();
     }
-    Ks[j * S + c] = a.cb_k[c] + a.cw_k[c * 3 + 0] * k3[0] + a.cw_k[c * 3 + 1] * k3[1] + a.cw_k[c * 3 + 2] * k3[2];
-    Vs[j * S + c] = a.cb_v[c] + a.cw_v[c * 3 + 0] * v3[0] + a.cw_v[c * 3 + 1] * v3[1] + a.cw_v[c * 3 + 2] * v3[2];
   }
   __syncthreads();
 
-  const int lane = tid & 63, wave = tid >> 6;
-  const int G = 64 / dk;          // lane groups splitting the keys in P.V (2 at dk=32)
-  const int c = lane % dk, g = lane / dk;
-  for (int i = wave; i < Lq; i += NTHREADS / 64) {
-    const float* q = Qs + i * S;
-    float s[3];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int j = lane + 64 * u;
-      s[u] = -INFINITY;
-      if (j < Lk) {
-        const float* kr = Ks + j * S;
-        float acc = 0.f;
-        for (int cc = 0; cc < dk; ++cc) acc += q[cc] * kr[cc];
-        s[u] = acc * a.scale;
-        mx = fmaxf(mx, s[u]);
-      }
-    }
-    mx = wave_max(mx);
-    float sum = 0.f;
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int j = lane + 64 * u;
-      s[u] = j < Lk ? expf(s[u] - mx) : 0.f;
-      sum += s[u];
-    }
-    sum = wave_sum(sum);
-    const float inv = 1.0f / sum;
-#pragma unroll
-    for (int u = 0; u < 3; ++u) s[u] *= inv;
+  attn_core<T>(Qm, Km, Vt, Pw, G, Lq, Lk, dk, a.scale, (T*)a.out + (size_t)b * Lq * a.ldo + (size_t)h * dk, a.ldo);
+}
 
-    float o = 0.f;
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      if (64 * u >= Lk) break;
-      for (int jj = 0; jj < 64; jj += G) {
-        const int src = jj + g;
-        const float p = __shfl(s[u], src);
-        const int j = 64 * u + src;
-        if (j < Lk) o += p * Vs[j * S + c];
-      }
-    }
-    if (G == 2) o += __shfl_xor(o, 32);
-    if (g == 0) ((T*)a.out)[(size_t)(b * Lq + i) * a.ldo + (size_t)h * dk + c] = from_f32<T>(o);
-  }
+size_t attention_lds_bytes(int dtype, const AttnArgs& a) {
+  return dtype == 0 ? att_geom<float>(a.Lq, a.Lk, a.dk).total : att_geom<bf16_t>(a.Lq, a.Lk, a.dk).total;
 }
 
 hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s) {
   if (a.Lq > ATT_LMAX || a.Lk > ATT_LMAX || (a.dk != 32 && a.dk != 64)) return hipErrorInvalidValue;
-  const size_t lds = (size_t)(a.Lq + 2 * a.Lk) * (a.dk + 1) * sizeof(float);
+  const size_t lds = attention_lds_bytes(dtype, a);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)attn_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)attn_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)attn_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)attn_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   dim3 grid(a.heads, n);
@@ -413,67 +456,6 @@ hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s) 
   else
     hipLaunchKernelGGL(attn_kernel<bf16_t>, grid, dim3(NTHREADS), lds, s, a);
   return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// counter-based Gaussian noise (oracle/philox.py restates this bit for bit up to libm ulps)
-// ---------------------------------------------------------------------------
-constexpr uint32_t TAG_STEP = 0, TAG_XT = 1;
-
-__device__ __forceinline__ float philox_normal(uint64_t seed, uint32_t clip, uint32_t step, uint32_t tag,
-                                               uint32_t e) {
-#pragma clang fp contract(off)
-  uint32_t c0 = e >> 2, c1 = clip, c2 = step, c3 = tag;
-  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-  }
-  const int sel = e & 3;
-  const uint32_t ua_i = sel < 2 ? c0 : c2, ub_i = sel < 2 ? c1 : c3;
-  const float inv = 2.3283064365386963e-10f;
-  const float ua = ((float)ua_i + 1.0f) * inv;
-  const float ub = (float)ub_i * inv;
-  const float r = sqrtf(-2.0f * logf(ua));
-  const float th = 6.283185307179586f * ub;
-  return (sel & 1) ? r * sinf(th) : r * cosf(th);
-}
-
-// ---------------------------------------------------------------------------
-// diffusion update (gaussian_diffusion.py:268-275, 287-298, 207-232, 326-328, 465-483;
-// inpaint denoise_fn generator.py:272-281).  IEEE ops in the reference's order, no fma
-// contraction, so given the same eps and noise it matches the CPU oracle bit for bit.
-// ---------------------------------------------------------------------------
-struct UpdOut { float x0, raw, mean, xn; };
-
-__device__ __forceinline__ UpdOut upd_math(const StepRec& r, int alg, float x, float e, bool have_x0,
-                                           float x0_in, bool inp, float m, float p, float tf, float z) {
-#pragma clang fp contract(off)
-  UpdOut o;
-  float x0 = r.sra * x - r.srm1 * e;
-  o.raw = x0;
-  if (have_x0) x0 = x0_in;
-  if (inp) {
-    const float a1 = ((1.0f - tf) * m) * p;
-    const float a2 = (tf * m) * x0;
-    const float a3 = (1.0f - m) * x0;
-    x0 = (a1 + a2) + a3;
-  }
-  o.x0 = x0;
-  o.mean = r.c1 * x0 + r.c2 * x;
-  const float nzs = r.i != 0 ? r.sigma : 0.0f;
-  if (alg == 0) {
-    o.xn = o.mean + nzs * z;
-  } else {
-    const float e2 = (r.sra * x - x0) / r.srm1;
-    const float mp = x0 * r.sqrt_abp + r.c_eps * e2;
-    o.xn = mp + nzs * z;
-  }
-  return o;
 }
 
 __global__ void __launch_bounds__(NTHREADS) update_kernel(UpdArgs a) {

@@ -75,10 +75,25 @@ class SpeechEncoder:
         feat = feat.reshape(n, c * h, w).transpose(1, 2)
         return F.linear(feat, self.w[fc + ".weight"], self.w[fc + ".bias"])
 
+    CHUNK = 8  # clips per encoder call: fixed, so a clip's features never depend on its batch
+
     @th.no_grad()
     def __call__(self, wav):
-        """wav (N, T) f32 -> (z_low, z_mid, z_high), each (N, T_i, d_model)."""
+        """wav (N, T) f32 -> (z_low, z_mid, z_high), each (N, T_i, d_model).
+
+        Runs in fixed chunks of CHUNK clips (the last one zero padded): MIOpen and the GEMM
+        libraries pick algorithms by batch size, so a fixed batch keeps every clip's speech
+        memory bit-identical however the clips are sharded over GPUs or calls.
+        """
         wav = wav.to(self.device, th.float32)
+        n = wav.shape[0]
+        pad = (-n) % self.CHUNK
+        if pad:
+            wav = th.cat([wav, wav.new_zeros(pad, wav.shape[1])])
+        outs = [self._encode(wav[i:i + self.CHUNK]) for i in range(0, wav.shape[0], self.CHUNK)]
+        return tuple(th.cat([o[k] for o in outs])[:n] for k in range(3))
+
+    def _encode(self, wav):
         x = self.mel(wav) + 1e-6
         x = F.instance_norm(x, eps=1e-5)
         r = "wav_encoder.feat_extractor."

@@ -11,8 +11,8 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libggd.so")
-SOURCES = ["ggd_kernels.hip", "ggd_api.hip"]
-HEADERS = ["ggd_kernels.h", os.path.join("..", "..", "include", "ggd.h")]
+SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_diag.hip", "ggd_api.hip"]
+HEADERS = ["ggd_kernels.h", "ggd_common.h", os.path.join("..", "..", "include", "ggd.h")]
 
 GGD_OK, GGD_IGNORED = 0, 1
 GGD_ERR_ARG, GGD_ERR_UNSUPPORTED, GGD_ERR_HIP, GGD_ERR_STATE, GGD_ERR_NAME = -1, -2, -3, -4, -5
@@ -24,7 +24,7 @@ DDPM, DDIM = 0, 1
 EXPORTS = [
     "ggd_create", "ggd_destroy", "ggd_last_error", "ggd_load_weight", "ggd_finalize_weights",
     "ggd_set_schedule", "ggd_set_memory", "ggd_denoise", "ggd_posterior_step", "ggd_sample",
-    "ggd_set_profiling", "ggd_kernel_time", "ggd_version",
+    "ggd_set_profiling", "ggd_kernel_time", "ggd_diag", "ggd_version",
 ]
 
 
@@ -59,11 +59,19 @@ def build(force=False, verbose=False):
     """Compile libggd.so for gfx950 with hipcc (cross-compiles without a GPU)."""
     if not force and not is_stale():
         return LIB_PATH
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
-           "-Wno-unused-value", "-Wno-unused-result"] + \
-          [os.path.join(CSRC, s) for s in SOURCES] + ["-o", LIB_PATH + ".tmp"]
-    if verbose:
-        print(" ".join(cmd))
+    flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-value", "-Wno-unused-result"]
+    objs, procs = [], []
+    os.makedirs(os.path.join(PKG_DIR, "build"), exist_ok=True)
+    for src in SOURCES:  # one hipcc per translation unit, in parallel
+        obj = os.path.join(PKG_DIR, "build", src.replace(".hip", ".o"))
+        cmd = ["hipcc"] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append(subprocess.Popen(cmd, cwd=CSRC))
+        objs.append(obj)
+    if any(p.wait() != 0 for p in procs):
+        raise RuntimeError("hipcc failed")
+    cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", LIB_PATH + ".tmp"]
     subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
     return LIB_PATH
@@ -97,6 +105,7 @@ def load():
         "ggd_sample": (ctypes.c_int, [CTX, P(SampleArgs), VP]),
         "ggd_set_profiling": (ctypes.c_int, [CTX, I32]),
         "ggd_kernel_time": (ctypes.c_int, [CTX, I32, P(ctypes.c_double), P(I64)]),
+        "ggd_diag": (ctypes.c_int, [CTX, I32, VP, I32, I32, VP]),
         "ggd_version": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
