@@ -65,9 +65,9 @@ print(f"step eager n=32: {diag(2, [32], 50):8.2f} us")
 print(f"step graph n=32: {diag(3, [32], 200):8.2f} us")
 print(f"step graph n=8 : {diag(3, [8], 200):8.2f} us")
 print(f"step graph n=1 : {diag(3, [1], 200):8.2f} us")
-for which, name in enumerate(["KA ln1+qkv+sa", "KB oproj+ln2+q+ca", "KC oproj+ln3+ffn1", "KE out+upd+emb"]):
+for which, name in enumerate(["KA ln1+qkv+sa", "KB oproj+ln2+q+ca", "KC oproj+ln3+ffn1", "KD ffn2+resid", "KE out+upd+emb"]):
     print(f"fused {name:22s} n=32: {diag(4, [which, 32]):7.2f} us   n=1: {diag(4, [which, 1]):7.2f} us")
-for which, name in enumerate(["KA: ln|gemm|conv|attn", "KB: load|oproj|ln2|qgemm+kv|conv|attn", "KC: load|oproj|ln3|ffn1", "KE: ln|out|upd|emb"]):
+for which, name in enumerate(["KA: ln|gemm|conv|attn", "KB: load|oproj|ln2|qgemm+kv|conv|attn", "KC: load|oproj|ln3|ffn1", "KD: load|gemm|reduce", "KE: ln+out|stage|upd|emb"]):
     print(f"phases {name:40s}", stamps(which))
 print("--- calibration ---")
 print(f"empty launch 1 WG      : {diag(5, [0, 0, 1, 1]):7.2f} us")

@@ -43,7 +43,7 @@ struct Layer {
   float *ln1_g, *ln1_b, *ln2_g, *ln2_b, *ln3_g, *ln3_b;
   Lin qkv, o_sa, q_ca, kv_ca, o_ca, ff1, ff2;
   Conv3 sa_q, sa_k, sa_v, ca_q, ca_k, ca_v;
-  FLin f_qkv, f_o_sa, f_q_ca, f_o_ca, f_ff1;  // fused-path copies
+  FLin f_qkv, f_o_sa, f_q_ca, f_o_ca, f_ff1, f_ff2;  // fused-path copies
 };
 
 struct ProfEvents {
@@ -379,6 +379,7 @@ int launch_fused_layers(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     w.q_ca = Ly.f_q_ca.w; w.q_ca_b = Ly.f_q_ca.b;
     w.o_ca = Ly.f_o_ca.w; w.o_ca_b = Ly.f_o_ca.b;
     w.ff1 = Ly.f_ff1.w; w.ff1_b = Ly.f_ff1.b;
+    w.ff2 = Ly.f_ff2.w; w.ff2_b = Ly.f_ff2.b;
     w.ln1_g = Ly.ln1_g; w.ln1_b = Ly.ln1_b; w.ln2_g = Ly.ln2_g; w.ln2_b = Ly.ln2_b;
     w.ln3_g = Ly.ln3_g; w.ln3_b = Ly.ln3_b;
     w.sa_qw = Ly.sa_q.w; w.sa_qb = Ly.sa_q.b; w.sa_kw = Ly.sa_k.w; w.sa_kb = Ly.sa_k.b;
@@ -408,8 +409,8 @@ int launch_fused_layers(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     if (prof) { int r = prof_mark(c, s, 0); if (r) return r; }
     HIP_TRY(c, launch_fused(2, D.dtype, f, n, s));     // KC: out-proj + LN3 + FFN-up + ReLU^2
     if (prof) { int r = prof_mark(c, s, 1); if (r) return r; }
-    GemmArgs g = gemm_args(Ly.ff2, M, c->ffn, 4 * d, c->h, d);
-    GEMM(c, PRO_T, EPI_RESID, g, s);                   // KD: FFN-down + residual
+    f.h = c->h;
+    HIP_TRY(c, launch_fused(3, D.dtype, f, n, s));     // KD: FFN-down + residual (in place on h)
   }
   return GGD_OK;
 }
@@ -737,8 +738,8 @@ int ggd_finalize_weights(ggd_ctx* c) {
     TRY(pack_lin(c, Ly.ff1, {q + "feed_forward.layer1"}, 4 * d, d));
     TRY(pack_lin(c, Ly.ff2, {q + "feed_forward.layer2"}, d, 4 * d));
   }
-  c->fused = D.d_model == 256 && D.heads == 8 && D.seq_len <= 64 &&
-             fused_lds_max(D.dtype, D.seq_len, D.speech_len) <= 160 * 1024;
+  c->fused = D.decoder_type == GGD_DEC_ONEWAY &&
+             fused_supported(D.dtype, D.d_model, D.heads, D.seq_len, D.speech_len, D.d_pose);
   if (c->fused) {
     TRY(frag_from(c, c->f_emb, {P + "emb_x"}, d, C, iota_n(d)));
     TRY(frag_from(c, c->f_out, {P + "out_layers.1"}, C, d, iota_n(C)));
@@ -756,6 +757,7 @@ int ggd_finalize_weights(ggd_ctx* c) {
       TRY(frag_from(c, Ly.f_q_ca, {ca + "query.0.linear"}, d, d, iota_n(d)));
       TRY(frag_from(c, Ly.f_o_ca, {ca + "output"}, d, d, iota_n(d)));
       TRY(frag_from(c, Ly.f_ff1, {q + "feed_forward.layer1"}, 4 * d, d, iota_n(4 * d)));
+      TRY(frag_from(c, Ly.f_ff2, {q + "feed_forward.layer2"}, d, 4 * d, iota_n(d)));
     }
   }
   TRY(build_step_tables(c));
@@ -1007,14 +1009,14 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     }
     for (int it = 0; rc == GGD_OK && it < iters + 1; ++it) {
       if (it == 1) HIP_TRY(c, hipEventRecord(e0, s));
-      if (which < 3) {
+      if (which < 4) {
         // the layer-0 arguments of launch_fused_layers
         const Layer& Ly = c->layers[0];
         FusedArgs f{};
         FusedLayer& w = f.w;
         w.qkv = Ly.f_qkv.w; w.qkv_b = Ly.f_qkv.b; w.o_sa = Ly.f_o_sa.w; w.o_sa_b = Ly.f_o_sa.b;
         w.q_ca = Ly.f_q_ca.w; w.q_ca_b = Ly.f_q_ca.b; w.o_ca = Ly.f_o_ca.w; w.o_ca_b = Ly.f_o_ca.b;
-        w.ff1 = Ly.f_ff1.w; w.ff1_b = Ly.f_ff1.b;
+        w.ff1 = Ly.f_ff1.w; w.ff1_b = Ly.f_ff1.b; w.ff2 = Ly.f_ff2.w; w.ff2_b = Ly.f_ff2.b;
         w.ln1_g = Ly.ln1_g; w.ln1_b = Ly.ln1_b; w.ln2_g = Ly.ln2_g; w.ln2_b = Ly.ln2_b;
         w.ln3_g = Ly.ln3_g; w.ln3_b = Ly.ln3_b;
         w.sa_qw = Ly.sa_q.w; w.sa_qb = Ly.sa_q.b; w.sa_kw = Ly.sa_k.w; w.sa_kb = Ly.sa_k.b;

@@ -34,14 +34,17 @@ __device__ __forceinline__ float wave_sum(float v) {
 
 
 // ---------------------------------------------------------------------------
-// counter-based Gaussian noise (oracle/philox.py restates this bit for bit up to libm ulps)
+// counter-based Gaussian noise (oracle/philox.py restates it: Philox bits exact, the
+// Box-Muller floats within a few ulp -- hardware log2 / sin / cos against numpy's libm)
 // ---------------------------------------------------------------------------
 constexpr uint32_t TAG_STEP = 0, TAG_XT = 1;
 
-__device__ __forceinline__ float philox_normal(uint64_t seed, uint32_t clip, uint32_t step, uint32_t tag,
-                                               uint32_t e) {
+// the four normals of quad q (elements 4q .. 4q+3) from ONE Philox call:
+//   counter (q, clip, step, tag), key (seed_lo, seed_hi) -> u0..u3 -> two Box-Muller pairs
+__device__ __forceinline__ void philox_normal4(uint64_t seed, uint32_t clip, uint32_t step, uint32_t tag,
+                                               uint32_t q, float (&z)[4]) {
 #pragma clang fp contract(off)
-  uint32_t c0 = e >> 2, c1 = clip, c2 = step, c3 = tag;
+  uint32_t c0 = q, c1 = clip, c2 = step, c3 = tag;
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -51,14 +54,25 @@ __device__ __forceinline__ float philox_normal(uint64_t seed, uint32_t clip, uin
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
+  // hardware transcendentals: v_log_f32 is log2, v_sin/cos_f32 take revolutions (the angle
+  // 2 pi u is never formed); within a few ulp of the float32 libm form (oracle/philox.py)
+  const float inv = 2.3283064365386963e-10f, m2ln2 = -1.3862943611198906f;  // -2 ln 2
+  const float ra = __builtin_amdgcn_sqrtf(m2ln2 * __builtin_amdgcn_logf(((float)c0 + 1.0f) * inv));
+  const float rb = __builtin_amdgcn_sqrtf(m2ln2 * __builtin_amdgcn_logf(((float)c2 + 1.0f) * inv));
+  const float ua = (float)c1 * inv, ub = (float)c3 * inv;
+  z[0] = ra * __builtin_amdgcn_cosf(ua);
+  z[1] = ra * __builtin_amdgcn_sinf(ua);
+  z[2] = rb * __builtin_amdgcn_cosf(ub);
+  z[3] = rb * __builtin_amdgcn_sinf(ub);
+}
+
+// element e of the stream (the quad e / 4, lane e % 4)
+__device__ __forceinline__ float philox_normal(uint64_t seed, uint32_t clip, uint32_t step, uint32_t tag,
+                                               uint32_t e) {
+  float z[4];
+  philox_normal4(seed, clip, step, tag, e >> 2, z);
   const int sel = e & 3;
-  const uint32_t ua_i = sel < 2 ? c0 : c2, ub_i = sel < 2 ? c1 : c3;
-  const float inv = 2.3283064365386963e-10f;
-  const float ua = ((float)ua_i + 1.0f) * inv;
-  const float ub = (float)ub_i * inv;
-  const float r = sqrtf(-2.0f * logf(ua));
-  const float th = 6.283185307179586f * ub;
-  return (sel & 1) ? r * sinf(th) : r * cosf(th);
+  return sel == 0 ? z[0] : sel == 1 ? z[1] : sel == 2 ? z[2] : z[3];
 }
 
 // ---------------------------------------------------------------------------

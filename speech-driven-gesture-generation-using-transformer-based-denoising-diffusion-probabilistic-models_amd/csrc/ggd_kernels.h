@@ -99,8 +99,8 @@ struct PostArgs {
 
 // Fused per-clip decoder (ggd_fused.hip): fragment-packed weights of one layer.
 struct FusedLayer {
-  const void *qkv, *o_sa, *q_ca, *o_ca, *ff1;  // T fragments [tile][k step][64 lanes][16 B]
-  const float *qkv_b, *o_sa_b, *q_ca_b, *o_ca_b, *ff1_b;
+  const void *qkv, *o_sa, *q_ca, *o_ca, *ff1, *ff2;  // T fragments [tile][k step][64 lanes][16 B]
+  const float *qkv_b, *o_sa_b, *q_ca_b, *o_ca_b, *ff1_b, *ff2_b;
   const float *ln1_g, *ln1_b, *ln2_g, *ln2_b, *ln3_g, *ln3_b;
   const float *sa_qw, *sa_qb, *sa_kw, *sa_kb, *sa_vw, *sa_vb;
   const float *ca_qw, *ca_qb, *ca_kw, *ca_kb, *ca_vw, *ca_vb;
@@ -111,7 +111,7 @@ struct FusedArgs {
   FusedLayer w;
   int L, Ts;
   float* h;          // residual rows read (f32 [N*L][256])
-  float* h_out;      // KB / KC: updated residual rows written (ping-pong buffer)
+  float* h_out;      // KB / KC: updated residual rows written (ping-pong buffer); KD updates h in place
   void *o_sa, *o_ca, *hid;
   const int* t_clip; const StepRec* steps; int* step_counter; int bump_counter;
   float scale;
@@ -135,9 +135,9 @@ struct FinalArgs {
 };
 
 // launchers (return hipError_t of the launch)
-hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s);  // 0 KA, 1 KB, 2 KC
+hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s);  // 0 KA, 1 KB, 2 KC, 3 KD
 hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s);
-size_t fused_lds_max(int dtype, int L, int Ts);
+bool fused_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
 hipError_t launch_mb(int mode, void* buf, size_t buf_bytes, int arg, int blocks, hipStream_t s);  // ggd_diag.hip
 hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s);
