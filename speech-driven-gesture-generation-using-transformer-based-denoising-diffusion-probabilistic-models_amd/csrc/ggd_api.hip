@@ -49,7 +49,6 @@ struct Layer {
 struct ProfEvents {
   std::vector<hipEvent_t> ev;  // timing events; eager marks consume ev[next++]
   size_t next = 0;
-  bool capturing = false;      // marks inside stream capture use ev[0]/ev[1] as placeholders
 };
 
 }  // namespace
@@ -100,7 +99,6 @@ struct ggd_ctx {
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
   std::string graph_key;
-  std::vector<hipGraphNode_t> prof_nodes;
 
   // profiling
   bool profiling = false;
@@ -327,20 +325,15 @@ int build_step_tables(ggd_ctx* c) {
   return GGD_OK;
 }
 
-// Timing mark around the dominant kernel (the FFN-up GEMM of every layer).
-int prof_mark(ggd_ctx* c, hipStream_t s, int which) {
-  hipEvent_t e;
-  if (c->prof.capturing) {
-    e = c->prof.ev[which];
-  } else {
-    while (c->prof.ev.size() <= c->prof.next) {
-      hipEvent_t n;
-      HIP_TRY(c, hipEventCreate(&n));
-      c->prof.ev.push_back(n);
-    }
-    e = c->prof.ev[c->prof.next++];
+// Timing mark around the dominant kernel (profiling mode runs the loop eagerly; marks pair up
+// as start / end of consecutive launches of that kernel).
+int prof_mark(ggd_ctx* c, hipStream_t s) {
+  while (c->prof.ev.size() <= c->prof.next) {
+    hipEvent_t n;
+    HIP_TRY(c, hipEventCreate(&n));
+    c->prof.ev.push_back(n);
   }
-  HIP_TRY(c, hipEventRecord(e, s));
+  HIP_TRY(c, hipEventRecord(c->prof.ev[c->prof.next++], s));
   return GGD_OK;
 }
 
@@ -402,13 +395,13 @@ int launch_fused_layers(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     f.bump_counter = sampling && li == 0;
     HIP_TRY(c, launch_fused(0, D.dtype, f, n, s));     // KA: LN1 + QKV + conv + self-attention
     f.bump_counter = 0;
+    const bool prof = c->profiling && sampling;        // KB is the dominant kernel of the step
+    if (prof) { int r = prof_mark(c, s); if (r) return r; }
     HIP_TRY(c, launch_fused(1, D.dtype, f, n, s));     // KB: out-proj + LN2 + Q + cross-attention
+    if (prof) { int r = prof_mark(c, s); if (r) return r; }
     f.h = c->h2;
     f.h_out = c->h;
-    const bool prof = c->profiling && sampling;
-    if (prof) { int r = prof_mark(c, s, 0); if (r) return r; }
     HIP_TRY(c, launch_fused(2, D.dtype, f, n, s));     // KC: out-proj + LN3 + FFN-up + ReLU^2
-    if (prof) { int r = prof_mark(c, s, 1); if (r) return r; }
     f.h = c->h;
     HIP_TRY(c, launch_fused(3, D.dtype, f, n, s));     // KD: FFN-down + residual (in place on h)
   }
@@ -490,9 +483,9 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     g.ln_g = Ly.ln3_g;
     g.ln_b = Ly.ln3_b;
     const bool prof = c->profiling && sampling;
-    if (prof) { int r = prof_mark(c, s, 0); if (r) return r; }
+    if (prof) { int r = prof_mark(c, s); if (r) return r; }
     GEMM(c, PRO_LN, EPI_RELU2, g, s);
-    if (prof) { int r = prof_mark(c, s, 1); if (r) return r; }
+    if (prof) { int r = prof_mark(c, s); if (r) return r; }
 
     g = gemm_args(Ly.ff2, M, c->ffn, 4 * d, c->h, d);
     GEMM(c, PRO_T, EPI_RESID, g, s);
@@ -665,8 +658,7 @@ int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out) {
   build_pe(pe, c->pe_len, d);
   HIP_TRY(c, dalloc(c, &c->pe, sizeof(float) * pe.size()));
   HIP_TRY(c, hipMemcpy(c->pe, pe.data(), sizeof(float) * pe.size(), hipMemcpyHostToDevice));
-  c->prof.ev.resize(2);
-  for (auto& e : c->prof.ev) HIP_TRY(c, hipEventCreate(&e));
+
   return GGD_OK;
 }
 
@@ -1125,13 +1117,14 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   const int graph_steps = a->extras ? nsteps - 1 : nsteps;
   // pointer / shape key: a captured graph is reused only for identical arguments
   char keybuf[512];
-  std::snprintf(keybuf, sizeof keybuf, "%d|%d|%p|%llu|%lld|%p|%p|%p|%d", a->alg, a->n, (const void*)a->noise,
+  std::snprintf(keybuf, sizeof keybuf, "%d|%d|%p|%llu|%lld|%p|%p|%p", a->alg, a->n, (const void*)a->noise,
                 (unsigned long long)a->seed, (long long)a->clip_offset, (const void*)a->inpaint_poses,
-                (const void*)a->inpaint_masks, (const void*)a->trans, (int)c->profiling);
+                (const void*)a->inpaint_masks, (const void*)a->trans);
   const std::string key(keybuf);
-  std::vector<double> prof_ms;
   if (graph_steps > 0) {
-    if (a->use_graph) {
+    if (a->use_graph && !c->profiling) {
+      // one captured step, replayed: the step's kernels read the iteration from the device
+      // counter that the step's first kernel advances
       if (!c->gexec || c->graph_key != key) {
         if (c->gexec) {
           hipGraphExecDestroy(c->gexec);
@@ -1142,9 +1135,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
           c->graph = nullptr;
         }
         HIP_TRY(c, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-        c->prof.capturing = true;
         int r = launch_step(c, *a, nullptr, -1);
-        c->prof.capturing = false;
         hipGraph_t g = nullptr;
         hipError_t e = hipStreamEndCapture(s, &g);
         if (r) return r;
@@ -1152,67 +1143,21 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
         c->graph = g;
         HIP_TRY(c, hipGraphInstantiate(&c->gexec, g, nullptr, nullptr, 0));
         c->graph_key = key;
-        c->prof_nodes.clear();
-        if (c->profiling) {
-          size_t nn = 0;
-          HIP_TRY(c, hipGraphGetNodes(g, nullptr, &nn));
-          std::vector<hipGraphNode_t> nodes(nn);
-          HIP_TRY(c, hipGraphGetNodes(g, nodes.data(), &nn));
-          for (auto nd : nodes) {
-            hipGraphNodeType ty;
-            HIP_TRY(c, hipGraphNodeGetType(nd, &ty));
-            if (ty == hipGraphNodeTypeEventRecord) c->prof_nodes.push_back(nd);
-          }
-        }
       }
-      const size_t per = c->prof_nodes.size();
-      const size_t base = 2;  // ev[0], ev[1] are the capture placeholders
-      if (c->profiling && per) {
-        // give every replay fresh events so all launches of the timed loop can be read back
-        const size_t need = base + (size_t)graph_steps * per;
-        while (c->prof.ev.size() < need) {
-          hipEvent_t e;
-          HIP_TRY(c, hipEventCreate(&e));
-          c->prof.ev.push_back(e);
-        }
-      }
-      for (int k = 0; k < graph_steps; ++k) {
-        if (c->profiling && per)
-          for (size_t j = 0; j < per; ++j)
-            HIP_TRY(c, hipGraphExecEventRecordNodeSetEvent(c->gexec, c->prof_nodes[j],
-                                                           c->prof.ev[base + k * per + j]));
-        HIP_TRY(c, hipGraphLaunch(c->gexec, s));
-      }
-      if (c->profiling && per) {
-        HIP_TRY(c, hipStreamSynchronize(s));
-        double total = 0;
-        int64_t cnt = 0;
-        std::vector<float> tms(per);
-        for (int k = 0; k < graph_steps; ++k) {
-          // node enumeration order is unspecified: order each replay's marks by time; start and
-          // end of one launch are adjacent because the FFN-up launches are serialised
-          for (size_t j = 0; j < per; ++j)
-            HIP_TRY(c, hipEventElapsedTime(&tms[j], c->prof.ev[base + k * per], c->prof.ev[base + k * per + j]));
-          std::sort(tms.begin(), tms.end());
-          for (size_t j = 0; j + 1 < per; j += 2) {
-            total += (double)(tms[j + 1] - tms[j]) * 1000.0;
-            ++cnt;
-          }
-        }
-        c->prof_avg_us = cnt ? total / cnt : 0;
-        c->prof_launches = cnt;
-      }
+      for (int k = 0; k < graph_steps; ++k) HIP_TRY(c, hipGraphLaunch(c->gexec, s));
     } else {
-      c->prof.next = 2;
+      // eager launches; in profiling mode every launch of the dominant kernel is bracketed
+      // by a pair of events on the context stream (ggd_kernel_time reads them back)
+      c->prof.next = 0;
       for (int k = 0; k < graph_steps; ++k) {
         int r = launch_step(c, *a, nullptr, -1);
         if (r) return r;
       }
-      if (c->profiling && c->prof.next > 2) {
+      if (c->profiling && c->prof.next >= 2) {
         HIP_TRY(c, hipStreamSynchronize(s));
         double total = 0;
         int64_t cnt = 0;
-        for (size_t j = 2; j + 1 < c->prof.next; j += 2) {
+        for (size_t j = 0; j + 1 < c->prof.next; j += 2) {
           float ms = 0;
           HIP_TRY(c, hipEventElapsedTime(&ms, c->prof.ev[j], c->prof.ev[j + 1]));
           total += ms * 1000.0;
