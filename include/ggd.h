@@ -151,9 +151,13 @@ int ggd_kernel_time(ggd_ctx* ctx, int32_t which, double* avg_us, int64_t* launch
  * (hipEvents).  what = 0: GEMM, p = {pro, epi, M, N, K, force_mt, no_xcd_remap};
  * what = 1: attention, p = {cross, n}; what = 2: one full denoise step (eager launches),
  * p = {n}; what = 3: the same step as one hipGraph replay, p = {n}; what = 4: one fused kernel,
- * p = {0 KA | 1 KB | 2 KC | 3 KE, n}; what = 5: calibration micro-kernels, p = {mode, arg, blocks,
- * buffer MiB} with mode 0 empty launch, 1 dependent-load chase (arg loads), 2 shader clock
- * (returns GHz instead of microseconds), 3 / 4 bulk 64 KiB / 16 KiB load per block. */
+ * p = {0 KA | 1 KB | 2 KC | 3 KD | 4 KE, n}; what = 5: calibration micro-kernels, p = {mode, arg,
+ * blocks, buffer MiB} with mode 0 empty launch, 1 dependent-load chase (arg loads), 2 shader clock
+ * (returns GHz instead of microseconds), 3 / 4 bulk 64 KiB / 16 KiB load per block; what = 6: as
+ * 4 with in-kernel phase stamps (avg_us[0..7] = phase ends in us); what = 7: p = {1} routes
+ * ggd_sample through the per-step launches instead of the persistent kernel, {0} back (returns 1
+ * in *avg_us when the persistent kernel is available); what = 8: persistent-kernel phase stamps of
+ * iteration 0, p = {1} arm, {2} read (avg_us[0..7]), {0} disarm. */
 int ggd_diag(ggd_ctx* ctx, int32_t what, const int32_t* p, int32_t np, int32_t iters, double* avg_us);
 
 /* Library version string. */

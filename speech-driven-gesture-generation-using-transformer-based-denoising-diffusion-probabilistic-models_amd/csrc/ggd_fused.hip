@@ -28,378 +28,9 @@
 //   * weights are packed on the host in MFMA B-fragment order -- [n tile][k step][lane][16 B]
 //     -- and stream straight into registers with 1 KiB coalesced loads, issued before the
 //     activations they multiply have arrived.
-#include <algorithm>
-
-#include "ggd_common.h"
+#include "ggd_fusedlib.h"
 
 namespace ggd {
-
-constexpr int FD = 256, FDK = 32, FR = 64, FRT = 4, FLK = 64;  // d_model, d_k, rows, row tiles, max keys
-constexpr int SH = FD + 4;                                     // f32 residual image row stride
-typedef __attribute__((address_space(3))) void lds_void;
-
-template <typename T> struct Frag {
-  static constexpr int KF = 64 / sizeof(T);   // k covered by one fragment: 32 (bf16) / 16 (f32)
-  static constexpr int PT = 16 / sizeof(T);   // 16-byte LDS row pad
-  static constexpr int SX = FD + PT;          // operand image row stride (elements)
-};
-
-__host__ __device__ constexpr size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
-
-// diagnostics: phase stamps of workgroup (0, 0), written only when the stamp buffer is set
-#define STAMP(i)                                                                                \
-  do {                                                                                          \
-    if (a.stamps && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)                     \
-      a.stamps[i] = __builtin_amdgcn_s_memtime();                                               \
-  } while (0)
-#define STAMP_END(i)                                                                            \
-  do {                                                                                          \
-    if (a.stamps) {                                                                             \
-      __syncthreads();                                                                          \
-      STAMP(i);                                                                                 \
-    }                                                                                           \
-  } while (0)
-
-// ------------------------------------------------------------------------------------------
-// bounded stores: a raw buffer resource over a clip's output rows; the hardware drops stores
-// past num_records, so padded rows are written without a branch.  (A store under a divergent
-// branch makes the compiler re-wait vmcnt inside every branch, serialising the stores.)
-// ------------------------------------------------------------------------------------------
-struct OutRows {
-  __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ OutRows(void* base, uint32_t bytes)
-      : r(__builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000)) {}
-  __device__ __forceinline__ void put4(uint32_t elem, float4 v) const {  // 4 f32 at elem
-    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-    const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)(elem * 4), 0, 0);
-  }
-  template <typename T> __device__ __forceinline__ void put(uint32_t elem, float v) const {
-    if constexpr (sizeof(T) == 2)
-      __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, (int)(elem * 2), 0, 0);
-    else
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(elem * 4), 0, 0);
-  }
-};
-
-// ------------------------------------------------------------------------------------------
-// staging
-// ------------------------------------------------------------------------------------------
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, NOT for
-// its outstanding global loads (prefetches for later phases stay in flight) or stores.
-// __syncthreads() waits vmcnt(0) as well: use it where LDS-DMA writes must have landed.
-__device__ __forceinline__ void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// LDS-DMA copy of `rows` rows of `pieces` x 1 KiB from src (row stride ss bytes) into dst
-// (row stride sd bytes): wave w issues the pieces w, w + NW, ...; lane l moves bytes 16l..16l+15.
-template <int NT = NTHREADS>
-__device__ __forceinline__ void glds_rows(void* dst, size_t sd, const void* src, size_t ss, int rows, int pieces) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int p = wave; p < rows * pieces; p += NT / 64) {
-    const int r = p / pieces, q = p - r * pieces;
-    __builtin_amdgcn_global_load_lds((const void*)((const char*)src + r * ss + q * 1024 + lane * 16),
-                                     (lds_void*)((char*)dst + r * sd + q * 1024), 16, 0, 0);
-  }
-}
-
-// A [64][SX] operand image of L rows of d_model activations of type T (global rows of FD).
-// bf16 rows are 512 B (two rows per LDS-DMA instruction would cross the pad): registers.
-template <typename T> struct ImgStage {
-  static constexpr int NV = sizeof(T) == 2 ? FR * FD * 2 / 16 / NTHREADS : 1;
-  uint4 v[NV];
-  __device__ __forceinline__ void load(T* img, const T* src, int L) {
-    if constexpr (sizeof(T) == 4) {
-      glds_rows(img, sizeof(T) * Frag<T>::SX, src, sizeof(T) * FD, L, 1);
-    } else {
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int idx = threadIdx.x + i * NTHREADS, r = idx >> 5, c = idx & 31;
-        v[i] = *(const uint4*)(src + (size_t)min(r, L - 1) * FD + c * 8);
-      }
-    }
-  }
-  // every image row is written (rows >= L hold copies of row L - 1): a conditional store
-  // lets the compiler sink the global load into the branch and serialise the round trips
-  __device__ __forceinline__ void store(T* img, int L) {
-    if constexpr (sizeof(T) == 2) {
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int idx = threadIdx.x + i * NTHREADS, r = idx >> 5, c = idx & 31;
-        *(uint4*)(img + r * Frag<T>::SX + c * 8) = v[i];
-      }
-    }
-  }
-};
-
-// ------------------------------------------------------------------------------------------
-// MFMA against fragment-packed weights
-// ------------------------------------------------------------------------------------------
-// acc += A[rt*16 .. +16)[k step kf] x fragment wb   (A row-major in LDS, stride SA)
-template <typename T>
-__device__ __forceinline__ void mma_aw(f32x4& acc, const T* A, int SA, int rt, int kf, uint4 wb, int lane) {
-  const int r16 = lane & 15, g = lane >> 4;
-  if constexpr (sizeof(T) == 2) {
-    const bf16x8 av = *(const bf16x8*)(A + (rt * 16 + r16) * SA + kf * 32 + g * 8);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, wb), acc, 0, 0, 0);
-  } else {
-    const f32x4 av = *(const f32x4*)(A + (rt * 16 + r16) * SA + kf * 16 + g * 4);
-    const f32x4 bv = __builtin_bit_cast(f32x4, wb);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
-  }
-}
-
-// C[64 rows][NJ tiles] = A[64][K] x W tiles, K = KT fragment steps starting at step k0.
-// Fragments are held in registers in groups of G steps: bf16 the whole K (issued by
-// load(0) before the caller's activation staging), f32 (parity mode) in groups of 32 / NJ.
-template <typename T, int NJ, int KT>
-struct WGemm {
-  static constexpr int G = sizeof(T) == 2 ? KT : (32 / NJ < KT ? 32 / NJ : KT);
-  static_assert(KT % G == 0, "k steps must split into register groups");
-  uint4 wb[NJ][G];
-  const uint4* W;
-  int tiles[NJ];
-  int kt_total, k0;
-  __device__ __forceinline__ WGemm(const void* Wp, int kt_total_, int k0_) : W((const uint4*)Wp), kt_total(kt_total_), k0(k0_) {}
-  __device__ __forceinline__ void load(int g, int lane) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int k = 0; k < G; ++k) wb[j][k] = W[((size_t)tiles[j] * kt_total + k0 + g * G + k) * 64 + lane];
-  }
-  // group 0 must have been loaded; tiles j >= nj_on are skipped (wave-uniform)
-  __device__ __forceinline__ void run(f32x4 (&acc)[FRT][NJ], const T* A, int SA, int lane, int nj_on = NJ) {
-#pragma unroll
-    for (int rt = 0; rt < FRT; ++rt)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int g = 0; g < KT / G; ++g) {
-      if (g > 0) load(g, lane);
-#pragma unroll
-      for (int k = 0; k < G; ++k)
-#pragma unroll
-        for (int rt = 0; rt < FRT; ++rt)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-            if (j < nj_on) mma_aw<T>(acc[rt][j], A, SA, rt, g * G + k, wb[j][k], lane);
-    }
-  }
-};
-
-// ------------------------------------------------------------------------------------------
-// LayerNorm (eps 1e-5, two-pass) of the f32 rows Hs[0..L) (stride SH) into a T image
-// ------------------------------------------------------------------------------------------
-// statistics: 4 lanes per row, each summing 16 float4 (the generic GEMM's LN prologue order)
-__device__ __forceinline__ void ln_stats(const float* Hs, int L, float2* st) {
-  const int tid = threadIdx.x, r = tid >> 2, j = tid & 3;
-  if (r >= FR) return;
-  const int rr = min(r, L - 1);
-  float4 v[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) v[i] = *(const float4*)(Hs + rr * SH + (j + 4 * i) * 4);
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-  s += __shfl_xor(s, 1);
-  s += __shfl_xor(s, 2);
-  const float mu = s / (float)FD;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float d0 = v[i].x - mu, d1 = v[i].y - mu, d2 = v[i].z - mu, d3 = v[i].w - mu;
-    q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-  }
-  q += __shfl_xor(q, 1);
-  q += __shfl_xor(q, 2);
-  if (j == 0) st[r] = make_float2(mu, 1.0f / sqrtf(q / (float)FD + 1e-5f));
-}
-
-// normalize: thread t owns columns 4 (t & 63) .. +3 (gamma / beta preloaded), rows t >> 6 + NW i;
-// rows >= L are written as zeros.  All LDS reads are issued before the first write (one wave
-// per SIMD hides nothing: a read-use-read loop pays the LDS latency per row).
-template <typename T, int NT = NTHREADS>
-__device__ __forceinline__ void ln_apply(const float* Hs, int L, const float2* st, float4 g, float4 bb, T* img) {
-  constexpr int NW = NT / 64, NI = FR / NW;
-  const int c4 = (threadIdx.x & 63) * 4, r0 = threadIdx.x >> 6;
-  float4 v[NI];
-  float2 s[NI];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int rr = min(r0 + NW * i, L - 1);
-    v[i] = *(const float4*)(Hs + rr * SH + c4);
-    s[i] = st[rr];
-  }
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int r = r0 + NW * i;
-    const bool ok = r < L;
-    T* o = img + r * Frag<T>::SX + c4;
-    o[0] = from_f32<T>(ok ? (v[i].x - s[i].x) * s[i].y * g.x + bb.x : 0.f);
-    o[1] = from_f32<T>(ok ? (v[i].y - s[i].x) * s[i].y * g.y + bb.y : 0.f);
-    o[2] = from_f32<T>(ok ? (v[i].z - s[i].x) * s[i].y * g.z + bb.z : 0.f);
-    o[3] = from_f32<T>(ok ? (v[i].w - s[i].x) * s[i].y * g.w + bb.w : 0.f);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// depthwise 3-tap conv (Primer-EZ, transformer.py:28-44) and attention (transformer.py:88-118)
-// ------------------------------------------------------------------------------------------
-struct ConvW { float w0, w1, w2, b; };
-__device__ __forceinline__ ConvW conv_w(const float* w, const float* b, int c) {
-  return ConvW{w[c * 3 + 0], w[c * 3 + 1], w[c * 3 + 2], b[c]};
-}
-
-// dst rows (or transposed columns) i < 64 = conv over rows i-1, i, i+1 of the f32 source (row
-// stride ss, column c = tid & 31 of the thread; zero outside [0, rows)); rows >= `rows` are
-// written as zeros, so padded keys / values are finite
-template <typename T, bool TRANS>
-__device__ __forceinline__ void conv_rows(T* dst, int S, const float* src, int ss, int rows, ConvW w) {
-  const int c = threadIdx.x & 31, i0 = threadIdx.x >> 5;
-  float p0[8], p1[8], p2[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int i = i0 + 8 * k;
-    p0[k] = src[min(max(i - 1, 0), rows - 1) * ss + c];
-    p1[k] = src[min(i, rows - 1) * ss + c];
-    p2[k] = src[min(i + 1, rows - 1) * ss + c];
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int i = i0 + 8 * k;
-    const float v = w.b + w.w0 * (i > 0 ? p0[k] : 0.f) + w.w1 * p1[k] + w.w2 * (i + 1 < rows ? p2[k] : 0.f);
-    const T o = from_f32<T>(i < rows ? v : 0.f);
-    if (TRANS)
-      dst[c * S + i] = o;
-    else
-      dst[i * S + c] = o;
-  }
-}
-
-template <typename T> struct FAtt {
-  static constexpr int P = 16 / sizeof(T);
-  static constexpr int SQ = FDK + P;       // Q / K rows
-  static constexpr int SV = FLK + P;       // V^T rows (keys along the row)
-  static constexpr int SP = FLK + P;       // per-wave P tile rows
-  static constexpr size_t OQ = 0;
-  static constexpr size_t OK = OQ + sizeof(T) * FR * SQ;
-  static constexpr size_t OV = OK + sizeof(T) * FLK * SQ;
-  static constexpr size_t OP = OV + sizeof(T) * FDK * SV;
-  static constexpr size_t BYTES = OP + sizeof(T) * 4 * 16 * SP;
-};
-
-__device__ __forceinline__ void att_mma16(f32x4& acc, const bf16_t* X, int SX, const bf16_t* Y, int SY, int k0, int lane) {
-  const int r16 = lane & 15, g = lane >> 4;
-  const bf16x8 a = *(const bf16x8*)(X + r16 * SX + k0 + g * 8);
-  const bf16x8 b = *(const bf16x8*)(Y + r16 * SY + k0 + g * 8);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
-}
-__device__ __forceinline__ void att_mma16(f32x4& acc, const float* X, int SX, const float* Y, int SY, int k0, int lane) {
-  const int r16 = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int kk = 0; kk < 32; kk += 16) {
-    const f32x4 a = *(const f32x4*)(X + r16 * SX + k0 + kk + g * 4);
-    const f32x4 b = *(const f32x4*)(Y + r16 * SY + k0 + kk + g * 4);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
-  }
-}
-
-// O[Lq][32] = softmax(scale Q K^T) V for one head; wave w owns query rows 16w..16w+15.
-// LKT = key tiles of 16 (Lk <= 16 LKT, LKT even).  Keys >= Lk are masked by select (their K
-// rows may hold anything); V^T columns >= Lk must be finite (zeroed by the caller).
-template <typename T, int LKT>
-__device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float scale, T* out, int ldo) {
-  using A = FAtt<T>;
-  const T* Qm = (const T*)(att + A::OQ);
-  const T* Km = (const T*)(att + A::OK);
-  const T* Vt = (const T*)(att + A::OV);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c16 = lane & 15, g4 = lane >> 4;
-  T* P = (T*)(att + A::OP) + wave * 16 * A::SP;
-  const int rt = wave;
-  if (rt * 16 >= Lq) return;
-  f32x4 s[LKT];
-#pragma unroll
-  for (int t = 0; t < LKT; ++t) {
-    s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    att_mma16(s[t], Qm + rt * 16 * A::SQ, A::SQ, Km + t * 16 * A::SQ, A::SQ, 0, lane);
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float mx = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < LKT; ++t) {
-      const float v = t * 16 + c16 < Lk ? s[t][r] * scale : -INFINITY;
-      s[t][r] = v;
-      mx = fmaxf(mx, v);
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 1));
-    mx = fmaxf(mx, __shfl_xor(mx, 2));
-    mx = fmaxf(mx, __shfl_xor(mx, 4));
-    mx = fmaxf(mx, __shfl_xor(mx, 8));
-    float sum = 0.f;
-#pragma unroll
-    for (int t = 0; t < LKT; ++t) {
-      const float p = t * 16 + c16 < Lk ? expf(s[t][r] - mx) : 0.f;
-      s[t][r] = p;
-      sum += p;
-    }
-    sum += __shfl_xor(sum, 1);
-    sum += __shfl_xor(sum, 2);
-    sum += __shfl_xor(sum, 4);
-    sum += __shfl_xor(sum, 8);
-    const float inv = 1.0f / sum;
-#pragma unroll
-    for (int t = 0; t < LKT; ++t) P[(4 * g4 + r) * A::SP + t * 16 + c16] = from_f32<T>(s[t][r] * inv);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  const OutRows dst(out, (uint32_t)(sizeof(T) * ((size_t)(Lq - 1) * ldo + FDK)));  // rows >= Lq dropped
-#pragma unroll
-  for (int ct = 0; ct < FDK / 16; ++ct) {
-    f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k0 = 0; k0 < LKT * 16; k0 += 32) att_mma16(o, P, A::SP, Vt + ct * 16 * A::SV, A::SV, k0, lane);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dst.put<T>((uint32_t)((rt * 16 + 4 * g4 + r) * ldo + ct * 16 + c16), o[r]);
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void fattn_any(unsigned char* att, int Lq, int Lk, float scale, T* out, int ldo) {
-  if (Lk <= 32)
-    fattn<T, 2>(att, Lq, Lk, scale, out, ldo);
-  else
-    fattn<T, 4>(att, Lq, Lk, scale, out, ldo);
-}
-
-// ------------------------------------------------------------------------------------------
-// LDS plans (bytes; FR = 64 rows everywhere)
-// ------------------------------------------------------------------------------------------
-template <typename T> struct Plan {
-  static constexpr size_t IMG = al16(sizeof(T) * FR * Frag<T>::SX);
-  static constexpr size_t HS = al16(sizeof(float) * FR * SH);
-  static constexpr size_t ST = sizeof(float2) * FR;
-  static constexpr size_t Y_KA = al16(sizeof(float) * FR * (96 + 4));
-  static constexpr size_t YQ = al16(sizeof(float) * FR * (FDK + 4));
-  static constexpr size_t RAW = al16(sizeof(float) * 2 * (FLK + 2) * FDK);
-  // KA: [Xn][stats][Hs | Y + att]
-  static constexpr size_t KA = IMG + ST + std::max(HS, Y_KA + FAtt<T>::BYTES);
-  // KB: [Ax][stats][Hs | Yq + raw + att]
-  static constexpr size_t KB = IMG + ST + std::max(HS, YQ + RAW + FAtt<T>::BYTES);
-  // KC: [Ax][stats][Hs]
-  static constexpr size_t KC = IMG + ST + HS;
-  // KD: [hid pass image 64 x (KP + PT)] ; the cross-wave reduction reuses it
-  static constexpr int KP = sizeof(T) == 2 ? 4 * FD : 2 * FD;
-  static constexpr size_t KD = al16(sizeof(T) * FR * (KP + Frag<T>::PT));
-  // KE: [Xn / Xb][stats][Hs | E (64 x 132 f32) + Xs (64 x 128 f32)]
-  static constexpr size_t E = al16(sizeof(float) * FR * (128 + 4));
-  static constexpr size_t XS = al16(sizeof(float) * FR * 128);
-  static constexpr size_t KE = IMG + ST + std::max(HS, E + XS);
-};
-static_assert(Plan<float>::KA <= 160 * 1024 && Plan<float>::KB <= 160 * 1024 && Plan<float>::KE <= 160 * 1024 &&
-                  Plan<float>::KD <= 160 * 1024,
-              "fused LDS plans must fit 160 KiB");
 
 // ------------------------------------------------------------------------------------------
 // KA: LN1 + QKV(head) + conv + self-attention          grid (heads, clips)

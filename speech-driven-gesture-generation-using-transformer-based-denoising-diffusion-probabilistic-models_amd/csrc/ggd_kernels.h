@@ -134,10 +134,30 @@ struct FinalArgs {
   unsigned long long* stamps;  // diagnostics
 };
 
+// Persistent per-clip sampler (ggd_persist.hip): one workgroup per clip runs iterations
+// k0 .. k0 + n_steps - 1 of the reverse loop with the clip's state in LDS / registers.
+struct PersistArgs {
+  const FusedLayer* layers;    // device array [n_layers]
+  int n_layers, n, L, Ts, C, alg;
+  const float *ln_g, *ln_b;
+  const void* w_out; const float* b_out;   // packed out_layers.1 (8 tiles, K 256)
+  const void* w_emb; const float* b_emb;   // packed emb_x (16 tiles, K 128)
+  const float* pe;
+  float* x;                    // state (N, L, C): x_T in, final sample out
+  const StepRec* steps; int k0, n_steps;
+  const float* noise; uint64_t seed; int64_t clip_offset;
+  const float *inp_pose, *inp_mask, *trans;
+  float* extras;               // (6, N, C, L) of the last iteration, or null
+  float scale;
+  unsigned long long* stamps;  // diagnostics: workgroup 0 stamps phase boundaries of iteration 0
+};
+
 // launchers (return hipError_t of the launch)
 hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s);  // 0 KA, 1 KB, 2 KC, 3 KD
 hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s);
 bool fused_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
+hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
+bool persist_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
 hipError_t launch_mb(int mode, void* buf, size_t buf_bytes, int arg, int blocks, hipStream_t s);  // ggd_diag.hip
 hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s);

@@ -1,0 +1,602 @@
+// ggd_persist.hip -- the persistent per-clip sampler: ONE workgroup owns ONE clip for the whole
+// reverse loop (gaussian_diffusion.py:331-412 / 414-529 around nn.py:216-228), bf16 MFMA.
+//
+// Why: a denoise step of a 40-frame clip is ~0.3 GFLOP, far too little to fill the chip with
+// one launch per decoder phase; split over 8 workgroups per clip, every phase pays a launch
+// (or an in-kernel hand-off) of ~2-4 us plus a cold round trip for the activations.  Here the
+// clip's residual stream, LayerNorm images, attention operands, FFN chunk and pose state stay
+// in LDS / registers across all T' steps; nothing crosses workgroups, so there is no barrier
+// between clips, no counter and no hipGraph -- one launch runs the whole sampling call.
+// The only global traffic per step is the bf16 weights (7.5 MB, fragment-packed, L2 / MALL
+// resident, streamed with 1 KiB coalesced wave loads one GEMM ahead of their use) and the
+// clip's cached cross-attention memory rows.
+//
+// Per step (clip b, L <= 16 RT rows, d 256, 8 heads, Lk = 1 + Ts <= 64, C <= 128):
+//   emb:    Xb = bf16(x) ; Hs = Xb W_emb^T + b + PE                       (transformer.py:176-180)
+//   layer:  Xn = LN1(Hs); per head pair: Y = Xn Wqkv^T + b, per head conv Q/K/V + attention -> O
+//           Hs += O Wo^T + b ; Xn = LN2(Hs); per head: Q = conv(Xn Wq^T + b), K/V = conv(memory
+//           rows [step token(t); speech]) , attention -> O ; Hs += O Wo^T + b ; Xn = LN3(Hs);
+//           per 128-wide chunk: H = relu(Xn W1^T + b)^2, acc += H W2^T ; Hs += acc + b2
+//   out:    E = LN_out(Hs) W_out^T + b ; x = posterior update (Philox noise)  (nn.py:211-228)
+#include "ggd_fusedlib.h"
+
+namespace ggd {
+
+template <int RT> struct PPlan {
+  static constexpr int R = RT * 16;                  // padded rows
+  static constexpr int SX = FD + 8;                  // bf16 operand image stride
+  static constexpr int SY = 192 + 4;                 // f32 QKV of a head pair
+  static constexpr int SYQ = FDK + 4;                // f32 cross-attn Q of a head
+  static constexpr int SHD = 128 + 8;                // bf16 FFN chunk / emb operand
+  static constexpr int SE = 128 + 4;                 // f32 eps
+  static constexpr size_t HS = al16(sizeof(float) * R * SH);
+  static constexpr size_t IMG = al16(sizeof(bf16_t) * R * SX);
+  static constexpr size_t ST = al16(sizeof(float2) * R);
+  static constexpr size_t Y = al16(sizeof(float) * R * SY);
+  static constexpr size_t ATT = al16(FAtt<bf16_t, R>::BYTES);
+  static constexpr size_t YQ = al16(sizeof(float) * R * SYQ);
+  static constexpr size_t RAW = al16(sizeof(float) * 2 * (FLK + 2) * FDK);
+  static constexpr size_t HID = al16(sizeof(bf16_t) * R * SHD);
+  static constexpr size_t E = al16(sizeof(float) * R * SE);
+  static constexpr size_t SCR = std::max(std::max(Y + ATT, YQ + RAW + ATT), std::max(HID, E + HID));
+  static constexpr size_t OFF_XN = HS, OFF_O = HS + IMG, OFF_ST = HS + 2 * IMG, OFF_S = OFF_ST + ST;
+  static constexpr size_t TOTAL = OFF_S + SCR;
+};
+static_assert(PPlan<3>::TOTAL <= 160 * 1024, "persistent plan must fit 160 KiB of LDS");
+
+// fragments of NJ tiles x KS k steps (tile t, step k0 + s) -> f[j * KS + s]
+template <int NJ, int KS, int N, int NTL>
+__device__ __forceinline__ void pload(uint4 (&f)[N], const void* W, int kt_total, const int (&tiles)[NTL], int k0,
+                                      int lane) {
+  static_assert(NJ * KS <= N && NJ <= NTL, "fragment buffer / tile list too small");
+  // buffer loads: the SGPR resource + scalar byte offset carry the (tile, step) address, so all
+  // fragment loads of a wave share ONE vector register (lane * 16) instead of a 64-bit address each
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W), (short)0, 0x7fffffff,
+                                                                       0x00020000);
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (tiles[j] * kt_total + k0 + s) * 1024, 0);
+      f[j * KS + s] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+}
+
+// acc[rt][j] += A[rows of tile rt][k steps kc0 .. kc0 + KS) x f[j * KS + s] for j < nj (wave-
+// uniform).  The A fragments of step s + 1 are read from LDS before the MFMAs of step s issue,
+// so the LDS latency runs under the matrix work instead of between every MFMA.
+template <int RT, int NJ, int KS, int N>
+__device__ __forceinline__ void pmma_n(f32x4 (&acc)[RT][NJ], const bf16_t* A, int SA, int kc0, const uint4 (&f)[N],
+                                       int nj, int lane) {
+  const int r16 = lane & 15, g = lane >> 4;
+  const bf16_t* a0 = A + r16 * SA + kc0 * 32 + g * 8;
+  bf16x8 cur[RT], nxt[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) cur[rt] = *(const bf16x8*)(a0 + rt * 16 * SA);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s + 1 < KS) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) nxt[rt] = *(const bf16x8*)(a0 + rt * 16 * SA + (s + 1) * 32);
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        if (j < nj)
+          acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[rt], __builtin_bit_cast(bf16x8, f[j * KS + s]),
+                                                               acc[rt][j], 0, 0, 0);
+    if (s + 1 < KS) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) cur[rt] = nxt[rt];
+    }
+  }
+}
+
+template <int RT, int NJ, int KS, int N>
+__device__ __forceinline__ void pmma(f32x4 (&acc)[RT][NJ], const bf16_t* A, int SA, int kc0, const uint4 (&f)[N],
+                                     int lane) {
+  pmma_n<RT, NJ, KS, N>(acc, A, SA, kc0, f, NJ, lane);
+}
+
+template <int RT, int NJ>
+__device__ __forceinline__ void zero_acc(f32x4 (&acc)[RT][NJ]) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <int QR>
+__device__ __forceinline__ void fattn_lds(unsigned char* att, int Lq, int Lk, float scale, bf16_t* out, int ldo,
+                                          int tid) {
+  if (Lk <= 32)
+    fattn<bf16_t, 2, QR, true>(att, Lq, Lk, scale, out, ldo, tid);
+  else
+    fattn<bf16_t, 4, QR, true>(att, Lq, Lk, scale, out, ldo, tid);
+}
+
+// Per-loop-body thread ids.  threadIdx.x is laundered through an empty asm so that every
+// value derived from it is recomputed inside the loop body: LICM would otherwise hoist dozens
+// of lane-dependent offsets out of the step loop, keep them live for all T' steps and spill
+// them -- and each spill reload is a vmcnt wait that also drains the weight prefetches.
+#define LANE_IDS()                                                      \
+  int tid = threadIdx.x;                                                \
+  asm volatile("" : "+v"(tid));                                         \
+  const int lane = tid & 63, c16 = lane & 15, g4 = lane >> 4;           \
+  const int c4 = lane * 4;                                              \
+  (void)c16; (void)g4; (void)c4
+
+#define PSTAMP(i)                                                                               \
+  do {                                                                                          \
+    if (a.stamps && k == 0 && blockIdx.x == 0 && threadIdx.x == 0) a.stamps[i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define FSTAMP(i)                                                                               \
+  do {                                                                                          \
+    if (a.stamps && k == 0 && li == 0 && hd == 1 && blockIdx.x == 0 && threadIdx.x == 0)         \
+      a.stamps[i] = __builtin_amdgcn_s_memtime();                                               \
+  } while (0)
+
+constexpr int PK_THREADS = 512;  // 8 waves: two per SIMD, so one wave's LDS / L2 waits overlap the other's MFMAs
+
+template <int RT>
+__global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  using PL = PPlan<RT>;
+  using T = bf16_t;
+  using AT = FAtt<T, PL::R>;
+  constexpr int NT = PK_THREADS;
+  constexpr int R = PL::R, SX = PL::SX, SY = PL::SY, SYQ = PL::SYQ, SHD = PL::SHD, SE = PL::SE;
+  constexpr int NQ = (R * 128 / 4 + NT - 1) / NT;  // state quads per thread
+  float* Hs = (float*)smem;
+  T* Xn = (T*)(smem + PL::OFF_XN);
+  T* Ob = (T*)(smem + PL::OFF_O);
+  float2* st = (float2*)(smem + PL::OFF_ST);
+  unsigned char* scr = smem + PL::OFF_S;
+  float* Y = (float*)scr;                       // self-attention: QKV of a head pair
+  unsigned char* att_sa = scr + PL::Y;
+  float* Yq = (float*)scr;                      // cross-attention: Q of a head, raw memory K/V
+  float* raw = (float*)(scr + PL::YQ);
+  unsigned char* att_ca = scr + PL::YQ + PL::RAW;
+  T* Hd = (T*)scr;                              // FFN chunk
+  float* E = (float*)scr;                       // eps (out projection)
+  T* Xb = (T*)(scr + PL::E);                    // emb operand
+
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, c16 = lane & 15, g4 = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: tile indices live in SGPRs
+  const int Lk = 1 + a.Ts;
+  const size_t row0 = (size_t)b * a.L;
+  const int c4 = (tid & 63) * 4;
+  // QKV head pair: waves 0-3 own local tiles 2w, 2w+1; waves 4-7 own tile 8 + (w - 4)
+  const int nq = wave < 4 ? 2 : 1;
+  const int tq0 = wave < 4 ? 2 * wave : 8 + (wave - 4), tq1 = wave < 4 ? 2 * wave + 1 : tq0;
+
+  // pose state of the clip in registers: quad q = tid + NT j holds elements e = 4q + u of the
+  // reference (C, L) order (c = e / L, l = e % L); read from the internal (L, C) layout
+  float xr[NQ][4];
+  {
+    const int L = a.L, C = a.C, LC = L * C;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = min(4 * (tid + NT * j) + u, LC - 1), cc = e / L, l = e - cc * L;
+        xr[j][u] = a.x[(row0 + l) * C + cc];
+      }
+  }
+
+  // fa: 2 tiles x 8 k steps (QKV pair, out-projections, CA query, FFN-up, output projection)
+  // fb: 2 tiles x 4 k steps (FFN-down chunk, emb).  Each is refilled right after its last use
+  // with the next GEMM that uses it, so its loads run under the phases in between.
+  uint4 fa[16], fb[8];
+  {
+    const int te[2] = {2 * wave, 2 * wave + 1};
+    pload<2, 4>(fb, a.w_emb, 4, te, 0, lane);
+    const int tq[2] = {tq0, tq1};
+    if (nq == 2) pload<2, 8>(fa, a.layers[0].qkv, 8, tq, 0, lane);
+    else pload<1, 8>(fa, a.layers[0].qkv, 8, tq, 0, lane);
+  }
+
+  for (int k = 0; k < a.n_steps; ++k) {
+    LANE_IDS();
+    const StepRec rec = a.steps[a.k0 + k];
+    const int t = rec.t_orig;
+    // Laundered per-iteration copies of the shape scalars: index / address arithmetic derived
+    // from them is recomputed every step instead of being hoisted out of the step loop, where
+    // loop-invariant addresses would sit in registers for all T' steps and spill.
+    int L = a.L, C = a.C;
+    asm volatile("" : "+s"(L), "+s"(C));
+    const int LC = L * C;
+    PSTAMP(0);
+    // ---------------- emb_x + PE of the current state -> Hs (transformer.py:176-180) ----------------
+    {
+      float pe[2][RT][4], be[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = (2 * wave + j) * 16 + c16;
+        be[j] = a.b_emb[col];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pe[j][rt][r] = a.pe[(size_t)min(rt * 16 + 4 * g4 + r, L - 1) * FD + col];
+      }
+      for (int i = tid; i < R * SHD / 8; i += NT) ((uint4*)Xb)[i] = make_uint4(0, 0, 0, 0);
+      bar_lds();
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const int q = tid + NT * j;
+        int cc = (4 * q) / L, l = 4 * q - cc * L;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (4 * q + u < LC) Xb[l * SHD + cc] = from_f32<T>(xr[j][u]);
+          if (++l == L) { l = 0; ++cc; }
+        }
+      }
+      bar_lds();
+      f32x4 acc[RT][2];
+      zero_acc(acc);
+      pmma<RT, 2, 4>(acc, Xb, SHD, 0, fb, lane);
+      {  // fb <- layer 0's first FFN-down chunk
+        const int td[2] = {2 * wave, 2 * wave + 1};
+        pload<2, 4>(fb, a.layers[0].ff2, 32, td, 0, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = (2 * wave + j) * 16 + c16;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Hs[(rt * 16 + 4 * g4 + r) * SH + col] = acc[rt][j][r] + be[j] + pe[j][rt][r];
+      }
+      bar_lds();
+    }
+    PSTAMP(1);
+
+    for (int li = 0; li < a.n_layers; ++li) {
+      LANE_IDS();
+      const FusedLayer& w = a.layers[li];
+      // ---------------- self-attention block (nn.py:160-162) ----------------
+      {
+        const float4 g = *(const float4*)(w.ln1_g + c4), bb = *(const float4*)(w.ln1_b + c4);
+        ln_stats<R, 8>(Hs, L, st, tid);
+        bar_lds();
+        ln_apply<T, NT, R, SX>(Hs, L, st, g, bb, Xn, tid);
+        bar_lds();
+      }
+      for (int hp = 0; hp < 4; ++hp) {
+        LANE_IDS();
+        const float bq0 = w.qkv_b[hp * 192 + tq0 * 16 + c16], bq1 = w.qkv_b[hp * 192 + tq1 * 16 + c16];
+        const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
+                    cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
+        {
+          f32x4 acc[RT][2];
+          zero_acc(acc);
+          pmma_n<RT, 2, 8>(acc, Xn, SX, 0, fa, nq, lane);
+          if (hp < 3) {  // refill: the next head pair, or the SA out-projection
+            const int tq[2] = {12 * (hp + 1) + tq0, 12 * (hp + 1) + tq1};
+            if (nq == 2) pload<2, 8>(fa, w.qkv, 8, tq, 0, lane);
+            else pload<1, 8>(fa, w.qkv, 8, tq, 0, lane);
+          } else {
+            const int to[2] = {2 * wave, 2 * wave + 1};
+            pload<2, 8>(fa, w.o_sa, 8, to, 0, lane);
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if (j >= nq) break;
+            const int col = (j == 0 ? tq0 : tq1) * 16 + c16;
+            const float bias = j == 0 ? bq0 : bq1;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) Y[(rt * 16 + 4 * g4 + r) * SY + col] = acc[rt][j][r] + bias;
+          }
+        }
+        bar_lds();
+        for (int hh = 0; hh < 2; ++hh) {
+          LANE_IDS();
+          const float* Yh = Y + hh * 96;
+          conv_rows<T, false, R, NT>((T*)(att_sa + AT::OQ), AT::SQ, Yh, SY, L, cq, tid);
+          conv_rows<T, false, FLK, NT>((T*)(att_sa + AT::OK), AT::SQ, Yh + 32, SY, L, ck, tid);
+          conv_rows<T, true, FLK, NT>((T*)(att_sa + AT::OV), AT::SV, Yh + 64, SY, L, cv, tid);
+          bar_lds();
+          fattn_lds<R>(att_sa, L, L, a.scale, Ob + (2 * hp + hh) * FDK, SX, tid);
+          bar_lds();
+        }
+      }
+      PSTAMP(2);
+      // SA out-projection + residual
+      {
+        const float bo0 = w.o_sa_b[(2 * wave) * 16 + c16], bo1 = w.o_sa_b[(2 * wave + 1) * 16 + c16];
+        f32x4 acc[RT][2];
+        zero_acc(acc);
+        pmma<RT, 2, 8>(acc, Ob, SX, 0, fa, lane);
+        if (wave < 2) {  // fa <- cross-attn Q of head 0 (waves 0, 1 only)
+          const int tq[1] = {wave};
+          pload<1, 8>(fa, w.q_ca, 8, tq, 0, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = (2 * wave + j) * 16 + c16;
+          const float bo = j == 0 ? bo0 : bo1;
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float* p = Hs + (rt * 16 + 4 * g4 + r) * SH + col;
+              *p = *p + (acc[rt][j][r] + bo);
+            }
+        }
+        bar_lds();
+      }
+      // ---------------- cross-attention block (nn.py:163-167) ----------------
+      {
+        const float4 g = *(const float4*)(w.ln2_g + c4), bb = *(const float4*)(w.ln2_b + c4);
+        ln_stats<R, 8>(Hs, L, st, tid);
+        bar_lds();
+        ln_apply<T, NT, R, SX>(Hs, L, st, g, bb, Xn, tid);
+        bar_lds();
+      }
+      // memory K / V (pre-conv) of a head: row 0 = the step token of t, rows 1.. the cached
+      // speech rows; item v = (row, half, 16-byte piece), rows clamped into [0, Lk)
+      auto kv_load = [&](int hd, int i) -> float4 {
+        const int v = tid + i * NT, r = min(v >> 4, Lk - 1), half = (v >> 3) & 1, q = v & 7;
+        const float* src = r == 0 ? w.kv_step + (size_t)t * 2 * FD : w.kv_mem + ((size_t)b * a.Ts + (r - 1)) * 2 * FD;
+        return *(const float4*)(src + half * FD + hd * FDK + q * 4);
+      };
+      auto kv_store = [&](int i, float4 val) {
+        const int v = tid + i * NT, r = v >> 4, half = (v >> 3) & 1, q = v & 7;
+        if (r < Lk) *(float4*)(raw + half * (FLK + 2) * FDK + r * FDK + q * 4) = val;
+      };
+      static_assert(2 * FLK * 8 == 2 * PK_THREADS, "two 16-byte memory pieces per thread");
+      float4 kv0 = kv_load(0, 0), kv1 = kv_load(0, 1);
+      for (int hd = 0; hd < 8; ++hd) {
+        LANE_IDS();
+        FSTAMP(6);
+        const float bqc = w.q_ca_b[hd * FDK + (wave & 1) * 16 + c16];
+        const ConvW dq = conv_w(w.ca_qw, w.ca_qb, tid & 31), dk = conv_w(w.ca_kw, w.ca_kb, tid & 31),
+                    dv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
+        {
+          f32x4 acc[RT][1];
+          zero_acc(acc);
+          if (wave < 2) pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
+          if (hd < 7) {
+            if (wave < 2) {
+              const int tq[1] = {2 * (hd + 1) + wave};
+              pload<1, 8>(fa, w.q_ca, 8, tq, 0, lane);
+            }
+          } else {  // fa <- the CA out-projection
+            const int to[2] = {2 * wave, 2 * wave + 1};
+            pload<2, 8>(fa, w.o_ca, 8, to, 0, lane);
+          }
+          if (wave < 2) {
+            const int col = (wave & 1) * 16 + c16;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) Yq[(rt * 16 + 4 * g4 + r) * SYQ + col] = acc[rt][0][r] + bqc;
+          }
+        }
+        FSTAMP(7);
+        kv_store(0, kv0);
+        kv_store(1, kv1);
+        FSTAMP(8);
+        if (hd < 7) {
+          kv0 = kv_load(hd + 1, 0);
+          kv1 = kv_load(hd + 1, 1);
+        }
+        FSTAMP(9);
+        bar_lds();
+        FSTAMP(10);
+        conv_rows<T, false, R, NT>((T*)(att_ca + AT::OQ), AT::SQ, Yq, SYQ, L, dq, tid);
+        conv_rows<T, false, FLK, NT>((T*)(att_ca + AT::OK), AT::SQ, raw, FDK, Lk, dk, tid);
+        conv_rows<T, true, FLK, NT>((T*)(att_ca + AT::OV), AT::SV, raw + (FLK + 2) * FDK, FDK, Lk, dv, tid);
+        FSTAMP(11);
+        bar_lds();
+        FSTAMP(12);
+        fattn_lds<R>(att_ca, L, Lk, a.scale, Ob + hd * FDK, SX, tid);
+        FSTAMP(13);
+        bar_lds();
+        FSTAMP(14);
+      }
+      PSTAMP(3);
+      // CA out-projection + residual
+      {
+        const float bo0 = w.o_ca_b[(2 * wave) * 16 + c16], bo1 = w.o_ca_b[(2 * wave + 1) * 16 + c16];
+        f32x4 acc[RT][2];
+        zero_acc(acc);
+        pmma<RT, 2, 8>(acc, Ob, SX, 0, fa, lane);
+        {  // fa <- FFN-up chunk 0 (fb already holds FFN-down chunk 0)
+          const int tf[1] = {wave};
+          pload<1, 8>(fa, w.ff1, 8, tf, 0, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = (2 * wave + j) * 16 + c16;
+          const float bo = j == 0 ? bo0 : bo1;
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float* p = Hs + (rt * 16 + 4 * g4 + r) * SH + col;
+              *p = *p + (acc[rt][j][r] + bo);
+            }
+        }
+        bar_lds();
+      }
+      // ---------------- feed-forward block (nn.py:170-172) ----------------
+      {
+        const float4 g = *(const float4*)(w.ln3_g + c4), bb = *(const float4*)(w.ln3_b + c4);
+        ln_stats<R, 8>(Hs, L, st, tid);
+        bar_lds();
+        ln_apply<T, NT, R, SX>(Hs, L, st, g, bb, Xn, tid);
+        bar_lds();
+      }
+      {
+        const bool last = li + 1 == a.n_layers;
+        const FusedLayer& wn = a.layers[last ? li : li + 1];
+        f32x4 accd[RT][2];
+        zero_acc(accd);
+        for (int c = 0; c < 8; ++c) {
+          LANE_IDS();
+          const float bf = w.ff1_b[(8 * c + wave) * 16 + c16];
+          f32x4 acc[RT][1];
+          zero_acc(acc);
+                    pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
+          if (c < 7) {
+            const int tf[1] = {8 * (c + 1) + wave};
+            pload<1, 8>(fa, w.ff1, 8, tf, 0, lane);
+          } else if (!last) {  // fa <- the next layer's first QKV pair
+            const int tq[2] = {tq0, tq1};
+            if (nq == 2) pload<2, 8>(fa, wn.qkv, 8, tq, 0, lane);
+            else pload<1, 8>(fa, wn.qkv, 8, tq, 0, lane);
+          } else {             // fa <- the output projection
+            const int to[1] = {wave};
+            pload<1, 8>(fa, a.w_out, 8, to, 0, lane);
+          }
+          {
+            const int col = (8 * c + wave) * 16 + c16 - 128 * c;  // column inside the chunk
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float v = fmaxf(acc[rt][0][r] + bf, 0.f);
+                Hd[(rt * 16 + 4 * g4 + r) * SHD + col] = from_f32<T>(v * v);
+              }
+          }
+          bar_lds();
+          pmma<RT, 2, 4>(accd, Hd, SHD, 0, fb, lane);
+          {
+            const int td[2] = {2 * wave, 2 * wave + 1};
+            if (c < 7)
+              pload<2, 4>(fb, w.ff2, 32, td, 4 * (c + 1), lane);
+            else if (!last)  // fb <- the next layer's first FFN-down chunk
+              pload<2, 4>(fb, wn.ff2, 32, td, 0, lane);
+            else             // fb <- the next step's emb fragments
+              pload<2, 4>(fb, a.w_emb, 4, td, 0, lane);
+          }
+          bar_lds();
+        }
+        const float b20 = w.ff2_b[(2 * wave) * 16 + c16], b21 = w.ff2_b[(2 * wave + 1) * 16 + c16];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = (2 * wave + j) * 16 + c16;
+          const float b2 = j == 0 ? b20 : b21;
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float* p = Hs + (rt * 16 + 4 * g4 + r) * SH + col;
+              *p = *p + (accd[rt][j][r] + b2);
+            }
+        }
+        bar_lds();
+      }
+    }
+    PSTAMP(4);
+    // ---------------- out_layers + posterior update (nn.py:211-214,228; gaussian_diffusion.py) -------
+    {
+      const float4 g = *(const float4*)(a.ln_g + c4), bb = *(const float4*)(a.ln_b + c4);
+      ln_stats<R, 8>(Hs, L, st, tid);
+      bar_lds();
+      ln_apply<T, NT, R, SX>(Hs, L, st, g, bb, Xn, tid);
+      bar_lds();
+    }
+    {
+      const float bo = a.b_out[wave * 16 + c16];
+      f32x4 acc[RT][1];
+      zero_acc(acc);
+      pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
+      {  // fa <- layer 0's first QKV pair (next step)
+        const int tq[2] = {tq0, tq1};
+        if (nq == 2) pload<2, 8>(fa, a.layers[0].qkv, 8, tq, 0, lane);
+        else pload<1, 8>(fa, a.layers[0].qkv, 8, tq, 0, lane);
+      }
+      const int col = wave * 16 + c16;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) E[(rt * 16 + 4 * g4 + r) * SE + col] = acc[rt][0][r] + bo;
+    }
+    bar_lds();
+    {
+      const size_t plane = (size_t)a.n * LC;
+      const float* nz = a.noise ? a.noise + (size_t)(a.k0 + k) * plane + (size_t)b * LC : nullptr;
+      const bool inp = a.inp_mask != nullptr;
+      const bool ex = a.extras != nullptr && k + 1 == a.n_steps;
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const int q = tid + NT * j;
+        if (4 * q >= LC) continue;
+        float z[4];
+        if (nz) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) z[u] = nz[min(4 * q + u, LC - 1)];
+        } else {
+          philox_normal4(a.seed, (uint32_t)(a.clip_offset + b), (uint32_t)rec.i, TAG_STEP, (uint32_t)q, z);
+        }
+        int cc = (4 * q) / L, l = 4 * q - cc * L;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = 4 * q + u;
+          if (e < LC) {
+            const float ev = E[l * SE + cc];
+            const size_t gi = (row0 + l) * C + cc;
+            const UpdOut o = upd_math(rec, a.alg, xr[j][u], ev, false, 0.f, inp, inp ? a.inp_mask[row0 + l] : 0.f,
+                                      inp ? a.inp_pose[gi] : 0.f, inp ? a.trans[l] : 0.f, z[u]);
+            xr[j][u] = o.xn;
+            if (ex) {
+              const size_t ncl = (size_t)b * LC + e;
+              a.extras[0 * plane + ncl] = o.mean;
+              a.extras[1 * plane + ncl] = rec.var;
+              a.extras[2 * plane + ncl] = rec.logvar;
+              a.extras[3 * plane + ncl] = ev;
+              a.extras[4 * plane + ncl] = o.x0;
+              a.extras[5 * plane + ncl] = o.raw;
+            }
+          }
+          if (++l == L) { l = 0; ++cc; }
+        }
+      }
+    }
+    bar_lds();  // E is dead before the next step's Xb zero fill (same scratch)
+    PSTAMP(5);
+  }
+  // final state -> the internal (L, C) layout
+  const int L = a.L, C = a.C, LC = L * C;
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) {
+    const int q = tid + NT * j;
+    int cc = (4 * q) / L, l = 4 * q - cc * L;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (4 * q + u < LC) a.x[(row0 + l) * C + cc] = xr[j][u];
+      if (++l == L) { l = 0; ++cc; }
+    }
+  }
+}
+
+static bool persist_attrs_done = false;
+
+bool persist_supported(int dtype, int d_model, int heads, int L, int Ts, int C) {
+  return dtype == 1 && d_model == FD && heads == FD / FDK && L >= 1 && L <= 48 && Ts >= 1 && 1 + Ts <= FLK &&
+         C >= 1 && C <= 128;
+}
+
+hipError_t launch_persist(const PersistArgs& a, hipStream_t s) {
+  if (!persist_attrs_done) {
+    (void)hipFuncSetAttribute((const void*)psk_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)psk_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)psk_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    persist_attrs_done = true;
+  }
+  const int rt = (a.L + 15) / 16;
+  const dim3 grid(a.n), blk(PK_THREADS);
+  if (rt == 1) hipLaunchKernelGGL(psk_kernel<1>, grid, blk, PPlan<1>::TOTAL, s, a);
+  else if (rt == 2) hipLaunchKernelGGL(psk_kernel<2>, grid, blk, PPlan<2>::TOTAL, s, a);
+  else if (rt == 3) hipLaunchKernelGGL(psk_kernel<3>, grid, blk, PPlan<3>::TOTAL, s, a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace ggd

@@ -11,8 +11,8 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libggd.so")
-SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_diag.hip", "ggd_api.hip"]
-HEADERS = ["ggd_kernels.h", "ggd_common.h", os.path.join("..", "..", "include", "ggd.h")]
+SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_persist.hip", "ggd_diag.hip", "ggd_api.hip"]
+HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_fusedlib.h", os.path.join("..", "..", "include", "ggd.h")]
 
 GGD_OK, GGD_IGNORED = 0, 1
 GGD_ERR_ARG, GGD_ERR_UNSUPPORTED, GGD_ERR_HIP, GGD_ERR_STATE, GGD_ERR_NAME = -1, -2, -3, -4, -5
