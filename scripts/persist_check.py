@@ -25,7 +25,7 @@ arr = (ctypes.c_int32 * 1)
 
 
 def diag(what, v):
-    res = (ctypes.c_double * 16)()
+    res = (ctypes.c_double * 17)()
     native.check(ctx.h, lib.ggd_diag(ctx.h, what, arr(v), 1, 1, ctypes.cast(res, ctypes.c_void_p)), "diag")
     return list(res)
 
@@ -61,6 +61,7 @@ diag(8, 1)
 run(True, 1)
 st = diag(8, 2)
 print("persistent phases (us, iteration 0, wg 0): emb|layers...|out+update", [round(v, 2) for v in st[:5]])
-f = st[5:14]
-print("CA head 1 of layer 0 (us from its start): Qgemm+refill, kv_store, kv_load, bar, conv, bar, attn, bar",
-      [round(f[i + 1] - f[0], 3) for i in range(8)])
+f = st[5:16]
+print("CA head 1 of layer 0 (us from its start): Qgemm+refill, kv_store, kv_load, bar, conv, bar, attn",
+      [round(f[i + 1] - f[0], 3) for i in range(7)], "vmcnt(0) drain", round(f[8] - f[0], 3),
+      "pmma", round(f[9] - f[8], 3))

@@ -936,9 +936,9 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     if (p[0] == 1) HIP_TRY(c, hipMemset(c->stamps, 0, 64 * sizeof(unsigned long long)));
     if (p[0] == 2 && c->stamps) {
       HIP_TRY(c, hipStreamSynchronize(c->stream));
-      unsigned long long h[16];
+      unsigned long long h[17];
       HIP_TRY(c, hipMemcpy(h, c->stamps, sizeof h, hipMemcpyDeviceToHost));
-      for (int i = 0; i < 15; ++i)
+      for (int i = 0; i < 16; ++i)
         avg_us[i] = (h[0] && h[i + 1] >= h[0]) ? (double)(h[i + 1] - h[0]) / 2400.0 : -1.0;
     }
     if (p[0] == 0) c->stamps = nullptr;  // the buffer stays owned by the ctx allocation list

@@ -169,22 +169,50 @@ struct WGemm {
 #pragma unroll
       for (int k = 0; k < G; ++k) wb[j][k] = W[((size_t)tiles[j] * kt_total + k0 + g * G + k) * 64 + lane];
   }
-  // group 0 must have been loaded; tiles j >= nj_on are skipped (wave-uniform)
+  // group 0 must have been loaded; tiles j >= nj_on are skipped (wave-uniform).  bf16: the A
+  // fragments of k step k + 1 are read from LDS before the MFMAs of step k issue, so the LDS
+  // latency overlaps the matrix work (one wave per SIMD hides nothing on its own).
   __device__ __forceinline__ void run(f32x4 (&acc)[RT][NJ], const T* A, int SA, int lane, int nj_on = NJ) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int g = 0; g < KT / G; ++g) {
-      if (g > 0) load(g, lane);
+    if constexpr (sizeof(T) == 2) {
+      const int r16 = lane & 15, gq = lane >> 4;
+      const T* a0 = A + r16 * SA + gq * 8;
+      bf16x8 cur[RT], nxt[RT];
 #pragma unroll
-      for (int k = 0; k < G; ++k)
+      for (int rt = 0; rt < RT; ++rt) cur[rt] = *(const bf16x8*)(a0 + rt * 16 * SA);
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        if (k + 1 < KT) {
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) nxt[rt] = *(const bf16x8*)(a0 + rt * 16 * SA + (k + 1) * 32);
+        }
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
-            if (j < nj_on) mma_aw<T>(acc[rt][j], A, SA, rt, g * G + k, wb[j][k], lane);
+            if (j < nj_on)
+              acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[rt], __builtin_bit_cast(bf16x8, wb[j][k]),
+                                                                   acc[rt][j], 0, 0, 0);
+        if (k + 1 < KT) {
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) cur[rt] = nxt[rt];
+        }
+      }
+    } else {
+#pragma unroll 1
+      for (int g = 0; g < KT / G; ++g) {
+        if (g > 0) load(g, lane);
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              if (j < nj_on) mma_aw<T>(acc[rt][j], A, SA, rt, g * G + k, wb[j][k], lane);
+      }
     }
   }
 };

@@ -356,10 +356,13 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
         const float bqc = w.q_ca_b[hd * FDK + (wave & 1) * 16 + c16];
         const ConvW dq = conv_w(w.ca_qw, w.ca_qb, tid & 31), dk = conv_w(w.ca_kw, w.ca_kb, tid & 31),
                     dv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
+        if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        FSTAMP(14);
         {
           f32x4 acc[RT][1];
           zero_acc(acc);
           if (wave < 2) pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
+          FSTAMP(15);
           if (hd < 7) {
             if (wave < 2) {
               const int tq[1] = {2 * (hd + 1) + wave};
@@ -397,7 +400,6 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
         fattn_lds<R>(att_ca, L, Lk, a.scale, Ob + hd * FDK, SX, tid);
         FSTAMP(13);
         bar_lds();
-        FSTAMP(14);
       }
       PSTAMP(3);
       // CA out-projection + residual

@@ -49,6 +49,6 @@ def test_hip_f32_matches_golden(pkg, beat_cfg):
     eps = model(x.cuda(), t.cuda(), wav=wav.cuda()).cpu().numpy()
     assert np.abs(eps - GOLD["eps"]).max() <= 1e-4
     for alg, loop in (("ddpm", diffusion.p_sample_loop), ("ddim", diffusion.ddim_sample_loop)):
-        out = loop(model, (2, mg.D_POSE, mg.L), {"wav": wav.cuda()}, seed=3, clip_offset=0, n_steps=5)
+        out = loop(model, (2, mg.D_POSE, mg.L), model_kwargs={"wav": wav.cuda()}, seed=3, clip_offset=0, n_steps=5)
         err = np.abs(out["sample"].cpu().numpy() - GOLD[f"{alg}5_sample"]).max()
         assert err <= 1e-3, (alg, err)
