@@ -112,18 +112,23 @@ __device__ __forceinline__ void outproj_epilogue(float* Hs, const f32x4 (&acc)[F
   }
 }
 
-// rows [0, L) of Hs -> global rows: all 64 rows read, then bounded 16-byte stores
-__device__ __forceinline__ void store_rows(float* dst, const float* Hs, int L) {
+// rows [0, L) of Hs -> global rows, shared by the NP workgroups of a clip: workgroup `part`
+// writes rows r with r % NP == part (every row once; bounded 16-byte stores, no branch)
+template <int NP = 8>
+__device__ __forceinline__ void store_rows(float* dst, const float* Hs, int L, int part) {
+  constexpr int RP = FR / NP;  // rows per part
   const OutRows out(dst, (uint32_t)(sizeof(float) * L * FD));
-  float4 v[FR * FD / 4 / NTHREADS];
+  float4 v[RP * 64 / NTHREADS > 0 ? RP * 64 / NTHREADS : 1];
+  constexpr int NV = RP * 64 / NTHREADS;
+  static_assert(NV >= 1, "at least one 16-byte piece per thread");
 #pragma unroll
-  for (int i = 0; i < FR * FD / 4 / NTHREADS; ++i) {
-    const int idx = threadIdx.x + i * NTHREADS, r = idx >> 6, c = (idx & 63) * 4;
+  for (int i = 0; i < NV; ++i) {
+    const int idx = threadIdx.x + i * NTHREADS, r = (idx >> 6) * NP + part, c = (idx & 63) * 4;
     v[i] = *(const float4*)(Hs + min(r, L - 1) * SH + c);
   }
 #pragma unroll
-  for (int i = 0; i < FR * FD / 4 / NTHREADS; ++i) {
-    const int idx = threadIdx.x + i * NTHREADS, r = idx >> 6, c = (idx & 63) * 4;
+  for (int i = 0; i < NV; ++i) {
+    const int idx = threadIdx.x + i * NTHREADS, r = (idx >> 6) * NP + part, c = (idx & 63) * 4;
     out.put4((uint32_t)(r * FD + c), v[i]);
   }
 }
@@ -180,16 +185,16 @@ __global__ void __launch_bounds__(NTHREADS) kb_kernel(FusedArgs a) {
     const float* src = r == 0 ? w.kv_step + (size_t)t * 2 * FD : w.kv_mem + ((size_t)b * a.Ts + (r - 1)) * 2 * FD;
     return *(const float4*)(src + half * FD + h * FDK + q * 4);
   };
-  // named registers, not an array: an array live across the LN is demoted to scratch
+  f32x4 acc_o[FRT][4];
+  go.run(acc_o, Ax, Frag<T>::SX, lane);
+  // issued after the out-projection MFMAs: t comes from a two-load dependent chain, which
+  // must not stall them; the loads complete under the epilogue and LN2.  Named registers,
+  // not an array: an array live across the LN is demoted to scratch.
   const float4 kv0 = kv_load(0), kv1 = kv_load(1), kv2 = kv_load(2), kv3 = kv_load(3);
-  {
-    f32x4 acc[FRT][4];
-    go.run(acc, Ax, Frag<T>::SX, lane);
-    outproj_epilogue<T>(Hs, acc, bo, lane, wave);
-  }
+  outproj_epilogue<T>(Hs, acc_o, bo, lane, wave);
   bar_lds();
   STAMP(2);
-  if (h == 0) store_rows(a.h_out + row0 * FD, Hs, L);
+  store_rows<8>(a.h_out + row0 * FD, Hs, L, h);
   ln_stats(Hs, L, st);
   bar_lds();
   ln_apply<T>(Hs, L, st, lg, lb, Ax);
@@ -273,7 +278,7 @@ __global__ void __launch_bounds__(NTHREADS) kc_kernel(FusedArgs a) {
   }
   bar_lds();
   STAMP(2);
-  if (c == 0) store_rows(a.h_out + row0 * FD, Hs, L);
+  store_rows<8>(a.h_out + row0 * FD, Hs, L, c);
   ln_stats(Hs, L, st);
   bar_lds();
   ln_apply<T>(Hs, L, st, lg, lb, Ax);

@@ -266,11 +266,17 @@ __device__ __forceinline__ void ln_apply(const float* Hs, int L, const float2* s
   for (int i = 0; i < NI; ++i) {
     const int r = r0 + NW * i;
     const bool ok = r < L;
-    T* o = img + r * SXI + c4;
-    o[0] = from_f32<T>(ok ? (v[i].x - s[i].x) * s[i].y * g.x + bb.x : 0.f);
-    o[1] = from_f32<T>(ok ? (v[i].y - s[i].x) * s[i].y * g.y + bb.y : 0.f);
-    o[2] = from_f32<T>(ok ? (v[i].z - s[i].x) * s[i].y * g.z + bb.z : 0.f);
-    o[3] = from_f32<T>(ok ? (v[i].w - s[i].x) * s[i].y * g.w + bb.w : 0.f);
+    const float y0 = ok ? (v[i].x - s[i].x) * s[i].y * g.x + bb.x : 0.f;
+    const float y1 = ok ? (v[i].y - s[i].x) * s[i].y * g.y + bb.y : 0.f;
+    const float y2 = ok ? (v[i].z - s[i].x) * s[i].y * g.z + bb.z : 0.f;
+    const float y3 = ok ? (v[i].w - s[i].x) * s[i].y * g.w + bb.w : 0.f;
+    if constexpr (sizeof(T) == 2) {  // one 8-byte LDS store per row instead of four 2-byte ones
+      const uint32_t lo = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
+      const uint32_t hi = (uint32_t)f2bf(y2) | ((uint32_t)f2bf(y3) << 16);
+      *(uint2*)(img + r * SXI + c4) = make_uint2(lo, hi);
+    } else {
+      *(float4*)(img + r * SXI + c4) = make_float4(y0, y1, y2, y3);
+    }
   }
 }
 
