@@ -424,7 +424,15 @@ int launch_fused_layers(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     f.h = c->h;
     f.h_out = c->h2;
     f.bump_counter = sampling && li == 0;
-    HIP_TRY(c, launch_fused(0, D.dtype, f, n, s));     // KA: LN1 + QKV + conv + self-attention
+    if (li == 0) {  // layer 0's KA also computes h = emb_x(x) + PE from the state x
+      f.x_emb = c->x;
+      f.w_emb = c->f_emb.w;
+      f.b_emb = c->f_emb.b;
+      f.pe = c->pe;
+      f.C = D.d_pose;
+    }
+    HIP_TRY(c, launch_fused(0, D.dtype, f, n, s));     // KA: [emb +] LN1 + QKV + conv + self-attention
+    f.x_emb = nullptr;
     f.bump_counter = 0;
     const bool prof = c->profiling && sampling;        // KB is the dominant kernel of the step
     if (prof) { int r = prof_mark(c, s); if (r) return r; }
@@ -532,7 +540,7 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
 int launch_step(ggd_ctx* c, const ggd_sample_args& a, float* extras, int fixed_k) {
   int r = launch_decoder(c, a.n, true, nullptr);
   if (r) return r;
-  if (c->fused) {  // KE: LN_out + out-proj + update + the next step's emb_x + PE
+  if (c->fused) {  // KE: LN_out + out-proj + update (the next step's emb is in its first KA)
     FinalArgs f = final_args(c, a.n);
     f.alg = a.alg;
     f.noise = a.noise;
@@ -544,7 +552,6 @@ int launch_step(ggd_ctx* c, const ggd_sample_args& a, float* extras, int fixed_k
     f.extras = extras;
     f.do_out = 1;
     f.do_update = 1;
-    f.do_emb = 1;
     HIP_TRY(c, launch_final(c->desc.dtype, f, c->stream));
     return GGD_OK;
   }
@@ -864,12 +871,9 @@ int ggd_denoise(ggd_ctx* c, const float* x_t, const int32_t* t, float* eps, int3
   HIP_TRY(c, hipStreamWaitEvent(s, c->ev_in, 0));
   HIP_TRY(c, launch_init_state(c->x, x_t, 0, 0, n, D.d_pose, D.seq_len, s));
   if (c->fused) {
-    FinalArgs f = final_args(c, n);
-    f.do_emb = 1;  // emb_x + PE of x_t into h
-    HIP_TRY(c, launch_final(D.dtype, f, s));
-    int r = launch_decoder(c, n, false, t);
+    int r = launch_decoder(c, n, false, t);  // layer 0's KA embeds x_t
     if (r) return r;
-    f.do_emb = 0;
+    FinalArgs f = final_args(c, n);
     f.do_out = 1;  // LN_out + out-proj -> eps in (N, C, L)
     f.eps_out = eps;
     HIP_TRY(c, launch_final(D.dtype, f, s));
@@ -1018,11 +1022,6 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
       make_records(c, GGD_DDPM, 0.f, recs);
       HIP_TRY(c, hipMemcpyAsync(c->d_steps, recs.data(), sizeof(StepRec) * recs.size(), hipMemcpyHostToDevice, s));
       HIP_TRY(c, launch_init_state(c->x, nullptr, 1, 0, n, D.d_pose, D.seq_len, s));
-      if (c->fused) {
-        FinalArgs f = final_args(c, n);
-        f.do_emb = 1;
-        HIP_TRY(c, launch_final(D.dtype, f, s));
-      }
     }
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
@@ -1081,7 +1080,7 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
         HIP_TRY(c, launch_fused(which, D.dtype, f, n, s));
       } else {
         FinalArgs f = final_args(c, n);
-        f.do_out = 1; f.do_update = 1; f.do_emb = 1;
+        f.do_out = 1; f.do_update = 1;
         f.stamps = it == iters ? st : nullptr;
         HIP_TRY(c, launch_final(D.dtype, f, s));
       }
@@ -1213,11 +1212,6 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
     HIP_TRY(c, hipEventRecord(c->ev_out, s));
     HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
     return GGD_OK;
-  }
-  if (c->fused) {  // emb_x + PE of x_T; every later step's embedding is computed by that step's KE
-    FinalArgs f = final_args(c, a->n);
-    f.do_emb = 1;
-    HIP_TRY(c, launch_final(D.dtype, f, s));
   }
   HIP_TRY(c, launch_set_int(c->d_counter, -1, s));
 

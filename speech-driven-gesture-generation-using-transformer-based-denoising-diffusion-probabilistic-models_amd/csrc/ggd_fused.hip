@@ -32,68 +32,6 @@
 
 namespace ggd {
 
-// ------------------------------------------------------------------------------------------
-// KA: LN1 + QKV(head) + conv + self-attention          grid (heads, clips)
-// ------------------------------------------------------------------------------------------
-template <typename T>
-__global__ void __launch_bounds__(NTHREADS) ka_kernel(FusedArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using PL = Plan<T>;
-  constexpr int KT = FD / Frag<T>::KF, SY = 96 + 4;
-  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int L = a.L, c16 = lane & 15, g4 = lane >> 4;
-  T* Xn = (T*)smem;
-  float2* st = (float2*)(smem + PL::IMG);
-  unsigned char* un = smem + PL::IMG + PL::ST;
-  float* Hs = (float*)un;
-  float* Y = (float*)un;
-  unsigned char* att = un + PL::Y_KA;
-  const FusedLayer& w = a.w;
-
-  STAMP(0);
-  if (a.bump_counter && h == 0 && b == 0 && tid == 0) atomicAdd(a.step_counter, 1);
-  glds_rows(Hs, sizeof(float) * SH, a.h + (size_t)b * L * FD, sizeof(float) * FD, L, 1);
-  // QKV of head h: packed as 6 tiles [q0 q1 k0 k1 v0 v1]; wave w owns tiles w and w + 4 (< 6)
-  WGemm<T, 2, KT> gm(w.qkv, KT, 0);
-  gm.tiles[0] = h * 6 + wave;
-  gm.tiles[1] = h * 6 + min(wave + 4, 5);
-  gm.load(0, lane);
-  const float bias0 = w.qkv_b[h * 96 + wave * 16 + c16];
-  const float bias1 = w.qkv_b[h * 96 + min(wave + 4, 5) * 16 + c16];
-  const float4 lg = *(const float4*)(w.ln1_g + (tid & 63) * 4), lb = *(const float4*)(w.ln1_b + (tid & 63) * 4);
-  const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
-              cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
-  __syncthreads();  // LDS-DMA rows and every operand above have landed
-  ln_stats(Hs, L, st);
-  bar_lds();
-  ln_apply<T>(Hs, L, st, lg, lb, Xn);
-  bar_lds();
-  STAMP(1);
-  // Hs is dead from here: Y and the attention images overlay it
-  f32x4 acc[FRT][2];
-  gm.run(acc, Xn, Frag<T>::SX, lane, wave + 4 < 6 ? 2 : 1);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    if (j == 1 && wave + 4 >= 6) continue;
-    const int col = (j == 0 ? wave : wave + 4) * 16 + c16;
-    const float bias = j == 0 ? bias0 : bias1;
-#pragma unroll
-    for (int rt = 0; rt < FRT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Y[(rt * 16 + 4 * g4 + r) * SY + col] = acc[rt][j][r] + bias;
-  }
-  bar_lds();
-  STAMP(2);
-  using AT = FAtt<T>;
-  conv_rows<T, false>((T*)(att + AT::OQ), AT::SQ, Y, SY, L, cq);
-  conv_rows<T, false>((T*)(att + AT::OK), AT::SQ, Y + 32, SY, L, ck);
-  conv_rows<T, true>((T*)(att + AT::OV), AT::SV, Y + 64, SY, L, cv);
-  bar_lds();
-  STAMP(3);
-  fattn_any<T>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
-  STAMP_END(4);
-}
-
 // Hs[i][n] += A[i] . W[n] + bias[n] for all 64 rows; wave w owns columns [64w, 64w + 64)
 template <typename T>
 __device__ __forceinline__ void outproj_epilogue(float* Hs, const f32x4 (&acc)[FRT][4], const float (&bias)[4], int lane,
@@ -131,6 +69,100 @@ __device__ __forceinline__ void store_rows(float* dst, const float* Hs, int L, i
     const int idx = threadIdx.x + i * NTHREADS, r = (idx >> 6) * NP + part, c = (idx & 63) * 4;
     out.put4((uint32_t)(r * FD + c), v[i]);
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// KA: LN1 + QKV(head) + conv + self-attention          grid (heads, clips)
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(NTHREADS) ka_kernel(FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  using PL = Plan<T>;
+  constexpr int KT = FD / Frag<T>::KF, SY = 96 + 4;
+  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int L = a.L, c16 = lane & 15, g4 = lane >> 4;
+  T* Xn = (T*)smem;
+  float2* st = (float2*)(smem + PL::IMG);
+  unsigned char* un = smem + PL::IMG + PL::ST;
+  float* Hs = (float*)un;
+  float* Y = (float*)un;
+  unsigned char* att = un + PL::Y_KA;
+  const FusedLayer& w = a.w;
+
+  STAMP(0);
+  if (a.bump_counter && h == 0 && b == 0 && tid == 0) atomicAdd(a.step_counter, 1);
+  const bool emb = a.x_emb != nullptr;  // layer 0: h = emb_x(x) + PE computed here
+  glds_rows(Hs, sizeof(float) * SH, emb ? a.pe : a.h + (size_t)b * L * FD, sizeof(float) * FD, L, 1);
+  constexpr int KTE = 128 / Frag<T>::KF, SB = 128 + Frag<T>::PT, NXV = FR * 128 / NTHREADS;
+  WGemm<T, 4, KTE> ge(a.w_emb, KTE, 0);
+  float be[4], xv[NXV];
+  if (emb) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ge.tiles[j] = 4 * wave + j;
+    ge.load(0, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) be[j] = a.b_emb[(4 * wave + j) * 16 + c16];
+    const int C = a.C;
+#pragma unroll
+    for (int i = 0; i < NXV; ++i) {
+      const int idx = tid + i * NTHREADS, l = idx >> 7, c = idx & 127;
+      xv[i] = a.x_emb[((size_t)b * L + min(l, L - 1)) * C + min(c, C - 1)];
+    }
+  }
+  // QKV of head h: packed as 6 tiles [q0 q1 k0 k1 v0 v1]; wave w owns tiles w and w + 4 (< 6)
+  WGemm<T, 2, KT> gm(w.qkv, KT, 0);
+  gm.tiles[0] = h * 6 + wave;
+  gm.tiles[1] = h * 6 + min(wave + 4, 5);
+  gm.load(0, lane);
+  const float bias0 = w.qkv_b[h * 96 + wave * 16 + c16];
+  const float bias1 = w.qkv_b[h * 96 + min(wave + 4, 5) * 16 + c16];
+  const float4 lg = *(const float4*)(w.ln1_g + (tid & 63) * 4), lb = *(const float4*)(w.ln1_b + (tid & 63) * 4);
+  const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
+              cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
+  __syncthreads();  // LDS-DMA rows and every operand above have landed
+  if (emb) {
+    // Xb = bf16(x) (channels >= C zero; aliases the LN image), Hs = PE + Xb W_emb^T + b
+    T* Xb = Xn;
+#pragma unroll
+    for (int i = 0; i < NXV; ++i) {
+      const int idx = tid + i * NTHREADS, l = idx >> 7, c = idx & 127;
+      Xb[l * SB + c] = from_f32<T>(c < a.C ? xv[i] : 0.f);
+    }
+    bar_lds();
+    f32x4 acc[FRT][4];
+    ge.run(acc, Xb, SB, lane);
+    outproj_epilogue<T>(Hs, acc, be, lane, wave);
+    bar_lds();
+    store_rows<8>(a.h + (size_t)b * L * FD, Hs, L, h);  // the residual rows KB reads
+  }
+  ln_stats(Hs, L, st);
+  bar_lds();
+  ln_apply<T>(Hs, L, st, lg, lb, Xn);
+  bar_lds();
+  STAMP(1);
+  // Hs is dead from here: Y and the attention images overlay it
+  f32x4 acc[FRT][2];
+  gm.run(acc, Xn, Frag<T>::SX, lane, wave + 4 < 6 ? 2 : 1);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (j == 1 && wave + 4 >= 6) continue;
+    const int col = (j == 0 ? wave : wave + 4) * 16 + c16;
+    const float bias = j == 0 ? bias0 : bias1;
+#pragma unroll
+    for (int rt = 0; rt < FRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Y[(rt * 16 + 4 * g4 + r) * SY + col] = acc[rt][j][r] + bias;
+  }
+  bar_lds();
+  STAMP(2);
+  using AT = FAtt<T>;
+  conv_rows<T, false>((T*)(att + AT::OQ), AT::SQ, Y, SY, L, cq);
+  conv_rows<T, false>((T*)(att + AT::OK), AT::SQ, Y + 32, SY, L, ck);
+  conv_rows<T, true>((T*)(att + AT::OV), AT::SV, Y + 64, SY, L, cv);
+  bar_lds();
+  STAMP(3);
+  fattn_any<T>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
+  STAMP_END(4);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -365,113 +397,88 @@ __global__ void __launch_bounds__(NTHREADS) kd_kernel(FusedArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// KE: LN_out + out-proj (eps) [+ diffusion update] [+ next step's emb_x + PE]   grid (clips)
-// 512 threads: the update is VALU work (Philox, Box-Muller, the posterior arithmetic) on one
-// clip's L x C elements, and two waves per SIMD issue it twice as fast as one.
+// KE: LN_out + out-proj of 16 channels (eps) [+ diffusion update of those channels]
+// grid (8 channel blocks, clips).  Block p owns pose channels [16p, 16p + 16): wave w computes
+// eps for row tile w; the update of the block's L x 16 elements is one Philox quad per thread.
+// The next step's emb_x + PE is computed by that step's first KA (x_emb).
 // ------------------------------------------------------------------------------------------
-constexpr int KE_THREADS = 512;
-
 template <typename T>
-__global__ void __launch_bounds__(KE_THREADS) ke_kernel(FinalArgs a) {
+__global__ void __launch_bounds__(NTHREADS) ke_kernel(FinalArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
-  constexpr int NT = KE_THREADS;
-  constexpr int KT = FD / Frag<T>::KF, SE = 128 + 4, SB = 128 + Frag<T>::PT, KTE = 128 / Frag<T>::KF;
-  constexpr int NXV = FR * 128 / NT;  // staged state values per thread (max L x C)
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int KT = FD / Frag<T>::KF, SE = 16 + 4;
+  const int p = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int L = a.L, C = a.C, c16 = lane & 15, g4 = lane >> 4, LC = L * C;
   T* Xn = (T*)smem;
-  T* Xb = (T*)smem;  // the emb operand image reuses the LN image
   float2* st = (float2*)(smem + PL::IMG);
-  unsigned char* un = smem + PL::IMG + PL::ST;
-  float* Hs = (float*)un;
-  float* E = (float*)un;
-  float* Xs = (float*)(un + PL::E);
+  float* Hs = (float*)(smem + PL::IMG + PL::ST);
+  float* E = (float*)(smem + PL::IMG + PL::ST + PL::HS);
   const size_t row0 = (size_t)b * L;
+  const int c0 = 16 * p, cn = max(0, min(16, C - c0));       // the block's channels
+  const int e0 = c0 * L, ne = cn * L;                         // its elements, reference (C, L) order
+  const int h = p;                                            // STAMP uses (h, b)
 
   STAMP(0);
-  // state x of this clip (internal (L, C) order, contiguous) -> registers
-  float xv[NXV];
-  if (a.do_update || a.do_emb) {
-#pragma unroll
-    for (int i = 0; i < NXV; ++i) xv[i] = a.x[row0 * C + min(tid + i * NT, LC - 1)];
-  }
+  glds_rows(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
+  WGemm<T, 1, KT, 1> go(a.w_out, KT, 0);
+  go.tiles[0] = p;
+  go.load(0, lane);
+  const float bo = a.b_out[p * 16 + c16];
+  const float4 lg = *(const float4*)(a.ln_g + (tid & 63) * 4), lb = *(const float4*)(a.ln_b + (tid & 63) * 4);
+  // the thread's quad: elements e0 + 4 tid .. + 3 (issued now, consumed after the GEMM)
+  const bool upd = a.do_update && 4 * tid < ne;
   int k = 0;
   StepRec rec{};
+  float xq[4] = {0.f, 0.f, 0.f, 0.f}, zq[4] = {0.f, 0.f, 0.f, 0.f};
+  float mq[4] = {0.f, 0.f, 0.f, 0.f}, pq[4] = {0.f, 0.f, 0.f, 0.f}, tq[4] = {0.f, 0.f, 0.f, 0.f};
+  int cc0 = 0, l0 = 0;
+  const bool inp = a.inp_mask != nullptr;
+  const size_t plane = (size_t)a.n * LC;
   if (a.do_update) {
     k = *a.step_counter;
     rec = a.steps[k];
-  }
-  if (a.do_out) {
-    glds_rows<NT>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
-    WGemm<T, 1, KT> go(a.w_out, KT, 0);  // wave w: output tile w (d_pose <= 128)
-    go.tiles[0] = wave;
-    go.load(0, lane);
-    const float bo = a.b_out[wave * 16 + c16];
-    const float4 lg = *(const float4*)(a.ln_g + (tid & 63) * 4), lb = *(const float4*)(a.ln_b + (tid & 63) * 4);
-    __syncthreads();  // LDS-DMA rows and every operand above have landed
-    ln_stats(Hs, L, st);
-    bar_lds();
-    ln_apply<T, NT>(Hs, L, st, lg, lb, Xn);
-    bar_lds();
-    STAMP(1);
-    f32x4 acc[FRT][1];
-    go.run(acc, Xn, Frag<T>::SX, lane);
+    const int e = e0 + 4 * tid;  // tail threads (no valid element) only load clamped addresses
+    cc0 = e / L;
+    l0 = e - cc0 * L;
+    int cc = cc0, l = l0;
 #pragma unroll
-    for (int rt = 0; rt < FRT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) E[(rt * 16 + 4 * g4 + r) * SE + wave * 16 + c16] = acc[rt][0][r] + bo;
-  }
-  if (a.do_update || a.do_emb) {
-#pragma unroll
-    for (int i = 0; i < NXV; ++i) {
-      const int e = tid + i * NT;
-      if (e < LC) Xs[e] = xv[i];
+    for (int u = 0; u < 4; ++u) {
+      const size_t gi = (row0 + l) * C + min(cc, C - 1);
+      xq[u] = a.x[gi];
+      if (a.noise) zq[u] = a.noise[(size_t)k * plane + (size_t)b * LC + min(e + u, LC - 1)];
+      if (inp) {
+        mq[u] = a.inp_mask[row0 + l];
+        pq[u] = a.inp_pose[gi];
+        tq[u] = a.trans[l];
+      }
+      if (++l == L) { l = 0; ++cc; }
     }
   }
-  // emb_x + PE of the new state: fragments / PE / bias issued now, in flight across the update
-  WGemm<T, 2, KTE> ge(a.w_emb, KTE, 0);
-  float pe[2][FRT][4], be[2];
-  if (a.do_emb) {
-    ge.tiles[0] = 2 * wave;
-    ge.tiles[1] = 2 * wave + 1;
-    ge.load(0, lane);
+  __syncthreads();  // LDS-DMA rows and every operand above have landed
+  ln_stats(Hs, L, st);
+  bar_lds();
+  ln_apply<T>(Hs, L, st, lg, lb, Xn);
+  bar_lds();
+  STAMP(1);
+  {
+    f32x4 acc[1][1];
+    go.run(acc, Xn + wave * 16 * Frag<T>::SX, Frag<T>::SX, lane);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = (2 * wave + j) * 16 + c16;
-      be[j] = a.b_emb[col];
-#pragma unroll
-      for (int rt = 0; rt < FRT; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pe[j][rt][r] = a.pe[(size_t)min(rt * 16 + 4 * g4 + r, L - 1) * FD + col];
-    }
+    for (int r = 0; r < 4; ++r) E[(wave * 16 + 4 * g4 + r) * SE + c16] = acc[0][0][r] + bo;
   }
   bar_lds();
   STAMP(2);
-  if (a.do_update) {
-    // element e = cc * L + l of the reference (N, C, L) block; quads of 4 share one Philox call
-    const size_t plane = (size_t)a.n * LC;
-    const float* nz = a.noise ? a.noise + (size_t)k * plane + (size_t)b * LC : nullptr;
-    const bool inp = a.inp_mask != nullptr;
-    for (int q = tid; q * 4 < LC; q += NT) {
-      float z[4];
-      if (nz) {
+  if (upd) {
+    if (!a.noise)
+      philox_normal4(a.seed, (uint32_t)(a.clip_offset + b), (uint32_t)rec.i, TAG_STEP, (uint32_t)((e0 >> 2) + tid), zq);
+    int cc = cc0, l = l0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) z[u] = nz[min(4 * q + u, LC - 1)];
-      } else {
-        philox_normal4(a.seed, (uint32_t)(a.clip_offset + b), (uint32_t)rec.i, TAG_STEP, (uint32_t)q, z);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = 4 * q + u;
-        if (e >= LC) break;
-        const int cc = e / L, l = e - cc * L;
-        const int gi = l * C + cc;
-        const float x = Xs[gi], ev = E[l * SE + cc];
-        const UpdOut o = upd_math(rec, a.alg, x, ev, false, 0.f, inp, inp ? a.inp_mask[row0 + l] : 0.f,
-                                  inp ? a.inp_pose[row0 * C + gi] : 0.f, inp ? a.trans[l] : 0.f, z[u]);
-        a.x[row0 * C + gi] = o.xn;
-        Xs[gi] = o.xn;
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + 4 * tid + u;
+      if (e < e0 + ne) {
+        const float ev = E[l * SE + (cc - c0)];
+        const UpdOut o = upd_math(rec, a.alg, xq[u], ev, false, 0.f, inp, mq[u], pq[u], tq[u], zq[u]);
+        a.x[(row0 + l) * C + cc] = o.xn;
         if (a.extras) {
           const size_t ncl = (size_t)b * LC + e;
           a.extras[0 * plane + ncl] = o.mean;
@@ -482,37 +489,15 @@ __global__ void __launch_bounds__(KE_THREADS) ke_kernel(FinalArgs a) {
           a.extras[5 * plane + ncl] = o.raw;
         }
       }
+      if (++l == L) { l = 0; ++cc; }
     }
-  } else if (a.do_out) {
-    for (int e = tid; e < LC; e += NT) {
-      const int cc = e / L, l = e - cc * L;
-      a.eps_out[(size_t)b * LC + e] = E[l * SE + cc];
+  } else if (!a.do_update && a.do_out) {
+    for (int i = tid; i < ne; i += NTHREADS) {
+      const int e = e0 + i, cc = e / L, l = e - cc * L;
+      a.eps_out[(size_t)b * LC + e] = E[l * SE + (cc - c0)];
     }
   }
-  if (!a.do_emb) {
-    STAMP_END(3);
-    return;
-  }
-  bar_lds();
-  STAMP(3);
-  for (int idx = tid; idx < FR * 128; idx += NT) {
-    const int l = idx >> 7, cc = idx & 127;
-    Xb[l * SB + cc] = from_f32<T>(l < L && cc < C ? Xs[l * C + cc] : 0.f);
-  }
-  bar_lds();
-  f32x4 acc[FRT][2];
-  ge.run(acc, Xb, SB, lane);
-  const OutRows out(a.h + row0 * FD, (uint32_t)(sizeof(float) * L * FD));
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = (2 * wave + j) * 16 + c16;
-#pragma unroll
-    for (int rt = 0; rt < FRT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        out.put<float>((uint32_t)((rt * 16 + 4 * g4 + r) * FD + col), acc[rt][j][r] + be[j] + pe[j][rt][r]);
-  }
-  STAMP_END(4);
+  STAMP_END(3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -573,8 +558,8 @@ hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStre
 
 hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s) {
   fused_attrs();
-  if (dtype == 0) hipLaunchKernelGGL(ke_kernel<float>, dim3(a.n), dim3(KE_THREADS), Plan<float>::KE, s, a);
-  else hipLaunchKernelGGL(ke_kernel<bf16_t>, dim3(a.n), dim3(KE_THREADS), Plan<bf16_t>::KE, s, a);
+  if (dtype == 0) hipLaunchKernelGGL(ke_kernel<float>, dim3(8, a.n), dim3(NTHREADS), Plan<float>::KE, s, a);
+  else hipLaunchKernelGGL(ke_kernel<bf16_t>, dim3(8, a.n), dim3(NTHREADS), Plan<bf16_t>::KE, s, a);
   return hipGetLastError();
 }
 

@@ -435,10 +435,12 @@ template <typename T> struct Plan {
   // KD: [hid pass image 64 x (KP + PT)] ; the cross-wave reduction reuses it
   static constexpr int KP = sizeof(T) == 2 ? 4 * FD : 2 * FD;
   static constexpr size_t KD = al16(sizeof(T) * FR * (KP + Frag<T>::PT));
-  // KE: [Xn / Xb][stats][Hs | E (64 x 132 f32) + Xs (64 x 128 f32)]
-  static constexpr size_t E = al16(sizeof(float) * FR * (128 + 4));
-  static constexpr size_t XS = al16(sizeof(float) * FR * 128);
-  static constexpr size_t KE = IMG + ST + std::max(HS, E + XS);
+  // KE: [Xn][stats][Hs][E (64 x 20 f32: the block's 16 channels)]
+  static constexpr size_t E = al16(sizeof(float) * FR * (16 + 4));
+  static constexpr size_t KE = IMG + ST + HS + E;
+  // KA of layer 0 also stages the emb operand (64 x (128 + PT), aliasing the LN image)
+  static constexpr size_t XB = al16(sizeof(T) * FR * (128 + Frag<T>::PT));
+  static_assert(XB <= IMG, "emb operand must fit the LN image");
 };
 static_assert(Plan<float>::KA <= 160 * 1024 && Plan<float>::KB <= 160 * 1024 && Plan<float>::KE <= 160 * 1024 &&
                   Plan<float>::KD <= 160 * 1024,

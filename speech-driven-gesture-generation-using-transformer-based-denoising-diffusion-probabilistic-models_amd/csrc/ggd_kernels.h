@@ -115,9 +115,13 @@ struct FusedArgs {
   void *o_sa, *o_ca, *hid;
   const int* t_clip; const StepRec* steps; int* step_counter; int bump_counter;
   float scale;
+  // KA of layer 0 with x_emb set: h = emb_x(x) + PE is computed in the kernel (x_emb = state
+  // (N, L, C), packed emb_x weights, PE table) and written to h_out for KB's residual
+  const float* x_emb; const void* w_emb; const float* b_emb; const float* pe; int C;
   unsigned long long* stamps;  // diagnostics: block (0,0) writes s_memtime at phase boundaries
 };
 
+// KE: grid (8 channel blocks, clips); block p owns pose channels [16p, 16p + 16)
 struct FinalArgs {
   int n, L, C, alg;
   float* h; const float *ln_g, *ln_b;
@@ -130,7 +134,7 @@ struct FinalArgs {
   const float* noise; uint64_t seed; int64_t clip_offset;
   const float *inp_pose, *inp_mask, *trans;
   float* extras;
-  int do_out, do_update, do_emb;
+  int do_out, do_update;
   unsigned long long* stamps;  // diagnostics
 };
 
