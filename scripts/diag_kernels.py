@@ -82,3 +82,9 @@ print(f"bulk 64 KiB x 1 WG    : {diag(5, [3, 0, 1, 64]):7.2f} us")
 print(f"bulk 64 KiB x 256 WG  : {diag(5, [3, 0, 256, 64]):7.2f} us")
 print(f"bulk 16 KiB x 1 WG    : {diag(5, [4, 0, 1, 64]):7.2f} us")
 print(f"bulk 16 KiB x 256 WG  : {diag(5, [4, 0, 256, 64]):7.2f} us")
+print("--- clip-group hand-off (8 workgroups per group, sc1 stores / loads, atomic arrival) ---")
+for kb in (4, 40):
+    for blocks in (8, 256):
+        r1 = diag(5, [5, 1 | (kb << 16), blocks, 64], 3)
+        r100 = diag(5, [5, 101 | (kb << 16), blocks, 64], 3)
+        print(f"{blocks:4d} WGs, {kb:3d} KiB per WG: {(r100 - r1) / 100:7.3f} us per round (launch+1 round {r1:7.2f} us)")

@@ -43,6 +43,43 @@ __global__ void __launch_bounds__(256) mb_bulk_kernel(const uint4* src, size_t b
   if (acc.x == 0x12345678u) out[blockIdx.x] = acc;
 }
 
+// Clip-group hand-off cost: groups of 8 workgroups; each round every workgroup writes `kb`
+// KiB with sc1 (write-through) 16-byte stores, arrives on its group's counter (agent atomic,
+// after every wave's vmcnt(0) + a workgroup barrier), polls it with sc1 loads, then reads the
+// next member's slice with sc1 loads -- the protocol a persistent multi-workgroup-per-clip
+// kernel would use between decoder phases.  buf layout: [counters 4 KiB][slices].
+__global__ void __launch_bounds__(256) mb_groupsync_kernel(unsigned char* buf, int rounds, int kb) {
+  unsigned* ctr = (unsigned*)buf;
+  const int g = blockIdx.x >> 3, m = blockIdx.x & 7;
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(buf + 4096, (short)0, 0x7fffffff, 0x00020000);
+  const int slice = kb * 1024, per = slice / (256 * 16);
+  u32x4 acc = {0u, 0u, 0u, 0u};
+  for (int r = 0; r < rounds; ++r) {
+    for (int i = 0; i < per; ++i) {
+      const u32x4 v = {(unsigned)r, (unsigned)i, (unsigned)m, acc.x};
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, (threadIdx.x + i * 256) * 16, blockIdx.x * slice, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(ctr + g * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = 8u * (unsigned)(r + 1);
+      for (int spin = 0; spin < (1 << 24); ++spin) {
+        if (__hip_atomic_load(ctr + g * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    const int src = (g << 3) | ((m + 1) & 7);
+    for (int i = 0; i < per; ++i) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (threadIdx.x + i * 256) * 16, src * slice, 16);
+      acc += v;
+    }
+  }
+  if (acc.x == 0x12345678u) ctr[4095 / 4] = acc.y;
+}
+
 hipError_t launch_mb(int mode, void* buf, size_t buf_bytes, int arg, int blocks, hipStream_t s) {
   switch (mode) {
     case 0: hipLaunchKernelGGL(mb_empty_kernel, dim3(blocks), dim3(256), 0, s, (int*)buf); break;
@@ -52,6 +89,12 @@ hipError_t launch_mb(int mode, void* buf, size_t buf_bytes, int arg, int blocks,
                                (size_t)16 * 256, (uint4*)buf); break;  // 64 KiB per block
     case 4: hipLaunchKernelGGL(mb_bulk_kernel<4>, dim3(blocks), dim3(256), 0, s, (const uint4*)buf,
                                (size_t)4 * 256, (uint4*)buf); break;   // 16 KiB per block
+    case 5: {  // arg = rounds (low 16 bits) | KiB per workgroup << 16; counters must be zero
+      (void)hipMemsetAsync(buf, 0, 4096, s);
+      hipLaunchKernelGGL(mb_groupsync_kernel, dim3(blocks), dim3(256), 0, s, (unsigned char*)buf, arg & 0xffff,
+                         arg >> 16);
+      break;
+    }
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -32,21 +32,30 @@
 
 namespace ggd {
 
-// Hs[i][n] += A[i] . W[n] + bias[n] for all 64 rows; wave w owns columns [64w, 64w + 64)
-template <typename T>
-__device__ __forceinline__ void outproj_epilogue(float* Hs, const f32x4 (&acc)[FRT][4], const float (&bias)[4], int lane,
-                                                 int wave) {
+// Hs[i][n] += A[i] . W[n] + bias[n] for all 64 rows; wave w owns columns [64w, 64w + 64).
+// The accumulators start from Hs + bias (one batch of LDS reads issued before the MFMAs), so
+// the epilogue is a plain store instead of a dependent read-modify-write per element.
+template <typename T, int KT>
+__device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGemm<T, 4, KT>& g,
+                                              const float (&bias)[4], int lane, int wave) {
   const int c16 = lane & 15, g4 = lane >> 4;
+  f32x4 acc[FRT][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = (4 * wave + j) * 16 + c16;
 #pragma unroll
     for (int rt = 0; rt < FRT; ++rt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float* p = Hs + (rt * 16 + 4 * g4 + r) * SH + col;
-        *p = *p + (acc[rt][j][r] + bias[j]);
-      }
+      for (int r = 0; r < 4; ++r) acc[rt][j][r] = Hs[(rt * 16 + 4 * g4 + r) * SH + col] + bias[j];
+  }
+  g.run(acc, A, SA, lane, 4, false);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = (4 * wave + j) * 16 + c16;
+#pragma unroll
+    for (int rt = 0; rt < FRT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Hs[(rt * 16 + 4 * g4 + r) * SH + col] = acc[rt][j][r];
   }
 }
 
@@ -129,9 +138,7 @@ __global__ void __launch_bounds__(NTHREADS) ka_kernel(FusedArgs a) {
       Xb[l * SB + c] = from_f32<T>(c < a.C ? xv[i] : 0.f);
     }
     bar_lds();
-    f32x4 acc[FRT][4];
-    ge.run(acc, Xb, SB, lane);
-    outproj_epilogue<T>(Hs, acc, be, lane, wave);
+    residual_gemm<T, KTE>(Hs, Xb, SB, ge, be, lane, wave);
     bar_lds();
     store_rows<8>(a.h + (size_t)b * L * FD, Hs, L, h);  // the residual rows KB reads
   }
@@ -217,13 +224,11 @@ __global__ void __launch_bounds__(NTHREADS) kb_kernel(FusedArgs a) {
     const float* src = r == 0 ? w.kv_step + (size_t)t * 2 * FD : w.kv_mem + ((size_t)b * a.Ts + (r - 1)) * 2 * FD;
     return *(const float4*)(src + half * FD + h * FDK + q * 4);
   };
-  f32x4 acc_o[FRT][4];
-  go.run(acc_o, Ax, Frag<T>::SX, lane);
-  // issued after the out-projection MFMAs: t comes from a two-load dependent chain, which
-  // must not stall them; the loads complete under the epilogue and LN2.  Named registers,
-  // not an array: an array live across the LN is demoted to scratch.
+  residual_gemm<T, KT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
+  // issued after the out-projection: t comes from a two-load dependent chain, which must not
+  // stall it; the loads complete under LN2.  Named registers, not an array: an array live
+  // across the LN is demoted to scratch.
   const float4 kv0 = kv_load(0), kv1 = kv_load(1), kv2 = kv_load(2), kv3 = kv_load(3);
-  outproj_epilogue<T>(Hs, acc_o, bo, lane, wave);
   bar_lds();
   STAMP(2);
   store_rows<8>(a.h_out + row0 * FD, Hs, L, h);
@@ -303,11 +308,7 @@ __global__ void __launch_bounds__(NTHREADS) kc_kernel(FusedArgs a) {
   gf.tiles[1] = 8 * c + 2 * wave + 1;
   gf.load(0, lane);
   const float bf0 = w.ff1_b[(8 * c + 2 * wave) * 16 + c16], bf1 = w.ff1_b[(8 * c + 2 * wave + 1) * 16 + c16];
-  {
-    f32x4 acc[FRT][4];
-    go.run(acc, Ax, Frag<T>::SX, lane);
-    outproj_epilogue<T>(Hs, acc, bo, lane, wave);
-  }
+  residual_gemm<T, KT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
   bar_lds();
   STAMP(2);
   store_rows<8>(a.h_out + row0 * FD, Hs, L, c);

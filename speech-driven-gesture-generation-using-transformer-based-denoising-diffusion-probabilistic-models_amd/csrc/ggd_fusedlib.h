@@ -172,11 +172,15 @@ struct WGemm {
   // group 0 must have been loaded; tiles j >= nj_on are skipped (wave-uniform).  bf16: the A
   // fragments of k step k + 1 are read from LDS before the MFMAs of step k issue, so the LDS
   // latency overlaps the matrix work (one wave per SIMD hides nothing on its own).
-  __device__ __forceinline__ void run(f32x4 (&acc)[RT][NJ], const T* A, int SA, int lane, int nj_on = NJ) {
+  // zero = false: accumulate onto the caller's acc (e.g. residual + bias preloaded)
+  __device__ __forceinline__ void run(f32x4 (&acc)[RT][NJ], const T* A, int SA, int lane, int nj_on = NJ,
+                                      bool zero = true) {
+    if (zero) {
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     if constexpr (sizeof(T) == 2) {
       const int r16 = lane & 15, gq = lane >> 4;
       const T* a0 = A + r16 * SA + gq * 8;
