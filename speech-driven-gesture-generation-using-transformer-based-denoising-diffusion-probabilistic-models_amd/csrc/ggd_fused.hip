@@ -32,26 +32,28 @@
 
 namespace ggd {
 
-// Hs[i][n] += A[i] . W[n] + bias[n] for all 64 rows; wave w owns columns [64w, 64w + 64).
-// The accumulators start from Hs + bias (one batch of LDS reads issued before the MFMAs), so
-// the epilogue is a plain store instead of a dependent read-modify-write per element.
-template <typename T, int KT>
-__device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGemm<T, 4, KT>& g,
-                                              const float (&bias)[4], int lane, int wave) {
+constexpr int FT = 512;  // threads of the fused kernels: 8 waves, two per SIMD
+
+// Hs[i][n] += A[i] . W[n] + bias[n] for all 64 rows; wave w owns the NJ column tiles
+// NJ w .. NJ w + NJ - 1.  The accumulators start from Hs + bias (one batch of LDS reads issued
+// before the MFMAs), so the epilogue is a plain store, not a dependent read-modify-write.
+template <typename T, int KT, int NJ>
+__device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGemm<T, NJ, KT>& g,
+                                              const float (&bias)[NJ], int lane, int wave) {
   const int c16 = lane & 15, g4 = lane >> 4;
-  f32x4 acc[FRT][4];
+  f32x4 acc[FRT][NJ];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = (4 * wave + j) * 16 + c16;
+  for (int j = 0; j < NJ; ++j) {
+    const int col = (NJ * wave + j) * 16 + c16;
 #pragma unroll
     for (int rt = 0; rt < FRT; ++rt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[rt][j][r] = Hs[(rt * 16 + 4 * g4 + r) * SH + col] + bias[j];
   }
-  g.run(acc, A, SA, lane, 4, false);
+  g.run(acc, A, SA, lane, NJ, false);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = (4 * wave + j) * 16 + c16;
+  for (int j = 0; j < NJ; ++j) {
+    const int col = (NJ * wave + j) * 16 + c16;
 #pragma unroll
     for (int rt = 0; rt < FRT; ++rt)
 #pragma unroll
@@ -59,32 +61,20 @@ __device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGe
   }
 }
 
-// rows [0, L) of Hs -> global rows, shared by the NP workgroups of a clip: workgroup `part`
-// writes rows r with r % NP == part (every row once; bounded 16-byte stores, no branch)
-template <int NP = 8>
+// rows [0, L) of Hs -> global rows, shared by the 8 workgroups of a clip: workgroup `part`
+// writes rows r with r % 8 == part (every row once; bounded 16-byte stores, no branch)
 __device__ __forceinline__ void store_rows(float* dst, const float* Hs, int L, int part) {
-  constexpr int RP = FR / NP;  // rows per part
   const OutRows out(dst, (uint32_t)(sizeof(float) * L * FD));
-  float4 v[RP * 64 / NTHREADS > 0 ? RP * 64 / NTHREADS : 1];
-  constexpr int NV = RP * 64 / NTHREADS;
-  static_assert(NV >= 1, "at least one 16-byte piece per thread");
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int idx = threadIdx.x + i * NTHREADS, r = (idx >> 6) * NP + part, c = (idx & 63) * 4;
-    v[i] = *(const float4*)(Hs + min(r, L - 1) * SH + c);
-  }
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int idx = threadIdx.x + i * NTHREADS, r = (idx >> 6) * NP + part, c = (idx & 63) * 4;
-    out.put4((uint32_t)(r * FD + c), v[i]);
-  }
+  static_assert(FR / 8 * 64 == FT, "one 16-byte piece per thread");
+  const int idx = threadIdx.x, r = (idx >> 6) * 8 + part, c = (idx & 63) * 4;
+  out.put4((uint32_t)(r * FD + c), *(const float4*)(Hs + min(r, L - 1) * SH + c));
 }
 
 // ------------------------------------------------------------------------------------------
-// KA: LN1 + QKV(head) + conv + self-attention          grid (heads, clips)
+// KA: [emb_x + PE (layer 0)] + LN1 + QKV(head) + conv + self-attention      grid (heads, clips)
 // ------------------------------------------------------------------------------------------
 template <typename T>
-__global__ void __launch_bounds__(NTHREADS) ka_kernel(FusedArgs a) {
+__global__ void __launch_bounds__(FT) ka_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF, SY = 96 + 4;
@@ -101,30 +91,29 @@ __global__ void __launch_bounds__(NTHREADS) ka_kernel(FusedArgs a) {
   STAMP(0);
   if (a.bump_counter && h == 0 && b == 0 && tid == 0) atomicAdd(a.step_counter, 1);
   const bool emb = a.x_emb != nullptr;  // layer 0: h = emb_x(x) + PE computed here
-  glds_rows(Hs, sizeof(float) * SH, emb ? a.pe : a.h + (size_t)b * L * FD, sizeof(float) * FD, L, 1);
-  constexpr int KTE = 128 / Frag<T>::KF, SB = 128 + Frag<T>::PT, NXV = FR * 128 / NTHREADS;
-  WGemm<T, 4, KTE> ge(a.w_emb, KTE, 0);
-  float be[4], xv[NXV];
+  glds_rows<FT>(Hs, sizeof(float) * SH, emb ? a.pe : a.h + (size_t)b * L * FD, sizeof(float) * FD, L, 1);
+  constexpr int KTE = 128 / Frag<T>::KF, SB = 128 + Frag<T>::PT, NXV = FR * 128 / FT;
+  WGemm<T, 2, KTE> ge(a.w_emb, KTE, 0);
+  float be[2], xv[NXV];
   if (emb) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) ge.tiles[j] = 4 * wave + j;
+    ge.tiles[0] = 2 * wave;
+    ge.tiles[1] = 2 * wave + 1;
     ge.load(0, lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) be[j] = a.b_emb[(4 * wave + j) * 16 + c16];
+    be[0] = a.b_emb[(2 * wave) * 16 + c16];
+    be[1] = a.b_emb[(2 * wave + 1) * 16 + c16];
     const int C = a.C;
 #pragma unroll
     for (int i = 0; i < NXV; ++i) {
-      const int idx = tid + i * NTHREADS, l = idx >> 7, c = idx & 127;
+      const int idx = tid + i * FT, l = idx >> 7, c = idx & 127;
       xv[i] = a.x_emb[((size_t)b * L + min(l, L - 1)) * C + min(c, C - 1)];
     }
   }
-  // QKV of head h: packed as 6 tiles [q0 q1 k0 k1 v0 v1]; wave w owns tiles w and w + 4 (< 6)
-  WGemm<T, 2, KT> gm(w.qkv, KT, 0);
-  gm.tiles[0] = h * 6 + wave;
-  gm.tiles[1] = h * 6 + min(wave + 4, 5);
+  // QKV of head h: packed as 6 tiles [q0 q1 k0 k1 v0 v1]; waves 0-5 own one tile each
+  const int nq = wave < 6 ? 1 : 0;
+  WGemm<T, 1, KT> gm(w.qkv, KT, 0);
+  gm.tiles[0] = h * 6 + min(wave, 5);
   gm.load(0, lane);
-  const float bias0 = w.qkv_b[h * 96 + wave * 16 + c16];
-  const float bias1 = w.qkv_b[h * 96 + min(wave + 4, 5) * 16 + c16];
+  const float bias = w.qkv_b[h * 96 + min(wave, 5) * 16 + c16];
   const float4 lg = *(const float4*)(w.ln1_g + (tid & 63) * 4), lb = *(const float4*)(w.ln1_b + (tid & 63) * 4);
   const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
               cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
@@ -134,38 +123,37 @@ __global__ void __launch_bounds__(NTHREADS) ka_kernel(FusedArgs a) {
     T* Xb = Xn;
 #pragma unroll
     for (int i = 0; i < NXV; ++i) {
-      const int idx = tid + i * NTHREADS, l = idx >> 7, c = idx & 127;
+      const int idx = tid + i * FT, l = idx >> 7, c = idx & 127;
       Xb[l * SB + c] = from_f32<T>(c < a.C ? xv[i] : 0.f);
     }
     bar_lds();
-    residual_gemm<T, KTE>(Hs, Xb, SB, ge, be, lane, wave);
+    residual_gemm<T, KTE, 2>(Hs, Xb, SB, ge, be, lane, wave);
     bar_lds();
-    store_rows<8>(a.h + (size_t)b * L * FD, Hs, L, h);  // the residual rows KB reads
+    store_rows(a.h + (size_t)b * L * FD, Hs, L, h);  // the residual rows KB reads
   }
-  ln_stats(Hs, L, st);
+  ln_stats<FR, 8>(Hs, L, st);
   bar_lds();
-  ln_apply<T>(Hs, L, st, lg, lb, Xn);
+  ln_apply<T, FT>(Hs, L, st, lg, lb, Xn);
   bar_lds();
   STAMP(1);
   // Hs is dead from here: Y and the attention images overlay it
-  f32x4 acc[FRT][2];
-  gm.run(acc, Xn, Frag<T>::SX, lane, wave + 4 < 6 ? 2 : 1);
+  {
+    f32x4 acc[FRT][1];
+    gm.run(acc, Xn, Frag<T>::SX, lane, nq);
+    if (nq) {
+      const int col = wave * 16 + c16;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    if (j == 1 && wave + 4 >= 6) continue;
-    const int col = (j == 0 ? wave : wave + 4) * 16 + c16;
-    const float bias = j == 0 ? bias0 : bias1;
+      for (int rt = 0; rt < FRT; ++rt)
 #pragma unroll
-    for (int rt = 0; rt < FRT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Y[(rt * 16 + 4 * g4 + r) * SY + col] = acc[rt][j][r] + bias;
+        for (int r = 0; r < 4; ++r) Y[(rt * 16 + 4 * g4 + r) * SY + col] = acc[rt][0][r] + bias;
+    }
   }
   bar_lds();
   STAMP(2);
   using AT = FAtt<T>;
-  conv_rows<T, false>((T*)(att + AT::OQ), AT::SQ, Y, SY, L, cq);
-  conv_rows<T, false>((T*)(att + AT::OK), AT::SQ, Y + 32, SY, L, ck);
-  conv_rows<T, true>((T*)(att + AT::OV), AT::SV, Y + 64, SY, L, cv);
+  conv_rows<T, false, FR, FT>((T*)(att + AT::OQ), AT::SQ, Y, SY, L, cq);
+  conv_rows<T, false, FLK, FT>((T*)(att + AT::OK), AT::SQ, Y + 32, SY, L, ck);
+  conv_rows<T, true, FLK, FT>((T*)(att + AT::OV), AT::SV, Y + 64, SY, L, cv);
   bar_lds();
   STAMP(3);
   fattn_any<T>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
@@ -176,7 +164,7 @@ __global__ void __launch_bounds__(NTHREADS) ka_kernel(FusedArgs a) {
 // KB: SA out-proj + residual + LN2 + cross-attn Q(head) + conv + cross-attention  (heads, clips)
 // ------------------------------------------------------------------------------------------
 template <typename T>
-__global__ void __launch_bounds__(NTHREADS) kb_kernel(FusedArgs a) {
+__global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
   using AT = FAtt<T>;
@@ -195,16 +183,16 @@ __global__ void __launch_bounds__(NTHREADS) kb_kernel(FusedArgs a) {
 
   STAMP(0);
   const int t = a.t_clip ? a.t_clip[b] : a.steps[*a.step_counter].t_orig;
-  glds_rows(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
-  ImgStage<T> so;
+  glds_rows<FT>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
+  ImgStage<T, FT> so;
   so.load(Ax, (const T*)a.o_sa + row0 * FD, L);
-  WGemm<T, 4, KT> go(w.o_sa, KT, 0);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) go.tiles[j] = 4 * wave + j;
+  WGemm<T, 2, KT> go(w.o_sa, KT, 0);
+  go.tiles[0] = 2 * wave;
+  go.tiles[1] = 2 * wave + 1;
   go.load(0, lane);
-  float bo[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) bo[j] = w.o_sa_b[(4 * wave + j) * 16 + c16];
+  float bo[2];
+  bo[0] = w.o_sa_b[(2 * wave) * 16 + c16];
+  bo[1] = w.o_sa_b[(2 * wave + 1) * 16 + c16];
   const float4 lg = *(const float4*)(w.ln2_g + (tid & 63) * 4), lb = *(const float4*)(w.ln2_b + (tid & 63) * 4);
   so.store(Ax, L);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
@@ -212,60 +200,56 @@ __global__ void __launch_bounds__(NTHREADS) kb_kernel(FusedArgs a) {
   // cross-attn query of head h: waves 0, 1 own tiles 2h, 2h + 1 of the natural packing
   WGemm<T, 1, KT> gq(w.q_ca, KT, 0);
   gq.tiles[0] = 2 * h + (wave & 1);
-  gq.load(0, lane);
+  if (wave < 2) gq.load(0, lane);
   const float bq = w.q_ca_b[h * FDK + (wave & 1) * 16 + c16];
   const ConvW cq = conv_w(w.ca_qw, w.ca_qb, tid & 31), ck = conv_w(w.ca_kw, w.ca_kb, tid & 31),
               cv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
   // memory K / V of head h (pre-conv): row 0 = the step token of this clip's t, rows 1.. the
   // cached speech rows; item v = (row, half, 16-byte piece) with row clamped into [0, Lk)
-  static_assert(2 * FLK * 8 == 4 * NTHREADS, "four 16-byte memory pieces per thread");
+  static_assert(2 * FLK * 8 == 2 * FT, "two 16-byte memory pieces per thread");
   auto kv_load = [&](int i) -> float4 {
-    const int v = tid + i * NTHREADS, r = min(v >> 4, Lk - 1), half = (v >> 3) & 1, q = v & 7;
+    const int v = tid + i * FT, r = min(v >> 4, Lk - 1), half = (v >> 3) & 1, q = v & 7;
     const float* src = r == 0 ? w.kv_step + (size_t)t * 2 * FD : w.kv_mem + ((size_t)b * a.Ts + (r - 1)) * 2 * FD;
     return *(const float4*)(src + half * FD + h * FDK + q * 4);
   };
-  residual_gemm<T, KT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
+  residual_gemm<T, KT, 2>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
   // issued after the out-projection: t comes from a two-load dependent chain, which must not
   // stall it; the loads complete under LN2.  Named registers, not an array: an array live
   // across the LN is demoted to scratch.
-  const float4 kv0 = kv_load(0), kv1 = kv_load(1), kv2 = kv_load(2), kv3 = kv_load(3);
+  const float4 kv0 = kv_load(0), kv1 = kv_load(1);
   bar_lds();
   STAMP(2);
-  store_rows<8>(a.h_out + row0 * FD, Hs, L, h);
-  ln_stats(Hs, L, st);
+  store_rows(a.h_out + row0 * FD, Hs, L, h);
+  ln_stats<FR, 8>(Hs, L, st);
   bar_lds();
-  ln_apply<T>(Hs, L, st, lg, lb, Ax);
+  ln_apply<T, FT>(Hs, L, st, lg, lb, Ax);
   bar_lds();
   STAMP(3);
   // Hs is dead: Yq, raw and the attention images overlay it
   auto kv_store = [&](int i, float4 val) {
-    const int v = tid + i * NTHREADS, r = v >> 4, half = (v >> 3) & 1, q = v & 7;
+    const int v = tid + i * FT, r = v >> 4, half = (v >> 3) & 1, q = v & 7;
     if (r < Lk) *(float4*)(raw + half * (FLK + 2) * FDK + (r + 1) * FDK + q * 4) = val;
   };
   kv_store(0, kv0);
   kv_store(1, kv1);
-  kv_store(2, kv2);
-  kv_store(3, kv3);
   if (tid < 2 * 2 * FDK) {  // zero halo rows 0 and Lk + 1 of both halves
     const int half = tid >> 6, e = tid & 63, r = e < FDK ? 0 : Lk + 1;
     raw[half * (FLK + 2) * FDK + r * FDK + (e & 31)] = 0.f;
   }
-  {
+  if (wave < 2) {
     f32x4 acc[FRT][1];
-    gq.run(acc, Ax, Frag<T>::SX, lane, wave < 2 ? 1 : 0);
-    if (wave < 2) {
-      const int col = (wave & 1) * 16 + c16;
+    gq.run(acc, Ax, Frag<T>::SX, lane);
+    const int col = wave * 16 + c16;
 #pragma unroll
-      for (int rt = 0; rt < FRT; ++rt)
+    for (int rt = 0; rt < FRT; ++rt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Yq[(rt * 16 + 4 * g4 + r) * SYQ + col] = acc[rt][0][r] + bq;
-    }
+      for (int r = 0; r < 4; ++r) Yq[(rt * 16 + 4 * g4 + r) * SYQ + col] = acc[rt][0][r] + bq;
   }
   bar_lds();
   STAMP(4);
-  conv_rows<T, false>((T*)(att + AT::OQ), AT::SQ, Yq, SYQ, L, cq);
-  conv_rows<T, false>((T*)(att + AT::OK), AT::SQ, raw + FDK, FDK, Lk, ck);
-  conv_rows<T, true>((T*)(att + AT::OV), AT::SV, raw + (FLK + 2) * FDK + FDK, FDK, Lk, cv);
+  conv_rows<T, false, FR, FT>((T*)(att + AT::OQ), AT::SQ, Yq, SYQ, L, cq);
+  conv_rows<T, false, FLK, FT>((T*)(att + AT::OK), AT::SQ, raw + FDK, FDK, Lk, ck);
+  conv_rows<T, true, FLK, FT>((T*)(att + AT::OV), AT::SV, raw + (FLK + 2) * FDK + FDK, FDK, Lk, cv);
   bar_lds();
   STAMP(5);
   fattn_any<T>(att, L, Lk, a.scale, (T*)a.o_ca + row0 * FD + h * FDK, FD);
@@ -276,7 +260,7 @@ __global__ void __launch_bounds__(NTHREADS) kb_kernel(FusedArgs a) {
 // KC: CA out-proj + residual + LN3 + FFN-up chunk (128 hidden) + ReLU^2   grid (8 chunks, clips)
 // ------------------------------------------------------------------------------------------
 template <typename T>
-__global__ void __launch_bounds__(NTHREADS) kc_kernel(FusedArgs a) {
+__global__ void __launch_bounds__(FT) kc_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF;
@@ -287,70 +271,68 @@ __global__ void __launch_bounds__(NTHREADS) kc_kernel(FusedArgs a) {
   float* Hs = (float*)(smem + PL::IMG + PL::ST);
   const FusedLayer& w = a.w;
   const size_t row0 = (size_t)b * L;
+  const int h = c;  // STAMP uses (h, b)
 
   STAMP(0);
-  glds_rows(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
-  ImgStage<T> so;
+  glds_rows<FT>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
+  ImgStage<T, FT> so;
   so.load(Ax, (const T*)a.o_ca + row0 * FD, L);
-  WGemm<T, 4, KT> go(w.o_ca, KT, 0);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) go.tiles[j] = 4 * wave + j;
+  WGemm<T, 2, KT> go(w.o_ca, KT, 0);
+  go.tiles[0] = 2 * wave;
+  go.tiles[1] = 2 * wave + 1;
   go.load(0, lane);
-  float bo[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) bo[j] = w.o_ca_b[(4 * wave + j) * 16 + c16];
+  float bo[2];
+  bo[0] = w.o_ca_b[(2 * wave) * 16 + c16];
+  bo[1] = w.o_ca_b[(2 * wave + 1) * 16 + c16];
   const float4 lg = *(const float4*)(w.ln3_g + (tid & 63) * 4), lb = *(const float4*)(w.ln3_b + (tid & 63) * 4);
   so.store(Ax, L);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   STAMP(1);
-  WGemm<T, 2, KT> gf(w.ff1, KT, 0);  // prefetch: in flight across the out-projection
-  gf.tiles[0] = 8 * c + 2 * wave;
-  gf.tiles[1] = 8 * c + 2 * wave + 1;
+  WGemm<T, 1, KT> gf(w.ff1, KT, 0);  // prefetch: in flight across the out-projection
+  gf.tiles[0] = 8 * c + wave;
   gf.load(0, lane);
-  const float bf0 = w.ff1_b[(8 * c + 2 * wave) * 16 + c16], bf1 = w.ff1_b[(8 * c + 2 * wave + 1) * 16 + c16];
-  residual_gemm<T, KT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
+  const float bf = w.ff1_b[(8 * c + wave) * 16 + c16];
+  residual_gemm<T, KT, 2>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
   bar_lds();
   STAMP(2);
-  store_rows<8>(a.h_out + row0 * FD, Hs, L, c);
-  ln_stats(Hs, L, st);
+  store_rows(a.h_out + row0 * FD, Hs, L, c);
+  ln_stats<FR, 8>(Hs, L, st);
   bar_lds();
-  ln_apply<T>(Hs, L, st, lg, lb, Ax);
+  ln_apply<T, FT>(Hs, L, st, lg, lb, Ax);
   bar_lds();
   STAMP(3);
-  f32x4 acc[FRT][2];
+  f32x4 acc[FRT][1];
   gf.run(acc, Ax, Frag<T>::SX, lane);
   const OutRows out((T*)a.hid + row0 * (4 * FD), (uint32_t)(sizeof(T) * L * 4 * FD));
+  const int col = (8 * c + wave) * 16 + c16;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = (8 * c + 2 * wave + j) * 16 + c16;
-    const float bb = j == 0 ? bf0 : bf1;
+  for (int rt = 0; rt < FRT; ++rt)
 #pragma unroll
-    for (int rt = 0; rt < FRT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = fmaxf(acc[rt][j][r] + bb, 0.f);
-        out.put<T>((uint32_t)((rt * 16 + 4 * g4 + r) * (4 * FD) + col), v * v);
-      }
-  }
+    for (int r = 0; r < 4; ++r) {
+      const float v = fmaxf(acc[rt][0][r] + bf, 0.f);
+      out.put<T>((uint32_t)((rt * 16 + 4 * g4 + r) * (4 * FD) + col), v * v);
+    }
   STAMP_END(4);
 }
 
 // ------------------------------------------------------------------------------------------
 // KD: FFN-down (K = 1024) of 32 output columns + residual, in place     grid (8 chunks, clips)
-// wave w: column tile (w & 1), K half (w >> 1); the two K halves meet through LDS.
+// wave w: column tile (w & 1), K quarter (w >> 1); the four partial sums meet through LDS and
+// are added in a fixed order (deterministic).
 // ------------------------------------------------------------------------------------------
 template <typename T>
-__global__ void __launch_bounds__(NTHREADS) kd_kernel(FusedArgs a) {
+__global__ void __launch_bounds__(FT) kd_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
   constexpr int KP = PL::KP, NP = 4 * FD / KP, SA = KP + Frag<T>::PT;
-  constexpr int KTT = 4 * FD / Frag<T>::KF, KTW = KP / Frag<T>::KF / 2;  // k steps: total, per wave per pass
+  constexpr int KTT = 4 * FD / Frag<T>::KF, KTW = KP / Frag<T>::KF / 4;  // k steps: total, per wave per pass
   const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int L = a.L, c16 = lane & 15, g4 = lane >> 4, tile = 2 * c + (wave & 1), kh = wave >> 1;
+  const int L = a.L, c16 = lane & 15, g4 = lane >> 4, tile = 2 * c + (wave & 1), kq = wave >> 1;
   T* Hd = (T*)smem;
   const FusedLayer& w = a.w;
   const size_t row0 = (size_t)b * L;
   const int col = tile * 16 + c16;
+  const int h = c;  // STAMP uses (h, b)
 
   STAMP(0);
   float res[FRT][4];
@@ -365,33 +347,36 @@ __global__ void __launch_bounds__(NTHREADS) kd_kernel(FusedArgs a) {
 #pragma unroll 1
   for (int p = 0; p < NP; ++p) {
     if (p > 0) __syncthreads();  // the previous pass' image is consumed
-    glds_rows(Hd, sizeof(T) * SA, (const T*)a.hid + row0 * (4 * FD) + p * KP, sizeof(T) * 4 * FD, L,
-              (int)(sizeof(T) * KP / 1024));
-    WGemm<T, 1, KTW> gd(w.ff2, KTT, p * (KP / Frag<T>::KF) + kh * KTW);
+    glds_rows<FT>(Hd, sizeof(T) * SA, (const T*)a.hid + row0 * (4 * FD) + p * KP, sizeof(T) * 4 * FD, L,
+                  (int)(sizeof(T) * KP / 1024));
+    WGemm<T, 1, KTW> gd(w.ff2, KTT, p * (KP / Frag<T>::KF) + kq * KTW);
     gd.tiles[0] = tile;
     gd.load(0, lane);
     __syncthreads();
     if (p == 0) STAMP(1);
     f32x4 part[FRT][1];
-    gd.run(part, Hd + kh * KTW * Frag<T>::KF, SA, lane);
+    gd.run(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
 #pragma unroll
     for (int rt = 0; rt < FRT; ++rt) acc[rt][0] += part[rt][0];
   }
   bar_lds();
   STAMP(2);
-  f32x4* red = (f32x4*)smem;  // [2 tiles][FRT][64 lanes]
-  if (kh == 1)
+  f32x4* red = (f32x4*)smem;  // [3 quarters][2 tiles][FRT][64 lanes]
+  if (kq > 0)
 #pragma unroll
-    for (int rt = 0; rt < FRT; ++rt) red[((wave & 1) * FRT + rt) * 64 + lane] = acc[rt][0];
+    for (int rt = 0; rt < FRT; ++rt) red[(((kq - 1) * 2 + (wave & 1)) * FRT + rt) * 64 + lane] = acc[rt][0];
   bar_lds();
-  if (kh == 0) {
+  if (kq == 0) {
     const OutRows out(a.h + row0 * FD, (uint32_t)(sizeof(float) * L * FD));
 #pragma unroll
     for (int rt = 0; rt < FRT; ++rt) {
-      const f32x4 o = red[((wave & 1) * FRT + rt) * 64 + lane];
+      const f32x4 o1 = red[((0 * 2 + (wave & 1)) * FRT + rt) * 64 + lane];
+      const f32x4 o2 = red[((1 * 2 + (wave & 1)) * FRT + rt) * 64 + lane];
+      const f32x4 o3 = red[((2 * 2 + (wave & 1)) * FRT + rt) * 64 + lane];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        out.put<float>((uint32_t)((rt * 16 + 4 * g4 + r) * FD + col), res[rt][r] + ((acc[rt][0][r] + o[r]) + bias));
+        out.put<float>((uint32_t)((rt * 16 + 4 * g4 + r) * FD + col),
+                       res[rt][r] + ((((acc[rt][0][r] + o1[r]) + o2[r]) + o3[r]) + bias));
     }
   }
   STAMP_END(3);
@@ -404,7 +389,7 @@ __global__ void __launch_bounds__(NTHREADS) kd_kernel(FusedArgs a) {
 // The next step's emb_x + PE is computed by that step's first KA (x_emb).
 // ------------------------------------------------------------------------------------------
 template <typename T>
-__global__ void __launch_bounds__(NTHREADS) ke_kernel(FinalArgs a) {
+__global__ void __launch_bounds__(FT) ke_kernel(FinalArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF, SE = 16 + 4;
@@ -420,8 +405,8 @@ __global__ void __launch_bounds__(NTHREADS) ke_kernel(FinalArgs a) {
   const int h = p;                                            // STAMP uses (h, b)
 
   STAMP(0);
-  glds_rows(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
-  WGemm<T, 1, KT, 1> go(a.w_out, KT, 0);
+  glds_rows<FT>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
+  WGemm<T, 1, KT, 1> go(a.w_out, KT, 0);  // waves 0-3: row tile w of channel tile p
   go.tiles[0] = p;
   go.load(0, lane);
   const float bo = a.b_out[p * 16 + c16];
@@ -456,12 +441,12 @@ __global__ void __launch_bounds__(NTHREADS) ke_kernel(FinalArgs a) {
     }
   }
   __syncthreads();  // LDS-DMA rows and every operand above have landed
-  ln_stats(Hs, L, st);
+  ln_stats<FR, 8>(Hs, L, st);
   bar_lds();
-  ln_apply<T>(Hs, L, st, lg, lb, Xn);
+  ln_apply<T, FT>(Hs, L, st, lg, lb, Xn);
   bar_lds();
   STAMP(1);
-  {
+  if (wave < FRT) {
     f32x4 acc[1][1];
     go.run(acc, Xn + wave * 16 * Frag<T>::SX, Frag<T>::SX, lane);
 #pragma unroll
@@ -493,7 +478,7 @@ __global__ void __launch_bounds__(NTHREADS) ke_kernel(FinalArgs a) {
       if (++l == L) { l = 0; ++cc; }
     }
   } else if (!a.do_update && a.do_out) {
-    for (int i = tid; i < ne; i += NTHREADS) {
+    for (int i = tid; i < ne; i += FT) {
       const int e = e0 + i, cc = e / L, l = e - cc * L;
       a.eps_out[(size_t)b * LC + e] = E[l * SE + (cc - c0)];
     }
@@ -532,7 +517,7 @@ bool fused_supported(int dtype, int d_model, int heads, int L, int Ts, int C) {
 
 hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s) {
   fused_attrs();
-  const dim3 blk(NTHREADS), grid(8, n);
+  const dim3 blk(FT), grid(8, n);
   const bool f = dtype == 0;
   switch (which) {
     case 0:
@@ -559,8 +544,8 @@ hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStre
 
 hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s) {
   fused_attrs();
-  if (dtype == 0) hipLaunchKernelGGL(ke_kernel<float>, dim3(8, a.n), dim3(NTHREADS), Plan<float>::KE, s, a);
-  else hipLaunchKernelGGL(ke_kernel<bf16_t>, dim3(8, a.n), dim3(NTHREADS), Plan<bf16_t>::KE, s, a);
+  if (dtype == 0) hipLaunchKernelGGL(ke_kernel<float>, dim3(8, a.n), dim3(FT), Plan<float>::KE, s, a);
+  else hipLaunchKernelGGL(ke_kernel<bf16_t>, dim3(8, a.n), dim3(FT), Plan<bf16_t>::KE, s, a);
   return hipGetLastError();
 }
 

@@ -106,16 +106,16 @@ __device__ __forceinline__ void glds_rows(void* dst, size_t sd, const void* src,
 
 // A [64][SX] operand image of L rows of d_model activations of type T (global rows of FD).
 // bf16 rows are 512 B (two rows per LDS-DMA instruction would cross the pad): registers.
-template <typename T> struct ImgStage {
-  static constexpr int NV = sizeof(T) == 2 ? FR * FD * 2 / 16 / NTHREADS : 1;
+template <typename T, int NT = NTHREADS> struct ImgStage {
+  static constexpr int NV = sizeof(T) == 2 ? FR * FD * 2 / 16 / NT : 1;
   uint4 v[NV];
   __device__ __forceinline__ void load(T* img, const T* src, int L) {
     if constexpr (sizeof(T) == 4) {
-      glds_rows(img, sizeof(T) * Frag<T>::SX, src, sizeof(T) * FD, L, 1);
+      glds_rows<NT>(img, sizeof(T) * Frag<T>::SX, src, sizeof(T) * FD, L, 1);
     } else {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        const int idx = threadIdx.x + i * NTHREADS, r = idx >> 5, c = idx & 31;
+        const int idx = threadIdx.x + i * NT, r = idx >> 5, c = idx & 31;
         v[i] = *(const uint4*)(src + (size_t)min(r, L - 1) * FD + c * 8);
       }
     }
@@ -126,7 +126,7 @@ template <typename T> struct ImgStage {
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        const int idx = threadIdx.x + i * NTHREADS, r = idx >> 5, c = idx & 31;
+        const int idx = threadIdx.x + i * NT, r = idx >> 5, c = idx & 31;
         *(uint4*)(img + r * Frag<T>::SX + c * 8) = v[i];
       }
     }
