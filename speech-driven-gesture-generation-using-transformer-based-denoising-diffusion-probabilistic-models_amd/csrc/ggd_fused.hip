@@ -37,16 +37,16 @@ constexpr int FT = 512;  // threads of the fused kernels: 8 waves, two per SIMD
 // Hs[i][n] += A[i] . W[n] + bias[n] for all 64 rows; wave w owns the NJ column tiles
 // NJ w .. NJ w + NJ - 1.  The accumulators start from Hs + bias (one batch of LDS reads issued
 // before the MFMAs), so the epilogue is a plain store, not a dependent read-modify-write.
-template <typename T, int KT, int NJ>
-__device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGemm<T, NJ, KT>& g,
+template <typename T, int KT, int NJ, int RT>
+__device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGemm<T, NJ, KT, RT>& g,
                                               const float (&bias)[NJ], int lane, int wave) {
   const int c16 = lane & 15, g4 = lane >> 4;
-  f32x4 acc[FRT][NJ];
+  f32x4 acc[RT][NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = (NJ * wave + j) * 16 + c16;
 #pragma unroll
-    for (int rt = 0; rt < FRT; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[rt][j][r] = Hs[(rt * 16 + 4 * g4 + r) * SH + col] + bias[j];
   }
@@ -55,7 +55,7 @@ __device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGe
   for (int j = 0; j < NJ; ++j) {
     const int col = (NJ * wave + j) * 16 + c16;
 #pragma unroll
-    for (int rt = 0; rt < FRT; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) Hs[(rt * 16 + 4 * g4 + r) * SH + col] = acc[rt][j][r];
   }
@@ -73,7 +73,7 @@ __device__ __forceinline__ void store_rows(float* dst, const float* Hs, int L, i
 // ------------------------------------------------------------------------------------------
 // KA: [emb_x + PE (layer 0)] + LN1 + QKV(head) + conv + self-attention      grid (heads, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, int RT>
 __global__ void __launch_bounds__(FT) ka_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(FT) ka_kernel(FusedArgs a) {
   const bool emb = a.x_emb != nullptr;  // layer 0: h = emb_x(x) + PE computed here
   glds_rows<FT>(Hs, sizeof(float) * SH, emb ? a.pe : a.h + (size_t)b * L * FD, sizeof(float) * FD, L, 1);
   constexpr int KTE = 128 / Frag<T>::KF, SB = 128 + Frag<T>::PT, NXV = FR * 128 / FT;
-  WGemm<T, 2, KTE> ge(a.w_emb, KTE, 0);
+  WGemm<T, 2, KTE, RT> ge(a.w_emb, KTE, 0);
   float be[2], xv[NXV];
   if (emb) {
     ge.tiles[0] = 2 * wave;
@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(FT) ka_kernel(FusedArgs a) {
   }
   // QKV of head h: packed as 6 tiles [q0 q1 k0 k1 v0 v1]; waves 0-5 own one tile each
   const int nq = wave < 6 ? 1 : 0;
-  WGemm<T, 1, KT> gm(w.qkv, KT, 0);
+  WGemm<T, 1, KT, RT> gm(w.qkv, KT, 0);
   gm.tiles[0] = h * 6 + min(wave, 5);
   gm.load(0, lane);
   const float bias = w.qkv_b[h * 96 + min(wave, 5) * 16 + c16];
@@ -127,23 +127,23 @@ __global__ void __launch_bounds__(FT) ka_kernel(FusedArgs a) {
       Xb[l * SB + c] = from_f32<T>(c < a.C ? xv[i] : 0.f);
     }
     bar_lds();
-    residual_gemm<T, KTE, 2>(Hs, Xb, SB, ge, be, lane, wave);
+    residual_gemm<T, KTE, 2, RT>(Hs, Xb, SB, ge, be, lane, wave);
     bar_lds();
     store_rows(a.h + (size_t)b * L * FD, Hs, L, h);  // the residual rows KB reads
   }
-  ln_stats<FR, 8>(Hs, L, st);
+  ln_stats<RT * 16, 8>(Hs, L, st);
   bar_lds();
-  ln_apply<T, FT>(Hs, L, st, lg, lb, Xn);
+  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Xn);
   bar_lds();
   STAMP(1);
   // Hs is dead from here: Y and the attention images overlay it
   {
-    f32x4 acc[FRT][1];
+    f32x4 acc[RT][1];
     gm.run(acc, Xn, Frag<T>::SX, lane, nq);
     if (nq) {
       const int col = wave * 16 + c16;
 #pragma unroll
-      for (int rt = 0; rt < FRT; ++rt)
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) Y[(rt * 16 + 4 * g4 + r) * SY + col] = acc[rt][0][r] + bias;
     }
@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(FT) ka_kernel(FusedArgs a) {
   bar_lds();
   STAMP(2);
   using AT = FAtt<T>;
-  conv_rows<T, false, FR, FT>((T*)(att + AT::OQ), AT::SQ, Y, SY, L, cq);
+  conv_rows<T, false, RT * 16, FT>((T*)(att + AT::OQ), AT::SQ, Y, SY, L, cq);
   conv_rows<T, false, FLK, FT>((T*)(att + AT::OK), AT::SQ, Y + 32, SY, L, ck);
   conv_rows<T, true, FLK, FT>((T*)(att + AT::OV), AT::SV, Y + 64, SY, L, cv);
   bar_lds();
@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(FT) ka_kernel(FusedArgs a) {
 // ------------------------------------------------------------------------------------------
 // KB: SA out-proj + residual + LN2 + cross-attn Q(head) + conv + cross-attention  (heads, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, int RT>
 __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
   glds_rows<FT>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
   ImgStage<T, FT> so;
   so.load(Ax, (const T*)a.o_sa + row0 * FD, L);
-  WGemm<T, 2, KT> go(w.o_sa, KT, 0);
+  WGemm<T, 2, KT, RT> go(w.o_sa, KT, 0);
   go.tiles[0] = 2 * wave;
   go.tiles[1] = 2 * wave + 1;
   go.load(0, lane);
@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   STAMP(1);
   // cross-attn query of head h: waves 0, 1 own tiles 2h, 2h + 1 of the natural packing
-  WGemm<T, 1, KT> gq(w.q_ca, KT, 0);
+  WGemm<T, 1, KT, RT> gq(w.q_ca, KT, 0);
   gq.tiles[0] = 2 * h + (wave & 1);
   if (wave < 2) gq.load(0, lane);
   const float bq = w.q_ca_b[h * FDK + (wave & 1) * 16 + c16];
@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
     const float* src = r == 0 ? w.kv_step + (size_t)t * 2 * FD : w.kv_mem + ((size_t)b * a.Ts + (r - 1)) * 2 * FD;
     return *(const float4*)(src + half * FD + h * FDK + q * 4);
   };
-  residual_gemm<T, KT, 2>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
+  residual_gemm<T, KT, 2, RT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
   // issued after the out-projection: t comes from a two-load dependent chain, which must not
   // stall it; the loads complete under LN2.  Named registers, not an array: an array live
   // across the LN is demoted to scratch.
@@ -220,9 +220,9 @@ __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
   bar_lds();
   STAMP(2);
   store_rows(a.h_out + row0 * FD, Hs, L, h);
-  ln_stats<FR, 8>(Hs, L, st);
+  ln_stats<RT * 16, 8>(Hs, L, st);
   bar_lds();
-  ln_apply<T, FT>(Hs, L, st, lg, lb, Ax);
+  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Ax);
   bar_lds();
   STAMP(3);
   // Hs is dead: Yq, raw and the attention images overlay it
@@ -237,17 +237,17 @@ __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
     raw[half * (FLK + 2) * FDK + r * FDK + (e & 31)] = 0.f;
   }
   if (wave < 2) {
-    f32x4 acc[FRT][1];
+    f32x4 acc[RT][1];
     gq.run(acc, Ax, Frag<T>::SX, lane);
     const int col = wave * 16 + c16;
 #pragma unroll
-    for (int rt = 0; rt < FRT; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) Yq[(rt * 16 + 4 * g4 + r) * SYQ + col] = acc[rt][0][r] + bq;
   }
   bar_lds();
   STAMP(4);
-  conv_rows<T, false, FR, FT>((T*)(att + AT::OQ), AT::SQ, Yq, SYQ, L, cq);
+  conv_rows<T, false, RT * 16, FT>((T*)(att + AT::OQ), AT::SQ, Yq, SYQ, L, cq);
   conv_rows<T, false, FLK, FT>((T*)(att + AT::OK), AT::SQ, raw + FDK, FDK, Lk, ck);
   conv_rows<T, true, FLK, FT>((T*)(att + AT::OV), AT::SV, raw + (FLK + 2) * FDK + FDK, FDK, Lk, cv);
   bar_lds();
@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
 // ------------------------------------------------------------------------------------------
 // KC: CA out-proj + residual + LN3 + FFN-up chunk (128 hidden) + ReLU^2   grid (8 chunks, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, int RT>
 __global__ void __launch_bounds__(FT) kc_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(FT) kc_kernel(FusedArgs a) {
   glds_rows<FT>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
   ImgStage<T, FT> so;
   so.load(Ax, (const T*)a.o_ca + row0 * FD, L);
-  WGemm<T, 2, KT> go(w.o_ca, KT, 0);
+  WGemm<T, 2, KT, RT> go(w.o_ca, KT, 0);
   go.tiles[0] = 2 * wave;
   go.tiles[1] = 2 * wave + 1;
   go.load(0, lane);
@@ -288,25 +288,25 @@ __global__ void __launch_bounds__(FT) kc_kernel(FusedArgs a) {
   so.store(Ax, L);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   STAMP(1);
-  WGemm<T, 1, KT> gf(w.ff1, KT, 0);  // prefetch: in flight across the out-projection
+  WGemm<T, 1, KT, RT> gf(w.ff1, KT, 0);  // prefetch: in flight across the out-projection
   gf.tiles[0] = 8 * c + wave;
   gf.load(0, lane);
   const float bf = w.ff1_b[(8 * c + wave) * 16 + c16];
-  residual_gemm<T, KT, 2>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
+  residual_gemm<T, KT, 2, RT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
   bar_lds();
   STAMP(2);
   store_rows(a.h_out + row0 * FD, Hs, L, c);
-  ln_stats<FR, 8>(Hs, L, st);
+  ln_stats<RT * 16, 8>(Hs, L, st);
   bar_lds();
-  ln_apply<T, FT>(Hs, L, st, lg, lb, Ax);
+  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Ax);
   bar_lds();
   STAMP(3);
-  f32x4 acc[FRT][1];
+  f32x4 acc[RT][1];
   gf.run(acc, Ax, Frag<T>::SX, lane);
   const OutRows out((T*)a.hid + row0 * (4 * FD), (uint32_t)(sizeof(T) * L * 4 * FD));
   const int col = (8 * c + wave) * 16 + c16;
 #pragma unroll
-  for (int rt = 0; rt < FRT; ++rt)
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float v = fmaxf(acc[rt][0][r] + bf, 0.f);
@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(FT) kc_kernel(FusedArgs a) {
 // wave w: column tile (w & 1), K quarter (w >> 1); the four partial sums meet through LDS and
 // are added in a fixed order (deterministic).
 // ------------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, int RT>
 __global__ void __launch_bounds__(FT) kd_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
@@ -335,44 +335,44 @@ __global__ void __launch_bounds__(FT) kd_kernel(FusedArgs a) {
   const int h = c;  // STAMP uses (h, b)
 
   STAMP(0);
-  float res[FRT][4];
+  float res[RT][4];
 #pragma unroll
-  for (int rt = 0; rt < FRT; ++rt)
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) res[rt][r] = a.h[(row0 + min(rt * 16 + 4 * g4 + r, L - 1)) * FD + col];
   const float bias = w.ff2_b[col];
-  f32x4 acc[FRT][1];
+  f32x4 acc[RT][1];
 #pragma unroll
-  for (int rt = 0; rt < FRT; ++rt) acc[rt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int rt = 0; rt < RT; ++rt) acc[rt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int p = 0; p < NP; ++p) {
     if (p > 0) __syncthreads();  // the previous pass' image is consumed
     glds_rows<FT>(Hd, sizeof(T) * SA, (const T*)a.hid + row0 * (4 * FD) + p * KP, sizeof(T) * 4 * FD, L,
                   (int)(sizeof(T) * KP / 1024));
-    WGemm<T, 1, KTW> gd(w.ff2, KTT, p * (KP / Frag<T>::KF) + kq * KTW);
+    WGemm<T, 1, KTW, RT> gd(w.ff2, KTT, p * (KP / Frag<T>::KF) + kq * KTW);
     gd.tiles[0] = tile;
     gd.load(0, lane);
     __syncthreads();
     if (p == 0) STAMP(1);
-    f32x4 part[FRT][1];
+    f32x4 part[RT][1];
     gd.run(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
 #pragma unroll
-    for (int rt = 0; rt < FRT; ++rt) acc[rt][0] += part[rt][0];
+    for (int rt = 0; rt < RT; ++rt) acc[rt][0] += part[rt][0];
   }
   bar_lds();
   STAMP(2);
-  f32x4* red = (f32x4*)smem;  // [3 quarters][2 tiles][FRT][64 lanes]
+  f32x4* red = (f32x4*)smem;  // [3 quarters][2 tiles][RT][64 lanes]
   if (kq > 0)
 #pragma unroll
-    for (int rt = 0; rt < FRT; ++rt) red[(((kq - 1) * 2 + (wave & 1)) * FRT + rt) * 64 + lane] = acc[rt][0];
+    for (int rt = 0; rt < RT; ++rt) red[(((kq - 1) * 2 + (wave & 1)) * RT + rt) * 64 + lane] = acc[rt][0];
   bar_lds();
   if (kq == 0) {
     const OutRows out(a.h + row0 * FD, (uint32_t)(sizeof(float) * L * FD));
 #pragma unroll
-    for (int rt = 0; rt < FRT; ++rt) {
-      const f32x4 o1 = red[((0 * 2 + (wave & 1)) * FRT + rt) * 64 + lane];
-      const f32x4 o2 = red[((1 * 2 + (wave & 1)) * FRT + rt) * 64 + lane];
-      const f32x4 o3 = red[((2 * 2 + (wave & 1)) * FRT + rt) * 64 + lane];
+    for (int rt = 0; rt < RT; ++rt) {
+      const f32x4 o1 = red[((0 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
+      const f32x4 o2 = red[((1 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
+      const f32x4 o3 = red[((2 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         out.put<float>((uint32_t)((rt * 16 + 4 * g4 + r) * FD + col),
@@ -388,7 +388,7 @@ __global__ void __launch_bounds__(FT) kd_kernel(FusedArgs a) {
 // eps for row tile w; the update of the block's L x 16 elements is one Philox quad per thread.
 // The next step's emb_x + PE is computed by that step's first KA (x_emb).
 // ------------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, int RT>
 __global__ void __launch_bounds__(FT) ke_kernel(FinalArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using PL = Plan<T>;
@@ -441,12 +441,12 @@ __global__ void __launch_bounds__(FT) ke_kernel(FinalArgs a) {
     }
   }
   __syncthreads();  // LDS-DMA rows and every operand above have landed
-  ln_stats<FR, 8>(Hs, L, st);
+  ln_stats<RT * 16, 8>(Hs, L, st);
   bar_lds();
-  ln_apply<T, FT>(Hs, L, st, lg, lb, Xn);
+  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Xn);
   bar_lds();
   STAMP(1);
-  if (wave < FRT) {
+  if (wave < RT) {
     f32x4 acc[1][1];
     go.run(acc, Xn + wave * 16 * Frag<T>::SX, Frag<T>::SX, lane);
 #pragma unroll
@@ -494,19 +494,22 @@ static void set_lds_attr(K kernel) {
   (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
+template <typename T, int RT>
+static void set_attrs_rt() {
+  set_lds_attr(ka_kernel<T, RT>);
+  set_lds_attr(kb_kernel<T, RT>);
+  set_lds_attr(kc_kernel<T, RT>);
+  set_lds_attr(kd_kernel<T, RT>);
+  set_lds_attr(ke_kernel<T, RT>);
+}
+
 static bool fused_attrs_done = false;
 static void fused_attrs() {
   if (fused_attrs_done) return;
-  set_lds_attr(ka_kernel<float>);
-  set_lds_attr(ka_kernel<bf16_t>);
-  set_lds_attr(kb_kernel<float>);
-  set_lds_attr(kb_kernel<bf16_t>);
-  set_lds_attr(kc_kernel<float>);
-  set_lds_attr(kc_kernel<bf16_t>);
-  set_lds_attr(kd_kernel<float>);
-  set_lds_attr(kd_kernel<bf16_t>);
-  set_lds_attr(ke_kernel<float>);
-  set_lds_attr(ke_kernel<bf16_t>);
+  set_attrs_rt<float, 3>();
+  set_attrs_rt<float, 4>();
+  set_attrs_rt<bf16_t, 3>();
+  set_attrs_rt<bf16_t, 4>();
   fused_attrs_done = true;
 }
 
@@ -515,26 +518,26 @@ bool fused_supported(int dtype, int d_model, int heads, int L, int Ts, int C) {
   return d_model == FD && heads == FD / FDK && L >= 1 && L <= FR && Ts >= 1 && 1 + Ts <= FLK && C >= 1 && C <= 128;
 }
 
-hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s) {
-  fused_attrs();
+template <int RT>
+static hipError_t launch_fused_rt(int which, int dtype, const FusedArgs& a, int n, hipStream_t s) {
   const dim3 blk(FT), grid(8, n);
   const bool f = dtype == 0;
   switch (which) {
     case 0:
-      if (f) hipLaunchKernelGGL(ka_kernel<float>, grid, blk, Plan<float>::KA, s, a);
-      else hipLaunchKernelGGL(ka_kernel<bf16_t>, grid, blk, Plan<bf16_t>::KA, s, a);
+      if (f) hipLaunchKernelGGL((ka_kernel<float, RT>), grid, blk, Plan<float>::KA, s, a);
+      else hipLaunchKernelGGL((ka_kernel<bf16_t, RT>), grid, blk, Plan<bf16_t>::KA, s, a);
       break;
     case 1:
-      if (f) hipLaunchKernelGGL(kb_kernel<float>, grid, blk, Plan<float>::KB, s, a);
-      else hipLaunchKernelGGL(kb_kernel<bf16_t>, grid, blk, Plan<bf16_t>::KB, s, a);
+      if (f) hipLaunchKernelGGL((kb_kernel<float, RT>), grid, blk, Plan<float>::KB, s, a);
+      else hipLaunchKernelGGL((kb_kernel<bf16_t, RT>), grid, blk, Plan<bf16_t>::KB, s, a);
       break;
     case 2:
-      if (f) hipLaunchKernelGGL(kc_kernel<float>, grid, blk, Plan<float>::KC, s, a);
-      else hipLaunchKernelGGL(kc_kernel<bf16_t>, grid, blk, Plan<bf16_t>::KC, s, a);
+      if (f) hipLaunchKernelGGL((kc_kernel<float, RT>), grid, blk, Plan<float>::KC, s, a);
+      else hipLaunchKernelGGL((kc_kernel<bf16_t, RT>), grid, blk, Plan<bf16_t>::KC, s, a);
       break;
     case 3:
-      if (f) hipLaunchKernelGGL(kd_kernel<float>, grid, blk, Plan<float>::KD, s, a);
-      else hipLaunchKernelGGL(kd_kernel<bf16_t>, grid, blk, Plan<bf16_t>::KD, s, a);
+      if (f) hipLaunchKernelGGL((kd_kernel<float, RT>), grid, blk, Plan<float>::KD, s, a);
+      else hipLaunchKernelGGL((kd_kernel<bf16_t, RT>), grid, blk, Plan<bf16_t>::KD, s, a);
       break;
     default:
       return hipErrorInvalidValue;
@@ -542,10 +545,24 @@ hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStre
   return hipGetLastError();
 }
 
+// row tiles: 48 padded rows for clips of <= 48 frames (the C2 shape, L = 40), else 64
+static inline bool rt3(int L) { return L <= 48; }
+
+hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s) {
+  fused_attrs();
+  return rt3(a.L) ? launch_fused_rt<3>(which, dtype, a, n, s) : launch_fused_rt<4>(which, dtype, a, n, s);
+}
+
 hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s) {
   fused_attrs();
-  if (dtype == 0) hipLaunchKernelGGL(ke_kernel<float>, dim3(8, a.n), dim3(FT), Plan<float>::KE, s, a);
-  else hipLaunchKernelGGL(ke_kernel<bf16_t>, dim3(8, a.n), dim3(FT), Plan<bf16_t>::KE, s, a);
+  const dim3 blk(FT), grid(8, a.n);
+  if (rt3(a.L)) {
+    if (dtype == 0) hipLaunchKernelGGL((ke_kernel<float, 3>), grid, blk, Plan<float>::KE, s, a);
+    else hipLaunchKernelGGL((ke_kernel<bf16_t, 3>), grid, blk, Plan<bf16_t>::KE, s, a);
+  } else {
+    if (dtype == 0) hipLaunchKernelGGL((ke_kernel<float, 4>), grid, blk, Plan<float>::KE, s, a);
+    else hipLaunchKernelGGL((ke_kernel<bf16_t, 4>), grid, blk, Plan<bf16_t>::KE, s, a);
+  }
   return hipGetLastError();
 }
 
