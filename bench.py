@@ -10,9 +10,10 @@ the fused decoder + update chain) + the all-gather of the final poses.  Workload
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
 
 Prints ONE JSON line on rank 0.  ``roofline`` is measured live inside the timed region:
-the last timed pass runs its step loop eagerly (eager == graph replay within 1 %, see
-DESIGN.md) with a hipEvent pair on the context stream around every launch of the dominant
-kernel, kb_kernel (SA out-proj + LN2 + cross-attn Q + conv + cross-attention), whose
+during the last timed pass (the same hipGraph replay, re-captured with profiling on) every
+launch of the dominant kernel, kb_kernel (SA out-proj + LN2 + cross-attn Q + conv +
+cross-attention), stamps its own span on the device-wide realtime clock (min start / max
+end over its workgroups, ggd_api.hip ``spans``) — T x n_layers launches per pass.  Its
 algorithmic FLOPs per launch are kb_flop() below.
 ``cpu_baseline`` times the CPU oracle (a faithful fp32 restatement that recomputes the
 speech encoder every step, as models/model.py:95-96 does) on a bounded sample.
@@ -213,6 +214,7 @@ def main():
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 6), "traffic": None,
                 "kernel": f"kb_kernel<{args.dtype}> (SA out-proj + LN2 + cross-attn Q + conv + cross-attention)",
+                "timing": "device realtime-clock span of every KB launch of the last timed pass",
                 "flop_per_launch": kb, "avg_launch_us": round(avg_us, 3), "launches": prof_n}
     clip_step = clip_step_flops(L, Tm, d, d_pose, arch["n_layers"])
     frame_flop = (T * clip_step + ENCODER_FLOP_PER_CLIP) / L

@@ -1,0 +1,68 @@
+"""Where a bench pass spends its time: encoder, memory install, sampling loop (GPU box)."""
+import os
+import sys
+import time
+
+import torch as th
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+pkg = ge.load_package()
+enc_mod = __import__(ge.PKG_NAME + ".encoder", fromlist=["x"])
+cfg = pkg.load_config(os.path.join(ROOT, "configs", "beat-ours.json"))
+dev = th.device("cuda:0")
+model, diffusion, _, _, _ = pkg.create_model(123, cfg.Model, dtype="bf16", device=dev)
+model.load_state_dict(pkg.init_state_dict(model.arch, seed=0))
+wavs = [th.randn(32, 32000, device=dev) * 0.1 for _ in range(6)]
+
+
+def timed(fn, reps=5):
+    fn()
+    th.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    th.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+enc = model.encoder()
+print(f"encoder 32 clips (CHUNK={enc.CHUNK})      : {timed(lambda: enc(wavs[0])):8.2f} ms", flush=True)
+for ch in (16, 32):
+    enc.CHUNK = ch
+    print(f"encoder 32 clips (CHUNK={ch})     : {timed(lambda: enc(wavs[0])):8.2f} ms", flush=True)
+enc.CHUNK = 8
+# host-side issue time alone (no sync)
+th.cuda.synchronize()
+t0 = time.perf_counter()
+enc(wavs[1])
+t1 = time.perf_counter()
+th.cuda.synchronize()
+t2 = time.perf_counter()
+print(f"encoder host issue {1e3 * (t1 - t0):.2f} ms, drain {1e3 * (t2 - t1):.2f} ms", flush=True)
+
+k = [0]
+
+
+def prep():
+    k[0] += 1
+    model.prepare(wavs[k[0] % 6], 40)
+
+
+print(f"prepare (encoder + set_memory)      : {timed(prep):8.2f} ms", flush=True)
+ctx, n = model.prepare(wavs[0], 40)
+ctx.set_schedule(diffusion.betas, diffusion.timestep_map)
+samp = lambda: diffusion.p_sample_loop(model, (32, 123, 40), model_kwargs={"wav": wavs[0]}, seed=7, extras=False)
+print(f"p_sample_loop, memory cached        : {timed(samp, 3):8.2f} ms", flush=True)
+th.cuda.synchronize()
+t0 = time.perf_counter()
+samp()
+t1 = time.perf_counter()
+th.cuda.synchronize()
+t2 = time.perf_counter()
+print(f"p_sample_loop host issue {1e3 * (t1 - t0):.2f} ms, drain {1e3 * (t2 - t1):.2f} ms", flush=True)
+full = lambda: diffusion.p_sample_loop(model, (32, 123, 40), model_kwargs={"wav": wavs[(k.__setitem__(0, k[0] + 1) or k[0]) % 6]},
+                                       seed=7, extras=False)
+print(f"p_sample_loop, new wav each call    : {timed(full, 3):8.2f} ms", flush=True)

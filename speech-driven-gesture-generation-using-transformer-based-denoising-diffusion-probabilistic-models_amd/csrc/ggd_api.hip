@@ -112,6 +112,9 @@ struct ggd_ctx {
   ProfEvents prof;
   double prof_avg_us = 0;
   int64_t prof_launches = 0;
+  unsigned long long* span = nullptr;  // fused path: KB launch spans [2][T * n_layers] (realtime ticks)
+  int span_half = 0;                   // allocated slots per half
+  double wall_mhz = 100.0;             // realtime counter rate (hipDeviceAttributeWallClockRate)
 };
 
 namespace {
@@ -434,10 +437,13 @@ int launch_fused_layers(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     HIP_TRY(c, launch_fused(0, D.dtype, f, n, s));     // KA: [emb +] LN1 + QKV + conv + self-attention
     f.x_emb = nullptr;
     f.bump_counter = 0;
-    const bool prof = c->profiling && sampling;        // KB is the dominant kernel of the step
-    if (prof) { int r = prof_mark(c, s); if (r) return r; }
+    if (c->profiling && sampling && c->span) {         // KB is the dominant kernel of the step
+      f.span = c->span + li;
+      f.span_stride = D.n_layers;
+      f.span_half = c->span_half;
+    }
     HIP_TRY(c, launch_fused(1, D.dtype, f, n, s));     // KB: out-proj + LN2 + Q + cross-attention
-    if (prof) { int r = prof_mark(c, s); if (r) return r; }
+    f.span = nullptr;
     f.h = c->h2;
     f.h_out = c->h;
     HIP_TRY(c, launch_fused(2, D.dtype, f, n, s));     // KC: out-proj + LN3 + FFN-up + ReLU^2
@@ -581,7 +587,8 @@ int launch_step(ggd_ctx* c, const ggd_sample_args& a, float* extras, int fixed_k
 //   DDPM sigma = exp(0.5 * logvar_f32)                        gaussian_diffusion.py:328
 //   DDIM sigma = eta * sqrt((1-abp)/(1-ab)) * sqrt(1 - ab/abp) :468-472
 //        c_eps = sqrt(1 - abp - sigma^2)                       :477
-void make_records(ggd_ctx* c, int alg, float eta, std::vector<StepRec>& recs) {
+void make_records(ggd_ctx* c, int alg, float eta, std::vector<StepRec>& recs, uint64_t seed = 0,
+                  int64_t clip_offset = 0) {
 #pragma clang fp contract(off)
   const int T = (int)c->betas.size();
   std::vector<double> ac(T), acp(T);
@@ -627,7 +634,9 @@ void make_records(ggd_ctx* c, int alg, float eta, std::vector<StepRec>& recs) {
     }
     r.i = i;
     r.t_orig = c->tmap[i];
-    r.pad = 0;
+    r.seed_lo = (uint32_t)seed;
+    r.seed_hi = (uint32_t)(seed >> 32);
+    r.clip_offset = (uint32_t)clip_offset;
   }
 }
 
@@ -672,6 +681,11 @@ int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out) {
   *out = c;
   HIP_TRY(c, hipSetDevice(device));
   HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) == hipSuccess && khz > 0)
+      c->wall_mhz = khz / 1000.0;
+  }
   HIP_TRY(c, hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
   HIP_TRY(c, hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming));
 
@@ -1157,7 +1171,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   hipStream_t s = c->stream;
 
   std::vector<StepRec> recs;
-  make_records(c, a->alg, a->eta, recs);
+  make_records(c, a->alg, a->eta, recs, a->seed, a->clip_offset);
   HIP_TRY(c, hipEventRecord(c->ev_in, (hipStream_t)stream));
   HIP_TRY(c, hipStreamWaitEvent(s, c->ev_in, 0));
   HIP_TRY(c, hipMemcpyAsync(c->d_steps, recs.data(), sizeof(StepRec) * T, hipMemcpyHostToDevice, s));
@@ -1218,12 +1232,24 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   const int graph_steps = a->extras ? nsteps - 1 : nsteps;
   // pointer / shape key: a captured graph is reused only for identical arguments
   char keybuf[512];
-  std::snprintf(keybuf, sizeof keybuf, "%d|%d|%p|%llu|%lld|%p|%p|%p", a->alg, a->n, (const void*)a->noise,
-                (unsigned long long)a->seed, (long long)a->clip_offset, (const void*)a->inpaint_poses,
-                (const void*)a->inpaint_masks, (const void*)a->trans);
+  std::snprintf(keybuf, sizeof keybuf, "%d|%d|%p|%p|%p|%p|%d", a->alg, a->n, (const void*)a->noise,
+                (const void*)a->inpaint_poses, (const void*)a->inpaint_masks, (const void*)a->trans,
+                (int)c->profiling);
   const std::string key(keybuf);
+  // fused path profiling: KB stamps its own launch span per (step, layer) on the device clock,
+  // so the graph replays unchanged; the generic path brackets its launches with events (eager)
+  const bool spans = c->profiling && c->fused;
+  if (spans) {
+    const int need = T * D.n_layers;
+    if (c->span_half < need) {
+      HIP_TRY(c, dalloc(c, &c->span, 2 * (size_t)need * sizeof(unsigned long long)));
+      c->span_half = need;
+    }
+    HIP_TRY(c, hipMemsetAsync(c->span, 0xFF, (size_t)c->span_half * sizeof(unsigned long long), s));
+    HIP_TRY(c, hipMemsetAsync(c->span + c->span_half, 0, (size_t)c->span_half * sizeof(unsigned long long), s));
+  }
   if (graph_steps > 0) {
-    if (a->use_graph && !c->profiling) {
+    if (a->use_graph && (!c->profiling || spans)) {
       // one captured step, replayed: the step's kernels read the iteration from the device
       // counter that the step's first kernel advances
       if (!c->gexec || c->graph_key != key) {
@@ -1254,7 +1280,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
         int r = launch_step(c, *a, nullptr, -1);
         if (r) return r;
       }
-      if (c->profiling && c->prof.next >= 2) {
+      if (c->profiling && !spans && c->prof.next >= 2) {
         HIP_TRY(c, hipStreamSynchronize(s));
         double total = 0;
         int64_t cnt = 0;
@@ -1272,6 +1298,22 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   if (a->extras && nsteps > 0) {
     int r = launch_step(c, *a, a->extras, -1);
     if (r) return r;
+  }
+  if (spans) {
+    std::vector<unsigned long long> h(2 * (size_t)c->span_half);
+    HIP_TRY(c, hipMemcpyAsync(h.data(), c->span, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    double total = 0;
+    int64_t cnt = 0;
+    for (int j = 0; j < c->span_half; ++j) {
+      const unsigned long long b = h[j], e = h[c->span_half + j];
+      if (b != ~0ull && e >= b) {
+        total += (double)(e - b) / c->wall_mhz;
+        ++cnt;
+      }
+    }
+    c->prof_avg_us = cnt ? total / cnt : 0;
+    c->prof_launches = cnt;
   }
   HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));
   HIP_TRY(c, hipEventRecord(c->ev_out, s));

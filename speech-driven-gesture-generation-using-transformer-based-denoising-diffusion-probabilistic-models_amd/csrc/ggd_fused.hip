@@ -182,7 +182,10 @@ __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
   const size_t row0 = (size_t)b * L;
 
   STAMP(0);
-  const int t = a.t_clip ? a.t_clip[b] : a.steps[*a.step_counter].t_orig;
+  const int it = a.t_clip ? 0 : *a.step_counter;
+  const int span_slot = it * a.span_stride;
+  SPAN_BEGIN(span_slot);
+  const int t = a.t_clip ? a.t_clip[b] : a.steps[it].t_orig;
   glds_rows<FT>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
   ImgStage<T, FT> so;
   so.load(Ax, (const T*)a.o_sa + row0 * FD, L);
@@ -254,6 +257,7 @@ __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
   STAMP(5);
   fattn_any<T>(att, L, Lk, a.scale, (T*)a.o_ca + row0 * FD + h * FDK, FD);
   STAMP_END(6);
+  SPAN_END(span_slot);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -456,7 +460,8 @@ __global__ void __launch_bounds__(FT) ke_kernel(FinalArgs a) {
   STAMP(2);
   if (upd) {
     if (!a.noise)
-      philox_normal4(a.seed, (uint32_t)(a.clip_offset + b), (uint32_t)rec.i, TAG_STEP, (uint32_t)((e0 >> 2) + tid), zq);
+      philox_normal4(((uint64_t)rec.seed_hi << 32) | rec.seed_lo, rec.clip_offset + (uint32_t)b, (uint32_t)rec.i,
+                     TAG_STEP, (uint32_t)((e0 >> 2) + tid), zq);
     int cc = cc0, l = l0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {

@@ -34,6 +34,23 @@ __host__ __device__ constexpr size_t al16(size_t v) { return (v + 15) & ~(size_t
     }                                                                                           \
   } while (0)
 
+// profiling: launch span of a kernel from the device-wide realtime counter (the same clock in
+// every XCD): each workgroup's first thread folds its start into min, and after the workgroup's
+// last stores have drained, its end into max (ggd_api.hip reads the pairs back)
+#define SPAN_BEGIN(slot)                                                                        \
+  do {                                                                                          \
+    if (a.span && threadIdx.x == 0)                                                             \
+      atomicMin(a.span + (slot), (unsigned long long)__builtin_amdgcn_s_memrealtime());         \
+  } while (0)
+#define SPAN_END(slot)                                                                          \
+  do {                                                                                          \
+    if (a.span) {                                                                               \
+      __syncthreads();                                                                          \
+      if (threadIdx.x == 0)                                                                     \
+        atomicMax(a.span + a.span_half + (slot), (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+    }                                                                                           \
+  } while (0)
+
 // ------------------------------------------------------------------------------------------
 // bounded stores: a raw buffer resource over a clip's output rows; the hardware drops stores
 // past num_records, so padded rows are written without a branch.  (A store under a divergent

@@ -55,7 +55,9 @@ struct StepRec {
   float c_eps;    // DDIM: sqrt(1 - abp - sigma^2)
   int i;          // respaced index (nonzero mask)
   int t_orig;     // timestep_map[i] (model input)
-  int pad;
+  // the call's counter-noise key (the same in every record): kept in the table rather than in
+  // kernel arguments so one captured step graph serves every seed / shard offset
+  uint32_t seed_lo, seed_hi, clip_offset;
 };
 
 struct AttnArgs {
@@ -119,6 +121,10 @@ struct FusedArgs {
   // (N, L, C), packed emb_x weights, PE table) and written to h_out for KB's residual
   const float* x_emb; const void* w_emb; const float* b_emb; const float* pe; int C;
   unsigned long long* stamps;  // diagnostics: block (0,0) writes s_memtime at phase boundaries
+  // profiling: KB's launch span per (step, layer) from the device realtime clock —
+  // span[slot] = min start over workgroups, span[span_half + slot] = max end,
+  // slot = *step_counter * span_stride (the host offsets span by the layer index)
+  unsigned long long* span; int span_stride, span_half;
 };
 
 // KE: grid (8 channel blocks, clips); block p owns pose channels [16p, 16p + 16)

@@ -472,7 +472,8 @@ __global__ void __launch_bounds__(NTHREADS) update_kernel(UpdArgs a) {
   if (a.noise)
     z = a.noise[(size_t)k * a.n * a.C * a.L + ncl];
   else
-    z = philox_normal(a.seed, (uint32_t)(a.clip_offset + b), (uint32_t)r.i, TAG_STEP, (uint32_t)(c * a.L + l));
+    z = philox_normal(((uint64_t)r.seed_hi << 32) | r.seed_lo, r.clip_offset + (uint32_t)b, (uint32_t)r.i, TAG_STEP,
+                      (uint32_t)(c * a.L + l));
   const bool inp = a.inp_mask != nullptr;
   const float m = inp ? a.inp_mask[bl] : 0.f;
   const float p = inp ? a.inp_pose[idx] : 0.f;
