@@ -1,8 +1,9 @@
 """Benchmark: generated motion frames/s of the gesture-diffusion sampler (BASELINE.json metric).
 
 One "step" = one full sampling pass over one batch of synthetic BEAT-shaped clips:
-speech encoding (once per clip) + all T = 1000 DDPM denoise steps (hipGraph replay of
-the fused decoder + update chain) + the all-gather of the final poses.  Workload
+speech encoding (once per clip, a replayed graph) + all T = 1000 DDPM denoise steps (17
+fused kernel launches each, issued eagerly: on ROCm 7.2 a replayed hipGraph of the same
+chain measured 3-10 % slower) + the all-gather of the final poses.  Workload
 (config C2, BASELINE.json configs[1]): beat-ours, 32 clips per GPU, L = 40 frames,
 123 pose channels, 32,000-sample wav windows, bf16 decoder, random-init weights.
 
@@ -10,7 +11,7 @@ the fused decoder + update chain) + the all-gather of the final poses.  Workload
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
 
 Prints ONE JSON line on rank 0.  ``roofline`` is measured live inside the timed region:
-during the last timed pass (the same hipGraph replay, re-captured with profiling on) every
+during the last timed pass (the same launch sequence, with profiling on) every
 launch of the dominant kernel, kb_kernel (SA out-proj + LN2 + cross-attn Q + conv +
 cross-attention), stamps its own span on the device-wide realtime clock (min start / max
 end over its workgroups, ggd_api.hip ``spans``) — T x n_layers launches per pass.  Its
@@ -63,7 +64,8 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     p.add_argument("--alg", default="ddpm", choices=["ddpm", "ddim"])
     p.add_argument("--respacing", default="")
-    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--graph", action="store_true",
+                   help="replay each denoise step as a captured hipGraph (measured slower than eager launches)")
     p.add_argument("--no-profile", action="store_true", help="skip the in-loop kernel events")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=3)
@@ -157,7 +159,7 @@ def main():
     def one_pass(wav_all, seed):
         def fn(wav_local, offset):
             out = loop(model, (wav_local.shape[0], d_pose, L), model_kwargs={"wav": wav_local}, seed=seed,
-                       clip_offset=offset, use_graph=not args.no_graph, extras=False)
+                       clip_offset=offset, use_graph=args.graph, extras=False)
             return out["sample"]
         return sharding.sample_sharded(fn, wav_all, n_total, rank, world, dev)
 
@@ -185,15 +187,18 @@ def main():
         log(f"pass {k} issued")
         if profiled:
             lib.ggd_set_profiling(ctx.h, 0)
-            avg = ctypes.c_double()
-            cnt = ctypes.c_int64()
-            lib.ggd_kernel_time(ctx.h, 0, ctypes.byref(avg), ctypes.byref(cnt))
-            prof_us.append(avg.value * cnt.value)
-            prof_n += cnt.value
     th.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    prof_kind = 0
+    if prof:  # the stamps of the profiled pass are read back after the clock stopped
+        avg = ctypes.c_double()
+        cnt = ctypes.c_int64()
+        lib.ggd_kernel_time(ctx.h, 0, ctypes.byref(avg), ctypes.byref(cnt))
+        prof_kind = lib.ggd_profile_kind(ctx.h)
+        prof_us.append(avg.value * cnt.value)
+        prof_n += cnt.value
     if dist is not None:
         t = th.tensor([elapsed], device=dev, dtype=th.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -205,18 +210,23 @@ def main():
     value = frames / elapsed
     d = arch["d_model"]
     Tm = 1 + int(ctx.desc.speech_len)
-    kb = kb_flop(B, L, Tm, d)
+    clip_step = clip_step_flops(L, Tm, d, d_pose, arch["n_layers"])
     peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
     roof = None
     if prof and prof_n:
         avg_us = sum(prof_us) / prof_n
-        ach = kb / (avg_us * 1e-6) / 1e12
+        if prof_kind == 1:   # the persistent loop: one launch runs all T denoise steps of the batch
+            flop = clip_step * B * T
+            kernel = f"mk_kernel<{args.dtype}> (persistent reverse loop: all {T} denoise steps, 17 phases each)"
+            timing = "hipEvent pair around the loop's single launch in the last timed pass"
+        else:
+            flop = kb_flop(B, L, Tm, d)
+            kernel = f"kb_kernel<{args.dtype}> (SA out-proj + LN2 + cross-attn Q + conv + cross-attention)"
+            timing = "device realtime-clock span of every KB launch of the last timed pass"
+        ach = flop / (avg_us * 1e-6) / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 6), "traffic": None,
-                "kernel": f"kb_kernel<{args.dtype}> (SA out-proj + LN2 + cross-attn Q + conv + cross-attention)",
-                "timing": "device realtime-clock span of every KB launch of the last timed pass",
-                "flop_per_launch": kb, "avg_launch_us": round(avg_us, 3), "launches": prof_n}
-    clip_step = clip_step_flops(L, Tm, d, d_pose, arch["n_layers"])
+                "frac": round(ach / peak, 6), "traffic": None, "kernel": kernel, "timing": timing,
+                "flop_per_launch": flop, "avg_launch_us": round(avg_us, 3), "launches": prof_n}
     frame_flop = (T * clip_step + ENCODER_FLOP_PER_CLIP) / L
     res = {
         "metric": "generated motion frames/sec (whole node), T=1000 BEAT clips, 1/2/4/8 MI355X",

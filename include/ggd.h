@@ -140,11 +140,16 @@ typedef struct ggd_sample_args {
  * (generator.py:283-294). */
 int ggd_sample(ggd_ctx* ctx, const ggd_sample_args* args, void* stream);
 
-/* Timing of the dominant kernel over the last ggd_sample (hipEvents on the ctx
- * stream): average microseconds of one launch of `which` (0 = the FFN-up GEMM),
- * and the number of launches averaged.  Needs ggd_set_profiling(ctx, 1). */
+/* Timing of the dominant kernel over the last profiled ggd_sample: average microseconds of one
+ * launch of `which` (0 = the dominant kernel: fused path kb_kernel, timed by its own per-workgroup
+ * stamps on the device realtime clock while the step graph replays; generic path the FFN-up GEMM,
+ * timed by hipEvent pairs on the ctx stream), and the number of launches averaged.  Sampling
+ * with ggd_set_profiling(ctx, 1) records; this call synchronises the ctx stream and reduces. */
 int ggd_set_profiling(ggd_ctx* ctx, int32_t on);
 int ggd_kernel_time(ggd_ctx* ctx, int32_t which, double* avg_us, int64_t* launches);
+/* What the last profiled ggd_sample timed: 0 = kb_kernel launches of the per-phase path,
+ * 1 = the persistent loop (mk_kernel: one launch for all denoise steps). */
+int ggd_profile_kind(ggd_ctx* ctx);
 
 /* Diagnostics (not part of the reference surface): launch one kernel configuration `iters`
  * times back to back on the ctx stream and return the average microseconds per launch
@@ -153,11 +158,15 @@ int ggd_kernel_time(ggd_ctx* ctx, int32_t which, double* avg_us, int64_t* launch
  * p = {n}; what = 3: the same step as one hipGraph replay, p = {n}; what = 4: one fused kernel,
  * p = {0 KA | 1 KB | 2 KC | 3 KD | 4 KE, n}; what = 5: calibration micro-kernels, p = {mode, arg,
  * blocks, buffer MiB} with mode 0 empty launch, 1 dependent-load chase (arg loads), 2 shader clock
- * (returns GHz instead of microseconds), 3 / 4 bulk 64 KiB / 16 KiB load per block; what = 6: as
+ * (returns GHz instead of microseconds), 3 / 4 bulk 64 KiB / 16 KiB load per block, 6 clip-group
+ * hand-off inside one launch (arg = rounds | variant << 20; avg_us[1..3] = errors, misplaced,
+ * timeouts; scripts/handoff_bench.py); what = 6: as
  * 4 with in-kernel phase stamps (avg_us[0..7] = phase ends in us); what = 7: p = {1} routes
  * ggd_sample through the per-step launches instead of the persistent kernel, {0} back (returns 1
  * in *avg_us when the persistent kernel is available); what = 8: persistent-kernel phase stamps of
- * iteration 0, p = {1} arm, {2} read (avg_us[0..7]), {0} disarm. */
+ * iteration 0, p = {1} arm, {2} read (avg_us[0..7]), {0} disarm; what = 9: p = {1} routes
+ * ggd_sample through the per-phase launches instead of the persistent loop (ggd_mega.hip), {0}
+ * back (returns the loop's clip capacity in *avg_us). */
 int ggd_diag(ggd_ctx* ctx, int32_t what, const int32_t* p, int32_t np, int32_t iters, double* avg_us);
 
 /* Library version string. */

@@ -112,8 +112,22 @@ struct ggd_ctx {
   ProfEvents prof;
   double prof_avg_us = 0;
   int64_t prof_launches = 0;
-  unsigned long long* span = nullptr;  // fused path: KB launch spans [2][T * n_layers] (realtime ticks)
-  int span_half = 0;                   // allocated slots per half
+  unsigned long long* span = nullptr;  // fused path: KB stamps [T * n_layers][2][workgroups] (realtime ticks)
+  size_t span_cap = 0;                 // allocated stamps
+  size_t span_pending = 0, span_wg = 0;  // stamps written by the last profiled ggd_sample
+  int prof_kind = 0;                   // what the last profiled ggd_sample timed: 0 kb_kernel, 1 mk_kernel
+
+  // persistent reverse loop (ggd_mega.hip)
+  bool no_mega = false;                // ggd_diag what = 9: route sampling through per-phase launches
+  FusedArgs* mega_fa = nullptr;        // device [n_layers][4]
+  unsigned long long* mega_phase_stamps = nullptr;  // ggd_diag what = 11: layer 1's phases + KE
+  FinalArgs* mega_fe = nullptr;
+  unsigned* mega_ctl = nullptr;
+  int* mega_status = nullptr;
+  unsigned long long* mega_stamps = nullptr;  // ggd_diag what = 10
+  std::vector<FusedArgs> mega_fa_host;
+  FinalArgs mega_fe_host{};
+  int mega_status_host = 0;
   double wall_mhz = 100.0;             // realtime counter rate (hipDeviceAttributeWallClockRate)
 };
 
@@ -408,39 +422,46 @@ FusedLayer fused_layer(ggd_ctx* c, int li) {
   return w;
 }
 
+// KA / KB arguments of layer li (KC runs on h2 -> h, KD on h in place)
+FusedArgs fused_args(ggd_ctx* c, int li, const int* t_clip) {
+  const ggd_desc& D = c->desc;
+  FusedArgs f{};
+  f.w = fused_layer(c, li);
+  f.L = D.seq_len;
+  f.Ts = D.speech_len;
+  f.o_sa = c->att;
+  f.o_ca = c->q;
+  f.hid = c->ffn;
+  f.t_clip = t_clip;
+  f.steps = c->d_steps;
+  f.step_counter = c->d_counter;
+  f.scale = 1.0f / std::sqrt((float)(D.d_model / D.heads));
+  f.h = c->h;
+  f.h_out = c->h2;
+  if (li == 0) {  // layer 0's KA also computes h = emb_x(x) + PE from the state x
+    f.x_emb = c->x;
+    f.w_emb = c->f_emb.w;
+    f.b_emb = c->f_emb.b;
+    f.pe = c->pe;
+    f.C = D.d_pose;
+  }
+  return f;
+}
+
 int launch_fused_layers(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
   const ggd_desc& D = c->desc;
   const int L = D.seq_len, d = D.d_model, M = n * L;
   hipStream_t s = c->stream;
   for (int li = 0; li < D.n_layers; ++li) {
-    FusedArgs f{};
-    f.w = fused_layer(c, li);
-    f.L = L;
-    f.Ts = D.speech_len;
-    f.o_sa = c->att;
-    f.o_ca = c->q;
-    f.hid = c->ffn;
-    f.t_clip = t_clip;
-    f.steps = c->d_steps;
-    f.step_counter = c->d_counter;
-    f.scale = 1.0f / std::sqrt((float)(d / D.heads));
-    f.h = c->h;
-    f.h_out = c->h2;
+    FusedArgs f = fused_args(c, li, t_clip);
     f.bump_counter = sampling && li == 0;
-    if (li == 0) {  // layer 0's KA also computes h = emb_x(x) + PE from the state x
-      f.x_emb = c->x;
-      f.w_emb = c->f_emb.w;
-      f.b_emb = c->f_emb.b;
-      f.pe = c->pe;
-      f.C = D.d_pose;
-    }
     HIP_TRY(c, launch_fused(0, D.dtype, f, n, s));     // KA: [emb +] LN1 + QKV + conv + self-attention
     f.x_emb = nullptr;
     f.bump_counter = 0;
     if (c->profiling && sampling && c->span) {         // KB is the dominant kernel of the step
-      f.span = c->span + li;
+      f.span = c->span;
       f.span_stride = D.n_layers;
-      f.span_half = c->span_half;
+      f.span_layer = li;
     }
     HIP_TRY(c, launch_fused(1, D.dtype, f, n, s));     // KB: out-proj + LN2 + Q + cross-attention
     f.span = nullptr;
@@ -934,8 +955,36 @@ int ggd_set_profiling(ggd_ctx* c, int32_t on) {
   return GGD_OK;
 }
 
+int ggd_profile_kind(ggd_ctx* c) { return c ? c->prof_kind : GGD_ERR_ARG; }
+
 int ggd_kernel_time(ggd_ctx* c, int32_t which, double* avg_us, int64_t* launches) {
   if (!c || !avg_us || !launches || which != 0) return fail(c, GGD_ERR_ARG, "bad argument");
+  if (c->span_pending) {  // launch span = latest workgroup end - earliest workgroup start
+    const size_t n = c->span_pending, wg = c->span_wg;
+    c->span_pending = 0;
+    std::vector<unsigned long long> h(n);
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMemcpyAsync(h.data(), c->span, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    double total = 0;
+    int64_t cnt = 0;
+    for (size_t slot = 0; slot < n / (2 * wg); ++slot) {
+      const unsigned long long* b = h.data() + slot * 2 * wg;
+      unsigned long long lo = ~0ull, hi = 0;
+      bool full = true;
+      for (size_t w = 0; w < wg; ++w) {
+        full = full && b[w] && b[wg + w];
+        lo = std::min(lo, b[w]);
+        hi = std::max(hi, b[wg + w]);
+      }
+      if (full && hi >= lo) {
+        total += (double)(hi - lo) / c->wall_mhz;
+        ++cnt;
+      }
+    }
+    c->prof_avg_us = cnt ? total / cnt : 0;
+    c->prof_launches = cnt;
+  }
   *avg_us = c->prof_avg_us;
   *launches = c->prof_launches;
   return GGD_OK;
@@ -944,6 +993,42 @@ int ggd_kernel_time(ggd_ctx* c, int32_t which, double* avg_us, int64_t* launches
 int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t iters, double* avg_us) {
   if (!c || !p || !avg_us || iters <= 0) return fail(c, GGD_ERR_ARG, "bad argument");
   HIP_TRY(c, hipSetDevice(c->device));
+  if (what == 10 && np >= 1) {  // persistent-loop barrier stamps: {1} arm, {2} read, {0} off
+    const int NS = 2 * 17 * MEGA_STAMP_STEPS + 1;
+    if (p[0] == 1) {
+      if (!c->mega_stamps) HIP_TRY(c, dalloc(c, &c->mega_stamps, NS * sizeof(unsigned long long)));
+      HIP_TRY(c, hipMemset(c->mega_stamps, 0, NS * sizeof(unsigned long long)));
+    }
+    if (p[0] == 2 && c->mega_stamps) {  // avg_us[j] = us from the loop start to stamp j
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      std::vector<unsigned long long> h(NS);
+      HIP_TRY(c, hipMemcpy(h.data(), c->mega_stamps, NS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      for (int j = 0; j + 1 < NS; ++j) avg_us[j] = h[j] ? (double)(h[j] - h[NS - 1]) / 2400.0 : -1.0;
+    }
+    if (p[0] == 0) c->mega_stamps = nullptr;  // stays owned by the ctx allocation list
+    return GGD_OK;
+  }
+  if (what == 11 && np >= 1) {  // persistent-loop phase stamps of layer 1 + KE: {1} arm, {2} read, {0} off
+    if (p[0] == 1) {
+      if (!c->mega_phase_stamps) HIP_TRY(c, dalloc(c, &c->mega_phase_stamps, 80 * sizeof(unsigned long long)));
+      HIP_TRY(c, hipMemset(c->mega_phase_stamps, 0, 80 * sizeof(unsigned long long)));
+    }
+    if (p[0] == 2 && c->mega_phase_stamps) {  // avg_us[16 j + i] = us from phase j's stamp 0 to its stamp i
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      unsigned long long h[80];
+      HIP_TRY(c, hipMemcpy(h, c->mega_phase_stamps, sizeof h, hipMemcpyDeviceToHost));
+      for (int j = 0; j < 5; ++j)
+        for (int i = 0; i < 16; ++i)
+          avg_us[16 * j + i] = (h[16 * j] && h[16 * j + i] >= h[16 * j]) ? (double)(h[16 * j + i] - h[16 * j]) / 2400.0 : -1.0;
+    }
+    if (p[0] == 0) c->mega_phase_stamps = nullptr;
+    return GGD_OK;
+  }
+  if (what == 9 && np >= 1) {  // p[0] != 0: sample through the per-phase launches, not the persistent loop
+    c->no_mega = p[0] != 0;
+    *avg_us = c->fused ? (double)mega_capacity(c->desc.dtype, c->desc.seq_len) : 0.0;
+    return GGD_OK;
+  }
   if (what == 7 && np >= 1) {  // p[0] != 0: route ggd_sample through the per-step launches
     c->no_persist = p[0] != 0;
     *avg_us = c->persist ? 1.0 : 0.0;
@@ -973,6 +1058,7 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     void* v = nullptr;
     if (hipMalloc(&v, bytes) != hipSuccess) return nullptr;
     (void)hipMemset(v, 0x3c, bytes);  // small finite values in f32 and bf16
+    (void)hipDeviceSynchronize();     // ordered before work on the (non-blocking) ctx stream
     tmp.push_back(v);
     return v;
   };
@@ -1123,6 +1209,7 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
       for (size_t i = 0; i < n; ++i) nx[i] = (int)((i + stride) % n);
       HIP_TRY(c, hipMemcpy(buf, nx.data(), 4 * n, hipMemcpyHostToDevice));
     }
+    if (rc == GGD_OK && mode == 6) HIP_TRY(c, hipMemsetAsync((char*)buf + 4000, 0, 96, s));  // hand-off stats
     for (int it = 0; rc == GGD_OK && it < iters + 1; ++it) {
       if (it == 1) HIP_TRY(c, hipEventRecord(e0, s));
       HIP_TRY(c, launch_mb(mode, buf, bytes, arg, blocks, s));
@@ -1147,6 +1234,11 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     HIP_TRY(c, hipEventSynchronize(e1));
     HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
     *avg_us = ms * 1000.0 / iters;
+    if (what == 5 && np >= 4 && p[0] == 6) {  // avg_us[1..3] = errors, misplaced, timeouts (all launches)
+      unsigned st[3];
+      HIP_TRY(c, hipMemcpy(st, (char*)tmp.back() + 4000, sizeof st, hipMemcpyDeviceToHost));
+      for (int i = 0; i < 3; ++i) avg_us[1 + i] = st[i];
+    }
   }
   (void)hipStreamSynchronize(s);
   for (void* v : tmp) (void)hipFree(v);
@@ -1154,6 +1246,80 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
   (void)hipEventDestroy(e1);
   return rc;
 }
+
+}  // extern "C"
+
+namespace {
+
+// The first `nsteps` iterations as ONE persistent launch (ggd_mega.hip); blocks until it has
+// finished to report a barrier timeout (outputs are then invalid).
+int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
+  const ggd_desc& D = c->desc;
+  const int NL = D.n_layers;
+  hipStream_t s = c->stream;
+  if (!c->mega_fa) {
+    HIP_TRY(c, dalloc(c, &c->mega_fa, sizeof(FusedArgs) * 4 * NL));
+    HIP_TRY(c, dalloc(c, &c->mega_fe, sizeof(FinalArgs)));
+    HIP_TRY(c, dalloc(c, &c->mega_ctl, sizeof(unsigned) * MEGA_CTL_WORDS));
+    HIP_TRY(c, dalloc(c, &c->mega_status, sizeof(int)));
+  }
+  c->mega_fa_host.assign(4 * NL, FusedArgs{});
+  for (int li = 0; li < NL; ++li) {
+    FusedArgs f = fused_args(c, li, nullptr);
+    c->mega_fa_host[4 * li] = f;      // KA (layer 0: emb of x)
+    f.x_emb = nullptr;
+    c->mega_fa_host[4 * li + 1] = f;  // KB: h -> h2
+    f.h = c->h2;
+    f.h_out = c->h;
+    c->mega_fa_host[4 * li + 2] = f;  // KC: h2 -> h
+    f.h = c->h;
+    c->mega_fa_host[4 * li + 3] = f;  // KD: h in place
+  }
+  if (c->mega_phase_stamps && NL > 1)  // workgroup 0 stamps layer 1's phases (last step wins)
+    for (int j = 0; j < 4; ++j) c->mega_fa_host[4 + j].stamps = c->mega_phase_stamps + 16 * j;
+  FinalArgs& fe = c->mega_fe_host;
+  fe = final_args(c, a.n);
+  fe.alg = a.alg;
+  fe.noise = a.noise;
+  fe.inp_pose = a.inpaint_masks ? a.inpaint_poses : nullptr;
+  fe.inp_mask = a.inpaint_masks;
+  fe.trans = a.trans;
+  fe.do_out = 1;
+  fe.do_update = 1;
+  fe.stamps = c->mega_phase_stamps ? c->mega_phase_stamps + 64 : nullptr;
+  HIP_TRY(c, hipMemcpyAsync(c->mega_fa, c->mega_fa_host.data(), sizeof(FusedArgs) * 4 * NL, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->mega_fe, &fe, sizeof(FinalArgs), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemsetAsync(c->mega_status, 0, sizeof(int), s));
+  MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status, c->mega_stamps};
+  if (c->profiling) {
+    c->prof.next = 0;
+    int r = prof_mark(c, s);
+    if (r) return r;
+  }
+  HIP_TRY(c, launch_mega(D.dtype, D.seq_len, m, a.n, s));
+  if (c->profiling) {
+    int r = prof_mark(c, s);
+    if (r) return r;
+  }
+  HIP_TRY(c, hipMemcpyAsync(&c->mega_status_host, c->mega_status, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  if (c->mega_status_host)
+    return fail(c, GGD_ERR_HIP, c->mega_status_host == 2 ? "persistent loop: workgroups were not all resident"
+                                                          : "persistent loop: a clip-group barrier timed out");
+  if (c->profiling) {  // the whole loop is the one timed launch
+    float ms = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->prof.ev[0], c->prof.ev[1]));
+    c->prof_avg_us = ms * 1000.0;
+    c->prof_launches = 1;
+    c->prof_kind = 1;
+    c->span_pending = 0;
+  }
+  return GGD_OK;
+}
+
+}  // namespace
+
+extern "C" {
 
 int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   if (!c || !a || !a->out) return fail(c, GGD_ERR_ARG, "null argument");
@@ -1230,6 +1396,19 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   HIP_TRY(c, launch_set_int(c->d_counter, -1, s));
 
   const int graph_steps = a->extras ? nsteps - 1 : nsteps;
+  if (c->fused && !c->no_mega && graph_steps > 0 && a->n <= mega_capacity(D.dtype, D.seq_len)) {
+    int r = run_mega(c, *a, graph_steps);
+    if (r) return r;
+    if (a->extras) {  // the last iteration with its extras through the per-phase kernels
+      HIP_TRY(c, launch_set_int(c->d_counter, graph_steps - 1, s));
+      r = launch_step(c, *a, a->extras, -1);
+      if (r) return r;
+    }
+    HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));
+    HIP_TRY(c, hipEventRecord(c->ev_out, s));
+    HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
+    return GGD_OK;
+  }
   // pointer / shape key: a captured graph is reused only for identical arguments
   char keybuf[512];
   std::snprintf(keybuf, sizeof keybuf, "%d|%d|%p|%p|%p|%p|%d", a->alg, a->n, (const void*)a->noise,
@@ -1239,14 +1418,14 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   // fused path profiling: KB stamps its own launch span per (step, layer) on the device clock,
   // so the graph replays unchanged; the generic path brackets its launches with events (eager)
   const bool spans = c->profiling && c->fused;
+  const size_t span_wg = (size_t)D.heads * a->n;  // KB grid: (heads, clips)
+  const size_t span_n = (size_t)T * D.n_layers * 2 * span_wg;
   if (spans) {
-    const int need = T * D.n_layers;
-    if (c->span_half < need) {
-      HIP_TRY(c, dalloc(c, &c->span, 2 * (size_t)need * sizeof(unsigned long long)));
-      c->span_half = need;
+    if (c->span_cap < span_n) {  // arena memory is never returned; grow only
+      HIP_TRY(c, dalloc(c, &c->span, span_n * sizeof(unsigned long long)));
+      c->span_cap = span_n;
     }
-    HIP_TRY(c, hipMemsetAsync(c->span, 0xFF, (size_t)c->span_half * sizeof(unsigned long long), s));
-    HIP_TRY(c, hipMemsetAsync(c->span + c->span_half, 0, (size_t)c->span_half * sizeof(unsigned long long), s));
+    HIP_TRY(c, hipMemsetAsync(c->span, 0, span_n * sizeof(unsigned long long), s));
   }
   if (graph_steps > 0) {
     if (a->use_graph && (!c->profiling || spans)) {
@@ -1299,21 +1478,10 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
     int r = launch_step(c, *a, a->extras, -1);
     if (r) return r;
   }
-  if (spans) {
-    std::vector<unsigned long long> h(2 * (size_t)c->span_half);
-    HIP_TRY(c, hipMemcpyAsync(h.data(), c->span, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-    double total = 0;
-    int64_t cnt = 0;
-    for (int j = 0; j < c->span_half; ++j) {
-      const unsigned long long b = h[j], e = h[c->span_half + j];
-      if (b != ~0ull && e >= b) {
-        total += (double)(e - b) / c->wall_mhz;
-        ++cnt;
-      }
-    }
-    c->prof_avg_us = cnt ? total / cnt : 0;
-    c->prof_launches = cnt;
+  if (spans) {  // reduced on the host by ggd_kernel_time, outside the caller's timed region
+    c->span_pending = span_n;
+    c->span_wg = span_wg;
+    c->prof_kind = 0;
   }
   HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));
   HIP_TRY(c, hipEventRecord(c->ev_out, s));

@@ -1,494 +1,37 @@
-// ggd_fused.hip -- the fused per-clip decoder kernels (d_model 256, 8 heads, L <= 64,
-// memory rows 1 + Ts <= 64, d_pose <= 128).
-//
-// One denoise step of the one-way decoder (models/nn.py:154-228) is 4 launches per layer
-// plus one epilogue launch, instead of one launch per op:
-//
-//   KA (head, clip)   LN1 + QKV projection of the head + 3-tap conv + self-attention
-//   KB (head, clip)   SA out-proj + residual (+ h write) + LN2 + cross-attn query of the
-//                     head + conv + cross-attention to the cached speech memory
-//   KC (chunk, clip)  CA out-proj + residual (+ h write) + LN3 + FFN-up chunk + ReLU^2
-//   KD (chunk, clip)  FFN-down of a 32-column chunk + residual, in place
-//   KE (clip)         LN_out + output projection + DDPM/DDIM update (+ the next step's
-//                     emb_x + PE), or eps for the model protocol
-//
-// Every workgroup owns one clip's rows, so the depthwise conv, the attention and every
-// LayerNorm see whole sequences / whole rows in LDS.  The small out-projections are
-// recomputed by each head workgroup of a clip (x8 redundant MFMA work, served from L2)
-// instead of paying a launch boundary and an HBM round trip for them.
-//
-// The kernels are latency-bound (a clip is 40 rows; a step is ~17 dependent launches), so
-// they are written for few dependent memory round trips:
-//   * every global load is unconditional (row indices clamped into the clip) and issued in
-//     one batch at the top of its phase -- a load under a branch gets its own vmcnt(0) wait;
-//   * f32 rows of 1 KiB are staged by LDS-DMA (global_load_lds_dwordx4, one row per wave
-//     instruction), bf16 operand images through registers;
-//   * row tiles are padded to 64 rows at compile time: no runtime branch wraps an MFMA,
-//     rows >= L hold don't-care values whose results are never stored;
-//   * weights are packed on the host in MFMA B-fragment order -- [n tile][k step][lane][16 B]
-//     -- and stream straight into registers with 1 KiB coalesced loads, issued before the
-//     activations they multiply have arrived.
-#include "ggd_fusedlib.h"
+// ggd_fused.hip -- one launch per decoder phase (ggd_phases.h): the kernels, their launchers.
+#include "ggd_phases.h"
 
 namespace ggd {
 
-constexpr int FT = 512;  // threads of the fused kernels: 8 waves, two per SIMD
-
-// Hs[i][n] += A[i] . W[n] + bias[n] for all 64 rows; wave w owns the NJ column tiles
-// NJ w .. NJ w + NJ - 1.  The accumulators start from Hs + bias (one batch of LDS reads issued
-// before the MFMAs), so the epilogue is a plain store, not a dependent read-modify-write.
-template <typename T, int KT, int NJ, int RT>
-__device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGemm<T, NJ, KT, RT>& g,
-                                              const float (&bias)[NJ], int lane, int wave) {
-  const int c16 = lane & 15, g4 = lane >> 4;
-  f32x4 acc[RT][NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int col = (NJ * wave + j) * 16 + c16;
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[rt][j][r] = Hs[(rt * 16 + 4 * g4 + r) * SH + col] + bias[j];
-  }
-  g.run(acc, A, SA, lane, NJ, false);
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int col = (NJ * wave + j) * 16 + c16;
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Hs[(rt * 16 + 4 * g4 + r) * SH + col] = acc[rt][j][r];
-  }
-}
-
-// rows [0, L) of Hs -> global rows, shared by the 8 workgroups of a clip: workgroup `part`
-// writes rows r with r % 8 == part (every row once; bounded 16-byte stores, no branch)
-__device__ __forceinline__ void store_rows(float* dst, const float* Hs, int L, int part) {
-  const OutRows out(dst, (uint32_t)(sizeof(float) * L * FD));
-  static_assert(FR / 8 * 64 == FT, "one 16-byte piece per thread");
-  const int idx = threadIdx.x, r = (idx >> 6) * 8 + part, c = (idx & 63) * 4;
-  out.put4((uint32_t)(r * FD + c), *(const float4*)(Hs + min(r, L - 1) * SH + c));
-}
-
-// ------------------------------------------------------------------------------------------
-// KA: [emb_x + PE (layer 0)] + LN1 + QKV(head) + conv + self-attention      grid (heads, clips)
-// ------------------------------------------------------------------------------------------
 template <typename T, int RT>
 __global__ void __launch_bounds__(FT) ka_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using PL = Plan<T>;
-  constexpr int KT = FD / Frag<T>::KF, SY = 96 + 4;
-  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int L = a.L, c16 = lane & 15, g4 = lane >> 4;
-  T* Xn = (T*)smem;
-  float2* st = (float2*)(smem + PL::IMG);
-  unsigned char* un = smem + PL::IMG + PL::ST;
-  float* Hs = (float*)un;
-  float* Y = (float*)un;
-  unsigned char* att = un + PL::Y_KA;
-  const FusedLayer& w = a.w;
-
-  STAMP(0);
-  if (a.bump_counter && h == 0 && b == 0 && tid == 0) atomicAdd(a.step_counter, 1);
-  const bool emb = a.x_emb != nullptr;  // layer 0: h = emb_x(x) + PE computed here
-  glds_rows<FT>(Hs, sizeof(float) * SH, emb ? a.pe : a.h + (size_t)b * L * FD, sizeof(float) * FD, L, 1);
-  constexpr int KTE = 128 / Frag<T>::KF, SB = 128 + Frag<T>::PT, NXV = FR * 128 / FT;
-  WGemm<T, 2, KTE, RT> ge(a.w_emb, KTE, 0);
-  float be[2], xv[NXV];
-  if (emb) {
-    ge.tiles[0] = 2 * wave;
-    ge.tiles[1] = 2 * wave + 1;
-    ge.load(0, lane);
-    be[0] = a.b_emb[(2 * wave) * 16 + c16];
-    be[1] = a.b_emb[(2 * wave + 1) * 16 + c16];
-    const int C = a.C;
-#pragma unroll
-    for (int i = 0; i < NXV; ++i) {
-      const int idx = tid + i * FT, l = idx >> 7, c = idx & 127;
-      xv[i] = a.x_emb[((size_t)b * L + min(l, L - 1)) * C + min(c, C - 1)];
-    }
-  }
-  // QKV of head h: packed as 6 tiles [q0 q1 k0 k1 v0 v1]; waves 0-5 own one tile each
-  const int nq = wave < 6 ? 1 : 0;
-  WGemm<T, 1, KT, RT> gm(w.qkv, KT, 0);
-  gm.tiles[0] = h * 6 + min(wave, 5);
-  gm.load(0, lane);
-  const float bias = w.qkv_b[h * 96 + min(wave, 5) * 16 + c16];
-  const float4 lg = *(const float4*)(w.ln1_g + (tid & 63) * 4), lb = *(const float4*)(w.ln1_b + (tid & 63) * 4);
-  const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
-              cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
-  __syncthreads();  // LDS-DMA rows and every operand above have landed
-  if (emb) {
-    // Xb = bf16(x) (channels >= C zero; aliases the LN image), Hs = PE + Xb W_emb^T + b
-    T* Xb = Xn;
-#pragma unroll
-    for (int i = 0; i < NXV; ++i) {
-      const int idx = tid + i * FT, l = idx >> 7, c = idx & 127;
-      Xb[l * SB + c] = from_f32<T>(c < a.C ? xv[i] : 0.f);
-    }
-    bar_lds();
-    residual_gemm<T, KTE, 2, RT>(Hs, Xb, SB, ge, be, lane, wave);
-    bar_lds();
-    store_rows(a.h + (size_t)b * L * FD, Hs, L, h);  // the residual rows KB reads
-  }
-  ln_stats<RT * 16, 8>(Hs, L, st);
-  bar_lds();
-  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Xn);
-  bar_lds();
-  STAMP(1);
-  // Hs is dead from here: Y and the attention images overlay it
-  {
-    f32x4 acc[RT][1];
-    gm.run(acc, Xn, Frag<T>::SX, lane, nq);
-    if (nq) {
-      const int col = wave * 16 + c16;
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Y[(rt * 16 + 4 * g4 + r) * SY + col] = acc[rt][0][r] + bias;
-    }
-  }
-  bar_lds();
-  STAMP(2);
-  using AT = FAtt<T>;
-  conv_rows<T, false, RT * 16, FT>((T*)(att + AT::OQ), AT::SQ, Y, SY, L, cq);
-  conv_rows<T, false, FLK, FT>((T*)(att + AT::OK), AT::SQ, Y + 32, SY, L, ck);
-  conv_rows<T, true, FLK, FT>((T*)(att + AT::OV), AT::SV, Y + 64, SY, L, cv);
-  bar_lds();
-  STAMP(3);
-  fattn_any<T>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
-  STAMP_END(4);
+  if (a.bump_counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(a.step_counter, 1);
+  ka_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, smem);
 }
 
-// ------------------------------------------------------------------------------------------
-// KB: SA out-proj + residual + LN2 + cross-attn Q(head) + conv + cross-attention  (heads, clips)
-// ------------------------------------------------------------------------------------------
 template <typename T, int RT>
 __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using PL = Plan<T>;
-  using AT = FAtt<T>;
-  constexpr int KT = FD / Frag<T>::KF, SYQ = FDK + 4;
-  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int L = a.L, Lk = 1 + a.Ts, c16 = lane & 15, g4 = lane >> 4;
-  T* Ax = (T*)smem;                   // O_sa image, then LN2(h) image
-  float2* st = (float2*)(smem + PL::IMG);
-  unsigned char* un = smem + PL::IMG + PL::ST;
-  float* Hs = (float*)un;
-  float* Yq = (float*)un;
-  float* raw = (float*)(un + PL::YQ);
-  unsigned char* att = un + PL::YQ + PL::RAW;
-  const FusedLayer& w = a.w;
-  const size_t row0 = (size_t)b * L;
-
-  STAMP(0);
-  const int it = a.t_clip ? 0 : *a.step_counter;
-  const int span_slot = it * a.span_stride;
-  SPAN_BEGIN(span_slot);
-  const int t = a.t_clip ? a.t_clip[b] : a.steps[it].t_orig;
-  glds_rows<FT>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
-  ImgStage<T, FT> so;
-  so.load(Ax, (const T*)a.o_sa + row0 * FD, L);
-  WGemm<T, 2, KT, RT> go(w.o_sa, KT, 0);
-  go.tiles[0] = 2 * wave;
-  go.tiles[1] = 2 * wave + 1;
-  go.load(0, lane);
-  float bo[2];
-  bo[0] = w.o_sa_b[(2 * wave) * 16 + c16];
-  bo[1] = w.o_sa_b[(2 * wave + 1) * 16 + c16];
-  const float4 lg = *(const float4*)(w.ln2_g + (tid & 63) * 4), lb = *(const float4*)(w.ln2_b + (tid & 63) * 4);
-  so.store(Ax, L);
-  __syncthreads();  // LDS-DMA rows and every operand above have landed
-  STAMP(1);
-  // cross-attn query of head h: waves 0, 1 own tiles 2h, 2h + 1 of the natural packing
-  WGemm<T, 1, KT, RT> gq(w.q_ca, KT, 0);
-  gq.tiles[0] = 2 * h + (wave & 1);
-  if (wave < 2) gq.load(0, lane);
-  const float bq = w.q_ca_b[h * FDK + (wave & 1) * 16 + c16];
-  const ConvW cq = conv_w(w.ca_qw, w.ca_qb, tid & 31), ck = conv_w(w.ca_kw, w.ca_kb, tid & 31),
-              cv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
-  // memory K / V of head h (pre-conv): row 0 = the step token of this clip's t, rows 1.. the
-  // cached speech rows; item v = (row, half, 16-byte piece) with row clamped into [0, Lk)
-  static_assert(2 * FLK * 8 == 2 * FT, "two 16-byte memory pieces per thread");
-  auto kv_load = [&](int i) -> float4 {
-    const int v = tid + i * FT, r = min(v >> 4, Lk - 1), half = (v >> 3) & 1, q = v & 7;
-    const float* src = r == 0 ? w.kv_step + (size_t)t * 2 * FD : w.kv_mem + ((size_t)b * a.Ts + (r - 1)) * 2 * FD;
-    return *(const float4*)(src + half * FD + h * FDK + q * 4);
-  };
-  residual_gemm<T, KT, 2, RT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
-  // issued after the out-projection: t comes from a two-load dependent chain, which must not
-  // stall it; the loads complete under LN2.  Named registers, not an array: an array live
-  // across the LN is demoted to scratch.
-  const float4 kv0 = kv_load(0), kv1 = kv_load(1);
-  bar_lds();
-  STAMP(2);
-  store_rows(a.h_out + row0 * FD, Hs, L, h);
-  ln_stats<RT * 16, 8>(Hs, L, st);
-  bar_lds();
-  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Ax);
-  bar_lds();
-  STAMP(3);
-  // Hs is dead: Yq, raw and the attention images overlay it
-  auto kv_store = [&](int i, float4 val) {
-    const int v = tid + i * FT, r = v >> 4, half = (v >> 3) & 1, q = v & 7;
-    if (r < Lk) *(float4*)(raw + half * (FLK + 2) * FDK + (r + 1) * FDK + q * 4) = val;
-  };
-  kv_store(0, kv0);
-  kv_store(1, kv1);
-  if (tid < 2 * 2 * FDK) {  // zero halo rows 0 and Lk + 1 of both halves
-    const int half = tid >> 6, e = tid & 63, r = e < FDK ? 0 : Lk + 1;
-    raw[half * (FLK + 2) * FDK + r * FDK + (e & 31)] = 0.f;
-  }
-  if (wave < 2) {
-    f32x4 acc[RT][1];
-    gq.run(acc, Ax, Frag<T>::SX, lane);
-    const int col = wave * 16 + c16;
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Yq[(rt * 16 + 4 * g4 + r) * SYQ + col] = acc[rt][0][r] + bq;
-  }
-  bar_lds();
-  STAMP(4);
-  conv_rows<T, false, RT * 16, FT>((T*)(att + AT::OQ), AT::SQ, Yq, SYQ, L, cq);
-  conv_rows<T, false, FLK, FT>((T*)(att + AT::OK), AT::SQ, raw + FDK, FDK, Lk, ck);
-  conv_rows<T, true, FLK, FT>((T*)(att + AT::OV), AT::SV, raw + (FLK + 2) * FDK + FDK, FDK, Lk, cv);
-  bar_lds();
-  STAMP(5);
-  fattn_any<T>(att, L, Lk, a.scale, (T*)a.o_ca + row0 * FD + h * FDK, FD);
-  STAMP_END(6);
-  SPAN_END(span_slot);
+  kb_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, a.t_clip ? 0 : *a.step_counter, smem);
 }
 
-// ------------------------------------------------------------------------------------------
-// KC: CA out-proj + residual + LN3 + FFN-up chunk (128 hidden) + ReLU^2   grid (8 chunks, clips)
-// ------------------------------------------------------------------------------------------
 template <typename T, int RT>
 __global__ void __launch_bounds__(FT) kc_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using PL = Plan<T>;
-  constexpr int KT = FD / Frag<T>::KF;
-  const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int L = a.L, c16 = lane & 15, g4 = lane >> 4;
-  T* Ax = (T*)smem;
-  float2* st = (float2*)(smem + PL::IMG);
-  float* Hs = (float*)(smem + PL::IMG + PL::ST);
-  const FusedLayer& w = a.w;
-  const size_t row0 = (size_t)b * L;
-  const int h = c;  // STAMP uses (h, b)
-
-  STAMP(0);
-  glds_rows<FT>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
-  ImgStage<T, FT> so;
-  so.load(Ax, (const T*)a.o_ca + row0 * FD, L);
-  WGemm<T, 2, KT, RT> go(w.o_ca, KT, 0);
-  go.tiles[0] = 2 * wave;
-  go.tiles[1] = 2 * wave + 1;
-  go.load(0, lane);
-  float bo[2];
-  bo[0] = w.o_ca_b[(2 * wave) * 16 + c16];
-  bo[1] = w.o_ca_b[(2 * wave + 1) * 16 + c16];
-  const float4 lg = *(const float4*)(w.ln3_g + (tid & 63) * 4), lb = *(const float4*)(w.ln3_b + (tid & 63) * 4);
-  so.store(Ax, L);
-  __syncthreads();  // LDS-DMA rows and every operand above have landed
-  STAMP(1);
-  WGemm<T, 1, KT, RT> gf(w.ff1, KT, 0);  // prefetch: in flight across the out-projection
-  gf.tiles[0] = 8 * c + wave;
-  gf.load(0, lane);
-  const float bf = w.ff1_b[(8 * c + wave) * 16 + c16];
-  residual_gemm<T, KT, 2, RT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
-  bar_lds();
-  STAMP(2);
-  store_rows(a.h_out + row0 * FD, Hs, L, c);
-  ln_stats<RT * 16, 8>(Hs, L, st);
-  bar_lds();
-  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Ax);
-  bar_lds();
-  STAMP(3);
-  f32x4 acc[RT][1];
-  gf.run(acc, Ax, Frag<T>::SX, lane);
-  const OutRows out((T*)a.hid + row0 * (4 * FD), (uint32_t)(sizeof(T) * L * 4 * FD));
-  const int col = (8 * c + wave) * 16 + c16;
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = fmaxf(acc[rt][0][r] + bf, 0.f);
-      out.put<T>((uint32_t)((rt * 16 + 4 * g4 + r) * (4 * FD) + col), v * v);
-    }
-  STAMP_END(4);
+  kc_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, smem);
 }
 
-// ------------------------------------------------------------------------------------------
-// KD: FFN-down (K = 1024) of 32 output columns + residual, in place     grid (8 chunks, clips)
-// wave w: column tile (w & 1), K quarter (w >> 1); the four partial sums meet through LDS and
-// are added in a fixed order (deterministic).
-// ------------------------------------------------------------------------------------------
 template <typename T, int RT>
 __global__ void __launch_bounds__(FT) kd_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using PL = Plan<T>;
-  constexpr int KP = PL::KP, NP = 4 * FD / KP, SA = KP + Frag<T>::PT;
-  constexpr int KTT = 4 * FD / Frag<T>::KF, KTW = KP / Frag<T>::KF / 4;  // k steps: total, per wave per pass
-  const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int L = a.L, c16 = lane & 15, g4 = lane >> 4, tile = 2 * c + (wave & 1), kq = wave >> 1;
-  T* Hd = (T*)smem;
-  const FusedLayer& w = a.w;
-  const size_t row0 = (size_t)b * L;
-  const int col = tile * 16 + c16;
-  const int h = c;  // STAMP uses (h, b)
-
-  STAMP(0);
-  float res[RT][4];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) res[rt][r] = a.h[(row0 + min(rt * 16 + 4 * g4 + r, L - 1)) * FD + col];
-  const float bias = w.ff2_b[col];
-  f32x4 acc[RT][1];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) acc[rt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int p = 0; p < NP; ++p) {
-    if (p > 0) __syncthreads();  // the previous pass' image is consumed
-    glds_rows<FT>(Hd, sizeof(T) * SA, (const T*)a.hid + row0 * (4 * FD) + p * KP, sizeof(T) * 4 * FD, L,
-                  (int)(sizeof(T) * KP / 1024));
-    WGemm<T, 1, KTW, RT> gd(w.ff2, KTT, p * (KP / Frag<T>::KF) + kq * KTW);
-    gd.tiles[0] = tile;
-    gd.load(0, lane);
-    __syncthreads();
-    if (p == 0) STAMP(1);
-    f32x4 part[RT][1];
-    gd.run(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc[rt][0] += part[rt][0];
-  }
-  bar_lds();
-  STAMP(2);
-  f32x4* red = (f32x4*)smem;  // [3 quarters][2 tiles][RT][64 lanes]
-  if (kq > 0)
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) red[(((kq - 1) * 2 + (wave & 1)) * RT + rt) * 64 + lane] = acc[rt][0];
-  bar_lds();
-  if (kq == 0) {
-    const OutRows out(a.h + row0 * FD, (uint32_t)(sizeof(float) * L * FD));
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const f32x4 o1 = red[((0 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
-      const f32x4 o2 = red[((1 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
-      const f32x4 o3 = red[((2 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        out.put<float>((uint32_t)((rt * 16 + 4 * g4 + r) * FD + col),
-                       res[rt][r] + ((((acc[rt][0][r] + o1[r]) + o2[r]) + o3[r]) + bias));
-    }
-  }
-  STAMP_END(3);
+  kd_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, smem);
 }
 
-// ------------------------------------------------------------------------------------------
-// KE: LN_out + out-proj of 16 channels (eps) [+ diffusion update of those channels]
-// grid (8 channel blocks, clips).  Block p owns pose channels [16p, 16p + 16): wave w computes
-// eps for row tile w; the update of the block's L x 16 elements is one Philox quad per thread.
-// The next step's emb_x + PE is computed by that step's first KA (x_emb).
-// ------------------------------------------------------------------------------------------
 template <typename T, int RT>
 __global__ void __launch_bounds__(FT) ke_kernel(FinalArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using PL = Plan<T>;
-  constexpr int KT = FD / Frag<T>::KF, SE = 16 + 4;
-  const int p = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int L = a.L, C = a.C, c16 = lane & 15, g4 = lane >> 4, LC = L * C;
-  T* Xn = (T*)smem;
-  float2* st = (float2*)(smem + PL::IMG);
-  float* Hs = (float*)(smem + PL::IMG + PL::ST);
-  float* E = (float*)(smem + PL::IMG + PL::ST + PL::HS);
-  const size_t row0 = (size_t)b * L;
-  const int c0 = 16 * p, cn = max(0, min(16, C - c0));       // the block's channels
-  const int e0 = c0 * L, ne = cn * L;                         // its elements, reference (C, L) order
-  const int h = p;                                            // STAMP uses (h, b)
-
-  STAMP(0);
-  glds_rows<FT>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
-  WGemm<T, 1, KT, 1> go(a.w_out, KT, 0);  // waves 0-3: row tile w of channel tile p
-  go.tiles[0] = p;
-  go.load(0, lane);
-  const float bo = a.b_out[p * 16 + c16];
-  const float4 lg = *(const float4*)(a.ln_g + (tid & 63) * 4), lb = *(const float4*)(a.ln_b + (tid & 63) * 4);
-  // the thread's quad: elements e0 + 4 tid .. + 3 (issued now, consumed after the GEMM)
-  const bool upd = a.do_update && 4 * tid < ne;
-  int k = 0;
-  StepRec rec{};
-  float xq[4] = {0.f, 0.f, 0.f, 0.f}, zq[4] = {0.f, 0.f, 0.f, 0.f};
-  float mq[4] = {0.f, 0.f, 0.f, 0.f}, pq[4] = {0.f, 0.f, 0.f, 0.f}, tq[4] = {0.f, 0.f, 0.f, 0.f};
-  int cc0 = 0, l0 = 0;
-  const bool inp = a.inp_mask != nullptr;
-  const size_t plane = (size_t)a.n * LC;
-  if (a.do_update) {
-    k = *a.step_counter;
-    rec = a.steps[k];
-    const int e = e0 + 4 * tid;  // tail threads (no valid element) only load clamped addresses
-    cc0 = e / L;
-    l0 = e - cc0 * L;
-    int cc = cc0, l = l0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const size_t gi = (row0 + l) * C + min(cc, C - 1);
-      xq[u] = a.x[gi];
-      if (a.noise) zq[u] = a.noise[(size_t)k * plane + (size_t)b * LC + min(e + u, LC - 1)];
-      if (inp) {
-        mq[u] = a.inp_mask[row0 + l];
-        pq[u] = a.inp_pose[gi];
-        tq[u] = a.trans[l];
-      }
-      if (++l == L) { l = 0; ++cc; }
-    }
-  }
-  __syncthreads();  // LDS-DMA rows and every operand above have landed
-  ln_stats<RT * 16, 8>(Hs, L, st);
-  bar_lds();
-  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Xn);
-  bar_lds();
-  STAMP(1);
-  if (wave < RT) {
-    f32x4 acc[1][1];
-    go.run(acc, Xn + wave * 16 * Frag<T>::SX, Frag<T>::SX, lane);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) E[(wave * 16 + 4 * g4 + r) * SE + c16] = acc[0][0][r] + bo;
-  }
-  bar_lds();
-  STAMP(2);
-  if (upd) {
-    if (!a.noise)
-      philox_normal4(((uint64_t)rec.seed_hi << 32) | rec.seed_lo, rec.clip_offset + (uint32_t)b, (uint32_t)rec.i,
-                     TAG_STEP, (uint32_t)((e0 >> 2) + tid), zq);
-    int cc = cc0, l = l0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + 4 * tid + u;
-      if (e < e0 + ne) {
-        const float ev = E[l * SE + (cc - c0)];
-        const UpdOut o = upd_math(rec, a.alg, xq[u], ev, false, 0.f, inp, mq[u], pq[u], tq[u], zq[u]);
-        a.x[(row0 + l) * C + cc] = o.xn;
-        if (a.extras) {
-          const size_t ncl = (size_t)b * LC + e;
-          a.extras[0 * plane + ncl] = o.mean;
-          a.extras[1 * plane + ncl] = rec.var;
-          a.extras[2 * plane + ncl] = rec.logvar;
-          a.extras[3 * plane + ncl] = ev;
-          a.extras[4 * plane + ncl] = o.x0;
-          a.extras[5 * plane + ncl] = o.raw;
-        }
-      }
-      if (++l == L) { l = 0; ++cc; }
-    }
-  } else if (!a.do_update && a.do_out) {
-    for (int i = tid; i < ne; i += FT) {
-      const int e = e0 + i, cc = e / L, l = e - cc * L;
-      a.eps_out[(size_t)b * LC + e] = E[l * SE + (cc - c0)];
-    }
-  }
-  STAMP_END(3);
+  ke_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, a.do_update ? *a.step_counter : 0, smem);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -35,43 +35,85 @@ __host__ __device__ constexpr size_t al16(size_t v) { return (v + 15) & ~(size_t
   } while (0)
 
 // profiling: launch span of a kernel from the device-wide realtime counter (the same clock in
-// every XCD): each workgroup's first thread folds its start into min, and after the workgroup's
-// last stores have drained, its end into max (ggd_api.hip reads the pairs back)
+// every XCD).  Each workgroup stores its own start and, after its last stores have drained, its
+// end into slot `slot` = [2][workgroups] — plain stores, no atomics (a same-address atomic from
+// every workgroup serialises past the L2s and cost ~3 us per launch); ggd_api.hip reduces them
 #define SPAN_BEGIN(slot)                                                                        \
   do {                                                                                          \
     if (a.span && threadIdx.x == 0)                                                             \
-      atomicMin(a.span + (slot), (unsigned long long)__builtin_amdgcn_s_memrealtime());         \
+      a.span[(size_t)(slot) * 2 * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x] = \
+          __builtin_amdgcn_s_memrealtime();                                                     \
   } while (0)
 #define SPAN_END(slot)                                                                          \
   do {                                                                                          \
     if (a.span) {                                                                               \
       __syncthreads();                                                                          \
       if (threadIdx.x == 0)                                                                     \
-        atomicMax(a.span + a.span_half + (slot), (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+        a.span[((size_t)(slot) * 2 + 1) * gridDim.x * gridDim.y + blockIdx.y * gridDim.x + blockIdx.x] = \
+            __builtin_amdgcn_s_memrealtime();                                                   \
     }                                                                                           \
   } while (0)
 
 // ------------------------------------------------------------------------------------------
+// Cache policy of the loads / stores that carry data between decoder phases.  CP_KERNEL (0):
+// the phases are separate launches, the kernel boundary makes their data visible.  CP_COH (sc1):
+// the phases run inside one persistent launch (ggd_mega.hip) and hand data to the other
+// workgroups of their clip group -- stores write through and loads skip the CU's vector L1
+// (device-coherent on any placement; with the group on one XCD both stay in its L2).
+// ------------------------------------------------------------------------------------------
+constexpr int CP_KERNEL = 0, CP_COH = 16;
+
 // bounded stores: a raw buffer resource over a clip's output rows; the hardware drops stores
 // past num_records, so padded rows are written without a branch.  (A store under a divergent
 // branch makes the compiler re-wait vmcnt inside every branch, serialising the stores.)
-// ------------------------------------------------------------------------------------------
-struct OutRows {
+template <int CP = CP_KERNEL> struct OutRowsP {
   __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ OutRows(void* base, uint32_t bytes)
+  __device__ __forceinline__ OutRowsP(void* base, uint32_t bytes)
       : r(__builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000)) {}
   __device__ __forceinline__ void put4(uint32_t elem, float4 v) const {  // 4 f32 at elem
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
     const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)(elem * 4), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)(elem * 4), 0, CP);
   }
   template <typename T> __device__ __forceinline__ void put(uint32_t elem, float v) const {
     if constexpr (sizeof(T) == 2)
-      __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, (int)(elem * 2), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, (int)(elem * 2), 0, CP);
     else
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(elem * 4), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(elem * 4), 0, CP);
   }
 };
+using OutRows = OutRowsP<CP_KERNEL>;
+
+// one f32 / 16 bytes at a uniform base + per-lane element offset, with cache policy CP
+template <int CP>
+__device__ __forceinline__ float ld_f32(const float* base, uint32_t idx) {
+  if constexpr (CP == CP_KERNEL) {
+    return base[idx];
+  } else {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(idx * 4), 0, CP));
+  }
+}
+template <int CP>
+__device__ __forceinline__ uint4 ld_16B(const void* base, uint32_t byte_off) {
+  if constexpr (CP == CP_KERNEL) {
+    return *(const uint4*)((const char*)base + byte_off);
+  } else {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, CP);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+}
+
+// thread index as an opaque value: inside the persistent step loop (ggd_mega.hip) values derived
+// from threadIdx.x are loop invariant, and the compiler hoists them out of the loop and keeps
+// them live across every phase (spilling); an opaque index keeps them inside their phase
+__device__ __forceinline__ int ltid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
 
 // ------------------------------------------------------------------------------------------
 // lane-group reductions on DPP (VALU-rate lane moves, no LDS round trip; __shfl_xor lowers to
@@ -111,29 +153,30 @@ __device__ __forceinline__ void bar_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n
 
 // LDS-DMA copy of `rows` rows of `pieces` x 1 KiB from src (row stride ss bytes) into dst
 // (row stride sd bytes): wave w issues the pieces w, w + NW, ...; lane l moves bytes 16l..16l+15.
-template <int NT = NTHREADS>
+template <int NT = NTHREADS, int CP = CP_KERNEL>
 __device__ __forceinline__ void glds_rows(void* dst, size_t sd, const void* src, size_t ss, int rows, int pieces) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
   for (int p = wave; p < rows * pieces; p += NT / 64) {
     const int r = p / pieces, q = p - r * pieces;
     __builtin_amdgcn_global_load_lds((const void*)((const char*)src + r * ss + q * 1024 + lane * 16),
-                                     (lds_void*)((char*)dst + r * sd + q * 1024), 16, 0, 0);
+                                     (lds_void*)((char*)dst + r * sd + q * 1024), 16, 0, CP);
   }
 }
 
 // A [64][SX] operand image of L rows of d_model activations of type T (global rows of FD).
 // bf16 rows are 512 B (two rows per LDS-DMA instruction would cross the pad): registers.
-template <typename T, int NT = NTHREADS> struct ImgStage {
+template <typename T, int NT = NTHREADS, int CP = CP_KERNEL> struct ImgStage {
   static constexpr int NV = sizeof(T) == 2 ? FR * FD * 2 / 16 / NT : 1;
   uint4 v[NV];
   __device__ __forceinline__ void load(T* img, const T* src, int L) {
     if constexpr (sizeof(T) == 4) {
-      glds_rows<NT>(img, sizeof(T) * Frag<T>::SX, src, sizeof(T) * FD, L, 1);
+      glds_rows<NT, CP>(img, sizeof(T) * Frag<T>::SX, src, sizeof(T) * FD, L, 1);
     } else {
+      const int tid = ltid();
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        const int idx = threadIdx.x + i * NT, r = idx >> 5, c = idx & 31;
-        v[i] = *(const uint4*)(src + (size_t)min(r, L - 1) * FD + c * 8);
+        const int idx = tid + i * NT, r = idx >> 5, c = idx & 31;
+        v[i] = ld_16B<CP>(src, (uint32_t)(sizeof(T) * ((size_t)min(r, L - 1) * FD + c * 8)));
       }
     }
   }
@@ -141,9 +184,10 @@ template <typename T, int NT = NTHREADS> struct ImgStage {
   // lets the compiler sink the global load into the branch and serialise the round trips
   __device__ __forceinline__ void store(T* img, int L) {
     if constexpr (sizeof(T) == 2) {
+      const int tid = ltid();
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        const int idx = threadIdx.x + i * NT, r = idx >> 5, c = idx & 31;
+        const int idx = tid + i * NT, r = idx >> 5, c = idx & 31;
         *(uint4*)(img + r * Frag<T>::SX + c * 8) = v[i];
       }
     }
@@ -244,7 +288,7 @@ struct WGemm {
 // statistics: LPR lanes per row (4: the generic GEMM's LN prologue order), each summing 64 / LPR
 // float4 of the row; rows r < NR are computed for threads r * LPR .. r * LPR + LPR - 1
 template <int NR = FR, int LPR = 4>
-__device__ __forceinline__ void ln_stats(const float* Hs, int L, float2* st, int tid = threadIdx.x) {
+__device__ __forceinline__ void ln_stats(const float* Hs, int L, float2* st, int tid = ltid()) {
   constexpr int NV = 64 / LPR;
   const int r = tid / LPR, j = tid % LPR;
   if (r >= NR) return;
@@ -272,7 +316,7 @@ __device__ __forceinline__ void ln_stats(const float* Hs, int L, float2* st, int
 // per SIMD hides nothing: a read-use-read loop pays the LDS latency per row).
 template <typename T, int NT = NTHREADS, int NR = FR, int SXI = Frag<T>::SX>
 __device__ __forceinline__ void ln_apply(const float* Hs, int L, const float2* st, float4 g, float4 bb, T* img,
-                                         int tid = threadIdx.x) {
+                                         int tid = ltid()) {
   constexpr int NW = NT / 64, NI = NR / NW;
   const int c4 = (tid & 63) * 4, r0 = tid >> 6;
   float4 v[NI];
@@ -314,7 +358,7 @@ __device__ __forceinline__ ConvW conv_w(const float* w, const float* b, int c) {
 // written as zeros, so padded keys / values are finite
 template <typename T, bool TRANS, int NR = 64, int NT = NTHREADS>
 __device__ __forceinline__ void conv_rows(T* dst, int S, const float* src, int ss, int rows, ConvW w,
-                                          int tid = threadIdx.x) {
+                                          int tid = ltid()) {
   constexpr int RS = NT / 32, NK = NR / RS;  // row stride between a thread's rows, rows per thread
   static_assert(NR % RS == 0, "rows must split over the thread groups");
   const int c = tid & 31, i0 = tid >> 5;
@@ -372,9 +416,9 @@ __device__ __forceinline__ void att_mma16(f32x4& acc, const float* X, int SX, co
 // rows may hold anything); V^T columns >= Lk must be finite (zeroed by the caller).
 // TO_LDS: `out` is an LDS operand image and every query row (padding included) is written;
 // otherwise `out` is global and rows >= Lq are dropped by the bounded buffer stores.
-template <typename T, int LKT, int QR = FR, bool TO_LDS = false>
+template <typename T, int LKT, int QR = FR, bool TO_LDS = false, int CP = CP_KERNEL>
 __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float scale, T* out, int ldo,
-                                      int tid = threadIdx.x) {
+                                      int tid = ltid()) {
   using A = FAtt<T, QR>;
   const T* Qm = (const T*)(att + A::OQ);
   const T* Km = (const T*)(att + A::OK);
@@ -413,7 +457,7 @@ __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float 
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  const OutRows dst(out, (uint32_t)(sizeof(T) * ((size_t)(Lq - 1) * ldo + FDK)));  // rows >= Lq dropped
+  const OutRowsP<CP> dst(out, (uint32_t)(sizeof(T) * ((size_t)(Lq - 1) * ldo + FDK)));  // rows >= Lq dropped
 #pragma unroll
   for (int ct = 0; ct < FDK / 16; ++ct) {
     f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -424,17 +468,17 @@ __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float 
       if constexpr (TO_LDS)
         out[(rt * 16 + 4 * g4 + r) * ldo + ct * 16 + c16] = from_f32<T>(o[r]);
       else
-        dst.put<T>((uint32_t)((rt * 16 + 4 * g4 + r) * ldo + ct * 16 + c16), o[r]);
+        dst.template put<T>((uint32_t)((rt * 16 + 4 * g4 + r) * ldo + ct * 16 + c16), o[r]);
     }
   }
 }
 
-template <typename T>
+template <typename T, int CP = CP_KERNEL>
 __device__ __forceinline__ void fattn_any(unsigned char* att, int Lq, int Lk, float scale, T* out, int ldo) {
   if (Lk <= 32)
-    fattn<T, 2>(att, Lq, Lk, scale, out, ldo);
+    fattn<T, 2, FR, false, CP>(att, Lq, Lk, scale, out, ldo);
   else
-    fattn<T, 4>(att, Lq, Lk, scale, out, ldo);
+    fattn<T, 4, FR, false, CP>(att, Lq, Lk, scale, out, ldo);
 }
 
 // ------------------------------------------------------------------------------------------

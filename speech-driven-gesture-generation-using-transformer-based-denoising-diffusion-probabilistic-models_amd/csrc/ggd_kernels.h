@@ -121,10 +121,9 @@ struct FusedArgs {
   // (N, L, C), packed emb_x weights, PE table) and written to h_out for KB's residual
   const float* x_emb; const void* w_emb; const float* b_emb; const float* pe; int C;
   unsigned long long* stamps;  // diagnostics: block (0,0) writes s_memtime at phase boundaries
-  // profiling: KB's launch span per (step, layer) from the device realtime clock —
-  // span[slot] = min start over workgroups, span[span_half + slot] = max end,
-  // slot = *step_counter * span_stride (the host offsets span by the layer index)
-  unsigned long long* span; int span_stride, span_half;
+  // profiling: KB's per-workgroup start / end on the device realtime clock, slot
+  // (*step_counter * span_stride + span_layer) holds [2][workgroups] stamps (host reduces min / max)
+  unsigned long long* span; int span_stride, span_layer;
 };
 
 // KE: grid (8 channel blocks, clips); block p owns pose channels [16p, 16p + 16)
@@ -162,12 +161,30 @@ struct PersistArgs {
   unsigned long long* stamps;  // diagnostics: workgroup 0 stamps phase boundaries of iteration 0
 };
 
+// Persistent reverse loop (ggd_mega.hip): ONE launch of 8 workgroups per clip runs iterations
+// k0 .. k0 + n_steps - 1; the phases of ggd_phases.h meet at clip-group barriers instead of
+// kernel boundaries.  Workgroups pick their (clip, part) from their XCD, so a clip's group
+// shares one L2; data between phases is written through / read past L1 (CP_COH).
+struct MegaArgs {
+  const FusedArgs* fa;   // device [n_layers][4]: KA, KB, KC, KD args
+  const FinalArgs* fe;   // device: KE args (do_out, do_update)
+  int n_layers, k0, n_steps;
+  unsigned* ctl;         // control words (MEGA_CTL_WORDS), zeroed before every launch
+  int* status;           // 0 ok, 1 clip-group barrier timed out, 2 workgroups not co-resident
+  unsigned long long* stamps;  // diagnostics: clip 0 / part 0 stamps s_memtime around every barrier
+                               // of the first MEGA_STAMP_STEPS iterations ([phase][2]: done, passed)
+};
+constexpr int MEGA_STAMP_STEPS = 2;
+constexpr int MEGA_CTL_WORDS = 256 + 32 * 16;
+
 // launchers (return hipError_t of the launch)
 hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s);  // 0 KA, 1 KB, 2 KC, 3 KD
 hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s);
 bool fused_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
 bool persist_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
+hipError_t launch_mega(int dtype, int L, const MegaArgs& a, int n, hipStream_t s);
+int mega_capacity(int dtype, int L);   // clips one launch can hold (all workgroups co-resident)
 hipError_t launch_mb(int mode, void* buf, size_t buf_bytes, int arg, int blocks, hipStream_t s);  // ggd_diag.hip
 hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s);

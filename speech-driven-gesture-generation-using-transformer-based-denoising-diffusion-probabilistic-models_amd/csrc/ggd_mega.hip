@@ -1,0 +1,178 @@
+// ggd_mega.hip -- the reverse loop as ONE persistent launch.
+//
+// The per-phase launches of ggd_fused.hip pay a kernel boundary (grid fill / drain, and loads
+// that start cold behind the boundary's cache maintenance) 17 times per denoise step.  Here
+// the same phase bodies (ggd_phases.h, instantiated with CP_COH) run back to back inside one
+// launch of 8 workgroups per clip; consecutive phases of a clip meet at a barrier of the
+// clip's 8 workgroups only (no grid-wide barrier).
+//
+// Placement: dispatch order and the workgroup -> XCD map are not guaranteed, so a workgroup
+// reads its XCC id and takes a ticket on that XCD's counter; clip group g lives on XCD g % 8
+// and is filled from that XCD's tickets, so its 8 members share one L2 (measured on MI355X,
+// scripts/handoff_bench.py: a 64 KiB clip-row gather + barrier costs 2.0 us per round
+// XCD-local against 4.3 us across XCDs).  Workgroups that land on an over-full XCD fill the
+// remaining slots elsewhere.  Correctness does not depend on placement: every byte handed
+// between workgroups is stored write-through (sc1) and drained before the arrival, and read
+// with sc1 loads after the barrier.
+//
+// Residency: every workgroup must be resident at once (one per CU: 132 KiB LDS); the host
+// sizes the grid from the occupancy query, and all waits are bounded -- a barrier that times
+// out sets `status` and its workgroups leave, so a wrong assumption ends the launch instead
+// of hanging the GPU.
+#include "ggd_phases.h"
+
+namespace ggd {
+
+constexpr int MK_SPIN_LIMIT = 1 << 21;   // ~ seconds: only a broken launch ever gets there
+constexpr int MK_ARRIVE = 128, MK_OVF = 144, MK_GROUP = 256;
+
+__device__ __forceinline__ unsigned mk_load(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned mk_add(unsigned* p, unsigned v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// slots of XCD x: 8 x the number of groups g < G with g % 8 == x
+__device__ __forceinline__ int mk_slots(int x, int G) { return x < G ? 8 * ((G - 1 - x) / 8 + 1) : 0; }
+
+// thread 0: (clip << 3 | part), or -1 (status set)
+__device__ int mk_role(const MegaArgs& m, int nwg) {
+  unsigned* ctl = m.ctl;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 7;
+  const int t = (int)mk_add(ctl + xcc * 16, 1u);
+  mk_add(ctl + MK_ARRIVE, 1u);
+  for (int spin = 0; mk_load(ctl + MK_ARRIVE) < (unsigned)nwg; ++spin) {  // every workgroup is resident
+    if (spin > MK_SPIN_LIMIT) {
+      atomicMax(m.status, 2);
+      return -1;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  const int G = nwg / 8;
+  int x = (int)xcc, s = t;
+  if (t >= mk_slots(x, G)) {  // over-full XCD: take the o-th unfilled slot, in XCD order
+    int o = (int)mk_add(ctl + MK_OVF, 1u);
+    for (x = 0; x < 8; ++x) {
+      const int have = min((int)mk_load(ctl + x * 16), mk_slots(x, G)), holes = mk_slots(x, G) - have;
+      if (o < holes) {
+        s = have + o;
+        break;
+      }
+      o -= holes;
+    }
+    if (x == 8) {
+      atomicMax(m.status, 2);
+      return -1;
+    }
+  }
+  return ((x + 8 * (s >> 3)) << 3) | (s & 7);
+}
+
+// barrier of the clip's 8 workgroups; epoch counts the barriers passed so far (+1)
+__device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned epoch, int* status, int* s_ok,
+                                        unsigned long long* st) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores landed
+  __syncthreads();
+  if (st && threadIdx.x == 0) st[2 * (epoch - 1)] = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) {
+    mk_add(ctr, 1u);
+    const unsigned target = 8u * epoch;
+    int ok = 1;
+    for (int spin = 0; mk_load(ctr) < target; ++spin) {
+      if ((spin & 255) == 255 && (spin > MK_SPIN_LIMIT || __hip_atomic_load(status, __ATOMIC_RELAXED,
+                                                                             __HIP_MEMORY_SCOPE_AGENT))) {
+        atomicMax(status, 1);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    *s_ok = ok;
+  }
+  __syncthreads();
+  if (st && threadIdx.x == 0) st[2 * (epoch - 1) + 1] = __builtin_amdgcn_s_memtime();
+  return *s_ok != 0;
+}
+
+template <typename T, int RT>
+__global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int s_role, s_ok;
+  if (threadIdx.x == 0) s_role = mk_role(m, gridDim.x);
+  __syncthreads();
+  const int role = s_role;
+  if (role < 0) return;
+  const int b = role >> 3, part = role & 7;
+  unsigned* ctr = m.ctl + MK_GROUP + b * 16;
+  unsigned epoch = 0;
+  if (m.stamps && role == 0 && threadIdx.x == 0) m.stamps[2 * 17 * MEGA_STAMP_STEPS] = __builtin_amdgcn_s_memtime();
+  for (int k = 0; k < m.n_steps; ++k) {
+    const int it = m.k0 + k;
+    unsigned long long* st = (m.stamps && role == 0 && k < MEGA_STAMP_STEPS) ? m.stamps : nullptr;
+    for (int li = 0; li < m.n_layers; ++li) {
+      const FusedArgs* f = m.fa + 4 * li;
+      asm volatile("" : "+s"(f));  // per-layer arguments are re-read, not held across the loop
+      ka_phase<T, RT, CP_COH>(f[0], part, b, smem);
+      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
+      kb_phase<T, RT, CP_COH>(f[1], part, b, it, smem);
+      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
+      kc_phase<T, RT, CP_COH>(f[2], part, b, smem);
+      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
+      kd_phase<T, RT, CP_COH>(f[3], part, b, smem);
+      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
+    }
+    ke_phase<T, RT, CP_COH>(*m.fe, part, b, it, smem);
+    if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
+  }
+}
+
+template <typename T, int RT>
+static size_t mk_lds() {
+  using PL = Plan<T>;
+  return std::max({PL::KA, PL::KB, PL::KC, PL::KD, PL::KE});
+}
+
+template <typename T, int RT>
+static int mk_capacity_t() {
+  static int cap = -1;
+  if (cap < 0) {
+    (void)hipFuncSetAttribute((const void*)mk_kernel<T, RT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    // residency from the LDS budget (the occupancy query rejects > 64 KiB of dynamic LDS):
+    // one 512-thread workgroup per CU
+    int dev = 0, cus = 0, lds_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
+    (void)hipGetLastError();  // nothing above may leave a sticky error for the next launch
+    const int per = lds_cu >= (int)mk_lds<T, RT>() ? 1 : 0;  // registers: 186+ VGPRs also allow only one
+    cap = std::min(32, per * cus / 8);  // control words hold 32 groups
+  }
+  return cap;
+}
+
+static inline bool mk_rt3(int L) { return L <= 48; }
+
+int mega_capacity(int dtype, int L) {
+  if (dtype == 0) return mk_rt3(L) ? mk_capacity_t<float, 3>() : mk_capacity_t<float, 4>();
+  return mk_rt3(L) ? mk_capacity_t<bf16_t, 3>() : mk_capacity_t<bf16_t, 4>();
+}
+
+hipError_t launch_mega(int dtype, int L, const MegaArgs& a, int n, hipStream_t s) {
+  if (n < 1 || n > mega_capacity(dtype, L)) return hipErrorInvalidValue;
+  const dim3 blk(FT), grid(8 * n);
+  hipError_t e = hipMemsetAsync(a.ctl, 0, sizeof(unsigned) * MEGA_CTL_WORDS, s);
+  if (e != hipSuccess) return e;
+  if (dtype == 0) {
+    if (mk_rt3(L)) hipLaunchKernelGGL((mk_kernel<float, 3>), grid, blk, (mk_lds<float, 3>()), s, a);
+    else hipLaunchKernelGGL((mk_kernel<float, 4>), grid, blk, (mk_lds<float, 4>()), s, a);
+  } else {
+    if (mk_rt3(L)) hipLaunchKernelGGL((mk_kernel<bf16_t, 3>), grid, blk, (mk_lds<bf16_t, 3>()), s, a);
+    else hipLaunchKernelGGL((mk_kernel<bf16_t, 4>), grid, blk, (mk_lds<bf16_t, 4>()), s, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace ggd

@@ -148,7 +148,7 @@ class GaussianSpacedDiffusion(GaussianDiffusion):
         return self._loop(native.DDIM, float(eta), model, shape, model_kwargs, noise, denoise_fn, device, **kw)
 
     def _loop(self, alg, eta, model, shape, model_kwargs, noise, denoise_fn, device, step_noise=None,
-              seed=None, clip_offset=0, n_steps=None, use_graph=True, extras=True):
+              seed=None, clip_offset=0, n_steps=None, use_graph=False, extras=True):
         assert isinstance(shape, (tuple, list)) and len(shape) == 3, "shape must be (N, C, L)"
         model_kwargs = dict(model_kwargs or {})
         wav = model_kwargs.pop("wav", None)

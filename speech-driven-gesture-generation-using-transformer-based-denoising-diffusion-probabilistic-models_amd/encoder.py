@@ -14,7 +14,11 @@ temporal heads -> shared Linear(32 -> d_model).
 
 MI355X mapping: the STFT is a real-DFT GEMM against a cached [cos | sin] basis
 (1024 x 1026) and the mel projection a second GEMM; the convolutions go to
-MIOpen.  A HIP implicit-GEMM port is the next scope row.
+MIOpen.  The ~270 launches of one chunk are captured once per (chunk, wav length)
+as a hipGraph (torch.cuda.CUDAGraph) and replayed: issued eagerly from Python the
+chunk is host-bound (11.6 ms for 32 clips in chunks of 8 against 3.4 ms replayed
+as one 32-clip graph, MI355X).  A HIP implicit-GEMM port is the next scope row
+(SURVEY.md 8f rank 1).
 """
 import math
 
@@ -75,7 +79,8 @@ class SpeechEncoder:
         feat = feat.reshape(n, c * h, w).transpose(1, 2)
         return F.linear(feat, self.w[fc + ".weight"], self.w[fc + ".bias"])
 
-    CHUNK = 8  # clips per encoder call: fixed, so a clip's features never depend on its batch
+    CHUNK = 32  # clips per encoder call: fixed, so a clip's features never depend on its batch
+    use_graph = True  # replay each chunk as a captured graph (cuda devices)
 
     @th.no_grad()
     def __call__(self, wav):
@@ -94,8 +99,30 @@ class SpeechEncoder:
         # 1e-6 between two identical calls); the deterministic solvers make the memory a
         # pure function of the clip's audio
         with th.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
-            outs = [self._encode(wav[i:i + self.CHUNK]) for i in range(0, wav.shape[0], self.CHUNK)]
+            outs = [self._run_chunk(wav[i:i + self.CHUNK]) for i in range(0, wav.shape[0], self.CHUNK)]
         return tuple(th.cat([o[k] for o in outs])[:n] for k in range(3))
+
+    def _run_chunk(self, x):
+        if not (self.use_graph and self.device.type == "cuda"):
+            return self._encode(x)
+        key = tuple(x.shape)
+        graphs = self.__dict__.setdefault("_graphs", {})
+        if key not in graphs:
+            static_in = x.clone()
+            side = th.cuda.Stream(self.device)
+            side.wait_stream(th.cuda.current_stream(self.device))
+            with th.cuda.stream(side):
+                self._encode(static_in)                    # library / algorithm selection
+            th.cuda.current_stream(self.device).wait_stream(side)
+            g = th.cuda.CUDAGraph()
+            with th.cuda.graph(g):
+                static_out = self._encode(static_in)
+            graphs[key] = (g, static_in, static_out)
+        g, static_in, static_out = graphs[key]
+        static_in.copy_(x)
+        g.replay()
+        # the next replay overwrites the static outputs
+        return tuple(o.clone() for o in static_out)
 
     def _encode(self, wav):
         x = self.mel(wav) + 1e-6

@@ -11,8 +11,8 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libggd.so")
-SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_persist.hip", "ggd_diag.hip", "ggd_api.hip"]
-HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_fusedlib.h", os.path.join("..", "..", "include", "ggd.h")]
+SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_diag.hip", "ggd_api.hip"]
+HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_fusedlib.h", "ggd_phases.h", os.path.join("..", "..", "include", "ggd.h")]
 
 GGD_OK, GGD_IGNORED = 0, 1
 GGD_ERR_ARG, GGD_ERR_UNSUPPORTED, GGD_ERR_HIP, GGD_ERR_STATE, GGD_ERR_NAME = -1, -2, -3, -4, -5
@@ -24,7 +24,7 @@ DDPM, DDIM = 0, 1
 EXPORTS = [
     "ggd_create", "ggd_destroy", "ggd_last_error", "ggd_load_weight", "ggd_finalize_weights",
     "ggd_set_schedule", "ggd_set_memory", "ggd_denoise", "ggd_posterior_step", "ggd_sample",
-    "ggd_set_profiling", "ggd_kernel_time", "ggd_diag", "ggd_version",
+    "ggd_set_profiling", "ggd_kernel_time", "ggd_profile_kind", "ggd_diag", "ggd_version",
 ]
 
 
@@ -105,6 +105,7 @@ def load():
         "ggd_sample": (ctypes.c_int, [CTX, P(SampleArgs), VP]),
         "ggd_set_profiling": (ctypes.c_int, [CTX, I32]),
         "ggd_kernel_time": (ctypes.c_int, [CTX, I32, P(ctypes.c_double), P(I64)]),
+        "ggd_profile_kind": (ctypes.c_int, [CTX]),
         "ggd_diag": (ctypes.c_int, [CTX, I32, VP, I32, I32, VP]),
         "ggd_version": (ctypes.c_char_p, []),
     }
