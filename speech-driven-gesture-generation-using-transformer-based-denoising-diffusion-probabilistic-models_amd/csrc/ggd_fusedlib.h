@@ -20,6 +20,20 @@ template <typename T> struct Frag {
 
 __host__ __device__ constexpr size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
 
+// Global-memory view of a pointer.  Pointers read out of argument structs in memory (the
+// persistent loop's per-phase arguments) are generic, and generic loads are FLAT loads, which
+// count against lgkmcnt too: every LDS wait of a phase would then also wait for its in-flight
+// weight stream.  The kernels' own arguments are promoted to global by the compiler anyway.
+template <typename T> using gptr = const __attribute__((address_space(1))) T*;
+template <typename T> __device__ __forceinline__ gptr<T> G(const T* p) { return (gptr<T>)p; }
+// 16 bytes (float4) through the global view
+__device__ __forceinline__ float4 ld_f4(const float* p) {
+  typedef __attribute__((ext_vector_type(4))) float f32v4;
+  const f32v4 v = *G((const f32v4*)p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+
 // diagnostics: phase stamps of workgroup (0, 0), written only when the stamp buffer is set
 #define STAMP(i)                                                                                \
   do {                                                                                          \
@@ -88,7 +102,7 @@ using OutRows = OutRowsP<CP_KERNEL>;
 template <int CP>
 __device__ __forceinline__ float ld_f32(const float* base, uint32_t idx) {
   if constexpr (CP == CP_KERNEL) {
-    return base[idx];
+    return G(base)[idx];
   } else {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(idx * 4), 0, CP));
@@ -97,7 +111,9 @@ __device__ __forceinline__ float ld_f32(const float* base, uint32_t idx) {
 template <int CP>
 __device__ __forceinline__ uint4 ld_16B(const void* base, uint32_t byte_off) {
   if constexpr (CP == CP_KERNEL) {
-    return *(const uint4*)((const char*)base + byte_off);
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+    const u32x4 v = *G((const u32x4*)((const char*)base + byte_off));
+    return make_uint4(v.x, v.y, v.z, v.w);
   } else {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
@@ -228,7 +244,11 @@ struct WGemm {
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int k = 0; k < G; ++k) wb[j][k] = W[((size_t)tiles[j] * kt_total + k0 + g * G + k) * 64 + lane];
+      for (int k = 0; k < G; ++k) {
+        typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+        const u32x4 v = ggd::G((const u32x4*)W)[((size_t)tiles[j] * kt_total + k0 + g * G + k) * 64 + lane];
+        wb[j][k] = make_uint4(v.x, v.y, v.z, v.w);
+      }
   }
   // group 0 must have been loaded; tiles j >= nj_on are skipped (wave-uniform).  bf16: the A
   // fragments of k step k + 1 are read from LDS before the MFMAs of step k issue, so the LDS
@@ -350,7 +370,7 @@ __device__ __forceinline__ void ln_apply(const float* Hs, int L, const float2* s
 // ------------------------------------------------------------------------------------------
 struct ConvW { float w0, w1, w2, b; };
 __device__ __forceinline__ ConvW conv_w(const float* w, const float* b, int c) {
-  return ConvW{w[c * 3 + 0], w[c * 3 + 1], w[c * 3 + 2], b[c]};
+  return ConvW{G(w)[c * 3 + 0], G(w)[c * 3 + 1], G(w)[c * 3 + 2], G(b)[c]};
 }
 
 // dst rows (or transposed columns) i < 64 = conv over rows i-1, i, i+1 of the f32 source (row

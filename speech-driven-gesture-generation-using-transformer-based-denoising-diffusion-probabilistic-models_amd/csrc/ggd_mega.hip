@@ -109,11 +109,14 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m) {
   unsigned* ctr = m.ctl + MK_GROUP + b * 16;
   unsigned epoch = 0;
   if (m.stamps && role == 0 && threadIdx.x == 0) m.stamps[2 * 17 * MEGA_STAMP_STEPS] = __builtin_amdgcn_s_memtime();
+  // per-phase arguments as constant-address-space objects: field reads are scalar loads
+  typedef const __attribute__((address_space(4))) FusedArgs* cfa_t;
+  typedef const __attribute__((address_space(4))) FinalArgs* cfe_t;
   for (int k = 0; k < m.n_steps; ++k) {
     const int it = m.k0 + k;
     unsigned long long* st = (m.stamps && role == 0 && k < MEGA_STAMP_STEPS) ? m.stamps : nullptr;
     for (int li = 0; li < m.n_layers; ++li) {
-      const FusedArgs* f = m.fa + 4 * li;
+      cfa_t f = (cfa_t)m.fa + 4 * li;
       asm volatile("" : "+s"(f));  // per-layer arguments are re-read, not held across the loop
       ka_phase<T, RT, CP_COH>(f[0], part, b, smem);
       if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
@@ -124,15 +127,19 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m) {
       kd_phase<T, RT, CP_COH>(f[3], part, b, smem);
       if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
     }
-    ke_phase<T, RT, CP_COH>(*m.fe, part, b, it, smem);
+    cfe_t fe = (cfe_t)m.fe;
+    asm volatile("" : "+s"(fe));
+    ke_phase<T, RT, CP_COH>(*fe, part, b, it, smem);
     if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
   }
 }
 
+// LDS: the phases' private regions sit behind the resident residual rows (Res<T>); the kernel's
+// static words (role, barrier verdict) need room beside the dynamic allocation
+constexpr size_t MK_LDS_STATIC = 256;
 template <typename T, int RT>
 static size_t mk_lds() {
-  using PL = Plan<T>;
-  return std::max({PL::KA, PL::KB, PL::KC, PL::KD, PL::KE});
+  return 160 * 1024 - MK_LDS_STATIC;
 }
 
 template <typename T, int RT>

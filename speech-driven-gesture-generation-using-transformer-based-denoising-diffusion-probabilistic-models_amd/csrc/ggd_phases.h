@@ -36,6 +36,26 @@ namespace ggd {
 
 constexpr int FT = 512;  // threads of the fused kernels: 8 waves, two per SIMD
 
+// a step record through the global view (see G in ggd_fusedlib.h)
+__device__ __forceinline__ StepRec ld_rec(const StepRec* p) {
+  static_assert(sizeof(StepRec) % 4 == 0, "step records are whole dwords");
+  StepRec r;
+  unsigned* d = (unsigned*)&r;
+  const gptr<unsigned> src = G((const unsigned*)p);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(StepRec) / 4); ++i) d[i] = src[i];
+  return r;
+}
+
+// Residual rows resident in LDS (persistent loop, bf16): a workgroup keeps its clip's f32
+// residual rows (Hs, at LDS offset 0) from KA through KB and KC to KD -- KB and KC compute the
+// full rows redundantly anyway -- so only KA / KE gather them and only KD publishes them.
+// (As separate launches, or with f32 images that do not fit beside them, Hs is re-read.)
+template <typename T, int CP> struct Res {
+  static constexpr bool ON = CP == CP_COH && sizeof(T) == 2;
+  static constexpr size_t BASE = ON ? Plan<T>::HS : 0;  // start of the phase-private LDS
+};
+
 // Hs[i][n] += A[i] . W[n] + bias[n] for all 64 rows; wave w owns the NJ column tiles
 // NJ w .. NJ w + NJ - 1.  The accumulators start from Hs + bias (one batch of LDS reads issued
 // before the MFMAs), so the epilogue is a plain store, not a dependent read-modify-write.
@@ -76,19 +96,22 @@ __device__ __forceinline__ void store_rows(float* dst, const float* Hs, int L, i
 // ------------------------------------------------------------------------------------------
 // KA: [emb_x + PE (layer 0)] + LN1 + QKV(head) + conv + self-attention      grid (heads, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T, int RT, int CP>
-__device__ __forceinline__ void ka_phase(const FusedArgs& a, int h, int b, unsigned char* smem) {
+template <typename T, int RT, int CP, typename FA>
+__device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned char* smem) {
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF, SY = 96 + 4;
   const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
   const int L = a.L, c16 = lane & 15, g4 = lane >> 4;
-  T* Xn = (T*)smem;
-  float2* st = (float2*)(smem + PL::IMG);
-  unsigned char* un = smem + PL::IMG + PL::ST;
-  float* Hs = (float*)un;
+  using R = Res<T, CP>;
+  unsigned char* pv = smem + R::BASE;
+  T* Xn = (T*)pv;
+  float2* st = (float2*)(pv + PL::IMG);
+  unsigned char* un = pv + PL::IMG + PL::ST;
+  float* Hs = R::ON ? (float*)smem : (float*)un;
   float* Y = (float*)un;
   unsigned char* att = un + PL::Y_KA;
-  const FusedLayer& w = a.w;
+  static_assert(R::BASE + PL::IMG + PL::ST + PL::Y_KA + FAtt<T>::BYTES <= 160 * 1024 - 256, "KA LDS");
+  const auto& w = a.w;
 
   STAMP(0);
   const bool emb = a.x_emb != nullptr;  // layer 0: h = emb_x(x) + PE computed here
@@ -100,8 +123,8 @@ __device__ __forceinline__ void ka_phase(const FusedArgs& a, int h, int b, unsig
     ge.tiles[0] = 2 * wave;
     ge.tiles[1] = 2 * wave + 1;
     ge.load(0, lane);
-    be[0] = a.b_emb[(2 * wave) * 16 + c16];
-    be[1] = a.b_emb[(2 * wave + 1) * 16 + c16];
+    be[0] = G(a.b_emb)[(2 * wave) * 16 + c16];
+    be[1] = G(a.b_emb)[(2 * wave + 1) * 16 + c16];
     const int C = a.C;
 #pragma unroll
     for (int i = 0; i < NXV; ++i) {
@@ -114,8 +137,8 @@ __device__ __forceinline__ void ka_phase(const FusedArgs& a, int h, int b, unsig
   WGemm<T, 1, KT, RT> gm(w.qkv, KT, 0);
   gm.tiles[0] = h * 6 + min(wave, 5);
   gm.load(0, lane);
-  const float bias = w.qkv_b[h * 96 + min(wave, 5) * 16 + c16];
-  const float4 lg = *(const float4*)(w.ln1_g + (tid & 63) * 4), lb = *(const float4*)(w.ln1_b + (tid & 63) * 4);
+  const float bias = G(w.qkv_b)[h * 96 + min(wave, 5) * 16 + c16];
+  const float4 lg = ld_f4(w.ln1_g + (tid & 63) * 4), lb = ld_f4(w.ln1_b + (tid & 63) * 4);
   const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
               cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
@@ -130,14 +153,14 @@ __device__ __forceinline__ void ka_phase(const FusedArgs& a, int h, int b, unsig
     bar_lds();
     residual_gemm<T, KTE, 2, RT>(Hs, Xb, SB, ge, be, lane, wave);
     bar_lds();
-    store_rows<CP>(a.h + (size_t)b * L * FD, Hs, L, h);  // the residual rows KB reads
+    if (!R::ON) store_rows<CP>(a.h + (size_t)b * L * FD, Hs, L, h);  // the residual rows KB reads
   }
   ln_stats<RT * 16, 8>(Hs, L, st);
   bar_lds();
   ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Xn);
   bar_lds();
   STAMP(1);
-  // Hs is dead from here: Y and the attention images overlay it
+  // (kernel path) Hs is dead from here: Y and the attention images overlay it
   {
     f32x4 acc[RT][1];
     gm.run(acc, Xn, Frag<T>::SX, lane, nq);
@@ -164,28 +187,31 @@ __device__ __forceinline__ void ka_phase(const FusedArgs& a, int h, int b, unsig
 // ------------------------------------------------------------------------------------------
 // KB: SA out-proj + residual + LN2 + cross-attn Q(head) + conv + cross-attention  (heads, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T, int RT, int CP>
-__device__ __forceinline__ void kb_phase(const FusedArgs& a, int h, int b, int it, unsigned char* smem) {
+template <typename T, int RT, int CP, typename FA>
+__device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsigned char* smem) {
   using PL = Plan<T>;
   using AT = FAtt<T>;
   constexpr int KT = FD / Frag<T>::KF, SYQ = FDK + 4;
   const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
   const int L = a.L, Lk = 1 + a.Ts, c16 = lane & 15, g4 = lane >> 4;
-  T* Ax = (T*)smem;                   // O_sa image, then LN2(h) image
-  float2* st = (float2*)(smem + PL::IMG);
-  unsigned char* un = smem + PL::IMG + PL::ST;
-  float* Hs = (float*)un;
+  using R = Res<T, CP>;
+  unsigned char* pv = smem + R::BASE;
+  T* Ax = (T*)pv;                     // O_sa image, then LN2(h) image
+  float2* st = (float2*)(pv + PL::IMG);
+  unsigned char* un = pv + PL::IMG + PL::ST;
+  float* Hs = R::ON ? (float*)smem : (float*)un;
   float* Yq = (float*)un;
   float* raw = (float*)(un + PL::YQ);
   unsigned char* att = un + PL::YQ + PL::RAW;
-  const FusedLayer& w = a.w;
+  static_assert(R::BASE + PL::IMG + PL::ST + PL::YQ + PL::RAW + FAtt<T>::BYTES <= 160 * 1024 - 256, "KB LDS");
+  const auto& w = a.w;
   const size_t row0 = (size_t)b * L;
 
   STAMP(0);
   const int span_slot = it * a.span_stride + a.span_layer;
   SPAN_BEGIN(span_slot);
-  const int t = a.t_clip ? a.t_clip[b] : a.steps[it].t_orig;
-  glds_rows<FT, CP>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
+  const int t = a.t_clip ? a.t_clip[b] : G(a.steps)[it].t_orig;
+  if (!R::ON) glds_rows<FT, CP>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
   ImgStage<T, FT, CP> so;
   so.load(Ax, (const T*)a.o_sa + row0 * FD, L);
   WGemm<T, 2, KT, RT> go(w.o_sa, KT, 0);
@@ -193,9 +219,9 @@ __device__ __forceinline__ void kb_phase(const FusedArgs& a, int h, int b, int i
   go.tiles[1] = 2 * wave + 1;
   go.load(0, lane);
   float bo[2];
-  bo[0] = w.o_sa_b[(2 * wave) * 16 + c16];
-  bo[1] = w.o_sa_b[(2 * wave + 1) * 16 + c16];
-  const float4 lg = *(const float4*)(w.ln2_g + (tid & 63) * 4), lb = *(const float4*)(w.ln2_b + (tid & 63) * 4);
+  bo[0] = G(w.o_sa_b)[(2 * wave) * 16 + c16];
+  bo[1] = G(w.o_sa_b)[(2 * wave + 1) * 16 + c16];
+  const float4 lg = ld_f4(w.ln2_g + (tid & 63) * 4), lb = ld_f4(w.ln2_b + (tid & 63) * 4);
   so.store(Ax, L);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   STAMP(1);
@@ -203,7 +229,7 @@ __device__ __forceinline__ void kb_phase(const FusedArgs& a, int h, int b, int i
   WGemm<T, 1, KT, RT> gq(w.q_ca, KT, 0);
   gq.tiles[0] = 2 * h + (wave & 1);
   if (wave < 2) gq.load(0, lane);
-  const float bq = w.q_ca_b[h * FDK + (wave & 1) * 16 + c16];
+  const float bq = G(w.q_ca_b)[h * FDK + (wave & 1) * 16 + c16];
   const ConvW cq = conv_w(w.ca_qw, w.ca_qb, tid & 31), ck = conv_w(w.ca_kw, w.ca_kb, tid & 31),
               cv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
   // memory K / V of head h (pre-conv): row 0 = the step token of this clip's t, rows 1.. the
@@ -212,7 +238,7 @@ __device__ __forceinline__ void kb_phase(const FusedArgs& a, int h, int b, int i
   auto kv_load = [&](int i) -> float4 {
     const int v = tid + i * FT, r = min(v >> 4, Lk - 1), half = (v >> 3) & 1, q = v & 7;
     const float* src = r == 0 ? w.kv_step + (size_t)t * 2 * FD : w.kv_mem + ((size_t)b * a.Ts + (r - 1)) * 2 * FD;
-    return *(const float4*)(src + half * FD + h * FDK + q * 4);
+    return ld_f4(src + half * FD + h * FDK + q * 4);
   };
   residual_gemm<T, KT, 2, RT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
   // issued after the out-projection: t comes from a two-load dependent chain, which must not
@@ -221,13 +247,13 @@ __device__ __forceinline__ void kb_phase(const FusedArgs& a, int h, int b, int i
   const float4 kv0 = kv_load(0), kv1 = kv_load(1);
   bar_lds();
   STAMP(2);
-  store_rows<CP>(a.h_out + row0 * FD, Hs, L, h);
+  if (!R::ON) store_rows<CP>(a.h_out + row0 * FD, Hs, L, h);
   ln_stats<RT * 16, 8>(Hs, L, st);
   bar_lds();
   ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Ax);
   bar_lds();
   STAMP(3);
-  // Hs is dead: Yq, raw and the attention images overlay it
+  // (kernel path) Hs is dead: Yq, raw and the attention images overlay it
   auto kv_store = [&](int i, float4 val) {
     const int v = tid + i * FT, r = v >> 4, half = (v >> 3) & 1, q = v & 7;
     if (r < Lk) *(float4*)(raw + half * (FLK + 2) * FDK + (r + 1) * FDK + q * 4) = val;
@@ -262,21 +288,23 @@ __device__ __forceinline__ void kb_phase(const FusedArgs& a, int h, int b, int i
 // ------------------------------------------------------------------------------------------
 // KC: CA out-proj + residual + LN3 + FFN-up chunk (128 hidden) + ReLU^2   grid (8 chunks, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T, int RT, int CP>
-__device__ __forceinline__ void kc_phase(const FusedArgs& a, int c, int b, unsigned char* smem) {
+template <typename T, int RT, int CP, typename FA>
+__device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned char* smem) {
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF;
   const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
   const int L = a.L, c16 = lane & 15, g4 = lane >> 4;
-  T* Ax = (T*)smem;
-  float2* st = (float2*)(smem + PL::IMG);
-  float* Hs = (float*)(smem + PL::IMG + PL::ST);
-  const FusedLayer& w = a.w;
+  using R = Res<T, CP>;
+  unsigned char* pv = smem + R::BASE;
+  T* Ax = (T*)pv;
+  float2* st = (float2*)(pv + PL::IMG);
+  float* Hs = R::ON ? (float*)smem : (float*)(pv + PL::IMG + PL::ST);
+  const auto& w = a.w;
   const size_t row0 = (size_t)b * L;
   const int h = c;  // STAMP uses (h, b)
 
   STAMP(0);
-  glds_rows<FT, CP>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
+  if (!R::ON) glds_rows<FT, CP>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
   ImgStage<T, FT, CP> so;
   so.load(Ax, (const T*)a.o_ca + row0 * FD, L);
   WGemm<T, 2, KT, RT> go(w.o_ca, KT, 0);
@@ -284,20 +312,20 @@ __device__ __forceinline__ void kc_phase(const FusedArgs& a, int c, int b, unsig
   go.tiles[1] = 2 * wave + 1;
   go.load(0, lane);
   float bo[2];
-  bo[0] = w.o_ca_b[(2 * wave) * 16 + c16];
-  bo[1] = w.o_ca_b[(2 * wave + 1) * 16 + c16];
-  const float4 lg = *(const float4*)(w.ln3_g + (tid & 63) * 4), lb = *(const float4*)(w.ln3_b + (tid & 63) * 4);
+  bo[0] = G(w.o_ca_b)[(2 * wave) * 16 + c16];
+  bo[1] = G(w.o_ca_b)[(2 * wave + 1) * 16 + c16];
+  const float4 lg = ld_f4(w.ln3_g + (tid & 63) * 4), lb = ld_f4(w.ln3_b + (tid & 63) * 4);
   so.store(Ax, L);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   STAMP(1);
   WGemm<T, 1, KT, RT> gf(w.ff1, KT, 0);  // prefetch: in flight across the out-projection
   gf.tiles[0] = 8 * c + wave;
   gf.load(0, lane);
-  const float bf = w.ff1_b[(8 * c + wave) * 16 + c16];
+  const float bf = G(w.ff1_b)[(8 * c + wave) * 16 + c16];
   residual_gemm<T, KT, 2, RT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
   bar_lds();
   STAMP(2);
-  store_rows<CP>(a.h_out + row0 * FD, Hs, L, c);
+  if (!R::ON) store_rows<CP>(a.h_out + row0 * FD, Hs, L, c);
   ln_stats<RT * 16, 8>(Hs, L, st);
   bar_lds();
   ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Ax);
@@ -322,27 +350,36 @@ __device__ __forceinline__ void kc_phase(const FusedArgs& a, int c, int b, unsig
 // wave w: column tile (w & 1), K quarter (w >> 1); the four partial sums meet through LDS and
 // are added in a fixed order (deterministic).
 // ------------------------------------------------------------------------------------------
-template <typename T, int RT, int CP>
-__device__ __forceinline__ void kd_phase(const FusedArgs& a, int c, int b, unsigned char* smem) {
+template <typename T, int RT, int CP, typename FA>
+__device__ __forceinline__ void kd_phase(const FA& a, int c, int b, unsigned char* smem) {
   using PL = Plan<T>;
   constexpr int KP = PL::KP, NP = 4 * FD / KP, SA = KP + Frag<T>::PT;
   constexpr int KTT = 4 * FD / Frag<T>::KF, KTW = KP / Frag<T>::KF / 4;  // k steps: total, per wave per pass
   const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
   const int L = a.L, c16 = lane & 15, g4 = lane >> 4, tile = 2 * c + (wave & 1), kq = wave >> 1;
   T* Hd = (T*)smem;
-  const FusedLayer& w = a.w;
+  const auto& w = a.w;
   const size_t row0 = (size_t)b * L;
   const int col = tile * 16 + c16;
   const int h = c;  // STAMP uses (h, b)
 
   STAMP(0);
   float res[RT][4];
+  if constexpr (Res<T, CP>::ON) {  // the residual rows KC left in LDS; then the image may overlay them
+    const float* Hs = (const float*)smem;
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      res[rt][r] = ld_f32<CP>(a.h, (uint32_t)((row0 + min(rt * 16 + 4 * g4 + r, L - 1)) * FD + col));
-  const float bias = w.ff2_b[col];
+      for (int r = 0; r < 4; ++r) res[rt][r] = Hs[min(rt * 16 + 4 * g4 + r, L - 1) * SH + col];
+    bar_lds();
+  } else {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        res[rt][r] = ld_f32<CP>(a.h, (uint32_t)((row0 + min(rt * 16 + 4 * g4 + r, L - 1)) * FD + col));
+  }
+  const float bias = G(w.ff2_b)[col];
   f32x4 acc[RT][1];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) acc[rt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -390,8 +427,8 @@ __device__ __forceinline__ void kd_phase(const FusedArgs& a, int c, int b, unsig
 // eps for row tile w; the update of the block's L x 16 elements is one Philox quad per thread.
 // The next step's emb_x + PE is computed by that step's first KA (x_emb).
 // ------------------------------------------------------------------------------------------
-template <typename T, int RT, int CP>
-__device__ __forceinline__ void ke_phase(const FinalArgs& a, int p, int b, int k, unsigned char* smem) {
+template <typename T, int RT, int CP, typename FA>
+__device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsigned char* smem) {
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF, SE = 16 + 4;
   const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
@@ -410,8 +447,8 @@ __device__ __forceinline__ void ke_phase(const FinalArgs& a, int p, int b, int k
   WGemm<T, 1, KT, 1> go(a.w_out, KT, 0);  // waves 0-3: row tile w of channel tile p
   go.tiles[0] = p;
   go.load(0, lane);
-  const float bo = a.b_out[p * 16 + c16];
-  const float4 lg = *(const float4*)(a.ln_g + (tid & 63) * 4), lb = *(const float4*)(a.ln_b + (tid & 63) * 4);
+  const float bo = G(a.b_out)[p * 16 + c16];
+  const float4 lg = ld_f4(a.ln_g + (tid & 63) * 4), lb = ld_f4(a.ln_b + (tid & 63) * 4);
   // the thread's quad: elements e0 + 4 tid .. + 3 (issued now, consumed after the GEMM)
   const bool upd = a.do_update && 4 * tid < ne;
   StepRec rec{};
@@ -421,7 +458,7 @@ __device__ __forceinline__ void ke_phase(const FinalArgs& a, int p, int b, int k
   const bool inp = a.inp_mask != nullptr;
   const size_t plane = (size_t)a.n * LC;
   if (a.do_update) {
-    rec = a.steps[k];
+    rec = ld_rec(a.steps + k);
     const int e = e0 + 4 * tid;  // tail threads (no valid element) only load clamped addresses
     cc0 = e / L;
     l0 = e - cc0 * L;
@@ -430,11 +467,11 @@ __device__ __forceinline__ void ke_phase(const FinalArgs& a, int p, int b, int k
     for (int u = 0; u < 4; ++u) {
       const size_t gi = (row0 + l) * C + min(cc, C - 1);
       xq[u] = ld_f32<CP>(a.x, (uint32_t)gi);
-      if (a.noise) zq[u] = a.noise[(size_t)k * plane + (size_t)b * LC + min(e + u, LC - 1)];
+      if (a.noise) zq[u] = G(a.noise)[(size_t)k * plane + (size_t)b * LC + min(e + u, LC - 1)];
       if (inp) {
-        mq[u] = a.inp_mask[row0 + l];
-        pq[u] = a.inp_pose[gi];
-        tq[u] = a.trans[l];
+        mq[u] = G(a.inp_mask)[row0 + l];
+        pq[u] = G(a.inp_pose)[gi];
+        tq[u] = G(a.trans)[l];
       }
       if (++l == L) { l = 0; ++cc; }
     }
