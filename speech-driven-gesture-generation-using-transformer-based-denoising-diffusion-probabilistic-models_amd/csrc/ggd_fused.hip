@@ -7,31 +7,41 @@ template <typename T, int RT>
 __global__ void __launch_bounds__(FT) ka_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (a.bump_counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(a.step_counter, 1);
-  ka_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, smem);
+  KAPre<T, RT> pre = ka_pre<T, RT>(a, blockIdx.x, ltid() >> 6);
+  pre.load(ltid() & 63);
+  ka_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, smem, pre);
 }
 
 template <typename T, int RT>
 __global__ void __launch_bounds__(FT) kb_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  kb_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, a.t_clip ? 0 : *a.step_counter, smem);
+  KBPre<T, RT> pre(a, ltid() >> 6);
+  pre.load(ltid() & 63);
+  kb_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, a.t_clip ? 0 : *a.step_counter, smem, pre);
 }
 
 template <typename T, int RT>
 __global__ void __launch_bounds__(FT) kc_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  kc_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, smem);
+  KCPre<T, RT> pre(a, blockIdx.x, ltid() >> 6);
+  pre.load(ltid() & 63);
+  kc_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, smem, pre);
 }
 
 template <typename T, int RT>
 __global__ void __launch_bounds__(FT) kd_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  kd_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, smem);
+  KDPre<T, RT> pre(a, blockIdx.x, ltid() >> 6);
+  pre.load(ltid() & 63);
+  kd_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, smem, pre);
 }
 
 template <typename T, int RT>
 __global__ void __launch_bounds__(FT) ke_kernel(FinalArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  ke_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, a.do_update ? *a.step_counter : 0, smem);
+  KEPre<T, RT> pre = ke_pre<T, RT>(a, blockIdx.x);
+  pre.load(ltid() & 63);
+  ke_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, a.do_update ? *a.step_counter : 0, smem, pre);
 }
 
 // ------------------------------------------------------------------------------------------

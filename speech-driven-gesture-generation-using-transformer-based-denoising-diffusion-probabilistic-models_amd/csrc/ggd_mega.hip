@@ -71,14 +71,18 @@ __device__ int mk_role(const MegaArgs& m, int nwg) {
   return ((x + 8 * (s >> 3)) << 3) | (s & 7);
 }
 
-// barrier of the clip's 8 workgroups; epoch counts the barriers passed so far (+1)
+// barrier of the clip's 8 workgroups; epoch counts the barriers passed so far (+1).  After the
+// arrival every wave issues `prefetch` (the next phase's weight fragments); the exit barrier does
+// not wait for vector memory, so that stream stays in flight across the wait.
+template <typename F>
 __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned epoch, int* status, int* s_ok,
-                                        unsigned long long* st) {
+                                        unsigned long long* st, F&& prefetch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores landed
   __syncthreads();
   if (st && threadIdx.x == 0) st[2 * (epoch - 1)] = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) mk_add(ctr, 1u);
+  prefetch();
   if (threadIdx.x == 0) {
-    mk_add(ctr, 1u);
     const unsigned target = 8u * epoch;
     int ok = 1;
     for (int spin = 0; mk_load(ctr) < target; ++spin) {
@@ -92,7 +96,7 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned epoch, int* stat
     }
     *s_ok = ok;
   }
-  __syncthreads();
+  bar_lds();
   if (st && threadIdx.x == 0) st[2 * (epoch - 1) + 1] = __builtin_amdgcn_s_memtime();
   return *s_ok != 0;
 }
@@ -105,32 +109,42 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m) {
   __syncthreads();
   const int role = s_role;
   if (role < 0) return;
-  const int b = role >> 3, part = role & 7;
+  const int b = role >> 3, part = role & 7, lane = ltid() & 63, wave = ltid() >> 6;
   unsigned* ctr = m.ctl + MK_GROUP + b * 16;
   unsigned epoch = 0;
   if (m.stamps && role == 0 && threadIdx.x == 0) m.stamps[2 * 17 * MEGA_STAMP_STEPS] = __builtin_amdgcn_s_memtime();
   // per-phase arguments as constant-address-space objects: field reads are scalar loads
   typedef const __attribute__((address_space(4))) FusedArgs* cfa_t;
   typedef const __attribute__((address_space(4))) FinalArgs* cfe_t;
+  const int NL = m.n_layers;
+  cfa_t fa0 = (cfa_t)m.fa;
+  cfe_t fe = (cfe_t)m.fe;
+  // weights of the next phase, issued at the barrier in front of it (the first one here); KA's
+  // and KE's tiles share one register set (Pre1)
+  Pre1<T, RT> pn = ka_pre<T, RT>(fa0[0], part, wave);
+  pn.load(lane);
   for (int k = 0; k < m.n_steps; ++k) {
     const int it = m.k0 + k;
     unsigned long long* st = (m.stamps && role == 0 && k < MEGA_STAMP_STEPS) ? m.stamps : nullptr;
-    for (int li = 0; li < m.n_layers; ++li) {
-      cfa_t f = (cfa_t)m.fa + 4 * li;
+    for (int li = 0; li < NL; ++li) {
+      cfa_t f = fa0 + 4 * li;
       asm volatile("" : "+s"(f));  // per-layer arguments are re-read, not held across the loop
-      ka_phase<T, RT, CP_COH>(f[0], part, b, smem);
-      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
-      kb_phase<T, RT, CP_COH>(f[1], part, b, it, smem);
-      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
-      kc_phase<T, RT, CP_COH>(f[2], part, b, smem);
-      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
-      kd_phase<T, RT, CP_COH>(f[3], part, b, smem);
-      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
+      ka_phase<T, RT, CP_COH>(f[0], part, b, smem, pn);
+      KBPre<T, RT> pb(f[1], wave);
+      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st, [&] { pb.load(lane); })) return;
+      kb_phase<T, RT, CP_COH>(f[1], part, b, it, smem, pb);
+      KCPre<T, RT> pc(f[2], part, wave);
+      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st, [&] { pc.load(lane); })) return;
+      kc_phase<T, RT, CP_COH>(f[2], part, b, smem, pc);
+      KDPre<T, RT> pd(f[3], part, wave);
+      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st, [&] { pd.load(lane); })) return;
+      kd_phase<T, RT, CP_COH>(f[3], part, b, smem, pd);
+      pn = li + 1 < NL ? ka_pre<T, RT>(f[4], part, wave) : ke_pre<T, RT>(*fe, part);
+      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); })) return;
     }
-    cfe_t fe = (cfe_t)m.fe;
-    asm volatile("" : "+s"(fe));
-    ke_phase<T, RT, CP_COH>(*fe, part, b, it, smem);
-    if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st)) return;
+    ke_phase<T, RT, CP_COH>(*fe, part, b, it, smem, pn);
+    pn = ka_pre<T, RT>(fa0[0], part, wave);
+    if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); })) return;
   }
 }
 

@@ -94,10 +94,64 @@ __device__ __forceinline__ void store_rows(float* dst, const float* Hs, int L, i
 }
 
 // ------------------------------------------------------------------------------------------
+// The weight fragments a phase streams into registers, separable from the phase: the kernels
+// load them at their start; the persistent loop issues them while the clip group meets at the
+// barrier in front of the phase, so the weight stream overlaps the wait.
+// ------------------------------------------------------------------------------------------
+// one 16-column tile over K = 256 per wave: KA's QKV tile and KE's output tile share the type,
+// so the persistent loop carries ONE set of registers for "the next phase's tile" across layers
+template <typename T, int RT> struct Pre1 {
+  WGemm<T, 1, FD / Frag<T>::KF, RT> g;
+  __device__ __forceinline__ Pre1(const void* w, int tile) : g(w, FD / Frag<T>::KF, 0) { g.tiles[0] = tile; }
+  __device__ __forceinline__ void load(int lane) { g.load(0, lane); }
+};
+template <typename T, int RT> using KAPre = Pre1<T, RT>;
+template <typename T, int RT> using KEPre = Pre1<T, RT>;
+template <typename T, int RT, typename FA>  // QKV of head h: waves 0-5 one tile each
+__device__ __forceinline__ KAPre<T, RT> ka_pre(const FA& a, int h, int wave) {
+  return KAPre<T, RT>(a.w.qkv, h * 6 + min(wave, 5));
+}
+template <typename T, int RT, typename FA>  // output channel tile p
+__device__ __forceinline__ KEPre<T, RT> ke_pre(const FA& a, int p) {
+  return KEPre<T, RT>(a.w_out, p);
+}
+template <typename T, int RT> struct KBPre {  // SA out-projection, all 16 tiles (2 per wave)
+  WGemm<T, 2, FD / Frag<T>::KF, RT> go;
+  template <typename FA>
+  __device__ __forceinline__ KBPre(const FA& a, int wave) : go(a.w.o_sa, FD / Frag<T>::KF, 0) {
+    go.tiles[0] = 2 * wave;
+    go.tiles[1] = 2 * wave + 1;
+  }
+  __device__ __forceinline__ void load(int lane) { go.load(0, lane); }
+};
+template <typename T, int RT> struct KCPre {  // CA out-projection (the FFN-up tile loads in the phase)
+  WGemm<T, 2, FD / Frag<T>::KF, RT> go;
+  template <typename FA>
+  __device__ __forceinline__ KCPre(const FA& a, int c, int wave) : go(a.w.o_ca, FD / Frag<T>::KF, 0) {
+    (void)c;
+    go.tiles[0] = 2 * wave;
+    go.tiles[1] = 2 * wave + 1;
+  }
+  __device__ __forceinline__ void load(int lane) { go.load(0, lane); }
+};
+template <typename T, int RT> struct KDPre {  // FFN-down: column tile (w & 1), K quarter (w >> 1)
+  static constexpr int KP = Plan<T>::KP, KTT = 4 * FD / Frag<T>::KF, KTW = KP / Frag<T>::KF / 4;
+  static constexpr bool ONE_PASS = KP == 4 * FD;  // bf16: the whole K in one image
+  WGemm<T, 1, KTW, RT> gd;
+  template <typename FA>
+  __device__ __forceinline__ KDPre(const FA& a, int c, int wave) : gd(a.w.ff2, KTT, (wave >> 1) * KTW) {
+    gd.tiles[0] = 2 * c + (wave & 1);
+  }
+  __device__ __forceinline__ void load(int lane) {
+    if (ONE_PASS) gd.load(0, lane);
+  }
+};
+
+// ------------------------------------------------------------------------------------------
 // KA: [emb_x + PE (layer 0)] + LN1 + QKV(head) + conv + self-attention      grid (heads, clips)
 // ------------------------------------------------------------------------------------------
 template <typename T, int RT, int CP, typename FA>
-__device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned char* smem) {
+__device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned char* smem, KAPre<T, RT>& pre) {
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF, SY = 96 + 4;
   const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
@@ -134,9 +188,7 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
   }
   // QKV of head h: packed as 6 tiles [q0 q1 k0 k1 v0 v1]; waves 0-5 own one tile each
   const int nq = wave < 6 ? 1 : 0;
-  WGemm<T, 1, KT, RT> gm(w.qkv, KT, 0);
-  gm.tiles[0] = h * 6 + min(wave, 5);
-  gm.load(0, lane);
+  auto& gm = pre.g;
   const float bias = G(w.qkv_b)[h * 96 + min(wave, 5) * 16 + c16];
   const float4 lg = ld_f4(w.ln1_g + (tid & 63) * 4), lb = ld_f4(w.ln1_b + (tid & 63) * 4);
   const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
@@ -188,7 +240,7 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
 // KB: SA out-proj + residual + LN2 + cross-attn Q(head) + conv + cross-attention  (heads, clips)
 // ------------------------------------------------------------------------------------------
 template <typename T, int RT, int CP, typename FA>
-__device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsigned char* smem) {
+__device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsigned char* smem, KBPre<T, RT>& pre) {
   using PL = Plan<T>;
   using AT = FAtt<T>;
   constexpr int KT = FD / Frag<T>::KF, SYQ = FDK + 4;
@@ -214,10 +266,7 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   if (!R::ON) glds_rows<FT, CP>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
   ImgStage<T, FT, CP> so;
   so.load(Ax, (const T*)a.o_sa + row0 * FD, L);
-  WGemm<T, 2, KT, RT> go(w.o_sa, KT, 0);
-  go.tiles[0] = 2 * wave;
-  go.tiles[1] = 2 * wave + 1;
-  go.load(0, lane);
+  auto& go = pre.go;
   float bo[2];
   bo[0] = G(w.o_sa_b)[(2 * wave) * 16 + c16];
   bo[1] = G(w.o_sa_b)[(2 * wave + 1) * 16 + c16];
@@ -289,7 +338,7 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
 // KC: CA out-proj + residual + LN3 + FFN-up chunk (128 hidden) + ReLU^2   grid (8 chunks, clips)
 // ------------------------------------------------------------------------------------------
 template <typename T, int RT, int CP, typename FA>
-__device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned char* smem) {
+__device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned char* smem, KCPre<T, RT>& pre) {
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF;
   const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
@@ -307,10 +356,7 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   if (!R::ON) glds_rows<FT, CP>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
   ImgStage<T, FT, CP> so;
   so.load(Ax, (const T*)a.o_ca + row0 * FD, L);
-  WGemm<T, 2, KT, RT> go(w.o_ca, KT, 0);
-  go.tiles[0] = 2 * wave;
-  go.tiles[1] = 2 * wave + 1;
-  go.load(0, lane);
+  auto& go = pre.go;
   float bo[2];
   bo[0] = G(w.o_ca_b)[(2 * wave) * 16 + c16];
   bo[1] = G(w.o_ca_b)[(2 * wave + 1) * 16 + c16];
@@ -318,7 +364,7 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   so.store(Ax, L);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   STAMP(1);
-  WGemm<T, 1, KT, RT> gf(w.ff1, KT, 0);  // prefetch: in flight across the out-projection
+  WGemm<T, 1, KT, RT> gf(w.ff1, KT, 0);  // in flight across the out-projection
   gf.tiles[0] = 8 * c + wave;
   gf.load(0, lane);
   const float bf = G(w.ff1_b)[(8 * c + wave) * 16 + c16];
@@ -351,7 +397,7 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
 // are added in a fixed order (deterministic).
 // ------------------------------------------------------------------------------------------
 template <typename T, int RT, int CP, typename FA>
-__device__ __forceinline__ void kd_phase(const FA& a, int c, int b, unsigned char* smem) {
+__device__ __forceinline__ void kd_phase(const FA& a, int c, int b, unsigned char* smem, KDPre<T, RT>& pre) {
   using PL = Plan<T>;
   constexpr int KP = PL::KP, NP = 4 * FD / KP, SA = KP + Frag<T>::PT;
   constexpr int KTT = 4 * FD / Frag<T>::KF, KTW = KP / Frag<T>::KF / 4;  // k steps: total, per wave per pass
@@ -388,13 +434,19 @@ __device__ __forceinline__ void kd_phase(const FA& a, int c, int b, unsigned cha
     if (p > 0) __syncthreads();  // the previous pass' image is consumed
     glds_rows<FT, CP>(Hd, sizeof(T) * SA, (const T*)a.hid + row0 * (4 * FD) + p * KP, sizeof(T) * 4 * FD, L,
                   (int)(sizeof(T) * KP / 1024));
-    WGemm<T, 1, KTW, RT> gd(w.ff2, KTT, p * (KP / Frag<T>::KF) + kq * KTW);
-    gd.tiles[0] = tile;
-    gd.load(0, lane);
-    __syncthreads();
-    if (p == 0) STAMP(1);
     f32x4 part[RT][1];
-    gd.run(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
+    if constexpr (KDPre<T, RT>::ONE_PASS) {
+      __syncthreads();
+      STAMP(1);
+      pre.gd.run(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
+    } else {
+      WGemm<T, 1, KTW, RT> gd(w.ff2, KTT, p * (KP / Frag<T>::KF) + kq * KTW);
+      gd.tiles[0] = tile;
+      gd.load(0, lane);
+      __syncthreads();
+      if (p == 0) STAMP(1);
+      gd.run(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
+    }
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) acc[rt][0] += part[rt][0];
   }
@@ -428,7 +480,7 @@ __device__ __forceinline__ void kd_phase(const FA& a, int c, int b, unsigned cha
 // The next step's emb_x + PE is computed by that step's first KA (x_emb).
 // ------------------------------------------------------------------------------------------
 template <typename T, int RT, int CP, typename FA>
-__device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsigned char* smem) {
+__device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsigned char* smem, KEPre<T, RT>& pre) {
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF, SE = 16 + 4;
   const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
@@ -444,9 +496,10 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
 
   STAMP(0);
   glds_rows<FT, CP>(Hs, sizeof(float) * SH, a.h + row0 * FD, sizeof(float) * FD, L, 1);
-  WGemm<T, 1, KT, 1> go(a.w_out, KT, 0);  // waves 0-3: row tile w of channel tile p
+  WGemm<T, 1, KT, 1> go(a.w_out, KT, 0);  // waves 0..RT-1: row tile w of channel tile p (prefetched)
   go.tiles[0] = p;
-  go.load(0, lane);
+#pragma unroll
+  for (int k = 0; k < KT; ++k) go.wb[0][k] = pre.g.wb[0][k];
   const float bo = G(a.b_out)[p * 16 + c16];
   const float4 lg = ld_f4(a.ln_g + (tid & 63) * 4), lb = ld_f4(a.ln_b + (tid & 63) * 4);
   // the thread's quad: elements e0 + 4 tid .. + 3 (issued now, consumed after the GEMM)
