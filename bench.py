@@ -34,7 +34,12 @@ BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3
 
 
-ENCODER_FLOP_PER_CLIP = 4.764e9   # SURVEY.md 8d, Tw = 32,000 (computed once per clip)
+# SURVEY.md 8d speech-encoder FLOPs per clip (computed once per clip): Tw = 32,000 / 128,000
+ENCODER_FLOP_PER_CLIP = {32000: 4.764e9, 128000: 18.873e9}
+
+
+def encoder_flop(wav_len):
+    return ENCODER_FLOP_PER_CLIP.get(wav_len, 4.764e9 * wav_len / 32000)
 
 
 def clip_step_flops(L, Tm, d, C, layers):
@@ -54,22 +59,44 @@ def kb_flop(n, L, Lk, d):
     return n * (4 * L * d * d + 4 * L * Lk * d + 6 * L * d + 12 * Lk * d)
 
 
+# BASELINE.json configs as bench workloads (per GPU); C3 is C2 on 8 GPUs (--gpus 8)
+WORKLOADS = {
+    "c2": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=1,
+               label="beat-ours C2"),
+    "c4": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=4,
+               label="beat-ours C4 long clip (seq_len x4)"),
+    "c5": dict(batch_per_gpu=128, alg="ddim", respacing="ddim50", seq_mult=1,
+               label="beat-ours C5 DDIM-50"),
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--config", default=os.path.join(ROOT, "configs", "beat-ours.json"))
-    p.add_argument("--batch-per-gpu", type=int, default=32)
+    p.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
+                   help="BASELINE.json config: c2 (default, the metric's config), c4 long clip, c5 DDIM-50")
+    p.add_argument("--batch-per-gpu", type=int, default=None)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    p.add_argument("--alg", default="ddpm", choices=["ddpm", "ddim"])
-    p.add_argument("--respacing", default="")
+    p.add_argument("--alg", default=None, choices=["ddpm", "ddim"])
+    p.add_argument("--respacing", default=None)
     p.add_argument("--graph", action="store_true",
                    help="replay each denoise step as a captured hipGraph (measured slower than eager launches)")
     p.add_argument("--no-profile", action="store_true", help="skip the in-loop kernel events")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-steps", type=int, default=3)
-    return p.parse_args()
+    p.add_argument("--cpu-steps", type=int, default=None,
+                   help="denoise steps of the CPU sample (default: ~10 s of oracle work, 40 steps at C2)")
+    a = p.parse_args()
+    w = WORKLOADS[a.workload]
+    for k in ("batch_per_gpu", "alg", "respacing"):
+        if getattr(a, k) is None:
+            setattr(a, k, w[k])
+    a.seq_mult = w["seq_mult"]
+    if a.cpu_steps is None:
+        a.cpu_steps = max(3, round(40 * 32 / (a.batch_per_gpu * a.seq_mult)))
+    return a
 
 
 def log(*a):
@@ -79,7 +106,7 @@ def log(*a):
 T_START = time.perf_counter()
 
 
-def cpu_baseline(pkg, cfg, sd, arch, B, L, T, n_steps):
+def cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, n_steps, alg):
     """Oracle on the host cores: faithful per-step encoder, n_steps denoise steps, extrapolated x T."""
     from oracle import ref_denoiser, ref_diffusion
     cores = len(os.sched_getaffinity(0))
@@ -90,13 +117,13 @@ def cpu_baseline(pkg, cfg, sd, arch, B, L, T, n_steps):
     ocfg = {k: arch[k] for k in ("type", "d_model", "decoder", "heads", "n_layers")}
     om = ref_denoiser.OracleModel(sd, ocfg, cache_speech=False)
     g = th.Generator().manual_seed(1)
-    wav = th.randn(B, 32000, generator=g) * 0.1
-    sch = ref_diffusion.make_schedule("linear", T, "")
+    wav = th.randn(B, wav_len, generator=g) * 0.1
+    sch = ref_diffusion.make_schedule("linear", 1000, "ddim%d" % T if alg == "ddim" and T < 1000 else "")
     noise = ref_diffusion.TorchNoise(2)
-    ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, "ddpm", n_steps=1)
+    ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, alg, n_steps=1)
     log("cpu baseline warm-up step done")
     t0 = time.perf_counter()
-    ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, "ddpm", n_steps=n_steps)
+    ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, alg, n_steps=n_steps)
     dt = time.perf_counter() - t0
     per_step = dt / n_steps
     model_name = ""
@@ -110,7 +137,7 @@ def cpu_baseline(pkg, cfg, sd, arch, B, L, T, n_steps):
         "unit": "frames/s",
         "cores": th.get_num_threads(),
         "kind": "port",
-        "sample": (f"{n_steps} DDPM denoise steps of B={B} clips (per-step speech encoder, fp32 oracle) "
+        "sample": (f"{n_steps} {alg.upper()} denoise steps of B={B} clips (per-step speech encoder, fp32 oracle) "
                    f"after 1 warm-up, measured {dt:.2f} s = {per_step * 1e3:.0f} ms/step, extrapolated x{T} steps; "
                    f"CPU: {model_name}"),
     }
@@ -137,7 +164,7 @@ def main():
     sharding = __import__(ge.PKG_NAME + ".sharding", fromlist=["x"])
     cfg = pkg.load_config(args.config)
     d_pose = int(cfg.Data.get("d_pose", 123)) if "Data" in cfg else 123
-    L = int(cfg.Data.pose_window_len)
+    L = int(cfg.Data.pose_window_len) * args.seq_mult
     wav_len = int(cfg.Data.wav_sr * L / cfg.Data.pose_fps)
     model, diffusion, _, _, _ = pkg.create_model(d_pose, cfg.Model, dtype=args.dtype, device=dev)
     if args.respacing:
@@ -227,7 +254,7 @@ def main():
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 6), "traffic": None, "kernel": kernel, "timing": timing,
                 "flop_per_launch": flop, "avg_launch_us": round(avg_us, 3), "launches": prof_n}
-    frame_flop = (T * clip_step + ENCODER_FLOP_PER_CLIP) / L
+    frame_flop = (T * clip_step + encoder_flop(wav_len)) / L
     res = {
         "metric": "generated motion frames/sec (whole node), T=1000 BEAT clips, 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -241,7 +268,7 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (random-init weights of the beat-ours architecture, N(0,0.1^2) wav, counter-stream noise)",
-        "config": {"workload": f"beat-ours C2: {B} clips/GPU x L={L} x C={d_pose}, wav {wav_len}, "
+        "config": {"workload": f"{WORKLOADS[args.workload]['label']}: {B} clips/GPU x L={L} x C={d_pose}, wav {wav_len}, "
                                f"{args.alg.upper()} T'={T}, {args.dtype} decoder",
                    "global_batch": n_total, "seq_len": L, "parallelism": f"dp{world}",
                    "diffusion_steps": T},
@@ -251,7 +278,7 @@ def main():
                       "frac_of_peak": round(value * frame_flop / world / 1e12 / peak, 5)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(pkg, cfg, sd, arch, B, L, T, args.cpu_steps)
+        res["cpu_baseline"] = cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, args.cpu_steps, args.alg)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:
