@@ -70,6 +70,29 @@ WORKLOADS = {
 }
 
 
+# HBM-side bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of
+# this same command (scripts/pmc.sh + pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
+# correction of MI355X_MICROARCH.md); PMC cannot run inside the timed region, so the figure is
+# the profile's, keyed by kernel symbol and workload
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01i_pmc_summary.json")
+
+
+def pmc_traffic(kernel_prefix, workload):
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+    except OSError:
+        return None
+    if d.get("_workload", "c2") != workload:
+        return None
+    for k, e in d.items():
+        if k.startswith("void ggd::" + kernel_prefix) and "hbm_read_bytes" in e and "hbm_write_bytes" in e:
+            return {"bytes_per_launch": e["hbm_read_bytes"] + e["hbm_write_bytes"],
+                    "read": e["hbm_read_bytes"], "write": e["hbm_write_bytes"],
+                    "source": os.path.relpath(PMC_SUMMARY, ROOT)}
+    return None
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -251,8 +274,9 @@ def main():
             kernel = f"kb_kernel<{args.dtype}> (SA out-proj + LN2 + cross-attn Q + conv + cross-attention)"
             timing = "device realtime-clock span of every KB launch of the last timed pass"
         ach = flop / (avg_us * 1e-6) / 1e12
+        tr = pmc_traffic("mk_kernel" if prof_kind == 1 else "kb_kernel", args.workload)
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 6), "traffic": None, "kernel": kernel, "timing": timing,
+                "frac": round(ach / peak, 6), "traffic": tr and tr["bytes_per_launch"], "traffic_detail": tr, "kernel": kernel, "timing": timing,
                 "flop_per_launch": flop, "avg_launch_us": round(avg_us, 3), "launches": prof_n}
     frame_flop = (T * clip_step + encoder_flop(wav_len)) / L
     res = {
