@@ -169,6 +169,39 @@ int ggd_profile_kind(ggd_ctx* ctx);
  * back (returns the loop's clip capacity in *avg_us). */
 int ggd_diag(ggd_ctx* ctx, int32_t what, const int32_t* p, int32_t np, int32_t iters, double* avg_us);
 
+/* ------------------------------------------------------------------------------------
+ * Speech encoder: HA2GSpeechEncoder (models/modules/ha2g/speech_encoder.py:9-61 ->
+ * ha2g/model/hierarchy_net.py:10-19 -> ResNetSE34V2.py:118-188 / ResNetBlocks.py:7-96),
+ * run once per clip.  Its own context: the reference module is constructed inside
+ * Speech2GestureModelV2.__init__ (models/model.py:79-80) and called at model.py:95-96.
+ * -------------------------------------------------------------------------------------- */
+typedef struct ggd_enc ggd_enc;
+
+/* Encoder for wav windows of `wav_len` samples (16 kHz), batches up to max_batch, tokens
+ * projected to d_model.  dtype GGD_BF16: convolutions on bf16 MFMA (f32 accumulate, f32
+ * front end / norms / heads); GGD_F32: every product in f32.
+ * Replaces: HA2GSpeechEncoder.__init__, speech_encoder.py:9-34. */
+int ggd_enc_create(int device, int32_t d_model, int32_t wav_len, int32_t max_batch, int32_t dtype, ggd_enc** out);
+int ggd_enc_destroy(ggd_enc* enc);
+const char* ggd_enc_last_error(const ggd_enc* enc);
+
+/* Stage one "speech_encoder.*" state_dict tensor (other names return GGD_IGNORED).
+ * Replaces: the encoder part of model.load_state_dict, main.py:113-115. */
+int ggd_enc_load_weight(ggd_enc* enc, const char* name, const float* host_data, int64_t numel);
+
+/* Check every encoder tensor, fold the eval-mode BatchNorms, pack the convolution filters and
+ * upload them; size the workspaces. */
+int ggd_enc_finalize(ggd_enc* enc);
+
+/* Token counts of z_low / z_mid / z_high for this wav length (31 / 30 / 30 at 32,000). */
+int ggd_enc_lengths(const ggd_enc* enc, int32_t* t_low, int32_t* t_mid, int32_t* t_high);
+
+/* wav: device f32 (N, wav_len) -> z_low (N, t_low, d), z_mid (N, t_mid, d), z_high (N, t_high, d),
+ * device f32, caller-owned.  Enqueued on `stream`.
+ * Replaces: HA2GSpeechEncoder.forward, speech_encoder.py:37-61. */
+int ggd_enc_run(ggd_enc* enc, const float* wav, int32_t n, float* z_low, float* z_mid, float* z_high,
+                void* stream);
+
 /* Library version string. */
 const char* ggd_version(void);
 

@@ -1,0 +1,849 @@
+// ggd_encoder.hip -- the HA2G speech encoder (models/modules/ha2g/speech_encoder.py:9-61) as
+// hand-written gfx950 kernels behind the ggd_enc_* entry points of include/ggd.h.
+//
+// Runs ONCE per clip (the reference recomputes it inside every denoise step, model.py:95-96;
+// in eval mode it is a pure function of the clip's audio).  Pipeline per chunk of clips:
+//
+//   frames   pre-emphasis (ha2g/model/utils.py:22-38) + centre reflect pad + framing  -> f32 [n*F][1024]
+//   DFT      frames x [cos | -sin] basis with the Hann window folded in (f32 MFMA GEMM,
+//            launch_gemm)                                                            -> f32 [n*F][1088]
+//   power    re^2 + im^2                                                              -> f32 [n*F][516]
+//   mel      power x HTK filterbank (f32 MFMA GEMM)                                   -> f32 [n*F][128]
+//   inorm    +1e-6, InstanceNorm1d(128) over frames (speech_encoder.py:28,57-58)     -> f32 [n][128][F]
+//   conv1    3x3 1->32 + bias, ReLU, BN (ResNetSE34V2.py:118-126) on VALU             -> f32 NHWC [n][128][F][32]
+//   blocks   SE-ResNet [3,4,6,3] x [32,64,128,256] (ResNetBlocks.py:7-37,81-96):
+//              conv3x3(s)+ReLU+BN | conv3x3+BN | [1x1(s)+BN downsample] | SE mean+fc+ReLU+fc+sigmoid |
+//              relu(v * se + residual)
+//   heads    low conv2x2 / mid shuffle2+conv3x3 / high shuffle4+conv3x3, ReLU, BN, flatten (c*H + h),
+//            Linear -> 32, wav_proj Linear 32 -> d (ResNetSE34V2.py:157-188, speech_encoder.py:59-61)
+//
+// Convolutions are implicit GEMMs on MFMA: rows = output pixels (NHWC, channels innermost),
+// columns = output channels, K = taps x input channels in chunks of 32.  Every lane reads its
+// own operand fragment straight from global memory (8 consecutive channels of one pixel, 8
+// consecutive input channels of one filter tap), so there is no LDS staging and no barrier:
+// neighbouring taps re-read the same lines from L1 / L2.  bf16 contexts multiply on
+// v_mfma_f32_16x16x32_bf16 (activations rounded to bf16 at the load, f32 accumulate); f32
+// contexts on v_mfma_f32_16x16x4_f32 with the 32-channel chunk split into 8 k steps (lane group
+// g owns channels 8g .. 8g+7, step s multiplies channel 8g+s), i.e. exact f32 products.  Each
+// output element is one lane's fixed-order accumulation, so a clip's features do not depend on
+// the batch it is encoded in.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/ggd.h"
+#include "ggd_common.h"
+
+using namespace ggd;
+
+namespace {
+
+constexpr int NFFT = 1024, HOP = 512, NBIN = NFFT / 2 + 1, NMEL = 128;
+constexpr int SPEC_LD = 1088;   // 2 * 513 columns padded to the GEMM's 64-column tiles
+constexpr int POW_LD = 516;     // 513 power bins, rows 16-byte aligned
+constexpr int CONV_TPB = 256;   // 4 waves; a wave owns 32 output pixels
+
+// ------------------------------------------------------------------------------------------
+// front end
+// ------------------------------------------------------------------------------------------
+__global__ void enc_frames_kernel(const float* __restrict__ wav, float* __restrict__ frames, int n, int Tw, int F,
+                                  float coef) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x, total = (size_t)n * F * NFFT;
+  if (idx >= total) return;
+  const int k = (int)(idx % NFFT), f = (int)((idx / NFFT) % F), b = (int)(idx / ((size_t)NFFT * F));
+  // centre reflect padding of n_fft / 2 (torch.stft center=True, pad_mode='reflect')
+  int src = f * HOP + k - NFFT / 2;
+  if (src < 0) src = -src;
+  if (src >= Tw) src = 2 * (Tw - 1) - src;
+  // pre-emphasis y[j] = x[j] - c x[j - 1], reflect-padded on the left: y[0] = x[0] - c x[1]
+  const float* x = wav + (size_t)b * Tw;
+  const int prev = src == 0 ? 1 : src - 1;
+  frames[idx] = x[src] - coef * x[prev];
+}
+
+__global__ void enc_power_kernel(const float* __restrict__ spec, float* __restrict__ pw, int M) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)M * POW_LD) return;
+  const int f = (int)(idx % POW_LD);
+  const size_t m = idx / POW_LD;
+  float v = 0.f;
+  if (f < NBIN) {
+    const float re = spec[m * SPEC_LD + f], im = spec[m * SPEC_LD + NBIN + f];
+    v = re * re + im * im;
+  }
+  pw[idx] = v;
+}
+
+// +1e-6, instance norm over frames per (clip, mel bin) -> image [n][128][F]; one workgroup per clip
+__global__ void __launch_bounds__(NMEL) enc_inorm_kernel(const float* __restrict__ mel, float* __restrict__ img,
+                                                         int F) {
+  const int b = blockIdx.x, m = threadIdx.x;
+  const float* src = mel + (size_t)b * F * NMEL + m;
+  float s = 0.f;
+  for (int f = 0; f < F; ++f) s += src[(size_t)f * NMEL] + 1e-6f;
+  const float mean = s / (float)F;
+  float v = 0.f;
+  for (int f = 0; f < F; ++f) {
+    const float d = (src[(size_t)f * NMEL] + 1e-6f) - mean;
+    v += d * d;
+  }
+  const float inv = 1.0f / sqrtf(v / (float)F + 1e-5f);
+  float* dst = img + ((size_t)b * NMEL + m) * F;
+  for (int f = 0; f < F; ++f) dst[f] = ((src[(size_t)f * NMEL] + 1e-6f) - mean) * inv;
+}
+
+// conv1 (1 -> 32, 3x3, pad 1) + bias, ReLU, BN; one thread per (pixel, 8 output channels)
+__global__ void enc_conv1_kernel(const float* __restrict__ img, const float* __restrict__ w,
+                                 const float* __restrict__ bias, const float* __restrict__ s,
+                                 const float* __restrict__ t, float* __restrict__ out, int n, int H, int W) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x, total = (size_t)n * H * W * 4;
+  if (idx >= total) return;
+  const int cg = (int)(idx & 3);
+  const size_t p = idx >> 2;
+  const int x = (int)(p % W), y = (int)((p / W) % H), b = (int)(p / ((size_t)W * H));
+  float tap[9];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int iy = y + ky - 1, ix = x + kx - 1;
+      tap[ky * 3 + kx] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? img[((size_t)b * H + iy) * W + ix] : 0.f;
+    }
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cg * 8 + j;
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) acc += w[c * 9 + q] * tap[q];
+    o[j] = fmaxf(acc + bias[c], 0.f) * s[c] + t[c];
+  }
+  float4* dst = (float4*)(out + p * 32 + cg * 8);
+  dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+  dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+}
+
+// ------------------------------------------------------------------------------------------
+// implicit-GEMM convolution
+// ------------------------------------------------------------------------------------------
+enum { CONV_BN = 0, CONV_RELU_BN = 1 };
+enum { LAYOUT_NHWC = 0, LAYOUT_NWCH = 1 };
+
+struct ConvArgs {
+  const float* in;          // f32 NHWC [N][H][W][Cin] (Cin a multiple of 32)
+  const void* w;            // T [Cout_pad][KH * KW][Cin]
+  const float *bias, *s, *t;  // [Cout_pad]: BN folded to y = x * s + t
+  float* out;
+  int N, H, W, Cin, Ho, Wo, Cout_pad, Cvalid, KH, KW, stride, pad, mode, layout;
+};
+
+template <typename T> struct ConvB;
+template <> struct ConvB<bf16_t> {
+  bf16x8 v;
+  __device__ __forceinline__ void load(const bf16_t* p) { v = *(const bf16x8*)p; }
+};
+template <> struct ConvB<float> {
+  float v[8];
+  __device__ __forceinline__ void load(const float* p) {
+    const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+};
+
+struct ConvA {
+  float v[8];
+};
+
+__device__ __forceinline__ void mma(f32x4& acc, const ConvA& a, const ConvB<bf16_t>& b) {
+  bf16x8 av;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) av[i] = (__bf16)a.v[i];
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b.v, acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mma(f32x4& acc, const ConvA& a, const ConvB<float>& b) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[s], b.v[s], acc, 0, 0, 0);
+}
+
+template <typename T, int NJ>
+struct ConvStage {
+  ConvA a[2];
+  ConvB<T> b[NJ];
+};
+
+template <typename T, int NJ>
+__global__ void __launch_bounds__(CONV_TPB) enc_conv_kernel(ConvArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
+  const int HWo = a.Ho * a.Wo, P = a.N * HWo;
+  const int p0 = blockIdx.x * 128 + wave * 32, n0 = blockIdx.y * (NJ * 16);
+  // this lane's A pixels (row tiles 0, 1): clamped into the image; `ok` masks the padding
+  int base[2], iy0[2], ix0[2];
+  bool pv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = p0 + i * 16 + r16;
+    pv[i] = p < P;
+    const int pc = min(p, P - 1), b = pc / HWo, rem = pc - b * HWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+    base[i] = b * a.H * a.W;
+    iy0[i] = oy * a.stride - a.pad;
+    ix0[i] = ox * a.stride - a.pad;
+  }
+  const int taps = a.KH * a.KW, cch = a.Cin >> 5, nk = taps * cch;
+  const T* wb = (const T*)a.w + (size_t)(n0 + r16) * taps * a.Cin + g * 8;
+  const size_t wj = (size_t)16 * taps * a.Cin;  // next column tile
+
+  auto fetch = [&](int kk, ConvStage<T, NJ>& st) {
+    const int tap = kk / cch, c0 = (kk - tap * cch) << 5, ky = tap / a.KW, kx = tap - ky * a.KW;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int iy = iy0[i] + ky, ix = ix0[i] + kx;
+      const bool ok = pv[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+      const int pix = base[i] + min(max(iy, 0), a.H - 1) * a.W + min(max(ix, 0), a.W - 1);
+      const float* src = a.in + (size_t)pix * a.Cin + c0 + g * 8;
+      const float4 u = *(const float4*)src, v = *(const float4*)(src + 4);
+      const float m = ok ? 1.f : 0.f;
+      st.a[i].v[0] = u.x * m; st.a[i].v[1] = u.y * m; st.a[i].v[2] = u.z * m; st.a[i].v[3] = u.w * m;
+      st.a[i].v[4] = v.x * m; st.a[i].v[5] = v.y * m; st.a[i].v[6] = v.z * m; st.a[i].v[7] = v.w * m;
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) st.b[j].load(wb + j * wj + (size_t)tap * a.Cin + c0);
+  };
+
+  f32x4 acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  ConvStage<T, NJ> cur, nxt;
+  fetch(0, cur);
+  for (int kk = 0; kk < nk; ++kk) {
+    if (kk + 1 < nk) fetch(kk + 1, nxt);  // next chunk in flight under this chunk's MFMAs
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) mma(acc[i][j], cur.a[i], cur.b[j]);
+    cur = nxt;
+  }
+
+  // epilogue: C/D layout of the 16x16 MFMA -- column = lane & 15, row = 4 (lane >> 4) + r
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int co = n0 + j * 16 + r16;
+    const float bi = a.bias[co], sc = a.s[co], sh = a.t[co];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = p0 + i * 16 + 4 * g + r;
+        if (p >= P) continue;
+        float v = acc[i][j][r];
+        v = a.mode == CONV_RELU_BN ? fmaxf(v + bi, 0.f) * sc + sh : (v + bi) * sc + sh;
+        if (a.layout == LAYOUT_NHWC) {
+          a.out[(size_t)p * a.Cout_pad + co] = v;
+        } else if (co < a.Cvalid) {
+          const int b = p / HWo, rem = p - b * HWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
+          a.out[(((size_t)b * a.Wo + ox) * a.Cvalid + co) * a.Ho + oy] = v;
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// squeeze-excitation, residual, pixel shuffle, heads
+// ------------------------------------------------------------------------------------------
+// one workgroup per clip: y[c] = sigmoid(fc2(relu(fc0(mean_hw(v)))))   (ResNetBlocks.py:81-96)
+__global__ void __launch_bounds__(256) enc_se_kernel(const float* __restrict__ v, int HW, int C,
+                                                     const float* __restrict__ w0, const float* __restrict__ b0,
+                                                     const float* __restrict__ w2, const float* __restrict__ b2,
+                                                     float* __restrict__ y) {
+  __shared__ float part[256], mean[256], hid[32];
+  const int b = blockIdx.x, tid = threadIdx.x, stripes = 256 / C, c = tid % C, st = tid / C;
+  const float* src = v + (size_t)b * HW * C;
+  float s = 0.f;
+  if (st < stripes)
+    for (int p = st; p < HW; p += stripes) s += src[(size_t)p * C + c];
+  part[tid] = s;
+  __syncthreads();
+  if (tid < C) {
+    float tot = 0.f;
+    for (int k = 0; k < stripes; ++k) tot += part[k * C + tid];
+    mean[tid] = tot / (float)HW;
+  }
+  __syncthreads();
+  const int Ch = C / 8;
+  if (tid < Ch) {
+    float a = b0[tid];
+    for (int k = 0; k < C; ++k) a += w0[tid * C + k] * mean[k];
+    hid[tid] = fmaxf(a, 0.f);
+  }
+  __syncthreads();
+  if (tid < C) {
+    float a = b2[tid];
+    for (int k = 0; k < Ch; ++k) a += w2[tid * Ch + k] * hid[k];
+    y[(size_t)b * C + tid] = 1.0f / (1.0f + expf(-a));
+  }
+}
+
+// out = relu(v * y[clip][c] + res), NHWC
+__global__ void enc_se_apply_kernel(const float* __restrict__ v, const float* __restrict__ y,
+                                    const float* __restrict__ res, float* __restrict__ out, int HW, int C,
+                                    size_t total4) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total4) return;
+  const size_t e = idx * 4;
+  const int c = (int)(e % C);
+  const size_t b = e / ((size_t)HW * C);
+  const float4 a = ((const float4*)v)[idx], r = ((const float4*)res)[idx];
+  const float* ys = y + b * C + c;
+  float4 o;
+  o.x = fmaxf(a.x * ys[0] + r.x, 0.f);
+  o.y = fmaxf(a.y * ys[1] + r.y, 0.f);
+  o.z = fmaxf(a.z * ys[2] + r.z, 0.f);
+  o.w = fmaxf(a.w * ys[3] + r.w, 0.f);
+  ((float4*)out)[idx] = o;
+}
+
+// PixelShuffle(r): in NHWC [n][H][W][C r^2] -> out NHWC [n][H r][W r][Cp] (channels >= C zero)
+__global__ void enc_shuffle_kernel(const float* __restrict__ in, float* __restrict__ out, int n, int H, int W,
+                                   int C, int r, int Cp) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int Ho = H * r, Wo = W * r;
+  if (idx >= (size_t)n * Ho * Wo * Cp) return;
+  const int c = (int)(idx % Cp);
+  const size_t p = idx / Cp;
+  const int x = (int)(p % Wo), yy = (int)((p / Wo) % Ho), b = (int)(p / ((size_t)Wo * Ho));
+  float v = 0.f;
+  if (c < C) {
+    const int h = yy / r, i = yy - h * r, w = x / r, j = x - w * r;
+    v = in[(((size_t)b * H + h) * W + w) * (C * r * r) + c * r * r + i * r + j];
+  }
+  out[idx] = v;
+}
+
+// one workgroup per (clip, time) row: z = Wp (W1 a + b1) + bp, a = the row's (c, h) features
+__global__ void __launch_bounds__(256) enc_head_fc_kernel(const float* __restrict__ feat, int K,
+                                                          const float* __restrict__ w1, const float* __restrict__ b1,
+                                                          const float* __restrict__ wp, const float* __restrict__ bp,
+                                                          float* __restrict__ z, int d) {
+  __shared__ float red[4][32], h1[32];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* a = feat + (size_t)row * K;
+  float acc[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) acc[j] = 0.f;
+  for (int k = tid; k < K; k += 256) {
+    const float x = a[k];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) acc[j] += w1[(size_t)j * K + k] * x;
+  }
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const float s = wave_sum(acc[j]);
+    if (lane == 0) red[wave][j] = s;
+  }
+  __syncthreads();
+  if (tid < 32) h1[tid] = ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])) + b1[tid];
+  __syncthreads();
+  for (int o = tid; o < d; o += 256) {
+    float s = bp[o];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) s += wp[o * 32 + j] * h1[j];
+    z[(size_t)row * d + o] = s;
+  }
+}
+
+inline unsigned blocks_for(size_t n, int tpb) { return (unsigned)((n + tpb - 1) / tpb); }
+
+hipError_t launch_conv(int dtype, const ConvArgs& a, hipStream_t s) {
+  const int P = a.N * a.Ho * a.Wo;
+  const int nj = a.Cout_pad % 64 == 0 ? 4 : 2;
+  if (a.Cin % 32 || a.Cout_pad % (nj * 16) || P <= 0) return hipErrorInvalidValue;
+  const dim3 grid(blocks_for(P, 128), a.Cout_pad / (nj * 16));
+  if (dtype == GGD_BF16) {
+    if (nj == 4) hipLaunchKernelGGL((enc_conv_kernel<bf16_t, 4>), grid, dim3(CONV_TPB), 0, s, a);
+    else hipLaunchKernelGGL((enc_conv_kernel<bf16_t, 2>), grid, dim3(CONV_TPB), 0, s, a);
+  } else {
+    if (nj == 4) hipLaunchKernelGGL((enc_conv_kernel<float, 4>), grid, dim3(CONV_TPB), 0, s, a);
+    else hipLaunchKernelGGL((enc_conv_kernel<float, 2>), grid, dim3(CONV_TPB), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+struct EConv {            // one convolution + its folded BN epilogue
+  int cin = 0, cin_pad = 0, cout = 0, cout_pad = 0, kh = 0, kw = 0, stride = 1, pad = 0;
+  void* w = nullptr;      // T [cout_pad][kh*kw][cin_pad]
+  float *bias = nullptr, *s = nullptr, *t = nullptr;
+};
+
+struct EBlock {
+  EConv c1, c2, ds;
+  bool has_ds = false;
+  int planes = 0;
+  float *se_w0 = nullptr, *se_b0 = nullptr, *se_w2 = nullptr, *se_b2 = nullptr;
+};
+
+struct EHead {
+  EConv conv;
+  int shuffle = 1, K = 0;
+  float *fc_w = nullptr, *fc_b = nullptr;
+};
+
+}  // namespace
+
+struct ggd_enc {
+  int device = 0, dtype = GGD_BF16, d_model = 0, wav_len = 0, max_batch = 0, chunk = 0;
+  int F = 0;                                  // spectrogram frames
+  int H[5] = {}, W[5] = {};                   // feature map sizes after conv1 / layer1..4
+  int t_low = 0, t_mid = 0, t_high = 0;
+  std::string err;
+  std::map<std::string, std::vector<float>> staged;
+  std::vector<void*> allocs;
+  bool finalized = false;
+  // weights
+  float *basis = nullptr, *fbT = nullptr, *zeros = nullptr;
+  float coef = 0.97f;
+  float *c1_w = nullptr, *c1_b = nullptr, *c1_s = nullptr, *c1_t = nullptr;
+  std::vector<EBlock> blocks;
+  EHead head[3];
+  float *proj_w = nullptr, *proj_b = nullptr;
+  // workspaces (chunk clips)
+  float *frames = nullptr, *spec = nullptr, *pw = nullptr, *mel = nullptr, *img = nullptr;
+  float *buf[4] = {}, *feat[3] = {}, *se_y = nullptr, *hbuf = nullptr, *sbuf = nullptr;
+};
+
+namespace {
+
+int efail(ggd_enc* e, int code, const std::string& msg) {
+  if (e) e->err = msg;
+  return code;
+}
+
+#define ENC_TRY(e, expr)                                                                      \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) return efail(e, GGD_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <typename P>
+hipError_t ealloc(ggd_enc* e, P** p, size_t bytes) {
+  void* q = nullptr;
+  hipError_t r = hipMalloc(&q, std::max<size_t>(bytes, 16));
+  if (r != hipSuccess) return r;
+  e->allocs.push_back(q);
+  *p = (P*)q;
+  return hipSuccess;
+}
+
+hipError_t upload(ggd_enc* e, float** dst, const std::vector<float>& v) {
+  hipError_t r = ealloc(e, dst, sizeof(float) * v.size());
+  if (r != hipSuccess) return r;
+  return hipMemcpy(*dst, v.data(), sizeof(float) * v.size(), hipMemcpyHostToDevice);
+}
+
+const std::string PFX = "speech_encoder.", FE = "speech_encoder.wav_encoder.feat_extractor.";
+
+// torch conv2d output size
+int conv_out(int n, int k, int s, int p) { return (n + 2 * p - k) / s + 1; }
+
+}  // namespace
+
+extern "C" {
+
+int ggd_enc_create(int device, int32_t d_model, int32_t wav_len, int32_t max_batch, int32_t dtype, ggd_enc** out) {
+  if (!out) return GGD_ERR_ARG;
+  *out = nullptr;
+  ggd_enc* e = new ggd_enc();
+  *out = e;
+  if (d_model <= 0 || wav_len < NFFT || max_batch <= 0) return efail(e, GGD_ERR_ARG, "bad encoder geometry");
+  if (dtype != GGD_F32 && dtype != GGD_BF16) return efail(e, GGD_ERR_UNSUPPORTED, "unsupported dtype");
+  e->device = device;
+  e->d_model = d_model;
+  e->wav_len = wav_len;
+  e->max_batch = max_batch;
+  e->dtype = dtype;
+  e->chunk = std::min(max_batch, 128);
+  e->F = 1 + wav_len / HOP;
+  e->H[0] = NMEL;
+  e->W[0] = e->F;
+  e->H[1] = NMEL;
+  e->W[1] = e->F;
+  for (int l = 2; l <= 4; ++l) {
+    e->H[l] = conv_out(e->H[l - 1], 3, 2, 1);
+    e->W[l] = conv_out(e->W[l - 1], 3, 2, 1);
+  }
+  e->t_low = e->W[2] - 1;          // conv 2x2, no padding
+  e->t_mid = e->W[3] * 2 - 2;      // pixel shuffle x2, conv 3x3
+  e->t_high = e->W[4] * 4 - 2;     // pixel shuffle x4, conv 3x3
+  return GGD_OK;                   // no device call before ggd_enc_finalize (geometry is host-only)
+}
+
+int ggd_enc_destroy(ggd_enc* e) {
+  if (!e) return GGD_OK;
+  if (!e->allocs.empty()) {
+    (void)hipSetDevice(e->device);
+    (void)hipDeviceSynchronize();
+    for (void* p : e->allocs) (void)hipFree(p);
+  }
+  delete e;
+  return GGD_OK;
+}
+
+const char* ggd_enc_last_error(const ggd_enc* e) { return e ? e->err.c_str() : "null encoder context"; }
+
+int ggd_enc_lengths(const ggd_enc* e, int32_t* t_low, int32_t* t_mid, int32_t* t_high) {
+  if (!e || !t_low || !t_mid || !t_high) return GGD_ERR_ARG;
+  *t_low = e->t_low;
+  *t_mid = e->t_mid;
+  *t_high = e->t_high;
+  return GGD_OK;
+}
+
+int ggd_enc_load_weight(ggd_enc* e, const char* name, const float* host, int64_t numel) {
+  if (!e || !name || (!host && numel > 0) || numel < 0) return efail(e, GGD_ERR_ARG, "null argument");
+  const std::string n(name);
+  if (n.compare(0, PFX.size(), PFX) != 0) return GGD_IGNORED;
+  e->staged[n].assign(host, host + numel);
+  e->finalized = false;
+  return GGD_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int need(ggd_enc* e, const std::string& name, size_t numel, const std::vector<float>** out) {
+  auto it = e->staged.find(name);
+  if (it == e->staged.end()) return efail(e, GGD_ERR_NAME, "missing encoder weight " + name);
+  if (it->second.size() != numel)
+    return efail(e, GGD_ERR_NAME, "encoder weight " + name + " has " + std::to_string(it->second.size()) +
+                                      " elements, expected " + std::to_string(numel));
+  *out = &it->second;
+  return GGD_OK;
+}
+
+#define NEED(name, numel, ptr)                     \
+  do {                                             \
+    int _r = need(e, (name), (numel), &(ptr));     \
+    if (_r) return _r;                             \
+  } while (0)
+
+// BatchNorm2d (eval) folded to y = x * s + t; bias of the preceding conv kept apart (ReLU sits
+// between them in the ReLU-then-BN blocks)
+int fold_bn(ggd_enc* e, const std::string& bn, int c, int cpad, std::vector<float>& s, std::vector<float>& t) {
+  const std::vector<float> *g, *b, *rm, *rv;
+  NEED(bn + ".weight", c, g);
+  NEED(bn + ".bias", c, b);
+  NEED(bn + ".running_mean", c, rm);
+  NEED(bn + ".running_var", c, rv);
+  s.assign(cpad, 0.f);
+  t.assign(cpad, 0.f);
+  for (int i = 0; i < c; ++i) {
+    const double sc = (double)(*g)[i] / std::sqrt((double)(*rv)[i] + 1e-5);
+    s[i] = (float)sc;
+    t[i] = (float)((double)(*b)[i] - (double)(*rm)[i] * sc);
+  }
+  return GGD_OK;
+}
+
+int make_conv(ggd_enc* e, EConv& cv, const std::string& conv, const std::string& bn, int cin, int cout, int k,
+              int stride, int pad, bool bias) {
+  cv.cin = cin;
+  cv.cin_pad = (cin + 31) / 32 * 32;
+  cv.cout = cout;
+  cv.cout_pad = cout <= 32 ? 32 : (cout + 63) / 64 * 64;
+  cv.kh = cv.kw = k;
+  cv.stride = stride;
+  cv.pad = pad;
+  const std::vector<float>* w;
+  NEED(conv + ".weight", (size_t)cout * cin * k * k, w);
+  std::vector<float> bb(cv.cout_pad, 0.f), s, t;
+  if (bias) {
+    const std::vector<float>* b;
+    NEED(conv + ".bias", cout, b);
+    std::copy(b->begin(), b->end(), bb.begin());
+  }
+  int r = fold_bn(e, bn, cout, cv.cout_pad, s, t);
+  if (r) return r;
+  // [cout][cin][ky][kx] -> [cout_pad][ky * k + kx][cin_pad]
+  const int taps = k * k;
+  std::vector<float> p((size_t)cv.cout_pad * taps * cv.cin_pad, 0.f);
+  for (int o = 0; o < cout; ++o)
+    for (int i = 0; i < cin; ++i)
+      for (int q = 0; q < taps; ++q) p[((size_t)o * taps + q) * cv.cin_pad + i] = (*w)[((size_t)o * cin + i) * taps + q];
+  if (e->dtype == GGD_BF16) {
+    std::vector<uint16_t> h(p.size());
+    for (size_t i = 0; i < p.size(); ++i) {  // round to nearest even
+      uint32_t u;
+      std::memcpy(&u, &p[i], 4);
+      h[i] = (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+    }
+    ENC_TRY(e, ealloc(e, &cv.w, h.size() * 2));
+    ENC_TRY(e, hipMemcpy(cv.w, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  } else {
+    ENC_TRY(e, ealloc(e, &cv.w, p.size() * 4));
+    ENC_TRY(e, hipMemcpy(cv.w, p.data(), p.size() * 4, hipMemcpyHostToDevice));
+  }
+  ENC_TRY(e, upload(e, &cv.bias, bb));
+  ENC_TRY(e, upload(e, &cv.s, s));
+  ENC_TRY(e, upload(e, &cv.t, t));
+  return GGD_OK;
+}
+
+int make_lin(ggd_enc* e, const std::string& name, int out, int in, float** w, float** b) {
+  const std::vector<float> *pw, *pb;
+  NEED(name + ".weight", (size_t)out * in, pw);
+  NEED(name + ".bias", out, pb);
+  ENC_TRY(e, upload(e, w, *pw));
+  ENC_TRY(e, upload(e, b, *pb));
+  return GGD_OK;
+}
+
+int run_conv(ggd_enc* e, const EConv& cv, const float* in, int n, int H, int W, float* out, int mode, int layout,
+             hipStream_t s) {
+  ConvArgs a{};
+  a.in = in;
+  a.w = cv.w;
+  a.bias = cv.bias;
+  a.s = cv.s;
+  a.t = cv.t;
+  a.out = out;
+  a.N = n;
+  a.H = H;
+  a.W = W;
+  a.Cin = cv.cin_pad;
+  a.Ho = conv_out(H, cv.kh, cv.stride, cv.pad);
+  a.Wo = conv_out(W, cv.kw, cv.stride, cv.pad);
+  a.Cout_pad = cv.cout_pad;
+  a.Cvalid = cv.cout;
+  a.KH = cv.kh;
+  a.KW = cv.kw;
+  a.stride = cv.stride;
+  a.pad = cv.pad;
+  a.mode = mode;
+  a.layout = layout;
+  ENC_TRY(e, launch_conv(e->dtype, a, s));
+  return GGD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ggd_enc_finalize(ggd_enc* e) {
+  if (!e) return GGD_ERR_ARG;
+  ENC_TRY(e, hipSetDevice(e->device));
+  const std::vector<float> *win, *fb, *pre;
+  NEED(PFX + "wav2spec.1.spectrogram.window", NFFT, win);
+  NEED(PFX + "wav2spec.1.mel_scale.fb", (size_t)NBIN * NMEL, fb);
+  NEED(PFX + "wav2spec.0.flipped_filter", 2, pre);
+  e->coef = -(*pre)[0];
+  // DFT basis (rows = output columns of the GEMM): [cos | -sin](2 pi k f / n_fft) * window[k]
+  std::vector<float> basis((size_t)SPEC_LD * NFFT, 0.f);
+  for (int f = 0; f < NBIN; ++f)
+    for (int k = 0; k < NFFT; ++k) {
+      const double ang = 2.0 * M_PI * (double)((long)k * f % NFFT) / NFFT;
+      basis[(size_t)f * NFFT + k] = (float)(std::cos(ang) * (*win)[k]);
+      basis[(size_t)(NBIN + f) * NFFT + k] = (float)(-std::sin(ang) * (*win)[k]);
+    }
+  ENC_TRY(e, upload(e, &e->basis, basis));
+  std::vector<float> fbT((size_t)NMEL * 768, 0.f);
+  for (int m = 0; m < NMEL; ++m)
+    for (int f = 0; f < NBIN; ++f) fbT[(size_t)m * 768 + f] = (*fb)[(size_t)f * NMEL + m];
+  ENC_TRY(e, upload(e, &e->fbT, fbT));
+  ENC_TRY(e, upload(e, &e->zeros, std::vector<float>(SPEC_LD, 0.f)));
+
+  // conv1 + bn1
+  {
+    const std::vector<float> *w, *b;
+    NEED(FE + "conv1.weight", 32 * 9, w);
+    NEED(FE + "conv1.bias", 32, b);
+    std::vector<float> s, t;
+    int r = fold_bn(e, FE + "bn1", 32, 32, s, t);
+    if (r) return r;
+    ENC_TRY(e, upload(e, &e->c1_w, *w));
+    ENC_TRY(e, upload(e, &e->c1_b, *b));
+    ENC_TRY(e, upload(e, &e->c1_s, s));
+    ENC_TRY(e, upload(e, &e->c1_t, t));
+  }
+  e->blocks.clear();
+  int inplanes = 32;
+  const int planes_l[4] = {32, 64, 128, 256}, nblk[4] = {3, 4, 6, 3}, stride_l[4] = {1, 2, 2, 2};
+  for (int l = 0; l < 4; ++l)
+    for (int bi = 0; bi < nblk[l]; ++bi) {
+      const std::string q = FE + "layer" + std::to_string(l + 1) + "." + std::to_string(bi) + ".";
+      EBlock B;
+      B.planes = planes_l[l];
+      const int st = bi == 0 ? stride_l[l] : 1;
+      int r = make_conv(e, B.c1, q + "conv1", q + "bn1", inplanes, B.planes, 3, st, 1, false);
+      if (!r) r = make_conv(e, B.c2, q + "conv2", q + "bn2", B.planes, B.planes, 3, 1, 1, false);
+      if (r) return r;
+      B.has_ds = e->staged.count(q + "downsample.0.weight") != 0;
+      if (B.has_ds) {
+        r = make_conv(e, B.ds, q + "downsample.0", q + "downsample.1", inplanes, B.planes, 1, st, 0, false);
+        if (r) return r;
+      } else if (st != 1 || inplanes != B.planes) {
+        return efail(e, GGD_ERR_NAME, "missing " + q + "downsample.0.weight");
+      }
+      r = make_lin(e, q + "se.fc.0", B.planes / 8, B.planes, &B.se_w0, &B.se_b0);
+      if (!r) r = make_lin(e, q + "se.fc.2", B.planes, B.planes / 8, &B.se_w2, &B.se_b2);
+      if (r) return r;
+      e->blocks.push_back(B);
+      inplanes = B.planes;
+    }
+  // heads: (conv, bn, fc, shuffle, channels in / out, kernel)
+  const char* hn[3] = {"low", "mid", "high"};
+  const int hc[3] = {64, 32, 16}, hk[3] = {2, 3, 3}, hs[3] = {1, 2, 4};
+  const int hh[3] = {conv_out(e->H[2], 2, 1, 0), conv_out(e->H[3] * 2, 3, 1, 0), conv_out(e->H[4] * 4, 3, 1, 0)};
+  for (int i = 0; i < 3; ++i) {
+    EHead& h = e->head[i];
+    h.shuffle = hs[i];
+    int r = make_conv(e, h.conv, FE + "conv_" + hn[i], FE + "bn_" + hn[i], hc[i], hc[i], hk[i], 1, 0, true);
+    if (r) return r;
+    h.K = hc[i] * hh[i];
+    r = make_lin(e, FE + "fc_" + hn[i], 32, h.K, &h.fc_w, &h.fc_b);
+    if (r) return r;
+  }
+  {
+    int r = make_lin(e, PFX + "wav_proj_layer", e->d_model, 32, &e->proj_w, &e->proj_b);
+    if (r) return r;
+  }
+  // workspaces for one chunk of clips
+  const size_t n = e->chunk, F = e->F;
+  ENC_TRY(e, ealloc(e, &e->frames, sizeof(float) * n * F * NFFT));
+  ENC_TRY(e, ealloc(e, &e->spec, sizeof(float) * n * F * SPEC_LD));
+  ENC_TRY(e, ealloc(e, &e->pw, sizeof(float) * n * F * POW_LD));
+  ENC_TRY(e, ealloc(e, &e->mel, sizeof(float) * n * F * NMEL));
+  ENC_TRY(e, ealloc(e, &e->img, sizeof(float) * n * F * NMEL));
+  size_t big = 0;
+  for (int l = 1; l <= 4; ++l) big = std::max(big, (size_t)e->H[l] * e->W[l] * planes_l[l - 1]);
+  for (int i = 0; i < 4; ++i) ENC_TRY(e, ealloc(e, &e->buf[i], sizeof(float) * n * big));
+  for (int i = 0; i < 3; ++i)
+    ENC_TRY(e, ealloc(e, &e->feat[i], sizeof(float) * n * e->H[i + 2] * e->W[i + 2] * planes_l[i + 1]));
+  ENC_TRY(e, ealloc(e, &e->se_y, sizeof(float) * n * 256));
+  ENC_TRY(e, ealloc(e, &e->sbuf, sizeof(float) * n * 32 *
+                                    std::max((size_t)e->H[3] * 2 * e->W[3] * 2, (size_t)e->H[4] * 4 * e->W[4] * 4)));
+  size_t hb = 0;
+  for (int i = 0; i < 3; ++i) hb = std::max(hb, (size_t)e->head[i].K * (size_t)(e->W[2] + e->W[4] * 4));
+  ENC_TRY(e, ealloc(e, &e->hbuf, sizeof(float) * n * hb));
+  e->staged.clear();
+  e->finalized = true;
+  return GGD_OK;
+}
+
+int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_mid, float* z_high, void* stream) {
+  if (!e || !wav || !z_low || !z_mid || !z_high) return efail(e, GGD_ERR_ARG, "null argument");
+  if (!e->finalized) return efail(e, GGD_ERR_STATE, "encoder weights not finalized");
+  if (n <= 0 || n > e->max_batch) return efail(e, GGD_ERR_ARG, "batch outside [1, max_batch]");
+  ENC_TRY(e, hipSetDevice(e->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int F = e->F, d = e->d_model;
+  for (int c0 = 0; c0 < n; c0 += e->chunk) {
+    const int m = std::min(e->chunk, n - c0);
+    const float* w = wav + (size_t)c0 * e->wav_len;
+    // front end
+    const size_t nf = (size_t)m * F * NFFT;
+    hipLaunchKernelGGL(enc_frames_kernel, dim3(blocks_for(nf, 256)), dim3(256), 0, s, w, e->frames, m, e->wav_len, F,
+                       e->coef);
+    ENC_TRY(e, hipGetLastError());
+    GemmArgs g{};
+    g.M = m * F;
+    g.N = SPEC_LD;
+    g.K = NFFT;
+    g.k_valid = NFFT;
+    g.A = e->frames;
+    g.lda = NFFT;
+    g.W = e->basis;
+    g.bias = e->zeros;
+    g.out = e->spec;
+    g.ldo = SPEC_LD;
+    g.n_valid = SPEC_LD;
+    ENC_TRY(e, launch_gemm(GGD_F32, PRO_F32, EPI_F32, g, s));
+    hipLaunchKernelGGL(enc_power_kernel, dim3(blocks_for((size_t)m * F * POW_LD, 256)), dim3(256), 0, s, e->spec,
+                       e->pw, m * F);
+    ENC_TRY(e, hipGetLastError());
+    g.N = NMEL;
+    g.K = 768;
+    g.k_valid = NBIN;
+    g.A = e->pw;
+    g.lda = POW_LD;
+    g.W = e->fbT;
+    g.out = e->mel;
+    g.ldo = NMEL;
+    g.n_valid = NMEL;
+    ENC_TRY(e, launch_gemm(GGD_F32, PRO_F32, EPI_F32, g, s));
+    hipLaunchKernelGGL(enc_inorm_kernel, dim3(m), dim3(NMEL), 0, s, e->mel, e->img, F);
+    ENC_TRY(e, hipGetLastError());
+    const size_t n1 = (size_t)m * e->H[1] * e->W[1] * 4;
+    hipLaunchKernelGGL(enc_conv1_kernel, dim3(blocks_for(n1, 256)), dim3(256), 0, s, e->img, e->c1_w, e->c1_b,
+                       e->c1_s, e->c1_t, e->buf[0], m, e->H[1], e->W[1]);
+    ENC_TRY(e, hipGetLastError());
+    // residual tower: x is the current input; u, v, r are the scratch buffers other than x
+    const float* x = e->buf[0];
+    int H = e->H[1], W = e->W[1], bidx = 0;
+    const int nblk[4] = {3, 4, 6, 3};
+    for (int l = 0; l < 4; ++l)
+      for (int bi = 0; bi < nblk[l]; ++bi, ++bidx) {
+        const EBlock& B = e->blocks[bidx];
+        float* sc[3];
+        for (int i = 0, k = 0; i < 4 && k < 3; ++i)
+          if (e->buf[i] != x) sc[k++] = e->buf[i];
+        float *u = sc[0], *v = sc[1], *r = sc[2];
+        const int Ho = conv_out(H, 3, B.c1.stride, 1), Wo = conv_out(W, 3, B.c1.stride, 1);
+        int rc = run_conv(e, B.c1, x, m, H, W, u, CONV_RELU_BN, LAYOUT_NHWC, s);
+        if (!rc) rc = run_conv(e, B.c2, u, m, Ho, Wo, v, CONV_BN, LAYOUT_NHWC, s);
+        const float* res = x;
+        if (!rc && B.has_ds) {
+          rc = run_conv(e, B.ds, x, m, H, W, r, CONV_BN, LAYOUT_NHWC, s);
+          res = r;
+        }
+        if (rc) return rc;
+        hipLaunchKernelGGL(enc_se_kernel, dim3(m), dim3(256), 0, s, v, Ho * Wo, B.planes, B.se_w0, B.se_b0, B.se_w2,
+                           B.se_b2, e->se_y);
+        ENC_TRY(e, hipGetLastError());
+        // the block output goes to u (consumed by conv2 already), or to the saved feature map
+        // of layers 2..4 that the heads read
+        float* o = (bi == nblk[l] - 1 && l >= 1) ? e->feat[l - 1] : u;
+        const size_t tot4 = (size_t)m * Ho * Wo * B.planes / 4;
+        hipLaunchKernelGGL(enc_se_apply_kernel, dim3(blocks_for(tot4, 256)), dim3(256), 0, s, v, e->se_y, res, o,
+                           Ho * Wo, B.planes, tot4);
+        ENC_TRY(e, hipGetLastError());
+        x = o;
+        H = Ho;
+        W = Wo;
+      }
+    // heads
+    float* zs[3] = {z_low + (size_t)c0 * e->t_low * d, z_mid + (size_t)c0 * e->t_mid * d,
+                    z_high + (size_t)c0 * e->t_high * d};
+    const int tl[3] = {e->t_low, e->t_mid, e->t_high};
+    for (int i = 0; i < 3; ++i) {
+      const EHead& h = e->head[i];
+      const float* fin = e->feat[i];
+      int Hh = e->H[i + 2], Wh = e->W[i + 2];
+      if (h.shuffle > 1) {
+        const int C = h.conv.cin, r = h.shuffle;
+        const size_t tot = (size_t)m * Hh * r * Wh * r * h.conv.cin_pad;
+        hipLaunchKernelGGL(enc_shuffle_kernel, dim3(blocks_for(tot, 256)), dim3(256), 0, s, fin, e->sbuf, m, Hh, Wh,
+                           C, r, h.conv.cin_pad);
+        ENC_TRY(e, hipGetLastError());
+        fin = e->sbuf;
+        Hh *= r;
+        Wh *= r;
+      }
+      int rc = run_conv(e, h.conv, fin, m, Hh, Wh, e->hbuf, CONV_RELU_BN, LAYOUT_NWCH, s);
+      if (rc) return rc;
+      const int Wo = conv_out(Wh, h.conv.kw, 1, 0);
+      if (Wo != tl[i]) return efail(e, GGD_ERR_STATE, "head length mismatch");
+      hipLaunchKernelGGL(enc_head_fc_kernel, dim3(m * Wo), dim3(256), 0, s, e->hbuf, h.K, h.fc_w, h.fc_b, e->proj_w,
+                         e->proj_b, zs[i], d);
+      ENC_TRY(e, hipGetLastError());
+    }
+  }
+  return GGD_OK;
+}
+
+}  // extern "C"

@@ -1,144 +1,99 @@
-"""HA2G speech encoder on the GPU (PyTorch-ROCm ops), run ONCE per clip.
+"""HA2G speech encoder on hand-written gfx950 kernels (csrc/ggd_encoder.hip), run ONCE per clip.
 
 The reference recomputes this encoder inside every denoise step
 (models/model.py:95-96 via gaussian_diffusion.py:256) although its input never
 changes over the reverse loop; in eval mode (BN running statistics, per-instance
 InstanceNorm, dropout 0) hoisting it out of the loop is exact.  It is 4.76 GFLOP
-per clip against 0.35 GFLOP per clip-step for the decoder.
+per clip against 0.31 GFLOP per clip-step for the decoder.
 
 Pipeline (ha2g/speech_encoder.py:37-61): pre-emphasis (utils.py:22-38) ->
 power mel spectrogram (torchaudio MelSpectrogram(16000, n_fft=1024, hop=512,
 n_mels=128): Hann window, centre reflect padding, |STFT|^2, HTK filterbank) ->
 +1e-6 -> InstanceNorm1d(128) -> SE-ResNet34 (ResNetSE34V2.py:118-188) -> three
-temporal heads -> shared Linear(32 -> d_model).
-
-MI355X mapping: the STFT is a real-DFT GEMM against a cached [cos | sin] basis
-(1024 x 1026) and the mel projection a second GEMM; the convolutions go to
-MIOpen.  The ~270 launches of one chunk are captured once per (chunk, wav length)
-as a hipGraph (torch.cuda.CUDAGraph) and replayed: issued eagerly from Python the
-chunk is host-bound (11.6 ms for 32 clips in chunks of 8 against 3.4 ms replayed
-as one 32-clip graph, MI355X).  A HIP implicit-GEMM port is the next scope row
-(SURVEY.md 8f rank 1).
+temporal heads -> shared Linear(32 -> d_model).  On the GPU: the STFT and the mel
+projection are f32 MFMA GEMMs, the convolutions implicit GEMMs on MFMA (bf16 or
+f32 products by the context dtype), BN folded into the conv epilogues; behind the
+ggd_enc_* C ABI (include/ggd.h).  There is no PyTorch / MIOpen fallback.
 """
-import math
+import ctypes
 
 import torch as th
 import torch.nn.functional as F
 
+from . import native
+
+_ENC_DTYPES = {"bf16": native.BF16, "f32": native.F32, "fp32": native.F32}
+
 
 class SpeechEncoder:
-    def __init__(self, sd, device, n_fft=1024, hop=512):
+    """HA2GSpeechEncoder (speech_encoder.py:9-61) behind ggd_enc_*; one context per wav length."""
+
+    def __init__(self, sd, device, dtype="f32", d_model=None, max_batch=1024):
         p = "speech_encoder."
         self.device = th.device(device)
-        self.w = {k[len(p):]: v.to(self.device, th.float32)
-                  for k, v in sd.items() if k.startswith(p) and v.is_floating_point()}
-        self.n_fft, self.hop = n_fft, hop
-        win = self.w["wav2spec.1.spectrogram.window"]
-        k = th.arange(n_fft, dtype=th.float64, device=self.device)
-        f = th.arange(n_fft // 2 + 1, dtype=th.float64, device=self.device)
-        ang = 2 * math.pi * k[:, None] * f[None, :] / n_fft
-        basis = th.cat([th.cos(ang), -th.sin(ang)], dim=1)          # (n_fft, 2F)
-        self.basis = (basis * win.double()[:, None]).float()          # window folded in
-        self.fb = self.w["wav2spec.1.mel_scale.fb"]
-        self.coef = -float(self.w["wav2spec.0.flipped_filter"].flatten()[0])
+        if self.device.type != "cuda":
+            raise ValueError("the HIP speech encoder runs on a GPU device only (no CPU fallback)")
+        self.sd = {k: v for k, v in sd.items() if k.startswith(p) and v.is_floating_point()}
+        self.d_model = int(d_model or self.sd[p + "wav_proj_layer.weight"].shape[0])
+        self.dtype = dtype
+        self.max_batch = max_batch
+        self.lib = native.load()
+        self._ctx = {}
 
-    def _bn(self, name, x):
-        w = self.w
-        return F.batch_norm(x, w[name + ".running_mean"], w[name + ".running_var"],
-                            w[name + ".weight"], w[name + ".bias"], False, 0.0, 1e-5)
+    def _context(self, wav_len):
+        h = self._ctx.get(wav_len)
+        if h is not None:
+            return h
+        lib = self.lib
+        h = ctypes.c_void_p()
+        with th.cuda.device(self.device):
+            rc = lib.ggd_enc_create(self.device.index or 0, self.d_model, wav_len, self.max_batch,
+                                    _ENC_DTYPES[self.dtype], ctypes.byref(h))
+            if rc != 0:
+                msg = lib.ggd_enc_last_error(h).decode() if h else "ggd_enc_create failed"
+                lib.ggd_enc_destroy(h)
+                raise ValueError(msg) if rc == native.GGD_ERR_UNSUPPORTED else native.GgdError(msg)
+            for name, v in self.sd.items():
+                a = v.detach().to("cpu", th.float32).contiguous()
+                native.check(h, lib.ggd_enc_load_weight(h, name.encode(), ctypes.c_void_p(a.data_ptr()), a.numel()),
+                             f"load {name}", "ggd_enc_last_error")
+            native.check(h, lib.ggd_enc_finalize(h), "finalize encoder", "ggd_enc_last_error")
+        self._ctx[wav_len] = h
+        return h
 
-    def _conv(self, name, x, stride=1, padding=0):
-        return F.conv2d(x, self.w[name + ".weight"], self.w.get(name + ".bias"), stride=stride, padding=padding)
-
-    def mel(self, wav):
-        """(N, T) -> (N, 128, frames) power mel spectrogram of the pre-emphasised signal."""
-        x = th.cat([wav[:, :1] - self.coef * wav[:, 1:2], wav[:, 1:] - self.coef * wav[:, :-1]], dim=1)
-        x = F.pad(x[:, None, :], (self.n_fft // 2, self.n_fft // 2), mode="reflect")[:, 0]
-        frames = x.unfold(1, self.n_fft, self.hop)                  # (N, frames, n_fft)
-        spec = frames @ self.basis                                   # (N, frames, 2F)
-        nf = self.n_fft // 2 + 1
-        power = spec[..., :nf] ** 2 + spec[..., nf:] ** 2
-        return (power @ self.fb).transpose(1, 2)
-
-    def _block(self, q, x, stride):
-        out = self._bn(q + "bn1", F.relu(self._conv(q + "conv1", x, stride, 1)))
-        out = self._bn(q + "bn2", self._conv(q + "conv2", out, 1, 1))
-        y = out.mean(dim=(2, 3))
-        y = F.relu(F.linear(y, self.w[q + "se.fc.0.weight"], self.w[q + "se.fc.0.bias"]))
-        y = th.sigmoid(F.linear(y, self.w[q + "se.fc.2.weight"], self.w[q + "se.fc.2.bias"]))
-        out = out * y[:, :, None, None]
-        if (q + "downsample.0.weight") in self.w:
-            x = self._bn(q + "downsample.1", self._conv(q + "downsample.0", x, stride))
-        return F.relu(out + x)
-
-    def _head(self, feat, conv, bn, fc, shuffle):
-        if shuffle > 1:
-            feat = F.pixel_shuffle(feat, shuffle)
-        feat = self._bn(bn, F.relu(self._conv(conv, feat)))
-        n, c, h, w = feat.shape
-        feat = feat.reshape(n, c * h, w).transpose(1, 2)
-        return F.linear(feat, self.w[fc + ".weight"], self.w[fc + ".bias"])
-
-    CHUNK = 32  # clips per encoder call: fixed, so a clip's features never depend on its batch
-    use_graph = True  # replay each chunk as a captured graph (cuda devices)
+    def lengths(self, wav_len):
+        h = self._context(wav_len)
+        t = [ctypes.c_int32() for _ in range(3)]
+        native.check(h, self.lib.ggd_enc_lengths(h, *[ctypes.byref(x) for x in t]), "lengths", "ggd_enc_last_error")
+        return tuple(x.value for x in t)
 
     @th.no_grad()
     def __call__(self, wav):
-        """wav (N, T) f32 -> (z_low, z_mid, z_high), each (N, T_i, d_model).
+        """wav (N, T) f32 -> (z_low, z_mid, z_high), each (N, T_i, d_model) on the device."""
+        wav = wav.to(self.device, th.float32).contiguous()
+        n, tw = wav.shape
+        if n > self.max_batch:
+            return tuple(th.cat(z) for z in zip(*[self(wav[i:i + self.max_batch])
+                                                   for i in range(0, n, self.max_batch)]))
+        h = self._context(tw)
+        tl = self.lengths(tw)
+        z = [th.empty(n, t, self.d_model, device=self.device) for t in tl]
+        stream = ctypes.c_void_p(th.cuda.current_stream(self.device).cuda_stream)
+        native.check(h, self.lib.ggd_enc_run(h, ctypes.c_void_p(wav.data_ptr()), n,
+                                             *[ctypes.c_void_p(x.data_ptr()) for x in z], stream),
+                     "encode", "ggd_enc_last_error")
+        return tuple(z)
 
-        Runs in fixed chunks of CHUNK clips (the last one zero padded): MIOpen and the GEMM
-        libraries pick algorithms by batch size, so a fixed batch keeps every clip's speech
-        memory bit-identical however the clips are sharded over GPUs or calls.
-        """
-        wav = wav.to(self.device, th.float32)
-        n = wav.shape[0]
-        pad = (-n) % self.CHUNK
-        if pad:
-            wav = th.cat([wav, wav.new_zeros(pad, wav.shape[1])])
-        # MIOpen's default convolution algorithms are not run-to-run deterministic (about
-        # 1e-6 between two identical calls); the deterministic solvers make the memory a
-        # pure function of the clip's audio
-        with th.backends.cudnn.flags(enabled=True, benchmark=False, deterministic=True):
-            outs = [self._run_chunk(wav[i:i + self.CHUNK]) for i in range(0, wav.shape[0], self.CHUNK)]
-        return tuple(th.cat([o[k] for o in outs])[:n] for k in range(3))
+    def close(self):
+        for h in self._ctx.values():
+            self.lib.ggd_enc_destroy(h)
+        self._ctx = {}
 
-    def _run_chunk(self, x):
-        if not (self.use_graph and self.device.type == "cuda"):
-            return self._encode(x)
-        key = tuple(x.shape)
-        graphs = self.__dict__.setdefault("_graphs", {})
-        if key not in graphs:
-            static_in = x.clone()
-            side = th.cuda.Stream(self.device)
-            side.wait_stream(th.cuda.current_stream(self.device))
-            with th.cuda.stream(side):
-                self._encode(static_in)                    # library / algorithm selection
-            th.cuda.current_stream(self.device).wait_stream(side)
-            g = th.cuda.CUDAGraph()
-            with th.cuda.graph(g):
-                static_out = self._encode(static_in)
-            graphs[key] = (g, static_in, static_out)
-        g, static_in, static_out = graphs[key]
-        static_in.copy_(x)
-        g.replay()
-        # the next replay overwrites the static outputs
-        return tuple(o.clone() for o in static_out)
-
-    def _encode(self, wav):
-        x = self.mel(wav) + 1e-6
-        x = F.instance_norm(x, eps=1e-5)
-        r = "wav_encoder.feat_extractor."
-        x = self._bn(r + "bn1", F.relu(self._conv(r + "conv1", x[:, None], 1, 1)))
-        feats = []
-        for li, (nblk, stride) in enumerate(zip((3, 4, 6, 3), (1, 2, 2, 2))):
-            for bi in range(nblk):
-                x = self._block(r + f"layer{li + 1}.{bi}.", x, stride if bi == 0 else 1)
-            feats.append(x)
-        z = (self._head(feats[1], r + "conv_low", r + "bn_low", r + "fc_low", 1),
-             self._head(feats[2], r + "conv_mid", r + "bn_mid", r + "fc_mid", 2),
-             self._head(feats[3], r + "conv_high", r + "bn_high", r + "fc_high", 4))
-        pw, pb = self.w["wav_proj_layer.weight"], self.w["wav_proj_layer.bias"]
-        return tuple(F.linear(a, pw, pb) for a in z)
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def speech_tokens(model_type, z):

@@ -142,7 +142,7 @@ class Speech2GestureModel:
         if self._encoder is None:
             if self._sd is None:
                 raise RuntimeError("load_state_dict() before use")
-            self._encoder = SpeechEncoder(self._sd, self.device)
+            self._encoder = SpeechEncoder(self._sd, self.device, dtype=self.dtype, d_model=self.arch["d_model"])
         return self._encoder
 
     def context(self, L, Ts, n):

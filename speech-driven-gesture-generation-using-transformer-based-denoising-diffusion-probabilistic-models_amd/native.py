@@ -11,7 +11,7 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libggd.so")
-SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_diag.hip", "ggd_api.hip"]
+SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_diag.hip", "ggd_encoder.hip", "ggd_api.hip"]
 HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_fusedlib.h", "ggd_phases.h", os.path.join("..", "..", "include", "ggd.h")]
 
 GGD_OK, GGD_IGNORED = 0, 1
@@ -25,6 +25,8 @@ EXPORTS = [
     "ggd_create", "ggd_destroy", "ggd_last_error", "ggd_load_weight", "ggd_finalize_weights",
     "ggd_set_schedule", "ggd_set_memory", "ggd_denoise", "ggd_posterior_step", "ggd_sample",
     "ggd_set_profiling", "ggd_kernel_time", "ggd_profile_kind", "ggd_diag", "ggd_version",
+    "ggd_enc_create", "ggd_enc_destroy", "ggd_enc_last_error", "ggd_enc_load_weight", "ggd_enc_finalize",
+    "ggd_enc_lengths", "ggd_enc_run",
 ]
 
 
@@ -108,6 +110,13 @@ def load():
         "ggd_profile_kind": (ctypes.c_int, [CTX]),
         "ggd_diag": (ctypes.c_int, [CTX, I32, VP, I32, I32, VP]),
         "ggd_version": (ctypes.c_char_p, []),
+        "ggd_enc_create": (ctypes.c_int, [ctypes.c_int, I32, I32, I32, I32, P(CTX)]),
+        "ggd_enc_destroy": (ctypes.c_int, [CTX]),
+        "ggd_enc_last_error": (ctypes.c_char_p, [CTX]),
+        "ggd_enc_load_weight": (ctypes.c_int, [CTX, ctypes.c_char_p, VP, I64]),
+        "ggd_enc_finalize": (ctypes.c_int, [CTX]),
+        "ggd_enc_lengths": (ctypes.c_int, [CTX, P(I32), P(I32), P(I32)]),
+        "ggd_enc_run": (ctypes.c_int, [CTX, VP, I32, VP, VP, VP, VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -121,11 +130,11 @@ class GgdError(RuntimeError):
     pass
 
 
-def check(ctx, code, what):
+def check(ctx, code, what, last_error="ggd_last_error"):
     """Map a ggd_status to the reference's exception types."""
     if code >= 0:
         return code
-    msg = load().ggd_last_error(ctx)
+    msg = getattr(load(), last_error)(ctx)
     msg = msg.decode() if msg else ""
     text = f"{what}: {msg}"
     if code == GGD_ERR_UNSUPPORTED:
