@@ -266,7 +266,7 @@ def main():
     if prof and prof_n:
         avg_us = sum(prof_us) / prof_n
         if prof_kind == 1:   # the persistent loop: one launch runs all T denoise steps of the batch
-            flop = clip_step * B * T
+            flop = clip_step * B * T / prof_n   # one launch per chunk of <= 32 clips
             kernel = f"mk_kernel<{args.dtype}> (persistent reverse loop: all {T} denoise steps, 17 phases each)"
             timing = "hipEvent pair around the loop's single launch in the last timed pass"
         else:

@@ -46,6 +46,15 @@ struct Layer {
   FLin f_qkv, f_o_sa, f_q_ca, f_o_ca, f_ff1, f_ff2;  // fused-path copies
 };
 
+// two-way decoder layer (CrossAttentionLayer, models/nn.py:55-125)
+struct Layer2 {
+  float *ln_sa_g, *ln_sa_b, *ln_sam_g, *ln_sam_b, *ln_ca_g, *ln_ca_b, *ln_ff_g, *ln_ff_b;
+  float *ln_ffm_g = nullptr, *ln_ffm_b = nullptr;
+  Lin qkv_sa, o_sa, qkv_sam, o_sam, qkv_ca, o_ca, ff1, ff2, ffm1, ffm2;
+  Conv3 sa_q, sa_k, sa_v, sam_q, sam_k, sam_v, ca_q, ca_k, ca_v;
+  bool has_ffm = false;  // every layer but the last feed-forwards the memory (nn.py:408-418)
+};
+
 struct ProfEvents {
   std::vector<hipEvent_t> ev;  // timing events; eager marks consume ev[next++]
   size_t next = 0;
@@ -81,6 +90,13 @@ struct ggd_ctx {
   float* pe = nullptr;       // [pe_len][d]
   int pe_len = 0;
   float* kv_step = nullptr;  // [layers][T_orig][2d]
+
+  // two-way decoder (generic kernels, joint layout [n][J = L + 1 + Ts][d])
+  bool twoway = false;
+  int J = 0;
+  std::vector<Layer2> layers2;
+  float *hj = nullptr, *mem_base = nullptr, *step_tab = nullptr;
+  void *qkvj = nullptr, *attj = nullptr, *zbuf = nullptr, *ffnj = nullptr;
 
   // schedule
   std::vector<double> betas;
@@ -119,6 +135,7 @@ struct ggd_ctx {
 
   // persistent reverse loop (ggd_mega.hip)
   bool no_mega = false;                // ggd_diag what = 9: route sampling through per-phase launches
+  int mega_place = 0;                  // ggd_diag what = 12: persistent-loop workgroup placement
   FusedArgs* mega_fa = nullptr;        // device [n_layers][4]
   unsigned long long* mega_phase_stamps = nullptr;  // ggd_diag what = 11: layer 1's phases + KE
   FinalArgs* mega_fe = nullptr;
@@ -347,12 +364,14 @@ int build_step_tables(ggd_ctx* c) {
   GEMM(c, PRO_F32, EPI_SILU, g, s);
   g = gemm_args(c->step2, T, hid, d, tok, d);
   GEMM(c, PRO_F32, EPI_F32, g, s);
-  g = gemm_args(c->emb_mem, T, tok, d, mem0, d);
+  // memory row 0 sits at position 0 of the memory stream (one-way, nn.py:223) or at position
+  // L of the joint sequence (two-way, nn.py:438-442)
+  g = gemm_args(c->emb_mem, T, tok, d, c->twoway ? c->step_tab : mem0, d);
   g.pe = c->pe;
   g.pe_period = 1;
-  g.pe_offset = 0;
+  g.pe_offset = c->twoway ? c->desc.seq_len : 0;
   GEMM(c, PRO_F32, EPI_PE, g, s);
-  for (int l = 0; l < c->desc.n_layers; ++l) {
+  for (int l = 0; l < (c->twoway ? 0 : c->desc.n_layers); ++l) {
     g = gemm_args(c->layers[l].kv_ca, T, mem0, d, c->kv_step + (size_t)l * T * 2 * d, 2 * d);
     GEMM(c, PRO_F32, EPI_F32, g, s);
   }
@@ -477,8 +496,101 @@ int launch_fused_layers(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
 // The decoder forward on the internal x state (M = n*L rows) ending in eps [M][cpad].
 // In sampling mode (`sampling`), the first GEMM advances the iteration counter and the
 // cross-attention reads t from the step records.
+// CrossAttention.forward (nn.py:428-447) with CrossAttentionLayer (nn.py:90-125) on the generic
+// kernels.  Joint layout: clip b's rows b*J .. b*J+J-1 hold [x (L rows); memory (1 + Ts rows)];
+// the x-only / memory-only sub-layers address their segment through GEMM row maps and the
+// attention's row offset, so [x; memory] is never concatenated or split by a copy.
+int launch_decoder_twoway(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
+  const ggd_desc& D = c->desc;
+  const int L = D.seq_len, d = D.d_model, J = c->J, Tm = J - L, dk = d / D.heads, dt = D.dtype;
+  hipStream_t s = c->stream;
+  // x rows: emb_x + PE[0 .. L) (the first launch of a step bumps the iteration counter)
+  GemmArgs g = gemm_args(c->emb_x, n * L, c->x, D.d_pose, c->hj, d);
+  g.pe = c->pe;
+  g.pe_period = L;
+  g.pe_offset = 0;
+  g.o_len = L;
+  g.o_stride = J;
+  g.step_counter = sampling ? c->d_counter : nullptr;
+  GEMM(c, PRO_F32, EPI_PE, g, s);
+  // memory rows: step token of t + the installed speech rows (both already carry their PE)
+  HIP_TRY(c, launch_mem_assemble(c->hj, c->mem_base, c->step_tab, t_clip, c->d_steps, c->d_counter, n, L,
+                                 D.speech_len, d, s));
+
+  struct Seg { int len, off, rows; };  // rows per clip of a segment and its first row
+  const Seg SX{L, 0, L}, SM{Tm, L, Tm}, SJ{J, 0, J};
+  auto ln = [&](const Seg& sg, const float* gm, const float* bt) -> hipError_t {
+    return launch_layernorm(dt, c->hj, sg.len == J ? 0 : sg.len, J, sg.off, gm, bt, c->zbuf, n * sg.rows, d, s);
+  };
+  // x_seg += MDHA(LN(x_seg)) over the segment's own sequence (nn.py:96-104, 106-113)
+  auto attn_block = [&](const Seg& sg, const float* gm, const float* bt, const Lin& qkv, const Lin& o,
+                        const Conv3& cq, const Conv3& ck, const Conv3& cv) -> int {
+    const int M = n * sg.rows, map = sg.len == J ? 0 : sg.len;
+    HIP_TRY(c, ln(sg, gm, bt));
+    GemmArgs q = gemm_args(qkv, M, c->zbuf, d, c->qkvj, 3 * d);
+    q.o_len = map;
+    q.o_stride = J;
+    q.o_off = sg.off;
+    GEMM(c, PRO_T, EPI_T, q, s);
+    AttnArgs at{};
+    at.cross = 0;
+    at.q = c->qkvj;
+    at.ldq = 3 * d;
+    at.k = (const char*)c->qkvj + c->tsize * d;
+    at.v = (const char*)c->qkvj + c->tsize * 2 * d;
+    at.ldkv = 3 * d;
+    at.cw_q = cq.w; at.cb_q = cq.b;
+    at.cw_k = ck.w; at.cb_k = ck.b;
+    at.cw_v = cv.w; at.cb_v = cv.b;
+    at.out = c->attj;
+    at.ldo = d;
+    at.Lq = at.Lk = sg.rows;
+    at.dk = dk;
+    at.heads = D.heads;
+    at.d = d;
+    at.scale = 1.0f / std::sqrt((float)dk);
+    at.seq_stride = J;
+    at.seq_off = sg.off;
+    HIP_TRY(c, launch_attention(dt, at, n, s));
+    GemmArgs op = gemm_args(o, M, c->attj, d, c->hj, d);
+    op.a_len = op.o_len = map;
+    op.a_stride = op.o_stride = J;
+    op.a_off = op.o_off = sg.off;
+    GEMM(c, PRO_T, EPI_RESID, op, s);
+    return GGD_OK;
+  };
+  // seg += FFN(LN(seg)) (nn.py:116-124)
+  auto ffn_block = [&](const Seg& sg, const float* gm, const float* bt, const Lin& f1, const Lin& f2) -> int {
+    const int M = n * sg.rows;
+    HIP_TRY(c, ln(sg, gm, bt));
+    GemmArgs a1 = gemm_args(f1, M, c->zbuf, d, c->ffnj, 4 * d);
+    GEMM(c, PRO_T, EPI_RELU2, a1, s);
+    GemmArgs a2 = gemm_args(f2, M, c->ffnj, 4 * d, c->hj, d);
+    a2.o_len = sg.len;
+    a2.o_stride = J;
+    a2.o_off = sg.off;
+    GEMM(c, PRO_T, EPI_RESID, a2, s);
+    return GGD_OK;
+  };
+  int r;
+  for (int li = 0; li < D.n_layers; ++li) {
+    const Layer2& Y = c->layers2[li];
+    if ((r = attn_block(SX, Y.ln_sa_g, Y.ln_sa_b, Y.qkv_sa, Y.o_sa, Y.sa_q, Y.sa_k, Y.sa_v))) return r;
+    if ((r = attn_block(SM, Y.ln_sam_g, Y.ln_sam_b, Y.qkv_sam, Y.o_sam, Y.sam_q, Y.sam_k, Y.sam_v))) return r;
+    if ((r = attn_block(SJ, Y.ln_ca_g, Y.ln_ca_b, Y.qkv_ca, Y.o_ca, Y.ca_q, Y.ca_k, Y.ca_v))) return r;
+    if ((r = ffn_block(SX, Y.ln_ff_g, Y.ln_ff_b, Y.ff1, Y.ff2))) return r;
+    if (Y.has_ffm && (r = ffn_block(SM, Y.ln_ffm_g, Y.ln_ffm_b, Y.ffm1, Y.ffm2))) return r;
+  }
+  // out_layers on the x rows (nn.py:434-436, 447)
+  HIP_TRY(c, ln(SX, c->out_ln_g, c->out_ln_b));
+  g = gemm_args(c->out_lin, n * L, c->zbuf, d, c->eps, c->cpad);
+  GEMM(c, PRO_T, EPI_F32, g, s);
+  return GGD_OK;
+}
+
 int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
   const ggd_desc& D = c->desc;
+  if (c->twoway) return launch_decoder_twoway(c, n, sampling, t_clip);
   if (c->fused) return launch_fused_layers(c, n, sampling, t_clip);
   const int L = D.seq_len, d = D.d_model, M = n * L, dk = d / D.heads;
   hipStream_t s = c->stream;
@@ -682,13 +794,19 @@ int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out) {
     *out = c;
     return GGD_ERR_ARG;
   }
-  if (D.decoder_type != GGD_DEC_ONEWAY) {
-    c->err = "decoder type cross_attention (two-way) has no HIP path yet";
+  const int dk = D.d_model / D.heads;
+  if (D.decoder_type == GGD_DEC_TWOWAY) {
+    // CrossAttention (nn.py:381-447) on the generic kernels: joint sequence [x; memory]
+    if ((dk != 32 && dk != 64) || D.d_model % 256 || D.d_model > 1024 || D.seq_len + 1 + D.speech_len > 192) {
+      c->err = "unsupported two-way shape (need d_model % 256 == 0, d_k in {32,64}, L + 1 + Ts <= 192)";
+      *out = c;
+      return GGD_ERR_UNSUPPORTED;
+    }
+  } else if (D.decoder_type != GGD_DEC_ONEWAY) {
+    c->err = "unknown decoder type";
     *out = c;
     return GGD_ERR_UNSUPPORTED;
-  }
-  const int dk = D.d_model / D.heads;
-  if ((dk != 32 && dk != 64) || D.d_model != 256 || D.seq_len > 192 || D.speech_len + 1 > 192) {
+  } else if ((dk != 32 && dk != 64) || D.d_model != 256 || D.seq_len > 192 || D.speech_len + 1 > 192) {
     c->err = "unsupported shape (need d_model == 256, d_k in {32,64}, L <= 192, memory <= 192)";
     *out = c;
     return GGD_ERR_UNSUPPORTED;
@@ -722,11 +840,25 @@ int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out) {
   HIP_TRY(c, dalloc(c, &c->ffn, c->tsize * M * 4 * d));
   HIP_TRY(c, dalloc(c, &c->d_counter, sizeof(int)));
   HIP_TRY(c, dalloc(c, &c->d_t, sizeof(int) * B));
-  HIP_TRY(c, dalloc(c, &c->kv_mem, sizeof(float) * D.n_layers * (size_t)B * Ts * 2 * d));
   HIP_TRY(c, dalloc(c, &c->mem_tmp, sizeof(float) * (size_t)B * Ts * d));
   HIP_TRY(c, dalloc(c, &c->tok_tmp, sizeof(float) * (size_t)B * Ts * d));
-  HIP_TRY(c, dalloc(c, &c->kv_step, sizeof(float) * D.n_layers * (size_t)D.diffusion_steps * 2 * d));
-  c->pe_len = std::max(L, Ts + 1) + 1;
+  if (D.decoder_type == GGD_DEC_TWOWAY) {
+    c->twoway = true;
+    c->J = L + 1 + Ts;
+    const size_t MJ = (size_t)B * c->J;
+    HIP_TRY(c, dalloc(c, &c->hj, sizeof(float) * MJ * d));
+    HIP_TRY(c, dalloc(c, &c->qkvj, c->tsize * MJ * 3 * d));
+    HIP_TRY(c, dalloc(c, &c->attj, c->tsize * MJ * d));
+    HIP_TRY(c, dalloc(c, &c->zbuf, c->tsize * MJ * d));
+    HIP_TRY(c, dalloc(c, &c->ffnj, c->tsize * (size_t)B * std::max(L, 1 + Ts) * 4 * d));
+    HIP_TRY(c, dalloc(c, &c->mem_base, sizeof(float) * (size_t)B * Ts * d));
+    HIP_TRY(c, dalloc(c, &c->step_tab, sizeof(float) * (size_t)D.diffusion_steps * d));
+    c->pe_len = c->J + 1;
+  } else {
+    HIP_TRY(c, dalloc(c, &c->kv_mem, sizeof(float) * D.n_layers * (size_t)B * Ts * 2 * d));
+    HIP_TRY(c, dalloc(c, &c->kv_step, sizeof(float) * D.n_layers * (size_t)D.diffusion_steps * 2 * d));
+    c->pe_len = std::max(L, Ts + 1) + 1;
+  }
   std::vector<float> pe;
   build_pe(pe, c->pe_len, d);
   HIP_TRY(c, dalloc(c, &c->pe, sizeof(float) * pe.size()));
@@ -778,6 +910,48 @@ int ggd_finalize_weights(ggd_ctx* c) {
   TRY(pack_lin(c, c->step0, {"diffusion_step_encoder.proj.0"}, d, d));
   TRY(pack_lin(c, c->step2, {"diffusion_step_encoder.proj.2"}, d, d));
   if (D.model_type == GGD_MODEL_S2G_V2) TRY(pack_lin(c, c->blend, {"blend_layer"}, d, 3 * d));
+  if (c->twoway) {
+    c->layers2.assign(D.n_layers, Layer2{});
+    for (int l = 0; l < D.n_layers; ++l) {
+      Layer2& Ly = c->layers2[l];
+      const std::string q = P + "layers." + std::to_string(l) + ".";
+      auto ln = [&](float** g, float** b, const std::string& name) {
+        int rr = upload_vec(c, g, q + name + ".weight", d);
+        return rr ? rr : upload_vec(c, b, q + name + ".bias", d);
+      };
+      auto mdha = [&](Lin& qkv, Lin& o, Conv3& cq, Conv3& ck, Conv3& cv, const std::string& name) {
+        const std::string a = q + name + ".";
+        int rr = pack_lin(c, qkv, {a + "query.0.linear", a + "key.0.linear", a + "value.0.linear"}, d, d);
+        if (!rr) rr = pack_lin(c, o, {a + "output"}, d, d);
+        if (!rr) rr = pack_conv(c, cq, a + "query.1", dk);
+        if (!rr) rr = pack_conv(c, ck, a + "key.1", dk);
+        if (!rr) rr = pack_conv(c, cv, a + "value.1", dk);
+        return rr;
+      };
+      TRY(ln(&Ly.ln_sa_g, &Ly.ln_sa_b, "norm_self_attn"));
+      TRY(mdha(Ly.qkv_sa, Ly.o_sa, Ly.sa_q, Ly.sa_k, Ly.sa_v, "self_attn"));
+      TRY(ln(&Ly.ln_sam_g, &Ly.ln_sam_b, "norm_self_attn_mem"));
+      TRY(mdha(Ly.qkv_sam, Ly.o_sam, Ly.sam_q, Ly.sam_k, Ly.sam_v, "self_attn_mem"));
+      TRY(ln(&Ly.ln_ca_g, &Ly.ln_ca_b, "norm_cross_attn"));
+      TRY(mdha(Ly.qkv_ca, Ly.o_ca, Ly.ca_q, Ly.ca_k, Ly.ca_v, "cross_attn"));
+      TRY(ln(&Ly.ln_ff_g, &Ly.ln_ff_b, "norm_ff"));
+      TRY(pack_lin(c, Ly.ff1, {q + "feed_forward.layer1"}, 4 * d, d));
+      TRY(pack_lin(c, Ly.ff2, {q + "feed_forward.layer2"}, d, 4 * d));
+      Ly.has_ffm = c->staged.count(q + "feed_forward_mem.layer1.weight") != 0;
+      if (Ly.has_ffm) {
+        TRY(ln(&Ly.ln_ffm_g, &Ly.ln_ffm_b, "norm_ff_mem"));
+        TRY(pack_lin(c, Ly.ffm1, {q + "feed_forward_mem.layer1"}, 4 * d, d));
+        TRY(pack_lin(c, Ly.ffm2, {q + "feed_forward_mem.layer2"}, d, 4 * d));
+      } else if (l + 1 < D.n_layers) {
+        return fail(c, GGD_ERR_NAME, "missing weight: " + q + "feed_forward_mem.layer1.weight");
+      }
+    }
+    TRY(build_step_tables(c));
+    c->fused = c->persist = false;
+    c->staged.clear();
+    c->finalized = true;
+    return GGD_OK;
+  }
   c->layers.assign(D.n_layers, Layer{});
   for (int l = 0; l < D.n_layers; ++l) {
     Layer& Ly = c->layers[l];
@@ -877,6 +1051,17 @@ int ggd_set_memory(ggd_ctx* c, const float* tok, int32_t n, int32_t ts, int32_t 
     g = gemm_args(c->blend, M, tok, dz, c->tok_tmp, d);
     GEMM(c, PRO_F32, EPI_F32, g, s);
     src = c->tok_tmp;
+  }
+  if (c->twoway) {  // emb_mem + PE at joint positions L+1 .. L+Ts (nn.py:433-442), assembled per step
+    g = gemm_args(c->emb_mem, M, src, d, c->mem_base, d);
+    g.pe = c->pe;
+    g.pe_period = ts;
+    g.pe_offset = D.seq_len + 1;
+    GEMM(c, PRO_F32, EPI_PE, g, s);
+    HIP_TRY(c, hipEventRecord(c->ev_out, s));
+    HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
+    c->mem_n = n;
+    return GGD_OK;
   }
   // emb_mem + PE at positions 1..Ts (row 0 is the step token), nn.py:223
   g = gemm_args(c->emb_mem, M, src, d, c->mem_tmp, d);
@@ -1022,6 +1207,11 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
           avg_us[16 * j + i] = (h[16 * j] && h[16 * j + i] >= h[16 * j]) ? (double)(h[16 * j + i] - h[16 * j]) / 2400.0 : -1.0;
     }
     if (p[0] == 0) c->mega_phase_stamps = nullptr;
+    return GGD_OK;
+  }
+  if (what == 12 && np >= 1) {  // persistent-loop placement: {0} clip group per XCD, {1} part p on XCD p
+    c->mega_place = p[0] == 1 ? 1 : 0;
+    *avg_us = c->mega_place;
     return GGD_OK;
   }
   if (what == 9 && np >= 1) {  // p[0] != 0: sample through the per-phase launches, not the persistent loop
@@ -1290,13 +1480,19 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
   HIP_TRY(c, hipMemcpyAsync(c->mega_fa, c->mega_fa_host.data(), sizeof(FusedArgs) * 4 * NL, hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipMemcpyAsync(c->mega_fe, &fe, sizeof(FinalArgs), hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipMemsetAsync(c->mega_status, 0, sizeof(int), s));
-  MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status, c->mega_stamps};
+  // batches above the loop's capacity run as consecutive launches of up to `cap` clips each
+  const int cap = mega_capacity(D.dtype, D.seq_len);
+  const int chunks = (a.n + cap - 1) / cap;
   if (c->profiling) {
     c->prof.next = 0;
     int r = prof_mark(c, s);
     if (r) return r;
   }
-  HIP_TRY(c, launch_mega(D.dtype, D.seq_len, m, a.n, s));
+  for (int c0 = 0; c0 < a.n; c0 += cap) {
+    MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status, c0 == 0 ? c->mega_stamps : nullptr,
+               c0, c->mega_place};
+    HIP_TRY(c, launch_mega(D.dtype, D.seq_len, m, std::min(cap, a.n - c0), s));
+  }
   if (c->profiling) {
     int r = prof_mark(c, s);
     if (r) return r;
@@ -1309,8 +1505,8 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
   if (c->profiling) {  // the whole loop is the one timed launch
     float ms = 0;
     HIP_TRY(c, hipEventElapsedTime(&ms, c->prof.ev[0], c->prof.ev[1]));
-    c->prof_avg_us = ms * 1000.0;
-    c->prof_launches = 1;
+    c->prof_avg_us = ms * 1000.0 / chunks;
+    c->prof_launches = chunks;
     c->prof_kind = 1;
     c->span_pending = 0;
   }
@@ -1396,7 +1592,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   HIP_TRY(c, launch_set_int(c->d_counter, -1, s));
 
   const int graph_steps = a->extras ? nsteps - 1 : nsteps;
-  if (c->fused && !c->no_mega && graph_steps > 0 && a->n <= mega_capacity(D.dtype, D.seq_len)) {
+  if (c->fused && !c->no_mega && graph_steps > 0 && mega_capacity(D.dtype, D.seq_len) > 0) {
     int r = run_mega(c, *a, graph_steps);
     if (r) return r;
     if (a->extras) {  // the last iteration with its extras through the per-phase kernels

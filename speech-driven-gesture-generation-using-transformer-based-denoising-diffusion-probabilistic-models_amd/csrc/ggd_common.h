@@ -125,9 +125,11 @@ struct AttGeom {
 
 template <typename T>
 __host__ __device__ inline AttGeom att_geom(int Lq, int Lk, int dk) {
+  // P V runs K = Lkp: 32-key steps on bf16 MFMA, 4-key steps on f32 (16-key padding suffices)
+  constexpr int KA = sizeof(T) == 2 ? 32 : 16;
   AttGeom g;
   g.Lqp = (Lq + 15) / 16 * 16;
-  g.Lkp = (Lk + 31) / 32 * 32;
+  g.Lkp = (Lk + KA - 1) / KA * KA;
   g.SQ = dk + AttPad<T>::P;
   g.SV = g.Lkp + AttPad<T>::P;
   g.SP = g.Lkp + AttPad<T>::P;
@@ -135,9 +137,11 @@ __host__ __device__ inline AttGeom att_geom(int Lq, int Lk, int dk) {
   g.off_k = g.off_q + sizeof(T) * (size_t)g.Lqp * g.SQ;
   g.off_v = g.off_k + sizeof(T) * (size_t)g.Lkp * g.SQ;
   g.off_p = g.off_v + sizeof(T) * (size_t)dk * g.SV;
-  g.off_raw = g.off_p + sizeof(T) * (size_t)4 * 16 * g.SP;
+  // the f32 staging rows (raw) live only before the core starts and P only inside it: they share
+  g.off_raw = g.off_p;
   const int lmax = Lq > Lk ? Lq : Lk;
-  g.total = g.off_raw + sizeof(float) * (size_t)(lmax + 2) * dk;
+  const size_t p_bytes = sizeof(T) * (size_t)4 * 16 * g.SP, raw_bytes = sizeof(float) * (size_t)(lmax + 2) * dk;
+  g.total = g.off_p + (p_bytes > raw_bytes ? p_bytes : raw_bytes);
   return g;
 }
 

@@ -47,6 +47,7 @@ constexpr int NFFT = 1024, HOP = 512, NBIN = NFFT / 2 + 1, NMEL = 128;
 constexpr int SPEC_LD = 1088;   // 2 * 513 columns padded to the GEMM's 64-column tiles
 constexpr int POW_LD = 516;     // 513 power bins, rows 16-byte aligned
 constexpr int CONV_TPB = 256;   // 4 waves; a wave owns 32 output pixels
+constexpr int SE_SLICES = 32;   // pixel slices of the SE squeeze's first stage
 
 // ------------------------------------------------------------------------------------------
 // front end
@@ -256,22 +257,37 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_kernel(ConvArgs a) {
 // ------------------------------------------------------------------------------------------
 // squeeze-excitation, residual, pixel shuffle, heads
 // ------------------------------------------------------------------------------------------
-// one workgroup per clip: y[c] = sigmoid(fc2(relu(fc0(mean_hw(v)))))   (ResNetBlocks.py:81-96)
-__global__ void __launch_bounds__(256) enc_se_kernel(const float* __restrict__ v, int HW, int C,
-                                                     const float* __restrict__ w0, const float* __restrict__ b0,
-                                                     const float* __restrict__ w2, const float* __restrict__ b2,
-                                                     float* __restrict__ y) {
-  __shared__ float part[256], mean[256], hid[32];
-  const int b = blockIdx.x, tid = threadIdx.x, stripes = 256 / C, c = tid % C, st = tid / C;
+// SE squeeze, stage 1: grid (clips, S slices); each workgroup sums its slice of the clip's pixels
+// for every channel -> part[clip][slice][C] (fixed partition and order: deterministic)
+__global__ void __launch_bounds__(256) enc_se_sum_kernel(const float* __restrict__ v, int HW, int C,
+                                                         float* __restrict__ part) {
+  __shared__ float red[256];
+  const int b = blockIdx.x, sl = blockIdx.y, S = gridDim.y, tid = threadIdx.x;
+  const int stripes = 256 / C, c = tid % C, st = tid / C;
+  const int p0 = (int)((long)HW * sl / S), p1 = (int)((long)HW * (sl + 1) / S);
   const float* src = v + (size_t)b * HW * C;
   float s = 0.f;
   if (st < stripes)
-    for (int p = st; p < HW; p += stripes) s += src[(size_t)p * C + c];
-  part[tid] = s;
+    for (int p = p0 + st; p < p1; p += stripes) s += src[(size_t)p * C + c];
+  red[tid] = s;
   __syncthreads();
   if (tid < C) {
     float tot = 0.f;
-    for (int k = 0; k < stripes; ++k) tot += part[k * C + tid];
+    for (int k = 0; k < stripes; ++k) tot += red[k * C + tid];
+    part[((size_t)b * S + sl) * C + tid] = tot;
+  }
+}
+
+// stage 2, one workgroup per clip: y[c] = sigmoid(fc2(relu(fc0(mean_hw(v)))))  (ResNetBlocks.py:81-96)
+__global__ void __launch_bounds__(256) enc_se_kernel(const float* __restrict__ part, int S, int HW, int C,
+                                                     const float* __restrict__ w0, const float* __restrict__ b0,
+                                                     const float* __restrict__ w2, const float* __restrict__ b2,
+                                                     float* __restrict__ y) {
+  __shared__ float mean[256], hid[32];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid < C) {
+    float tot = 0.f;
+    for (int k = 0; k < S; ++k) tot += part[((size_t)b * S + k) * C + tid];
     mean[tid] = tot / (float)HW;
   }
   __syncthreads();
@@ -413,7 +429,7 @@ struct ggd_enc {
   float *proj_w = nullptr, *proj_b = nullptr;
   // workspaces (chunk clips)
   float *frames = nullptr, *spec = nullptr, *pw = nullptr, *mel = nullptr, *img = nullptr;
-  float *buf[4] = {}, *feat[3] = {}, *se_y = nullptr, *hbuf = nullptr, *sbuf = nullptr;
+  float *buf[4] = {}, *feat[3] = {}, *se_y = nullptr, *se_part = nullptr, *hbuf = nullptr, *sbuf = nullptr;
 };
 
 namespace {
@@ -725,6 +741,7 @@ int ggd_enc_finalize(ggd_enc* e) {
   for (int i = 0; i < 3; ++i)
     ENC_TRY(e, ealloc(e, &e->feat[i], sizeof(float) * n * e->H[i + 2] * e->W[i + 2] * planes_l[i + 1]));
   ENC_TRY(e, ealloc(e, &e->se_y, sizeof(float) * n * 256));
+  ENC_TRY(e, ealloc(e, &e->se_part, sizeof(float) * n * SE_SLICES * 256));
   ENC_TRY(e, ealloc(e, &e->sbuf, sizeof(float) * n * 32 *
                                     std::max((size_t)e->H[3] * 2 * e->W[3] * 2, (size_t)e->H[4] * 4 * e->W[4] * 4)));
   size_t hb = 0;
@@ -802,8 +819,11 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
           res = r;
         }
         if (rc) return rc;
-        hipLaunchKernelGGL(enc_se_kernel, dim3(m), dim3(256), 0, s, v, Ho * Wo, B.planes, B.se_w0, B.se_b0, B.se_w2,
-                           B.se_b2, e->se_y);
+        const int S = std::max(1, std::min(SE_SLICES, Ho * Wo / 256));
+        hipLaunchKernelGGL(enc_se_sum_kernel, dim3(m, S), dim3(256), 0, s, v, Ho * Wo, B.planes, e->se_part);
+        ENC_TRY(e, hipGetLastError());
+        hipLaunchKernelGGL(enc_se_kernel, dim3(m), dim3(256), 0, s, e->se_part, S, Ho * Wo, B.planes, B.se_w0,
+                           B.se_b0, B.se_w2, B.se_b2, e->se_y);
         ENC_TRY(e, hipGetLastError());
         // the block output goes to u (consumed by conv2 already), or to the saved feature map
         // of layers 2..4 that the heads read

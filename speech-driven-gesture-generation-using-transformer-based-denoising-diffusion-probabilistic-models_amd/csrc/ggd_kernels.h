@@ -40,7 +40,15 @@ struct GemmArgs {
   int* step_counter;     // if non-null, block 0 thread 0 increments it (one step begins)
   int no_xcd_remap;      // diagnostics: 1 = plain blockIdx tile order
   int force_mt;          // diagnostics: 0 = automatic tile height, else 32 or 64
+  // row maps (0 = identity): logical row m of A / of out is physical row
+  // (m / len) * stride + off + m % len -- a segment of every clip's rows in a joint layout
+  int a_len, a_stride, a_off;
+  int o_len, o_stride, o_off;
 };
+
+__host__ __device__ __forceinline__ size_t map_row(int m, int len, int stride, int off) {
+  return len ? (size_t)(m / len) * stride + off + (m % len) : (size_t)m;
+}
 
 // Per-iteration diffusion coefficients, f32, computed on the host from fp64
 // tables in the reference's operation order (gaussian_diffusion.py:234-329,443-484).
@@ -74,6 +82,7 @@ struct AttnArgs {
   void* out; int ldo;      // T rows [N*Lq][ldo]
   int Lq, Lk, dk, heads, d;
   float scale;
+  int seq_stride, seq_off;  // self mode: clip b's rows start at b * seq_stride + seq_off (0: b * Lq)
 };
 
 // Fused diffusion update on the internal layout (one denoise step's epilogue).
@@ -173,6 +182,8 @@ struct MegaArgs {
   int* status;           // 0 ok, 1 clip-group barrier timed out, 2 workgroups not co-resident
   unsigned long long* stamps;  // diagnostics: clip 0 / part 0 stamps s_memtime around every barrier
                                // of the first MEGA_STAMP_STEPS iterations ([phase][2]: done, passed)
+  int clip0;             // first clip of this launch (batches above the capacity run as chunks)
+  int placement;         // 0: a clip's 8 workgroups share one XCD; 1: workgroup part p of every clip on XCD p
 };
 constexpr int MEGA_STAMP_STEPS = 2;
 constexpr int MEGA_CTL_WORDS = 256 + 32 * 16;
@@ -196,5 +207,12 @@ hipError_t launch_init_state(float* x, const float* x_T_ncl, uint64_t seed, int6
 hipError_t launch_nlc_to_ncl(float* dst, const float* src, int n, int C, int L, int ld_src,
                              hipStream_t s);
 hipError_t launch_set_int(int* p, int v, hipStream_t s);
+// LayerNorm (eps 1e-5) of f32 rows (row map len/stride/off) -> T rows [M][d], d <= 1024
+hipError_t launch_layernorm(int dtype, const float* in, int len, int stride, int off, const float* g, const float* b,
+                            void* out, int M, int d, hipStream_t s);
+// two-way decoder memory rows of every clip in the joint layout [n][L + 1 + Ts][d]:
+// row L = step token of the clip's t (tab[t] already holds emb_mem + PE[L]), rows L+1.. = base
+hipError_t launch_mem_assemble(float* h, const float* base, const float* tab, const int* t_clip, const StepRec* steps,
+                               const int* step_counter, int n, int L, int Ts, int d, hipStream_t s);
 
 }  // namespace ggd

@@ -59,7 +59,7 @@ __device__ __forceinline__ void load_a(ARegs<T, MT, PRO>& R, const GemmArgs& a, 
   } else if constexpr (PRO == PRO_LN) {
     const int r = tid >> 2, j = tid & 3, m = m0 + r;
     const bool ok = tid < MT * 4 && m < a.M;
-    const float* row = (const float*)a.A + (size_t)m * a.lda + kc0;
+    const float* row = (const float*)a.A + map_row(ok ? m : 0, a.a_len, a.a_stride, a.a_off) * a.lda + kc0;
 #pragma unroll
     for (int i = 0; i < N; ++i)
       R.v[i] = ok ? *(const float4*)(row + (j + 4 * i) * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -68,7 +68,7 @@ __device__ __forceinline__ void load_a(ARegs<T, MT, PRO>& R, const GemmArgs& a, 
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int v = tid + i * NTHREADS, r = v / KC, c = v % KC, m = m0 + r, k = kc0 + c;
-      R.v[i] = (m < a.M && k < a.k_valid) ? A[(size_t)m * a.lda + k] : 0.f;
+      R.v[i] = (m < a.M && k < a.k_valid) ? A[map_row(m, a.a_len, a.a_stride, a.a_off) * a.lda + k] : 0.f;
     }
   }
 }
@@ -134,13 +134,15 @@ __device__ __forceinline__ void store_a(const ARegs<T, MT, PRO>& R, const GemmAr
 // rows [r0, r0 + ROWS) x columns [kc0, kc0 + KC) of a row-major T matrix -> LDS tile
 // (rows >= nrows read as zero).  All loads of the tile are independent and issue together.
 template <typename T, int ROWS>
-__device__ __forceinline__ void copy_tile(T* dst, const T* src, int ld, int r0, int nrows, int kc0) {
+__device__ __forceinline__ void copy_tile(T* dst, const T* src, int ld, int r0, int nrows, int kc0, int len = 0,
+                                          int stride = 0, int off = 0) {
   constexpr int STR = KC + Tile<T>::PAD, VE = Tile<T>::VE, VPR = KC / VE, N = ROWS * VPR / NTHREADS;
   uint4 v[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const int e = threadIdx.x + i * NTHREADS, r = e / VPR, cv = e % VPR;
-    v[i] = r0 + r < nrows ? *(const uint4*)(src + (size_t)(r0 + r) * ld + kc0 + cv * VE) : make_uint4(0, 0, 0, 0);
+    v[i] = r0 + r < nrows ? *(const uint4*)(src + map_row(r0 + r, len, stride, off) * ld + kc0 + cv * VE)
+                          : make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
@@ -259,7 +261,7 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
   for (int c = 0; c < NCH; ++c) {
     if (c > 0) __syncthreads();  // previous chunk's MFMAs are done with the LDS tiles
     if constexpr (PRO == PRO_T) {
-      copy_tile<T, MT>(As, (const T*)a.A, a.lda, m0, a.M, c * KC);
+      copy_tile<T, MT>(As, (const T*)a.A, a.lda, m0, a.M, c * KC, a.a_len, a.a_stride, a.a_off);
     } else {
       ARegs<T, MT, PRO> ra;
       load_a<T, MT, PRO>(ra, a, m0, c * KC);
@@ -282,7 +284,7 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wr * WM + i * 16 + g * 4 + r, n = n0 + wc * WN + j * 16 + c16;
-          res[i][j][r] = m < a.M ? ((const float*)a.out)[(size_t)m * a.ldo + n] : 0.f;
+          res[i][j][r] = m < a.M ? ((const float*)a.out)[map_row(m, a.o_len, a.o_stride, a.o_off) * a.ldo + n] : 0.f;
         }
   }
 #pragma unroll
@@ -295,21 +297,22 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wr * WM + i * 16 + g * 4 + r;
         if (m >= a.M) continue;
+        const size_t mo = map_row(m, a.o_len, a.o_stride, a.o_off);
         float v = acc[i][j][r] + bn;
         if constexpr (EPI == EPI_T) {
-          ((T*)a.out)[(size_t)m * a.ldo + n] = from_f32<T>(v);
+          ((T*)a.out)[mo * a.ldo + n] = from_f32<T>(v);
         } else if constexpr (EPI == EPI_RELU2) {
           v = fmaxf(v, 0.f);
-          ((T*)a.out)[(size_t)m * a.ldo + n] = from_f32<T>(v * v);
+          ((T*)a.out)[mo * a.ldo + n] = from_f32<T>(v * v);
         } else if constexpr (EPI == EPI_F32) {
-          if (n < a.n_valid) ((float*)a.out)[(size_t)m * a.ldo + n] = v;
+          if (n < a.n_valid) ((float*)a.out)[mo * a.ldo + n] = v;
         } else if constexpr (EPI == EPI_SILU) {
-          ((float*)a.out)[(size_t)m * a.ldo + n] = v / (1.0f + expf(-v));
+          ((float*)a.out)[mo * a.ldo + n] = v / (1.0f + expf(-v));
         } else if constexpr (EPI == EPI_RESID) {
-          ((float*)a.out)[(size_t)m * a.ldo + n] = res[i][j][r] + v;
+          ((float*)a.out)[mo * a.ldo + n] = res[i][j][r] + v;
         } else {  // EPI_PE
           const int pos = (m % a.pe_period) + a.pe_offset;
-          ((float*)a.out)[(size_t)m * a.ldo + n] = v + a.pe[(size_t)pos * a.N + n];
+          ((float*)a.out)[mo * a.ldo + n] = v + a.pe[(size_t)pos * a.N + n];
         }
       }
     }
@@ -320,11 +323,17 @@ static hipError_t gemm_go(const GemmArgs& a, hipStream_t s) {
   dim3 grid(a.N / NT, (a.M + MT - 1) / MT);
   switch (a.K / KC) {
     case 1: hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 1>), grid, dim3(NTHREADS), 0, s, a); break;
+    case 2:
+      if constexpr (PRO != PRO_LN) hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 2>), grid, dim3(NTHREADS), 0, s, a);
+      break;
     case 3:
       if constexpr (PRO != PRO_LN) hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 3>), grid, dim3(NTHREADS), 0, s, a);
       break;
     case 4:
       if constexpr (PRO != PRO_LN) hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 4>), grid, dim3(NTHREADS), 0, s, a);
+      break;
+    case 8:
+      if constexpr (PRO == PRO_T) hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 8>), grid, dim3(NTHREADS), 0, s, a);
       break;
     default: return hipErrorInvalidValue;
   }
@@ -364,7 +373,8 @@ static hipError_t gemm_pro(int pro, int epi, const GemmArgs& a, hipStream_t s) {
 
 hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream_t s) {
   if (a.N % NT != 0 || a.K % KC != 0 || a.M <= 0) return hipErrorInvalidValue;
-  if (a.K != KC && a.K != 3 * KC && a.K != 4 * KC) return hipErrorInvalidValue;
+  if (a.K != KC && a.K != 2 * KC && a.K != 3 * KC && a.K != 4 * KC && !(a.K == 8 * KC && pro == PRO_T))
+    return hipErrorInvalidValue;
   if (pro == PRO_LN && a.K != KC) return hipErrorInvalidValue;  // LayerNorm width = one chunk
   if (dtype == 0) return gemm_pro<float>(pro, epi, a, s);
   return gemm_pro<bf16_t>(pro, epi, a, s);
@@ -400,16 +410,17 @@ __global__ void __launch_bounds__(NTHREADS) attn_kernel(AttnArgs a) {
     const int n16 = (int)(G.off_p / 16);
     for (int i = tid; i < n16; i += NTHREADS) z[i] = make_uint4(0, 0, 0, 0);
   }
-  att_stage_rows<T>(raw, a.q, (size_t)b * Lq, a.ldq, h * dk, Lq, dk);
+  const size_t row0 = a.seq_stride ? (size_t)b * a.seq_stride + a.seq_off : (size_t)b * Lq;
+  att_stage_rows<T>(raw, a.q, row0, a.ldq, h * dk, Lq, dk);
   __syncthreads();
   att_conv<T, false>(Qm, G.SQ, raw, Lq, dk, a.cw_q, a.cb_q);
   __syncthreads();
   if (!a.cross) {
-    att_stage_rows<T>(raw, a.k, (size_t)b * Lk, a.ldkv, h * dk, Lk, dk);
+    att_stage_rows<T>(raw, a.k, row0, a.ldkv, h * dk, Lk, dk);
     __syncthreads();
     att_conv<T, false>(Km, G.SQ, raw, Lk, dk, a.cw_k, a.cb_k);
     __syncthreads();
-    att_stage_rows<T>(raw, a.v, (size_t)b * Lk, a.ldkv, h * dk, Lk, dk);
+    att_stage_rows<T>(raw, a.v, row0, a.ldkv, h * dk, Lk, dk);
     __syncthreads();
     att_conv<T, true>(Vt, G.SV, raw, Lk, dk, a.cw_v, a.cb_v);
   } else {
@@ -433,7 +444,7 @@ __global__ void __launch_bounds__(NTHREADS) attn_kernel(AttnArgs a) {
   }
   __syncthreads();
 
-  attn_core<T>(Qm, Km, Vt, Pw, G, Lq, Lk, dk, a.scale, (T*)a.out + (size_t)b * Lq * a.ldo + (size_t)h * dk, a.ldo);
+  attn_core<T>(Qm, Km, Vt, Pw, G, Lq, Lk, dk, a.scale, (T*)a.out + row0 * a.ldo + (size_t)h * dk, a.ldo);
 }
 
 size_t attention_lds_bytes(int dtype, const AttnArgs& a) {
@@ -442,6 +453,7 @@ size_t attention_lds_bytes(int dtype, const AttnArgs& a) {
 
 hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s) {
   if (a.Lq > ATT_LMAX || a.Lk > ATT_LMAX || (a.dk != 32 && a.dk != 64)) return hipErrorInvalidValue;
+  if (a.seq_stride && (a.cross || a.Lq != a.Lk)) return hipErrorInvalidValue;
   const size_t lds = attention_lds_bytes(dtype, a);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
@@ -571,6 +583,76 @@ __global__ void set_int_kernel(int* p, int v) { *p = v; }
 
 hipError_t launch_set_int(int* p, int v, hipStream_t s) {
   hipLaunchKernelGGL(set_int_kernel, dim3(1), dim3(1), 0, s, p, v);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm of f32 rows -> T rows (nn.LayerNorm([d]), eps 1e-5; two-pass mean / centred
+// variance like PRO_LN), one wave per row.  Used where the normalised width exceeds the GEMM's
+// fused LN prologue (d = 512, two-way decoder).
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(NTHREADS) layernorm_kernel(const float* in, int len, int stride, int off,
+                                                             const float* g, const float* b, T* out, int M, int d) {
+  const int lane = threadIdx.x & 63, m = blockIdx.x * (NTHREADS / 64) + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const float* row = in + map_row(m, len, stride, off) * d;
+  constexpr int PER = 16;  // d <= 1024
+  float v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = lane + 64 * i;
+    v[i] = k < d ? row[k] : 0.f;
+    s += v[i];
+  }
+  const float mu = wave_sum(s) / (float)d;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = lane + 64 * i;
+    const float e = k < d ? v[i] - mu : 0.f;
+    q += e * e;
+  }
+  const float rs = 1.0f / sqrtf(wave_sum(q) / (float)d + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int k = lane + 64 * i;
+    if (k < d) out[(size_t)m * d + k] = from_f32<T>((v[i] - mu) * rs * g[k] + b[k]);
+  }
+}
+
+hipError_t launch_layernorm(int dtype, const float* in, int len, int stride, int off, const float* g, const float* b,
+                            void* out, int M, int d, hipStream_t s) {
+  if (d > 1024 || M <= 0) return hipErrorInvalidValue;
+  const dim3 grid((M + 3) / 4);
+  if (dtype == 0)
+    hipLaunchKernelGGL(layernorm_kernel<float>, grid, dim3(NTHREADS), 0, s, in, len, stride, off, g, b, (float*)out, M, d);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<bf16_t>, grid, dim3(NTHREADS), 0, s, in, len, stride, off, g, b, (bf16_t*)out,
+                       M, d);
+  return hipGetLastError();
+}
+
+__global__ void mem_assemble_kernel(float* h, const float* base, const float* tab, const int* t_clip,
+                                    const StepRec* steps, const int* step_counter, int L, int Ts, int d) {
+  const int b = blockIdx.y, r = blockIdx.x;  // r = 0: step token, 1..Ts: speech rows
+  const int J = L + 1 + Ts;
+  float* dst = h + ((size_t)b * J + L + r) * d;
+  const float* src;
+  if (r == 0) {
+    const int t = t_clip ? t_clip[b] : steps[*step_counter].t_orig;
+    src = tab + (size_t)t * d;
+  } else {
+    src = base + ((size_t)b * Ts + r - 1) * d;
+  }
+  for (int k = threadIdx.x; k < d; k += blockDim.x) dst[k] = src[k];
+}
+
+hipError_t launch_mem_assemble(float* h, const float* base, const float* tab, const int* t_clip, const StepRec* steps,
+                               const int* step_counter, int n, int L, int Ts, int d, hipStream_t s) {
+  hipLaunchKernelGGL(mem_assemble_kernel, dim3(1 + Ts, n), dim3(128), 0, s, h, base, tab, t_clip, steps, step_counter,
+                     L, Ts, d);
   return hipGetLastError();
 }
 

@@ -33,8 +33,12 @@ __device__ __forceinline__ unsigned mk_add(unsigned* p, unsigned v) {
   return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// slots of XCD x: 8 x the number of groups g < G with g % 8 == x
-__device__ __forceinline__ int mk_slots(int x, int G) { return x < G ? 8 * ((G - 1 - x) / 8 + 1) : 0; }
+// slots of XCD x.  placement 0: clip group g lives on XCD g % 8 (8 x the number of groups g < G
+// with g % 8 == x); placement 1: part p of every clip lives on XCD p (G slots on every XCD)
+__device__ __forceinline__ int mk_slots(int x, int G, int place) {
+  if (place == 1) return G;
+  return x < G ? 8 * ((G - 1 - x) / 8 + 1) : 0;
+}
 
 // thread 0: (clip << 3 | part), or -1 (status set)
 __device__ int mk_role(const MegaArgs& m, int nwg) {
@@ -51,12 +55,12 @@ __device__ int mk_role(const MegaArgs& m, int nwg) {
     }
     __builtin_amdgcn_s_sleep(2);
   }
-  const int G = nwg / 8;
+  const int G = nwg / 8, place = m.placement;
   int x = (int)xcc, s = t;
-  if (t >= mk_slots(x, G)) {  // over-full XCD: take the o-th unfilled slot, in XCD order
+  if (t >= mk_slots(x, G, place)) {  // over-full XCD: take the o-th unfilled slot, in XCD order
     int o = (int)mk_add(ctl + MK_OVF, 1u);
     for (x = 0; x < 8; ++x) {
-      const int have = min((int)mk_load(ctl + x * 16), mk_slots(x, G)), holes = mk_slots(x, G) - have;
+      const int have = min((int)mk_load(ctl + x * 16), mk_slots(x, G, place)), holes = mk_slots(x, G, place) - have;
       if (o < holes) {
         s = have + o;
         break;
@@ -68,6 +72,7 @@ __device__ int mk_role(const MegaArgs& m, int nwg) {
       return -1;
     }
   }
+  if (place == 1) return (s << 3) | x;
   return ((x + 8 * (s >> 3)) << 3) | (s & 7);
 }
 
@@ -109,8 +114,8 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m) {
   __syncthreads();
   const int role = s_role;
   if (role < 0) return;
-  const int b = role >> 3, part = role & 7, lane = ltid() & 63, wave = ltid() >> 6;
-  unsigned* ctr = m.ctl + MK_GROUP + b * 16;
+  const int grp = role >> 3, b = m.clip0 + grp, part = role & 7, lane = ltid() & 63, wave = ltid() >> 6;
+  unsigned* ctr = m.ctl + MK_GROUP + grp * 16;
   unsigned epoch = 0;
   if (m.stamps && role == 0 && threadIdx.x == 0) m.stamps[2 * 17 * MEGA_STAMP_STEPS] = __builtin_amdgcn_s_memtime();
   // per-phase arguments as constant-address-space objects: field reads are scalar loads

@@ -218,11 +218,58 @@ def test_counter_noise_values(pkg, beat_cfg, setup):
     assert (x_rec - want_xT).abs().max().item() <= 1e-3
 
 
-def test_unsupported_two_way_decoder_raises(pkg, tedexp_cfg, setup):
+@pytest.fixture(scope="module")
+def setup_c1(pkg, tedexp_cfg):
+    """Config C1: tedexp (legacy schema) -> default model, two-way CrossAttention decoder, d 512, 10 layers."""
     arch = pkg.arch_from_config(tedexp_cfg.Model, 126)
-    sd = pkg.init_state_dict(arch, seed=0)
-    model, _, _, _, _ = pkg.create_model(126, tedexp_cfg.Model, dtype="f32", device="cuda:0")
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    om = ref_denoiser.OracleModel(sd, oracle_cfg(arch), cache_speech=True)
+    g = th.Generator().manual_seed(21)
+    wav = th.randn(2, int(16000 * 34 / 15), generator=g) * 0.1
+    x = th.randn(2, 126, 34, generator=g)
+    return arch, sd, om, wav, x
+
+
+def make_c1(pkg, tedexp_cfg, sd, dtype, respacing=None):
+    model, diffusion, _, _, _ = pkg.create_model(126, tedexp_cfg.Model, dtype=dtype, device="cuda:0")
     model.load_state_dict(sd)
-    wav, x, t = th.randn(1, 36266) * 0.1, th.randn(1, 126, 34), th.tensor([10])
-    with pytest.raises(ValueError):
-        model(x.cuda(), t.cuda(), wav=wav.cuda())
+    if respacing is not None:
+        diffusion = pkg.create_diffusion({"type": "gaussian", "noise_schedule": "linear", "diffusion_steps": 1000,
+                                          "timestep_respacing": respacing, "model_var_type": "fixed_small"}, False)
+    return model, diffusion
+
+
+def test_two_way_denoise_f32(pkg, tedexp_cfg, setup_c1):
+    """nn.py:381-447 on the generic kernels (joint-layout row maps) vs the oracle, f32."""
+    _, sd, om, wav, x = setup_c1
+    model, _ = make_c1(pkg, tedexp_cfg, sd, "f32")
+    t = th.tensor([3, 871])
+    eps = model(x.cuda(), t.cuda(), wav=wav.cuda()).cpu()
+    ref = om(x, t, wav=wav)
+    err = (eps - ref).abs().max().item()
+    assert err <= 2e-4 * max(1.0, ref.abs().max().item()), err
+
+
+def test_two_way_denoise_bf16(pkg, tedexp_cfg, setup_c1):
+    _, sd, om, wav, x = setup_c1
+    model, _ = make_c1(pkg, tedexp_cfg, sd, "bf16")
+    t = th.tensor([500, 17])
+    eps = model(x.cuda(), t.cuda(), wav=wav.cuda()).cpu()
+    ref = om(x, t, wav=wav)
+    assert rel_rms(eps, ref) <= 2e-2
+
+
+def test_two_way_sample_respaced_f32(pkg, tedexp_cfg, setup_c1):
+    """C1's sampler: timestep_respacing "50" DDPM, injected noise, 4 steps vs the oracle loop."""
+    _, sd, om, wav, x = setup_c1
+    model, diffusion = make_c1(pkg, tedexp_cfg, sd, "f32", respacing="50")
+    steps = 4
+    zs = th.randn(steps, 2, 126, 34, generator=th.Generator().manual_seed(22))
+    out = diffusion.p_sample_loop(model, (2, 126, 34), model_kwargs={"wav": wav.cuda()}, noise=x.cuda(),
+                                  step_noise=zs.cuda(), n_steps=steps)
+    sch = ref_diffusion.make_schedule("linear", 1000, "50")
+    want = ref_diffusion.sample_loop(sch, om, (2, 126, 34), {"wav": wav}, ref_diffusion.InjectedNoise(x, zs),
+                                     "ddpm", x_T=x, n_steps=steps)
+    for k in ("sample", "eps", "pred_x_start"):
+        err = (out[k].cpu() - want[k]).abs().max().item()
+        assert err <= 1e-3 * max(1.0, want[k].abs().max().item()), (k, err)
