@@ -63,7 +63,7 @@ def kb_flop(n, L, Lk, d):
 WORKLOADS = {
     "c2": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=1,
                label="beat-ours C2"),
-    "c4": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=4,
+    "c4": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=4, dtype="fp8",
                label="beat-ours C4 long clip (seq_len x4)"),
     "c5": dict(batch_per_gpu=128, alg="ddim", respacing="ddim50", seq_mult=1,
                label="beat-ours C5 DDIM-50"),
@@ -102,7 +102,8 @@ def parse():
     p.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
                    help="BASELINE.json config: c2 (default, the metric's config), c4 long clip, c5 DDIM-50")
     p.add_argument("--batch-per-gpu", type=int, default=None)
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    p.add_argument("--dtype", default=None, choices=["bf16", "f32", "fp8"],
+                   help="fp8: bf16 activations + e4m3 per-step decoder weights (default for c4)")
     p.add_argument("--alg", default=None, choices=["ddpm", "ddim"])
     p.add_argument("--respacing", default=None)
     p.add_argument("--graph", action="store_true",
@@ -117,6 +118,8 @@ def parse():
         if getattr(a, k) is None:
             setattr(a, k, w[k])
     a.seq_mult = w["seq_mult"]
+    if a.dtype is None:
+        a.dtype = w.get("dtype", "bf16")
     if a.cpu_steps is None:
         a.cpu_steps = max(3, round(40 * 32 / (a.batch_per_gpu * a.seq_mult)))
     return a
@@ -261,7 +264,9 @@ def main():
     d = arch["d_model"]
     Tm = 1 + int(ctx.desc.speech_len)
     clip_step = clip_step_flops(L, Tm, d, d_pose, arch["n_layers"])
-    peak = BF16_PEAK_TFLOPS if args.dtype == "bf16" else F32_PEAK_TFLOPS
+    # fp8 weights are dequantized into bf16 MFMA tiles (non-scaled fp8 MFMA runs at the bf16 rate,
+    # MI355X_MICROARCH.md): priced against the bf16 peak
+    peak = F32_PEAK_TFLOPS if args.dtype == "f32" else BF16_PEAK_TFLOPS
     roof = None
     if prof and prof_n:
         avg_us = sum(prof_us) / prof_n
@@ -269,12 +274,17 @@ def main():
             flop = clip_step * B * T / prof_n   # one launch per chunk of <= 32 clips
             kernel = f"mk_kernel<{args.dtype}> (persistent reverse loop: all {T} denoise steps, 17 phases each)"
             timing = "hipEvent pair around the loop's single launch in the last timed pass"
+        elif prof_kind == 2:  # generic path: the FFN-up GEMM (LN prologue, ReLU^2 epilogue), per launch
+            flop = 2 * B * L * d * 4 * d
+            kernel = f"gemm_kernel<{args.dtype}> FFN-up (LN1 prologue + Linear {d}->{4 * d} + ReLU^2, M={B * L})"
+            timing = "hipEvent pair around every FFN-up launch of the last timed pass (context stream)"
         else:
             flop = kb_flop(B, L, Tm, d)
             kernel = f"kb_kernel<{args.dtype}> (SA out-proj + LN2 + cross-attn Q + conv + cross-attention)"
             timing = "device realtime-clock span of every KB launch of the last timed pass"
         ach = flop / (avg_us * 1e-6) / 1e12
-        tr = pmc_traffic("mk_kernel" if prof_kind == 1 else "kb_kernel", args.workload)
+        tr = pmc_traffic({1: "mk_kernel", 2: "gemm_kernel<unsigned short, 64, 1, 1"}.get(prof_kind, "kb_kernel"),
+                         args.workload)
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 6), "traffic": tr and tr["bytes_per_launch"], "traffic_detail": tr, "kernel": kernel, "timing": timing,
                 "flop_per_launch": flop, "avg_launch_us": round(avg_us, 3), "launches": prof_n}
@@ -290,10 +300,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": args.dtype,
+        "dtype": "bf16" if args.dtype == "fp8" else args.dtype,
         "data": "synthetic (random-init weights of the beat-ours architecture, N(0,0.1^2) wav, counter-stream noise)",
         "config": {"workload": f"{WORKLOADS[args.workload]['label']}: {B} clips/GPU x L={L} x C={d_pose}, wav {wav_len}, "
-                               f"{args.alg.upper()} T'={T}, {args.dtype} decoder",
+                               f"{args.alg.upper()} T'={T}, "
+                               + ("bf16 decoder with fp8-e4m3 per-channel-scaled step weights" if args.dtype == "fp8"
+                                  else f"{args.dtype} decoder"),
                    "global_batch": n_total, "seq_len": L, "parallelism": f"dp{world}",
                    "diffusion_steps": T},
         "roofline": roof,

@@ -47,8 +47,13 @@ enum ggd_status {
 enum ggd_model_type { GGD_MODEL_S2G_V2 = 0, GGD_MODEL_DEFAULT = 1 };
 /* models/model_creation.py:72-93 -- Decoder.type */
 enum ggd_decoder_type { GGD_DEC_ONEWAY = 0, GGD_DEC_TWOWAY = 1 };
-/* compute dtype of the decoder GEMM operands (accumulation is always f32) */
-enum ggd_dtype { GGD_F32 = 0, GGD_BF16 = 1 };
+/* compute dtype of the decoder GEMM operands (accumulation is always f32).
+ * GGD_FP8W: bf16 activations; the Linears evaluated inside every denoise step (emb_x, the
+ * attention / FFN projections of every layer, out_layers.1) are stored as OCP fp8 e4m3fn with
+ * one f32 scale per output channel (amax / 448), dequantized exactly into the bf16 MFMA tiles
+ * and scaled in the GEMM epilogue -- BASELINE.json configs[3] (long clip, fp8 weights).  The
+ * step-invariant projections (memory K/V, blend, step MLP) stay bf16.  Generic kernels only. */
+enum ggd_dtype { GGD_F32 = 0, GGD_BF16 = 1, GGD_FP8W = 2 };
 /* models/generator.py:34-45 -- sample_alg */
 enum ggd_alg { GGD_DDPM = 0, GGD_DDIM = 1 };
 
@@ -148,13 +153,14 @@ int ggd_sample(ggd_ctx* ctx, const ggd_sample_args* args, void* stream);
 int ggd_set_profiling(ggd_ctx* ctx, int32_t on);
 int ggd_kernel_time(ggd_ctx* ctx, int32_t which, double* avg_us, int64_t* launches);
 /* What the last profiled ggd_sample timed: 0 = kb_kernel launches of the per-phase path,
- * 1 = the persistent loop (mk_kernel: one launch for all denoise steps). */
+ * 1 = the persistent loop (mk_kernel: one launch for all denoise steps), 2 = the generic path's
+ * FFN-up GEMM (LayerNorm prologue + Linear d -> 4d + ReLU^2, hipEvent pairs per launch). */
 int ggd_profile_kind(ggd_ctx* ctx);
 
 /* Diagnostics (not part of the reference surface): launch one kernel configuration `iters`
  * times back to back on the ctx stream and return the average microseconds per launch
  * (hipEvents).  what = 0: GEMM, p = {pro, epi, M, N, K, force_mt, no_xcd_remap};
- * what = 1: attention, p = {cross, n}; what = 2: one full denoise step (eager launches),
+ * what = 1: attention, p = {cross, n[, no_qsplit]}; what = 2: one full denoise step (eager launches),
  * p = {n}; what = 3: the same step as one hipGraph replay, p = {n}; what = 4: one fused kernel,
  * p = {0 KA | 1 KB | 2 KC | 3 KD | 4 KE, n}; what = 5: calibration micro-kernels, p = {mode, arg,
  * blocks, buffer MiB} with mode 0 empty launch, 1 dependent-load chase (arg loads), 2 shader clock

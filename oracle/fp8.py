@@ -1,0 +1,94 @@
+"""OCP fp8 e4m3fn weight quantization, restated for the parity tests -- TEST INFRASTRUCTURE ONLY.
+
+The reference has no fp8 path (it is fp32 throughout, SURVEY.md 8 preamble); BASELINE.json
+configs[3] asks for fp8 weights on the long-clip config.  The HIP context's GGD_FP8W mode
+(include/ggd.h) stores every Linear that runs inside a denoise step as e4m3fn bytes with one f32
+scale per output channel (amax / 448) -- ggd_api.hip ``f2e4m3_host`` / ``pack_lin``.  This
+module restates that quantization in numpy so the oracle can run the SAME dequantized weights
+(q * scale) in fp32: the tests then bound the HIP fp8 path against (a) the oracle on the
+dequantized weights (bf16-activation tolerance) and (b) the oracle on the original weights
+(the fp8 tolerance of SURVEY.md 8d).
+
+e4m3fn: sign, 4 exponent bits (bias 7), 3 mantissa bits, no infinities, 0x7f / 0xff NaN,
+largest finite 448 (0x7e), subnormals m * 2^-9.  Rounding: nearest even, saturating.
+"""
+import re
+
+import numpy as np
+import torch as th
+
+E4M3_MAX = 448.0
+
+
+def e4m3_encode(x):
+    """float32 array -> uint8 e4m3fn codes (round to nearest even, saturate to +-448)."""
+    x = np.asarray(x, np.float32)
+    sign = np.where(np.signbit(x), 0x80, 0).astype(np.uint8)
+    a = np.abs(x).astype(np.float64)
+    out = np.zeros(x.shape, np.uint8)
+    sub = a < 2.0 ** -6
+    out[sub] = np.rint(a[sub] * 2.0 ** 9).astype(np.uint8)          # 0 .. 8 (8 = 2^-6, normal)
+    nor = ~sub
+    e = np.floor(np.log2(np.where(nor, a, 1.0)))
+    m = np.rint((np.where(nor, a, 1.0) / 2.0 ** e - 1.0) * 8.0)       # np.rint: ties to even
+    carry = m == 8
+    e = np.where(carry, e + 1, e)
+    m = np.where(carry, 0, m)
+    code = ((e + 7).astype(np.int64) << 3) | m.astype(np.int64)
+    sat = (e > 8) | ((e == 8) & (m > 6)) | (a >= E4M3_MAX)
+    code = np.where(sat, 0x7e, code)
+    out[nor] = code[nor].astype(np.uint8)
+    out = out | sign
+    out[np.isnan(x)] = 0x7f
+    return out
+
+
+def e4m3_decode(code):
+    """uint8 e4m3fn codes -> float32 values (NaN for 0x7f / 0xff)."""
+    c = np.asarray(code, np.uint8).astype(np.int64)
+    s = np.where(c & 0x80, -1.0, 1.0)
+    e = (c >> 3) & 0xF
+    m = c & 0x7
+    v = np.where(e == 0, m * 2.0 ** -9, (1.0 + m / 8.0) * 2.0 ** (e - 7))
+    v = np.where((c & 0x7F) == 0x7F, np.nan, v)
+    return (s * v).astype(np.float32)
+
+
+def quantize_rows(w):
+    """Per-output-channel (row) quantization of a torch Linear weight [out][in]:
+    returns (codes uint8 [out][in], scale f32 [out], dequantized f32 [out][in])."""
+    w = np.asarray(w, np.float32)
+    amax = np.abs(w).max(axis=1)
+    scale = np.where(amax > 0, amax / np.float32(E4M3_MAX), np.float32(1.0)).astype(np.float32)
+    codes = e4m3_encode(w / scale[:, None])
+    deq = e4m3_decode(codes) * scale[:, None]
+    return codes, scale, deq.astype(np.float32)
+
+
+# the Linears a GGD_FP8W context evaluates inside every denoise step (ggd_api.hip
+# ggd_finalize_weights, pack_lin(..., step = true)); the one-way decoder's cross-attention
+# key / value projections act on the step-invariant memory and stay bf16
+_STEP_LINEARS = [
+    r"pose_decoder\.emb_x\.weight",
+    r"pose_decoder\.out_layers\.1\.weight",
+    r"pose_decoder\.layers\.\d+\.self_attn(_mem)?\.(query|key|value)\.0\.linear\.weight",
+    r"pose_decoder\.layers\.\d+\.self_attn(_mem)?\.output\.weight",
+    r"pose_decoder\.layers\.\d+\.cross_attn\.query\.0\.linear\.weight",
+    r"pose_decoder\.layers\.\d+\.cross_attn\.output\.weight",
+    r"pose_decoder\.layers\.\d+\.feed_forward(_mem)?\.layer[12]\.weight",
+]
+_TWOWAY_EXTRA = [r"pose_decoder\.layers\.\d+\.cross_attn\.(key|value)\.0\.linear\.weight"]
+
+
+def step_linear_names(sd, twoway=False):
+    pats = [re.compile(p) for p in _STEP_LINEARS + (_TWOWAY_EXTRA if twoway else [])]
+    return [k for k in sd if any(p.fullmatch(k) for p in pats)]
+
+
+def dequantized_state_dict(sd, twoway=False):
+    """Copy of ``sd`` whose per-step Linear weights are replaced by their e4m3 dequantization."""
+    out = dict(sd)
+    for k in step_linear_names(sd, twoway):
+        _, _, deq = quantize_rows(sd[k].detach().cpu().float().numpy())
+        out[k] = th.from_numpy(deq)
+    return out

@@ -23,9 +23,10 @@ using namespace ggd;
 
 namespace {
 
-struct Lin {            // packed Linear: T [npad][kpad], f32 bias [npad]
+struct Lin {            // packed Linear: T [npad][kpad] (or e4m3 bytes + scale), f32 bias [npad]
   void* w = nullptr;
   float* b = nullptr;
+  float* scale = nullptr;  // GGD_FP8W per-step Linears: per-output-channel dequantization scale
   int n = 0, k = 0, npad = 0, kpad = 0;
 };
 
@@ -131,7 +132,8 @@ struct ggd_ctx {
   unsigned long long* span = nullptr;  // fused path: KB stamps [T * n_layers][2][workgroups] (realtime ticks)
   size_t span_cap = 0;                 // allocated stamps
   size_t span_pending = 0, span_wg = 0;  // stamps written by the last profiled ggd_sample
-  int prof_kind = 0;                   // what the last profiled ggd_sample timed: 0 kb_kernel, 1 mk_kernel
+  int prof_kind = 0;                   // what the last profiled ggd_sample timed: 0 kb_kernel, 1 mk_kernel,
+                                       // 2 the generic path's FFN-up GEMM (LN prologue, ReLU^2 epilogue)
 
   // persistent reverse loop (ggd_mega.hip)
   bool no_mega = false;                // ggd_diag what = 9: route sampling through per-phase launches
@@ -199,6 +201,27 @@ uint16_t f2bf_host(float f) {  // round to nearest even, NaN preserved
 
 int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
+// float -> OCP fp8 e4m3fn (bias 7, max 448, no infinities), round to nearest even, saturating.
+// Restated in oracle/fp8.py (the parity tests quantize the oracle's weights with it).
+uint8_t f2e4m3_host(float f) {
+  if (std::isnan(f)) return 0x7f;
+  const uint8_t sign = std::signbit(f) ? 0x80 : 0;
+  float a = std::fabs(f);
+  if (a >= 448.f) return sign | 0x7e;
+  if (a < std::ldexp(1.f, -6)) {                       // subnormal: steps of 2^-9
+    const int m = (int)std::nearbyint(std::ldexp(a, 9));  // 0 .. 8 (8 = smallest normal)
+    return sign | (uint8_t)m;
+  }
+  int e;
+  const float fr = std::frexp(a, &e);                   // a = fr * 2^e, fr in [0.5, 1)
+  int m = (int)std::nearbyint((fr * 2.f - 1.f) * 8.f);  // 3 mantissa bits of 1.m * 2^(e-1)
+  int ex = e - 1;
+  if (m == 8) { m = 0; ++ex; }
+  if (ex > 8 || (ex == 8 && m > 6)) return sign | 0x7e;
+  return sign | (uint8_t)(((ex + 7) << 3) | m);
+}
+
+
 const std::vector<float>* get(ggd_ctx* c, const std::string& name, size_t numel) {
   auto it = c->staged.find(name);
   if (it == c->staged.end()) {
@@ -213,8 +236,10 @@ const std::vector<float>* get(ggd_ctx* c, const std::string& name, size_t numel)
   return &it->second;
 }
 
-// Pack one or more torch Linear weights (rows stacked) into T [npad][kpad].
-int pack_lin(ggd_ctx* c, Lin& L, const std::vector<std::string>& prefixes, int n_each, int k) {
+// Pack one or more torch Linear weights (rows stacked) into T [npad][kpad].  `step`: the Linear
+// runs inside every denoise step, so a GGD_FP8W context stores it as e4m3 rows with one scale
+// per output channel (amax / 448; all-zero rows scale 1).
+int pack_lin(ggd_ctx* c, Lin& L, const std::vector<std::string>& prefixes, int n_each, int k, bool step = false) {
   const int n = n_each * (int)prefixes.size();
   L.n = n;
   L.k = k;
@@ -232,6 +257,22 @@ int pack_lin(ggd_ctx* c, Lin& L, const std::vector<std::string>& prefixes, int n
   }
   HIP_TRY(c, dalloc(c, &L.b, sizeof(float) * L.npad));
   HIP_TRY(c, hipMemcpy(L.b, b.data(), sizeof(float) * L.npad, hipMemcpyHostToDevice));
+  if (step && c->desc.dtype == GGD_FP8W) {
+    std::vector<uint8_t> q(w.size());
+    std::vector<float> sc(L.npad, 1.f);
+    for (int r = 0; r < L.npad; ++r) {
+      const float* row = &w[(size_t)r * L.kpad];
+      float amax = 0.f;
+      for (int j = 0; j < L.kpad; ++j) amax = std::max(amax, std::fabs(row[j]));
+      if (amax > 0.f) sc[r] = amax / 448.f;
+      for (int j = 0; j < L.kpad; ++j) q[(size_t)r * L.kpad + j] = f2e4m3_host(row[j] / sc[r]);
+    }
+    HIP_TRY(c, dalloc(c, &L.scale, sizeof(float) * L.npad));
+    HIP_TRY(c, hipMemcpy(L.scale, sc.data(), sizeof(float) * L.npad, hipMemcpyHostToDevice));
+    HIP_TRY(c, dalloc(c, &L.w, q.size()));
+    HIP_TRY(c, hipMemcpy(L.w, q.data(), q.size(), hipMemcpyHostToDevice));
+    return GGD_OK;
+  }
   HIP_TRY(c, dalloc(c, &L.w, c->tsize * w.size()));
   if (c->desc.dtype == GGD_F32) {
     HIP_TRY(c, hipMemcpy(L.w, w.data(), sizeof(float) * w.size(), hipMemcpyHostToDevice));
@@ -327,6 +368,7 @@ GemmArgs gemm_args(const Lin& L, int M, const void* A, int lda, void* out, int l
   g.out = out;
   g.ldo = ldo;
   g.n_valid = L.n;
+  g.wscale = L.scale;
   return g;
 }
 
@@ -811,7 +853,7 @@ int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out) {
     *out = c;
     return GGD_ERR_UNSUPPORTED;
   }
-  if (D.dtype != GGD_F32 && D.dtype != GGD_BF16) {
+  if (D.dtype != GGD_F32 && D.dtype != GGD_BF16 && D.dtype != GGD_FP8W) {
     c->err = "unsupported dtype";
     *out = c;
     return GGD_ERR_UNSUPPORTED;
@@ -902,9 +944,9 @@ int ggd_finalize_weights(ggd_ctx* c) {
   const std::string P = "pose_decoder.";
   int r;
 #define TRY(x) do { r = (x); if (r) return r; } while (0)
-  TRY(pack_lin(c, c->emb_x, {P + "emb_x"}, d, C));
+  TRY(pack_lin(c, c->emb_x, {P + "emb_x"}, d, C, true));
   TRY(pack_lin(c, c->emb_mem, {P + "emb_mem"}, d, d));
-  TRY(pack_lin(c, c->out_lin, {P + "out_layers.1"}, C, d));
+  TRY(pack_lin(c, c->out_lin, {P + "out_layers.1"}, C, d, true));
   TRY(upload_vec(c, &c->out_ln_g, P + "out_layers.0.weight", d));
   TRY(upload_vec(c, &c->out_ln_b, P + "out_layers.0.bias", d));
   TRY(pack_lin(c, c->step0, {"diffusion_step_encoder.proj.0"}, d, d));
@@ -921,8 +963,8 @@ int ggd_finalize_weights(ggd_ctx* c) {
       };
       auto mdha = [&](Lin& qkv, Lin& o, Conv3& cq, Conv3& ck, Conv3& cv, const std::string& name) {
         const std::string a = q + name + ".";
-        int rr = pack_lin(c, qkv, {a + "query.0.linear", a + "key.0.linear", a + "value.0.linear"}, d, d);
-        if (!rr) rr = pack_lin(c, o, {a + "output"}, d, d);
+        int rr = pack_lin(c, qkv, {a + "query.0.linear", a + "key.0.linear", a + "value.0.linear"}, d, d, true);
+        if (!rr) rr = pack_lin(c, o, {a + "output"}, d, d, true);
         if (!rr) rr = pack_conv(c, cq, a + "query.1", dk);
         if (!rr) rr = pack_conv(c, ck, a + "key.1", dk);
         if (!rr) rr = pack_conv(c, cv, a + "value.1", dk);
@@ -935,13 +977,13 @@ int ggd_finalize_weights(ggd_ctx* c) {
       TRY(ln(&Ly.ln_ca_g, &Ly.ln_ca_b, "norm_cross_attn"));
       TRY(mdha(Ly.qkv_ca, Ly.o_ca, Ly.ca_q, Ly.ca_k, Ly.ca_v, "cross_attn"));
       TRY(ln(&Ly.ln_ff_g, &Ly.ln_ff_b, "norm_ff"));
-      TRY(pack_lin(c, Ly.ff1, {q + "feed_forward.layer1"}, 4 * d, d));
-      TRY(pack_lin(c, Ly.ff2, {q + "feed_forward.layer2"}, d, 4 * d));
+      TRY(pack_lin(c, Ly.ff1, {q + "feed_forward.layer1"}, 4 * d, d, true));
+      TRY(pack_lin(c, Ly.ff2, {q + "feed_forward.layer2"}, d, 4 * d, true));
       Ly.has_ffm = c->staged.count(q + "feed_forward_mem.layer1.weight") != 0;
       if (Ly.has_ffm) {
         TRY(ln(&Ly.ln_ffm_g, &Ly.ln_ffm_b, "norm_ff_mem"));
-        TRY(pack_lin(c, Ly.ffm1, {q + "feed_forward_mem.layer1"}, 4 * d, d));
-        TRY(pack_lin(c, Ly.ffm2, {q + "feed_forward_mem.layer2"}, d, 4 * d));
+        TRY(pack_lin(c, Ly.ffm1, {q + "feed_forward_mem.layer1"}, 4 * d, d, true));
+        TRY(pack_lin(c, Ly.ffm2, {q + "feed_forward_mem.layer2"}, d, 4 * d, true));
       } else if (l + 1 < D.n_layers) {
         return fail(c, GGD_ERR_NAME, "missing weight: " + q + "feed_forward_mem.layer1.weight");
       }
@@ -963,21 +1005,21 @@ int ggd_finalize_weights(ggd_ctx* c) {
     TRY(upload_vec(c, &Ly.ln3_g, q + "norm_ff.weight", d));
     TRY(upload_vec(c, &Ly.ln3_b, q + "norm_ff.bias", d));
     const std::string sa = q + "self_attn.", ca = q + "cross_attn.";
-    TRY(pack_lin(c, Ly.qkv, {sa + "query.0.linear", sa + "key.0.linear", sa + "value.0.linear"}, d, d));
-    TRY(pack_lin(c, Ly.o_sa, {sa + "output"}, d, d));
-    TRY(pack_lin(c, Ly.q_ca, {ca + "query.0.linear"}, d, d));
+    TRY(pack_lin(c, Ly.qkv, {sa + "query.0.linear", sa + "key.0.linear", sa + "value.0.linear"}, d, d, true));
+    TRY(pack_lin(c, Ly.o_sa, {sa + "output"}, d, d, true));
+    TRY(pack_lin(c, Ly.q_ca, {ca + "query.0.linear"}, d, d, true));
     TRY(pack_lin(c, Ly.kv_ca, {ca + "key.0.linear", ca + "value.0.linear"}, d, d));
-    TRY(pack_lin(c, Ly.o_ca, {ca + "output"}, d, d));
+    TRY(pack_lin(c, Ly.o_ca, {ca + "output"}, d, d, true));
     TRY(pack_conv(c, Ly.sa_q, sa + "query.1", dk));
     TRY(pack_conv(c, Ly.sa_k, sa + "key.1", dk));
     TRY(pack_conv(c, Ly.sa_v, sa + "value.1", dk));
     TRY(pack_conv(c, Ly.ca_q, ca + "query.1", dk));
     TRY(pack_conv(c, Ly.ca_k, ca + "key.1", dk));
     TRY(pack_conv(c, Ly.ca_v, ca + "value.1", dk));
-    TRY(pack_lin(c, Ly.ff1, {q + "feed_forward.layer1"}, 4 * d, d));
-    TRY(pack_lin(c, Ly.ff2, {q + "feed_forward.layer2"}, d, 4 * d));
+    TRY(pack_lin(c, Ly.ff1, {q + "feed_forward.layer1"}, 4 * d, d, true));
+    TRY(pack_lin(c, Ly.ff2, {q + "feed_forward.layer2"}, d, 4 * d, true));
   }
-  c->fused = D.decoder_type == GGD_DEC_ONEWAY &&
+  c->fused = D.decoder_type == GGD_DEC_ONEWAY && D.dtype != GGD_FP8W &&
              fused_supported(D.dtype, D.d_model, D.heads, D.seq_len, D.speech_len, D.d_pose);
   if (c->fused) {
     TRY(frag_from(c, c->f_emb, {P + "emb_x"}, d, C, iota_n(d)));
@@ -1297,6 +1339,7 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     at.Lk = at.cross ? 1 + D.speech_len : D.seq_len;
     at.dk = d / D.heads; at.heads = D.heads; at.d = d;
     at.scale = 1.0f / std::sqrt((float)at.dk);
+    at.no_qsplit = np >= 3 ? p[2] : 0;
     for (int it = 0; rc == GGD_OK && it < iters + 1; ++it) {
       if (it == 1) HIP_TRY(c, hipEventRecord(e0, s));
       HIP_TRY(c, launch_attention(D.dtype, at, n, s));
@@ -1667,6 +1710,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
         }
         c->prof_avg_us = cnt ? total / cnt : 0;
         c->prof_launches = cnt;
+        c->prof_kind = 2;
       }
     }
   }

@@ -184,6 +184,34 @@ __device__ __forceinline__ void att_conv(T* dst, int S, const float* raw, int ro
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// lane-group reductions on DPP (VALU-rate lane moves, no LDS round trip; __shfl_xor lowers to
+// ds_bpermute whose ~100-cycle latency is exposed on every step of a dependent reduction)
+// ------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E;               // quad_perm [1,0,3,2], [2,3,0,1]
+constexpr int DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;    // within 8 / 16 lanes
+// reduce over aligned groups of G lanes (G = 2, 4, 8 or 16); every lane of a group gets the result
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+  if constexpr (G >= 2) v += dpp_mov<DPP_XOR1>(v);
+  if constexpr (G >= 4) v += dpp_mov<DPP_XOR2>(v);
+  if constexpr (G >= 8) v += dpp_mov<DPP_HALF_MIRROR>(v);
+  if constexpr (G >= 16) v += dpp_mov<DPP_MIRROR>(v);
+  return v;
+}
+template <int G>
+__device__ __forceinline__ float group_max(float v) {
+  if constexpr (G >= 2) v = fmaxf(v, dpp_mov<DPP_XOR1>(v));
+  if constexpr (G >= 4) v = fmaxf(v, dpp_mov<DPP_XOR2>(v));
+  if constexpr (G >= 8) v = fmaxf(v, dpp_mov<DPP_HALF_MIRROR>(v));
+  if constexpr (G >= 16) v = fmaxf(v, dpp_mov<DPP_MIRROR>(v));
+  return v;
+}
+
 // acc += X[xr0 + 0..15][0..K) . Y[yr0 + 0..15][0..K)^T   (both row-major with row stride S)
 template <typename T>
 __device__ __forceinline__ void att_mma(f32x4& acc, const T* X, int xr0, int SX, const T* Y, int yr0, int SY, int K,
@@ -236,10 +264,7 @@ __device__ __forceinline__ void attn_core(const T* Qm, const T* Km, const T* Vt,
         s[t][r] = v;
         mx = fmaxf(mx, v);
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 1));
-      mx = fmaxf(mx, __shfl_xor(mx, 2));
-      mx = fmaxf(mx, __shfl_xor(mx, 4));
-      mx = fmaxf(mx, __shfl_xor(mx, 8));
+      mx = group_max<16>(mx);
       float sum = 0.f;
 #pragma unroll
       for (int t = 0; t < ATT_KT; ++t) {
@@ -248,10 +273,7 @@ __device__ __forceinline__ void attn_core(const T* Qm, const T* Km, const T* Vt,
         s[t][r] = p;
         sum += p;
       }
-      sum += __shfl_xor(sum, 1);
-      sum += __shfl_xor(sum, 2);
-      sum += __shfl_xor(sum, 4);
-      sum += __shfl_xor(sum, 8);
+      sum = group_sum<16>(sum);
       const float inv = 1.0f / sum;
 #pragma unroll
       for (int t = 0; t < ATT_KT; ++t)

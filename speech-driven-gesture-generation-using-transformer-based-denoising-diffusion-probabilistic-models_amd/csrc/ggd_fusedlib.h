@@ -132,34 +132,6 @@ __device__ __forceinline__ int ltid() {
 }
 
 // ------------------------------------------------------------------------------------------
-// lane-group reductions on DPP (VALU-rate lane moves, no LDS round trip; __shfl_xor lowers to
-// ds_bpermute whose ~100-cycle latency is exposed on every step of a dependent reduction)
-// ------------------------------------------------------------------------------------------
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
-}
-constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E;               // quad_perm [1,0,3,2], [2,3,0,1]
-constexpr int DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140;    // within 8 / 16 lanes
-// reduce over aligned groups of G lanes (G = 2, 4, 8 or 16); every lane of a group gets the result
-template <int G>
-__device__ __forceinline__ float group_sum(float v) {
-  if constexpr (G >= 2) v += dpp_mov<DPP_XOR1>(v);
-  if constexpr (G >= 4) v += dpp_mov<DPP_XOR2>(v);
-  if constexpr (G >= 8) v += dpp_mov<DPP_HALF_MIRROR>(v);
-  if constexpr (G >= 16) v += dpp_mov<DPP_MIRROR>(v);
-  return v;
-}
-template <int G>
-__device__ __forceinline__ float group_max(float v) {
-  if constexpr (G >= 2) v = fmaxf(v, dpp_mov<DPP_XOR1>(v));
-  if constexpr (G >= 4) v = fmaxf(v, dpp_mov<DPP_XOR2>(v));
-  if constexpr (G >= 8) v = fmaxf(v, dpp_mov<DPP_HALF_MIRROR>(v));
-  if constexpr (G >= 16) v = fmaxf(v, dpp_mov<DPP_MIRROR>(v));
-  return v;
-}
-
-// ------------------------------------------------------------------------------------------
 // staging
 // ------------------------------------------------------------------------------------------
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, NOT for

@@ -44,6 +44,9 @@ struct GemmArgs {
   // (m / len) * stride + off + m % len -- a segment of every clip's rows in a joint layout
   int a_len, a_stride, a_off;
   int o_len, o_stride, o_off;
+  // fp8 weights (GGD_FP8W): non-null = W is OCP e4m3fn bytes [Npad][K] and out column n is
+  // scaled by wscale[n] before the bias (per-output-channel dequantization)
+  const float* wscale;
 };
 
 __host__ __device__ __forceinline__ size_t map_row(int m, int len, int stride, int off) {
@@ -83,6 +86,7 @@ struct AttnArgs {
   int Lq, Lk, dk, heads, d;
   float scale;
   int seq_stride, seq_off;  // self mode: clip b's rows start at b * seq_stride + seq_off (0: b * Lq)
+  int no_qsplit;            // diagnostics: 1 = one workgroup per (head, clip) (attn_kernel)
 };
 
 // Fused diffusion update on the internal layout (one denoise step's epilogue).

@@ -181,6 +181,38 @@ __device__ __forceinline__ void store_w(const WRegs<T>& R, T* Ws) {
   }
 }
 
+// fp8 weight tile (GGD_FP8W): rows [n0, n0 + NT) x columns [kc0, kc0 + KC) of OCP e4m3fn bytes
+// -> the bf16 LDS tile.  e4m3 values are exactly representable in bf16 (3 mantissa bits,
+// exponents -9 .. 8), so the dequantization is exact: v_cvt_pk_f32_fp8 (OCP on gfx950) and the
+// f32 -> bf16 truncation loses nothing; the per-channel scale is applied in the epilogue.
+// All 16-byte loads of the tile issue before the first conversion.
+__device__ __forceinline__ void copy_tile_w8(bf16_t* dst, const uint8_t* src, int ld, int n0, int kc0) {
+  constexpr int STR = KC + Tile<bf16_t>::PAD, VPR = KC / 16, N = NT * VPR / NTHREADS;
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  uint4 v[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int e = threadIdx.x + i * NTHREADS, r = e / VPR, cv = e % VPR;
+    v[i] = *(const uint4*)(src + (size_t)(n0 + r) * ld + kc0 + cv * 16);
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int e = threadIdx.x + i * NTHREADS, r = e / VPR, cv = e % VPR;
+    const unsigned w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+    unsigned o[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f2 lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[q], false);
+      const f2 hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[q], true);
+      o[2 * q] = (__float_as_uint(lo.x) >> 16) | (__float_as_uint(lo.y) & 0xffff0000u);
+      o[2 * q + 1] = (__float_as_uint(hi.x) >> 16) | (__float_as_uint(hi.y) & 0xffff0000u);
+    }
+    uint4* d = (uint4*)(dst + r * STR + cv * 16);
+    d[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    d[1] = make_uint4(o[4], o[5], o[6], o[7]);
+  }
+}
+
 template <typename T, int TM, int TN>
 __device__ __forceinline__ void mma_chunk(const T* As, const T* Ws, int arow0, int wcol0, int lane,
                                           f32x4 (&acc)[TM][TN]) {
@@ -225,8 +257,9 @@ __device__ __forceinline__ void mma_chunk(const T* As, const T* Ws, int arow0, i
   }
 }
 
-template <typename T, int MT, int PRO, int EPI, int NCH>
+template <typename T, int MT, int PRO, int EPI, int NCH, bool W8 = false>
 __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
+  static_assert(!W8 || sizeof(T) == 2, "fp8 weights feed the bf16 MFMA");
   constexpr int STR = KC + Tile<T>::PAD;
   constexpr int WM = MT / 2, WN = NT / 2;     // 2 x 2 waves
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -268,7 +301,8 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
       if constexpr (PRO == PRO_LN) ln_stats<T, MT>(ra, a.K);
       store_a<T, MT, PRO>(ra, a, As, c * KC);
     }
-    copy_tile<T, NT>(Ws, (const T*)a.W, a.K, n0, 1 << 30, c * KC);
+    if constexpr (W8) copy_tile_w8((bf16_t*)Ws, (const uint8_t*)a.W, a.K, n0, c * KC);
+    else copy_tile<T, NT>(Ws, (const T*)a.W, a.K, n0, 1 << 30, c * KC);
     __syncthreads();
     mma_chunk<T, TM, TN>(As, Ws, wr * WM, wc * WN, lane, acc);
   }
@@ -293,12 +327,13 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wc * WN + j * 16 + c16;
       const float bn = a.bias[n];
+      const float sn = W8 ? a.wscale[n] : 1.0f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wr * WM + i * 16 + g * 4 + r;
         if (m >= a.M) continue;
         const size_t mo = map_row(m, a.o_len, a.o_stride, a.o_off);
-        float v = acc[i][j][r] + bn;
+        float v = W8 ? acc[i][j][r] * sn + bn : acc[i][j][r] + bn;
         if constexpr (EPI == EPI_T) {
           ((T*)a.out)[mo * a.ldo + n] = from_f32<T>(v);
         } else if constexpr (EPI == EPI_RELU2) {
@@ -321,6 +356,19 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
 template <typename T, int MT, int PRO, int EPI>
 static hipError_t gemm_go(const GemmArgs& a, hipStream_t s) {
   dim3 grid(a.N / NT, (a.M + MT - 1) / MT);
+  if constexpr (sizeof(T) == 2) {
+    if (a.wscale) {  // fp8 weights: K = 256 (every d_model-input Linear) or 1024 (FFN down)
+      switch (a.K / KC) {
+        case 1: hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 1, true>), grid, dim3(NTHREADS), 0, s, a); break;
+        case 4:
+          if constexpr (PRO == PRO_T) hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 4, true>), grid, dim3(NTHREADS), 0, s, a);
+          else return hipErrorInvalidValue;
+          break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
+  }
   switch (a.K / KC) {
     case 1: hipLaunchKernelGGL((gemm_kernel<T, MT, PRO, EPI, 1>), grid, dim3(NTHREADS), 0, s, a); break;
     case 2:
@@ -376,7 +424,10 @@ hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream
   if (a.K != KC && a.K != 2 * KC && a.K != 3 * KC && a.K != 4 * KC && !(a.K == 8 * KC && pro == PRO_T))
     return hipErrorInvalidValue;
   if (pro == PRO_LN && a.K != KC) return hipErrorInvalidValue;  // LayerNorm width = one chunk
-  if (dtype == 0) return gemm_pro<float>(pro, epi, a, s);
+  if (dtype == 0) {
+    if (a.wscale) return hipErrorInvalidValue;  // fp8 weights feed the bf16 MFMA only
+    return gemm_pro<float>(pro, epi, a, s);
+  }
   return gemm_pro<bf16_t>(pro, epi, a, s);
 }
 
@@ -447,6 +498,158 @@ __global__ void __launch_bounds__(NTHREADS) attn_kernel(AttnArgs a) {
   attn_core<T>(Qm, Km, Vt, Pw, G, Lq, Lk, dk, a.scale, (T*)a.out + row0 * a.ldo + (size_t)h * dk, a.ldo);
 }
 
+// ---------------------------------------------------------------------------
+// Query-split attention (attn_q_kernel): one workgroup per (head, clip, 64-query block), so a
+// 160-frame clip (BASELINE configs[3]) spreads its 10 query tiles over 3 workgroups per head
+// instead of serialising them in one, and every wave runs exactly one 16-row query tile.
+// Staging skips the f32 raw image: each thread computes the 3-tap conv of its own 16-byte
+// channel vectors straight from global rows i-1, i, i+1 (rows outside the sequence are the
+// conv's zero padding), all loads of a batch issued before the first use.  The K / V conv is
+// recomputed by each query block (L2 hits; a few % of the block's work).
+// ---------------------------------------------------------------------------
+constexpr int AQ_QT = 64;  // query rows per workgroup: 4 waves x 16
+
+template <typename T>
+__host__ __device__ inline AttGeom aq_geom(int Lk, int dk) {
+  constexpr int KA = sizeof(T) == 2 ? 32 : 16;
+  AttGeom g;
+  g.Lqp = AQ_QT;
+  g.Lkp = (Lk + KA - 1) / KA * KA;
+  g.SQ = dk + AttPad<T>::P;
+  g.SV = g.Lkp + AttPad<T>::P;
+  g.SP = g.Lkp + AttPad<T>::P;
+  g.off_q = 0;
+  g.off_k = g.off_q + sizeof(T) * (size_t)AQ_QT * g.SQ;
+  g.off_v = g.off_k + sizeof(T) * (size_t)g.Lkp * g.SQ;
+  g.off_p = g.off_v + sizeof(T) * (size_t)dk * g.SV;
+  g.off_raw = g.off_p;
+  g.total = g.off_p + sizeof(T) * (size_t)AQ_QT * g.SP;
+  return g;
+}
+
+// VE channels (one 16-byte vector of T) of sequence row j as f32; rows outside [0, len) are 0.
+// Self mode reads T rows base[(row0 + j) * ld + col]; memory mode (step_row set) reads f32 rows:
+// j = 0 the step token step_row, j >= 1 the cached speech rows base[(row0 + j - 1) * ld + col].
+template <typename T> struct AqSrc {
+  static constexpr int VE = 16 / sizeof(T);
+  const void* base;
+  size_t row0;
+  int ld, col, len;
+  const float* step_row;
+  __device__ __forceinline__ void load(int j, int cv, float (&o)[VE]) const {
+    const bool in = j >= 0 && j < len;
+    const int jj = in ? j : 0;
+    if (step_row) {
+      const float* p = jj == 0 ? step_row + cv * VE : (const float*)base + (row0 + jj - 1) * (size_t)ld + col + cv * VE;
+#pragma unroll
+      for (int q = 0; q < VE / 4; ++q) {
+        const float4 v = *(const float4*)(p + 4 * q);
+        o[4 * q] = in ? v.x : 0.f;
+        o[4 * q + 1] = in ? v.y : 0.f;
+        o[4 * q + 2] = in ? v.z : 0.f;
+        o[4 * q + 3] = in ? v.w : 0.f;
+      }
+    } else {
+      const uint4 u = *(const uint4*)((const T*)base + (row0 + jj) * (size_t)ld + col + cv * VE);
+      if constexpr (sizeof(T) == 2) {
+        const bf16_t* h = (const bf16_t*)&u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = in ? bf2f(h[e]) : 0.f;
+      } else {
+        o[0] = in ? __uint_as_float(u.x) : 0.f;
+        o[1] = in ? __uint_as_float(u.y) : 0.f;
+        o[2] = in ? __uint_as_float(u.z) : 0.f;
+        o[3] = in ? __uint_as_float(u.w) : 0.f;
+      }
+    }
+  }
+};
+
+// image rows r = 0 .. rows-1 (sequence rows r0 + r) of conv3(src) -> T image, row-major
+// (dst[r * S + c]) or transposed (dst[c * S + r]).  Task = (row, 16-byte channel vector); a
+// thread's vector index is fixed (NTHREADS is a multiple of the vectors per row), so its conv
+// taps and bias are loaded once; (row) tasks run in batches of U per thread, every load of a
+// batch issued before the first conv.
+template <typename T, int DK, bool TRANS, int U = 4>
+__device__ __forceinline__ void aq_conv_stage(T* dst, int S, const AqSrc<T>& src, int r0, int rows, const float* w,
+                                              const float* b) {
+  constexpr int VE = AqSrc<T>::VE, VPR = DK / VE, RPB = NTHREADS / VPR;  // rows per batch slot
+  static_assert(NTHREADS % VPR == 0, "a thread keeps one channel vector");
+  const int cv = (int)threadIdx.x % VPR, rr = (int)threadIdx.x / VPR;
+  float w0[VE], w1[VE], w2[VE], bb[VE];
+#pragma unroll
+  for (int e = 0; e < VE; ++e) {
+    const int c = cv * VE + e;
+    w0[e] = w[c * 3 + 0];
+    w1[e] = w[c * 3 + 1];
+    w2[e] = w[c * 3 + 2];
+    bb[e] = b[c];
+  }
+  for (int base = 0; base < rows; base += U * RPB) {
+    float in[U][3][VE];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = min(base + u * RPB + rr, rows - 1);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) src.load(r0 + r - 1 + k, cv, in[u][k]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = base + u * RPB + rr;
+      if (r >= rows) continue;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        const int c = cv * VE + e;
+        const float v = bb[e] + w0[e] * in[u][0][e] + w1[e] * in[u][1][e] + w2[e] * in[u][2][e];
+        if (TRANS)
+          dst[c * S + r] = from_f32<T>(v);
+        else
+          dst[r * S + c] = from_f32<T>(v);
+      }
+    }
+  }
+}
+
+template <typename T, int DK>
+__global__ void __launch_bounds__(NTHREADS) attn_q_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int h = blockIdx.x, b = blockIdx.y, q0 = blockIdx.z * AQ_QT;
+  const int Lq = a.Lq, Lk = a.Lk;
+  const AttGeom G = aq_geom<T>(Lk, DK);
+  T* Qm = (T*)(smem + G.off_q);
+  T* Km = (T*)(smem + G.off_k);
+  T* Vt = (T*)(smem + G.off_v);
+  T* Pw = (T*)(smem + G.off_p);
+  const int tid = threadIdx.x;
+  {  // zero the padded operand images (rows >= Lq / Lk must be finite zeros)
+    uint4* z = (uint4*)smem;
+    const int n16 = (int)(G.off_p / 16);
+    for (int i = tid; i < n16; i += NTHREADS) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  const size_t row0 = a.seq_stride ? (size_t)b * a.seq_stride + a.seq_off : (size_t)b * Lq;
+  const int qrows = min(AQ_QT, Lq - q0);
+  const AqSrc<T> sq{a.q, row0, a.ldq, h * DK, Lq, nullptr};
+  aq_conv_stage<T, DK, false>(Qm, G.SQ, sq, q0, qrows, a.cw_q, a.cb_q);
+  if (!a.cross) {
+    const AqSrc<T> sk{a.k, row0, a.ldkv, h * DK, Lk, nullptr};
+    const AqSrc<T> sv{a.v, row0, a.ldkv, h * DK, Lk, nullptr};
+    aq_conv_stage<T, DK, false>(Km, G.SQ, sk, 0, Lk, a.cw_k, a.cb_k);
+    aq_conv_stage<T, DK, true>(Vt, G.SV, sv, 0, Lk, a.cw_v, a.cb_v);
+  } else {
+    // memory row 0 = the diffusion-step token of this clip's t; rows 1.. = cached speech K|V
+    const int t = a.t_clip ? a.t_clip[b] : a.steps[*a.step_counter].t_orig;
+    const float* r0 = a.kv_step + (size_t)t * 2 * a.d;
+    const size_t mrow0 = (size_t)b * (Lk - 1);
+    const AqSrc<T> sk{a.kv_mem, mrow0, 2 * a.d, h * DK, Lk, r0 + h * DK};
+    const AqSrc<T> sv{a.kv_mem, mrow0, 2 * a.d, a.d + h * DK, Lk, r0 + a.d + h * DK};
+    aq_conv_stage<T, DK, false>(Km, G.SQ, sk, 0, Lk, a.cw_k, a.cb_k);
+    aq_conv_stage<T, DK, true>(Vt, G.SV, sv, 0, Lk, a.cw_v, a.cb_v);
+  }
+  __syncthreads();
+  attn_core<T>(Qm, Km, Vt, Pw, G, qrows, Lk, DK, a.scale, (T*)a.out + (row0 + q0) * a.ldo + (size_t)h * DK, a.ldo);
+}
+
 size_t attention_lds_bytes(int dtype, const AttnArgs& a) {
   return dtype == 0 ? att_geom<float>(a.Lq, a.Lk, a.dk).total : att_geom<bf16_t>(a.Lq, a.Lk, a.dk).total;
 }
@@ -455,13 +658,36 @@ hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s) 
   if (a.Lq > ATT_LMAX || a.Lk > ATT_LMAX || (a.dk != 32 && a.dk != 64)) return hipErrorInvalidValue;
   if (a.seq_stride && (a.cross || a.Lq != a.Lk)) return hipErrorInvalidValue;
   const size_t lds = attention_lds_bytes(dtype, a);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)attn_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)attn_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
+  // query-split kernel whenever its images fit (every BASELINE.json shape); else one
+  // workgroup per (head, clip)
+  const size_t lq = dtype == 0 ? aq_geom<float>(a.Lk, a.dk).total : aq_geom<bf16_t>(a.Lk, a.dk).total;
+  static bool aq_attr = false;
+  if (!aq_attr) {
+    (void)hipFuncSetAttribute((const void*)attn_q_kernel<float, 32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)attn_q_kernel<float, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)attn_q_kernel<bf16_t, 32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)attn_q_kernel<bf16_t, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    aq_attr = true;
+  }
+  if (lq <= 160 * 1024 && !a.no_qsplit) {
+    const dim3 gq(a.heads, n, (a.Lq + AQ_QT - 1) / AQ_QT);
+    const bool d32 = a.dk == 32;
+    if (dtype == 0) {
+      if (d32) hipLaunchKernelGGL((attn_q_kernel<float, 32>), gq, dim3(NTHREADS), lq, s, a);
+      else hipLaunchKernelGGL((attn_q_kernel<float, 64>), gq, dim3(NTHREADS), lq, s, a);
+    } else {
+      if (d32) hipLaunchKernelGGL((attn_q_kernel<bf16_t, 32>), gq, dim3(NTHREADS), lq, s, a);
+      else hipLaunchKernelGGL((attn_q_kernel<bf16_t, 64>), gq, dim3(NTHREADS), lq, s, a);
+    }
+    return hipGetLastError();
+  }
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   dim3 grid(a.heads, n);
   if (dtype == 0)
     hipLaunchKernelGGL(attn_kernel<float>, grid, dim3(NTHREADS), lds, s, a);

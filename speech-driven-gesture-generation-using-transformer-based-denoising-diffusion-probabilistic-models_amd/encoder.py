@@ -22,7 +22,8 @@ import torch.nn.functional as F
 
 from . import native
 
-_ENC_DTYPES = {"bf16": native.BF16, "f32": native.F32, "fp32": native.F32}
+# the encoder runs once per clip: an fp8-weight decoder context keeps a bf16 encoder
+_ENC_DTYPES = {"bf16": native.BF16, "f32": native.F32, "fp32": native.F32, "fp8": native.BF16}
 
 
 class SpeechEncoder:

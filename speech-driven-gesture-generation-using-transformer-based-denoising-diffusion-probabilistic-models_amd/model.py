@@ -19,7 +19,8 @@ from . import native
 from .encoder import SpeechEncoder, speech_len, speech_tokens
 from .weights import arch_from_config, parameter_shapes
 
-_DTYPES = {"bf16": native.BF16, "f32": native.F32, "fp32": native.F32}
+# "fp8": bf16 activations, OCP e4m3 per-step decoder weights with per-channel scales (GGD_FP8W)
+_DTYPES = {"bf16": native.BF16, "f32": native.F32, "fp32": native.F32, "fp8": native.FP8W}
 
 
 class _Ctx:

@@ -18,7 +18,7 @@ GGD_OK, GGD_IGNORED = 0, 1
 GGD_ERR_ARG, GGD_ERR_UNSUPPORTED, GGD_ERR_HIP, GGD_ERR_STATE, GGD_ERR_NAME = -1, -2, -3, -4, -5
 MODEL_S2G_V2, MODEL_DEFAULT = 0, 1
 DEC_ONEWAY, DEC_TWOWAY = 0, 1
-F32, BF16 = 0, 1
+F32, BF16, FP8W = 0, 1, 2   # ggd_dtype (include/ggd.h)
 DDPM, DDIM = 0, 1
 
 EXPORTS = [
