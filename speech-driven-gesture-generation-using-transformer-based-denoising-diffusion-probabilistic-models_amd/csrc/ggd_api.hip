@@ -91,6 +91,7 @@ struct ggd_ctx {
   float* pe = nullptr;       // [pe_len][d]
   int pe_len = 0;
   float* kv_step = nullptr;  // [layers][T_orig][2d]
+  float* zero_row = nullptr; // 1 KiB of zeros: the attention conv's padding rows
 
   // two-way decoder (generic kernels, joint layout [n][J = L + 1 + Ts][d])
   bool twoway = false;
@@ -575,6 +576,7 @@ int launch_decoder_twoway(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     q.o_off = sg.off;
     GEMM(c, PRO_T, EPI_T, q, s);
     AttnArgs at{};
+    at.zero = c->zero_row;
     at.cross = 0;
     at.q = c->qkvj;
     at.ldq = 3 * d;
@@ -653,6 +655,7 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     GEMM(c, PRO_LN, EPI_T, g, s);
 
     AttnArgs at{};
+    at.zero = c->zero_row;
     at.cross = 0;
     at.q = c->qkv;
     at.ldq = 3 * d;
@@ -881,6 +884,7 @@ int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out) {
   HIP_TRY(c, dalloc(c, &c->q, c->tsize * M * d));
   HIP_TRY(c, dalloc(c, &c->ffn, c->tsize * M * 4 * d));
   HIP_TRY(c, dalloc(c, &c->d_counter, sizeof(int)));
+  HIP_TRY(c, dalloc(c, &c->zero_row, 1024));
   HIP_TRY(c, dalloc(c, &c->d_t, sizeof(int) * B));
   HIP_TRY(c, dalloc(c, &c->mem_tmp, sizeof(float) * (size_t)B * Ts * d));
   HIP_TRY(c, dalloc(c, &c->tok_tmp, sizeof(float) * (size_t)B * Ts * d));
@@ -1322,6 +1326,7 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     const int n = p[1];
     if (n > D.max_batch) rc = fail(c, GGD_ERR_ARG, "n > max_batch");
     AttnArgs at{};
+    at.zero = c->zero_row;
     const Layer& Ly = c->layers[0];
     at.cross = p[0];
     at.q = c->qkv; at.ldq = 3 * d;

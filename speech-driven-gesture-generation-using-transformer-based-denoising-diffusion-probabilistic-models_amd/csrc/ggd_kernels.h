@@ -87,6 +87,7 @@ struct AttnArgs {
   float scale;
   int seq_stride, seq_off;  // self mode: clip b's rows start at b * seq_stride + seq_off (0: b * Lq)
   int no_qsplit;            // diagnostics: 1 = one workgroup per (head, clip) (attn_kernel)
+  const float* zero;        // >= 256 zero bytes in global memory (the conv's padding rows)
 };
 
 // Fused diffusion update on the internal layout (one denoise step's epilogue).

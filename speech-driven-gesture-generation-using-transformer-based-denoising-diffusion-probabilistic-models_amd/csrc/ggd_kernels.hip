@@ -527,86 +527,107 @@ __host__ __device__ inline AttGeom aq_geom(int Lk, int dk) {
   return g;
 }
 
-// VE channels (one 16-byte vector of T) of sequence row j as f32; rows outside [0, len) are 0.
-// Self mode reads T rows base[(row0 + j) * ld + col]; memory mode (step_row set) reads f32 rows:
-// j = 0 the step token step_row, j >= 1 the cached speech rows base[(row0 + j - 1) * ld + col].
+// One 16-byte vector of T channels (VE of them) of sequence row j, as f32.  Rows outside
+// [0, len) are the conv's zero padding: their address is redirected to a zeroed global row
+// (`zero`), so no per-element select is needed.  Self mode reads T rows
+// base[(row0 + j) * ld + col]; memory mode (step_row set) reads f32 rows: j = 0 the step token
+// step_row, j >= 1 the cached speech rows base[(row0 + j - 1) * ld + col].
 template <typename T> struct AqSrc {
   static constexpr int VE = 16 / sizeof(T);
   const void* base;
   size_t row0;
   int ld, col, len;
   const float* step_row;
+  const float* zero;
   __device__ __forceinline__ void load(int j, int cv, float (&o)[VE]) const {
     const bool in = j >= 0 && j < len;
-    const int jj = in ? j : 0;
     if (step_row) {
-      const float* p = jj == 0 ? step_row + cv * VE : (const float*)base + (row0 + jj - 1) * (size_t)ld + col + cv * VE;
+      const float* p = !in ? zero : j == 0 ? step_row + cv * VE
+                                           : (const float*)base + (row0 + j - 1) * (size_t)ld + col + cv * VE;
 #pragma unroll
       for (int q = 0; q < VE / 4; ++q) {
         const float4 v = *(const float4*)(p + 4 * q);
-        o[4 * q] = in ? v.x : 0.f;
-        o[4 * q + 1] = in ? v.y : 0.f;
-        o[4 * q + 2] = in ? v.z : 0.f;
-        o[4 * q + 3] = in ? v.w : 0.f;
+        o[4 * q] = v.x;
+        o[4 * q + 1] = v.y;
+        o[4 * q + 2] = v.z;
+        o[4 * q + 3] = v.w;
       }
     } else {
-      const uint4 u = *(const uint4*)((const T*)base + (row0 + jj) * (size_t)ld + col + cv * VE);
+      const T* p = in ? (const T*)base + (row0 + j) * (size_t)ld + col + cv * VE : (const T*)zero;
+      const uint4 u = *(const uint4*)p;
       if constexpr (sizeof(T) == 2) {
-        const bf16_t* h = (const bf16_t*)&u;
+        const unsigned w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = in ? bf2f(h[e]) : 0.f;
+        for (int q = 0; q < 4; ++q) {
+          o[2 * q] = __uint_as_float(w[q] << 16);
+          o[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+        }
       } else {
-        o[0] = in ? __uint_as_float(u.x) : 0.f;
-        o[1] = in ? __uint_as_float(u.y) : 0.f;
-        o[2] = in ? __uint_as_float(u.z) : 0.f;
-        o[3] = in ? __uint_as_float(u.w) : 0.f;
+        o[0] = __uint_as_float(u.x);
+        o[1] = __uint_as_float(u.y);
+        o[2] = __uint_as_float(u.z);
+        o[3] = __uint_as_float(u.w);
       }
     }
   }
 };
 
-// image rows r = 0 .. rows-1 (sequence rows r0 + r) of conv3(src) -> T image, row-major
-// (dst[r * S + c]) or transposed (dst[c * S + r]).  Task = (row, 16-byte channel vector); a
-// thread's vector index is fixed (NTHREADS is a multiple of the vectors per row), so its conv
-// taps and bias are loaded once; (row) tasks run in batches of U per thread, every load of a
-// batch issued before the first conv.
-template <typename T, int DK, bool TRANS, int U = 4>
-__device__ __forceinline__ void aq_conv_stage(T* dst, int S, const AqSrc<T>& src, int r0, int rows, const float* w,
-                                              const float* b) {
-  constexpr int VE = AqSrc<T>::VE, VPR = DK / VE, RPB = NTHREADS / VPR;  // rows per batch slot
+// Conv staging by row strips: thread t owns channel vector cv = t % VPR and the strip of SL
+// consecutive rows sid * SL .. (sid = t / VPR), so it loads SL + 2 rows (not 3 SL) and every
+// load of the strip issues before the first conv.  SL = ceil(rows / NS) <= SLMAX.
+template <typename T, int DK> struct AqStrip {
+  static constexpr int VE = 16 / sizeof(T), VPR = DK / VE, NS = NTHREADS / VPR;
+  static constexpr int SLMAX = (ATT_LMAX + NS - 1) / NS;
   static_assert(NTHREADS % VPR == 0, "a thread keeps one channel vector");
-  const int cv = (int)threadIdx.x % VPR, rr = (int)threadIdx.x / VPR;
-  float w0[VE], w1[VE], w2[VE], bb[VE];
+  float x[SLMAX + 2][VE];
+  int r0, sl, rows;
+  __device__ __forceinline__ void load(const AqSrc<T>& src, int r0_, int rows_) {
+    r0 = r0_;
+    rows = rows_;
+    sl = (rows + NS - 1) / NS;
+    const int cv = (int)threadIdx.x % VPR, sid = (int)threadIdx.x / VPR;
 #pragma unroll
-  for (int e = 0; e < VE; ++e) {
-    const int c = cv * VE + e;
-    w0[e] = w[c * 3 + 0];
-    w1[e] = w[c * 3 + 1];
-    w2[e] = w[c * 3 + 2];
-    bb[e] = b[c];
+    for (int s = 0; s < SLMAX + 2; ++s)
+      if (s < sl + 2) src.load(r0 + sid * sl - 1 + s, cv, x[s]);
   }
-  for (int base = 0; base < rows; base += U * RPB) {
-    float in[U][3][VE];
+  // wl: LDS [4][DK] = tap 0, tap 1, tap 2, bias (transformer.py:28-44: out[i] = b + sum_k w_k in[i+k-1])
+  template <bool TRANS>
+  __device__ __forceinline__ void conv(T* dst, int S, const float* wl) const {
+    const int cv = (int)threadIdx.x % VPR, sid = (int)threadIdx.x / VPR;
+    float w0[VE], w1[VE], w2[VE], bb[VE];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int r = min(base + u * RPB + rr, rows - 1);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) src.load(r0 + r - 1 + k, cv, in[u][k]);
+    for (int e = 0; e < VE; ++e) {
+      const int c = cv * VE + e;
+      w0[e] = wl[c];
+      w1[e] = wl[DK + c];
+      w2[e] = wl[2 * DK + c];
+      bb[e] = wl[3 * DK + c];
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int r = base + u * RPB + rr;
-      if (r >= rows) continue;
+    for (int s = 0; s < SLMAX; ++s) {
+      const int r = sid * sl + s;
+      if (s >= sl || r >= rows) continue;
 #pragma unroll
       for (int e = 0; e < VE; ++e) {
         const int c = cv * VE + e;
-        const float v = bb[e] + w0[e] * in[u][0][e] + w1[e] * in[u][1][e] + w2[e] * in[u][2][e];
+        const float v = bb[e] + w0[e] * x[s][e] + w1[e] * x[s + 1][e] + w2[e] * x[s + 2][e];
         if (TRANS)
           dst[c * S + r] = from_f32<T>(v);
         else
           dst[r * S + c] = from_f32<T>(v);
       }
     }
+  }
+};
+
+// conv taps [dk][3] + bias [dk] of Q, K, V -> LDS wl[3][4][DK]
+template <int DK>
+__device__ __forceinline__ void aq_stage_taps(float* wl, const AttnArgs& a) {
+  const float* W[3] = {a.cw_q, a.cw_k, a.cw_v};
+  const float* B[3] = {a.cb_q, a.cb_k, a.cb_v};
+  for (int i = threadIdx.x; i < 3 * 4 * DK; i += NTHREADS) {
+    const int m = i / (4 * DK), k = (i / DK) % 4, c = i % DK;
+    wl[i] = k < 3 ? W[m][c * 3 + k] : B[m][c];
   }
 }
 
@@ -620,32 +641,37 @@ __global__ void __launch_bounds__(NTHREADS) attn_q_kernel(AttnArgs a) {
   T* Km = (T*)(smem + G.off_k);
   T* Vt = (T*)(smem + G.off_v);
   T* Pw = (T*)(smem + G.off_p);
+  float* wl = (float*)(smem + G.total);  // conv taps, after the attention images
   const int tid = threadIdx.x;
+  const size_t row0 = a.seq_stride ? (size_t)b * a.seq_stride + a.seq_off : (size_t)b * Lq;
+  const int qrows = min(AQ_QT, Lq - q0);
+  // issue the Q and K strips first: their loads fly while the images are zeroed and the taps staged
+  AqSrc<T> sq{a.q, row0, a.ldq, h * DK, Lq, nullptr, a.zero};
+  AqSrc<T> sk{a.k, row0, a.ldkv, h * DK, Lk, nullptr, a.zero};
+  AqSrc<T> sv{a.v, row0, a.ldkv, h * DK, Lk, nullptr, a.zero};
+  if (a.cross) {
+    // memory row 0 = the diffusion-step token of this clip's t; rows 1.. = cached speech K|V
+    const int t = a.t_clip ? a.t_clip[b] : a.steps[*a.step_counter].t_orig;
+    const float* r0 = a.kv_step + (size_t)t * 2 * a.d;
+    const size_t mrow0 = (size_t)b * (Lk - 1);
+    sk = AqSrc<T>{a.kv_mem, mrow0, 2 * a.d, h * DK, Lk, r0 + h * DK, a.zero};
+    sv = AqSrc<T>{a.kv_mem, mrow0, 2 * a.d, a.d + h * DK, Lk, r0 + a.d + h * DK, a.zero};
+  }
+  AqStrip<T, DK> xq, xk;
+  xq.load(sq, q0, qrows);
+  xk.load(sk, 0, Lk);
   {  // zero the padded operand images (rows >= Lq / Lk must be finite zeros)
     uint4* z = (uint4*)smem;
     const int n16 = (int)(G.off_p / 16);
     for (int i = tid; i < n16; i += NTHREADS) z[i] = make_uint4(0, 0, 0, 0);
   }
+  aq_stage_taps<DK>(wl, a);
   __syncthreads();
-  const size_t row0 = a.seq_stride ? (size_t)b * a.seq_stride + a.seq_off : (size_t)b * Lq;
-  const int qrows = min(AQ_QT, Lq - q0);
-  const AqSrc<T> sq{a.q, row0, a.ldq, h * DK, Lq, nullptr};
-  aq_conv_stage<T, DK, false>(Qm, G.SQ, sq, q0, qrows, a.cw_q, a.cb_q);
-  if (!a.cross) {
-    const AqSrc<T> sk{a.k, row0, a.ldkv, h * DK, Lk, nullptr};
-    const AqSrc<T> sv{a.v, row0, a.ldkv, h * DK, Lk, nullptr};
-    aq_conv_stage<T, DK, false>(Km, G.SQ, sk, 0, Lk, a.cw_k, a.cb_k);
-    aq_conv_stage<T, DK, true>(Vt, G.SV, sv, 0, Lk, a.cw_v, a.cb_v);
-  } else {
-    // memory row 0 = the diffusion-step token of this clip's t; rows 1.. = cached speech K|V
-    const int t = a.t_clip ? a.t_clip[b] : a.steps[*a.step_counter].t_orig;
-    const float* r0 = a.kv_step + (size_t)t * 2 * a.d;
-    const size_t mrow0 = (size_t)b * (Lk - 1);
-    const AqSrc<T> sk{a.kv_mem, mrow0, 2 * a.d, h * DK, Lk, r0 + h * DK};
-    const AqSrc<T> sv{a.kv_mem, mrow0, 2 * a.d, a.d + h * DK, Lk, r0 + a.d + h * DK};
-    aq_conv_stage<T, DK, false>(Km, G.SQ, sk, 0, Lk, a.cw_k, a.cb_k);
-    aq_conv_stage<T, DK, true>(Vt, G.SV, sv, 0, Lk, a.cw_v, a.cb_v);
-  }
+  xq.template conv<false>(Qm, G.SQ, wl);
+  AqStrip<T, DK> xv;
+  xv.load(sv, 0, Lk);
+  xk.template conv<false>(Km, G.SQ, wl + 4 * DK);
+  xv.template conv<true>(Vt, G.SV, wl + 8 * DK);
   __syncthreads();
   attn_core<T>(Qm, Km, Vt, Pw, G, qrows, Lk, DK, a.scale, (T*)a.out + (row0 + q0) * a.ldo + (size_t)h * DK, a.ldo);
 }
@@ -666,7 +692,8 @@ hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s) 
   }
   // query-split kernel whenever its images fit (every BASELINE.json shape); else one
   // workgroup per (head, clip)
-  const size_t lq = dtype == 0 ? aq_geom<float>(a.Lk, a.dk).total : aq_geom<bf16_t>(a.Lk, a.dk).total;
+  const size_t lq = (dtype == 0 ? aq_geom<float>(a.Lk, a.dk).total : aq_geom<bf16_t>(a.Lk, a.dk).total) +
+                    sizeof(float) * 12 * a.dk;  // + conv taps
   static bool aq_attr = false;
   if (!aq_attr) {
     (void)hipFuncSetAttribute((const void*)attn_q_kernel<float, 32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -675,7 +702,7 @@ hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s) 
     (void)hipFuncSetAttribute((const void*)attn_q_kernel<bf16_t, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     aq_attr = true;
   }
-  if (lq <= 160 * 1024 && !a.no_qsplit) {
+  if (lq <= 160 * 1024 && !a.no_qsplit && a.zero) {
     const dim3 gq(a.heads, n, (a.Lq + AQ_QT - 1) / AQ_QT);
     const bool d32 = a.dk == 32;
     if (dtype == 0) {
