@@ -44,7 +44,7 @@ enum ggd_status {
 };
 
 /* models/model_creation.py:133-161 -- Model.type */
-enum ggd_model_type { GGD_MODEL_S2G_V2 = 0, GGD_MODEL_DEFAULT = 1 };
+enum ggd_model_type { GGD_MODEL_S2G_V2 = 0, GGD_MODEL_DEFAULT = 1, GGD_MODEL_INPAINT = 2 };
 /* models/model_creation.py:72-93 -- Decoder.type */
 enum ggd_decoder_type { GGD_DEC_ONEWAY = 0, GGD_DEC_TWOWAY = 1 };
 /* compute dtype of the decoder GEMM operands (accumulation is always f32).
@@ -107,6 +107,15 @@ int ggd_set_schedule(ggd_ctx* ctx, const double* betas, int32_t T, const int64_t
  * (there recomputed on every denoise step). */
 int ggd_set_memory(ggd_ctx* ctx, const float* speech_tokens, int32_t n, int32_t ts, int32_t dz,
                    void* stream);
+
+/* Inpaint conditioning of a GGD_MODEL_INPAINT context: poses device f32 (N, L, C), masks device f32
+ * (N, L) (1 = seed frame).  Computes proj([pose*mask, mask]) = Linear(C+1 -> d) SiLU Linear(d -> d)
+ * SiLU Linear(d -> C) once; every following ggd_denoise / ggd_sample adds it to x_t before the
+ * decoder.  poses == NULL clears it (the model then sees x_t alone, i.e. an all-zero projection
+ * input is NOT assumed).  Step-invariant, like the speech memory.
+ * Replaces: Speech2GestureModelInpaint.myforward, models/model.py:152-166 (there recomputed on every
+ * denoise step). */
+int ggd_set_inpaint(ggd_ctx* ctx, const float* poses, const float* masks, int32_t n, void* stream);
 
 /* Model protocol: eps = model(x_t, t).  x_t, eps: device f32 (N, C, L);
  * t: device int32 (N,) ORIGINAL timesteps; N = the batch given to ggd_set_memory.

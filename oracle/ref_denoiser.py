@@ -289,12 +289,22 @@ def speech_memory(sd, cfg, z):
         padded = [F.pad(a, (0, 0, longest - a.shape[1], 0)) for a in z]
         blend = _lin(sd, "blend_layer", th.cat(padded, dim=-1))
         return blend.transpose(0, 1)
-    if cfg["type"] == "default":
+    if cfg["type"] in ("default", "inpaint"):  # Speech2GestureModelInpaint inherits it (model.py:118-166)
         return th.cat([a.transpose(0, 1) for a in z], dim=0)
     raise ValueError(f"Unsupported model type {cfg['type']}")
 
 
-def denoise(sd, cfg, x_t, t, wav=None, speech=None, pe=None):
+def inpaint_projection(sd, inpaint_pose, inpaint_mask):
+    """Speech2GestureModelInpaint.proj on [pose * mask, mask] (models/model.py:135-142, 160-162):
+    Linear(C+1 -> d) SiLU Linear(d -> d) SiLU Linear(d -> C) (+ Dropout, identity in eval).
+    inpaint_pose (L, N, C), inpaint_mask (L, N, 1) -> (L, N, C)."""
+    x_inp = th.cat([inpaint_pose * inpaint_mask, inpaint_mask], dim=-1)
+    h = F.silu(_lin(sd, "proj.0", x_inp))
+    h = F.silu(_lin(sd, "proj.2", h))
+    return _lin(sd, "proj.4", h)
+
+
+def denoise(sd, cfg, x_t, t, wav=None, speech=None, pe=None, inpaint_pose=None, inpaint_mask=None):
     """Speech2GestureModelBase.forward + myforward: models/model.py:12-15,41-73,81-117.
 
     x_t (N, C, L) fp32, t (N,) int64 original timesteps -> eps (N, C, L).
@@ -310,6 +320,8 @@ def denoise(sd, cfg, x_t, t, wav=None, speech=None, pe=None):
     step = step_encoder(sd, t, d)[None]
     memory = th.cat([step, speech], dim=0)
     x = x_t.permute(2, 0, 1)
+    if cfg["type"] == "inpaint":  # x = x + proj(x_inp)  (model.py:164)
+        x = x + inpaint_projection(sd, inpaint_pose, inpaint_mask)
     if cfg["decoder"] == "oneway_cross_attention":
         y = oneway_decoder(sd, x, memory, cfg["heads"], cfg["n_layers"], pe)
     elif cfg["decoder"] == "cross_attention":
@@ -330,9 +342,10 @@ class OracleModel:
         self._cache = None
 
     @th.no_grad()
-    def __call__(self, x_t, t, wav=None, speech=None):
+    def __call__(self, x_t, t, wav=None, speech=None, inpaint_pose=None, inpaint_mask=None):
         if speech is None and self.cache_speech:
             if self._cache is None or self._cache[0] is not wav:
                 self._cache = (wav, speech_memory(self.sd, self.cfg, speech_encoder(self.sd, wav)))
             speech = self._cache[1]
-        return denoise(self.sd, self.cfg, x_t, t, wav=wav, speech=speech, pe=self.pe)
+        return denoise(self.sd, self.cfg, x_t, t, wav=wav, speech=speech, pe=self.pe, inpaint_pose=inpaint_pose,
+                       inpaint_mask=inpaint_mask)

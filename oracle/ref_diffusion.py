@@ -256,7 +256,11 @@ def generate_sample(sch, model, shape, wavs, noise, inpaint_poses=None, inpaint_
         else:
             trans = 0
         denoise_fn = make_denoise_fn(inpaint_poses, inpaint_masks, trans)
-    out = sample_loop(sch, model, shape, {"wav": wavs}, noise, sample_alg, denoise_fn,
+    model_kwargs = {"wav": wavs}
+    if getattr(model, "cfg", {}).get("type") == "inpaint":  # generator.py:244-249
+        model_kwargs["inpaint_pose"] = inpaint_poses.transpose(0, 1)
+        model_kwargs["inpaint_mask"] = inpaint_masks.transpose(0, 1)
+    out = sample_loop(sch, model, shape, model_kwargs, noise, sample_alg, denoise_fn,
                       x_T=x_T, n_steps=n_steps)
     return out["sample"].transpose(1, 2)
 

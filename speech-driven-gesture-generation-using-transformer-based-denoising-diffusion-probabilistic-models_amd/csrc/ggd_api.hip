@@ -77,6 +77,9 @@ struct ggd_ctx {
 
   // weights
   Lin emb_x, emb_mem, out_lin, step0, step2, blend;
+  Lin inp0, inp2, inp4;      // Speech2GestureModelInpaint.proj (model.py:135-142)
+  float *inp_in = nullptr, *inp_h1 = nullptr, *inp_h2 = nullptr, *inp_delta = nullptr;
+  bool inp_on = false;       // ggd_set_inpaint installed a projection
   FLin f_emb, f_out;
   bool fused = false;        // per-clip fused kernels (L <= 64, d_model 256, 8 heads)
   bool persist = false;      // persistent per-clip sampler (bf16, L <= 48): ggd_sample runs it
@@ -549,6 +552,7 @@ int launch_decoder_twoway(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
   hipStream_t s = c->stream;
   // x rows: emb_x + PE[0 .. L) (the first launch of a step bumps the iteration counter)
   GemmArgs g = gemm_args(c->emb_x, n * L, c->x, D.d_pose, c->hj, d);
+  g.a_add = c->inp_on ? c->inp_delta : nullptr;
   g.pe = c->pe;
   g.pe_period = L;
   g.pe_offset = 0;
@@ -640,6 +644,7 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
   hipStream_t s = c->stream;
 
   GemmArgs g = gemm_args(c->emb_x, M, c->x, D.d_pose, c->h, d);
+  g.a_add = c->inp_on ? c->inp_delta : nullptr;
   g.pe = c->pe;
   g.pe_period = L;
   g.pe_offset = 0;
@@ -885,6 +890,12 @@ int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out) {
   HIP_TRY(c, dalloc(c, &c->ffn, c->tsize * M * 4 * d));
   HIP_TRY(c, dalloc(c, &c->d_counter, sizeof(int)));
   HIP_TRY(c, dalloc(c, &c->zero_row, 1024));
+  if (D.model_type == GGD_MODEL_INPAINT) {
+    HIP_TRY(c, dalloc(c, &c->inp_in, sizeof(float) * M * (D.d_pose + 1)));
+    HIP_TRY(c, dalloc(c, &c->inp_h1, sizeof(float) * M * d));
+    HIP_TRY(c, dalloc(c, &c->inp_h2, sizeof(float) * M * d));
+    HIP_TRY(c, dalloc(c, &c->inp_delta, sizeof(float) * M * D.d_pose));
+  }
   HIP_TRY(c, dalloc(c, &c->d_t, sizeof(int) * B));
   HIP_TRY(c, dalloc(c, &c->mem_tmp, sizeof(float) * (size_t)B * Ts * d));
   HIP_TRY(c, dalloc(c, &c->tok_tmp, sizeof(float) * (size_t)B * Ts * d));
@@ -933,7 +944,8 @@ int ggd_load_weight(ggd_ctx* c, const char* name, const float* host_data, int64_
   const std::string n(name);
   if (n.rfind("speech_encoder.", 0) == 0) return GGD_IGNORED;
   const bool known = n.rfind("pose_decoder.", 0) == 0 || n.rfind("diffusion_step_encoder.", 0) == 0 ||
-                     n.rfind("blend_layer.", 0) == 0;
+                     n.rfind("blend_layer.", 0) == 0 ||
+                     (c->desc.model_type == GGD_MODEL_INPAINT && n.rfind("proj.", 0) == 0);
   if (!known) return fail(c, GGD_ERR_NAME, "unknown weight name: " + n);
   c->staged[n].assign(host_data, host_data + numel);
   c->finalized = false;
@@ -956,6 +968,11 @@ int ggd_finalize_weights(ggd_ctx* c) {
   TRY(pack_lin(c, c->step0, {"diffusion_step_encoder.proj.0"}, d, d));
   TRY(pack_lin(c, c->step2, {"diffusion_step_encoder.proj.2"}, d, d));
   if (D.model_type == GGD_MODEL_S2G_V2) TRY(pack_lin(c, c->blend, {"blend_layer"}, d, 3 * d));
+  if (D.model_type == GGD_MODEL_INPAINT) {  // step-invariant: evaluated once per ggd_set_inpaint
+    TRY(pack_lin(c, c->inp0, {"proj.0"}, d, C + 1));
+    TRY(pack_lin(c, c->inp2, {"proj.2"}, d, d));
+    TRY(pack_lin(c, c->inp4, {"proj.4"}, C, d));
+  }
   if (c->twoway) {
     c->layers2.assign(D.n_layers, Layer2{});
     for (int l = 0; l < D.n_layers; ++l) {
@@ -1023,7 +1040,7 @@ int ggd_finalize_weights(ggd_ctx* c) {
     TRY(pack_lin(c, Ly.ff1, {q + "feed_forward.layer1"}, 4 * d, d, true));
     TRY(pack_lin(c, Ly.ff2, {q + "feed_forward.layer2"}, d, 4 * d, true));
   }
-  c->fused = D.decoder_type == GGD_DEC_ONEWAY && D.dtype != GGD_FP8W &&
+  c->fused = D.decoder_type == GGD_DEC_ONEWAY && D.dtype != GGD_FP8W && D.model_type != GGD_MODEL_INPAINT &&
              fused_supported(D.dtype, D.d_model, D.heads, D.seq_len, D.speech_len, D.d_pose);
   if (c->fused) {
     TRY(frag_from(c, c->f_emb, {P + "emb_x"}, d, C, iota_n(d)));
@@ -1123,6 +1140,34 @@ int ggd_set_memory(ggd_ctx* c, const float* tok, int32_t n, int32_t ts, int32_t 
   HIP_TRY(c, hipEventRecord(c->ev_out, s));
   HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
   c->mem_n = n;
+  return GGD_OK;
+}
+
+int ggd_set_inpaint(ggd_ctx* c, const float* poses, const float* masks, int32_t n, void* stream) {
+  if (!c) return GGD_ERR_ARG;
+  if (c->desc.model_type != GGD_MODEL_INPAINT) return fail(c, GGD_ERR_UNSUPPORTED, "not an inpaint model");
+  if (!c->finalized) return fail(c, GGD_ERR_STATE, "weights not finalized");
+  if (!poses) {
+    c->inp_on = false;
+    return GGD_OK;
+  }
+  if (!masks || n <= 0 || n > c->desc.max_batch) return fail(c, GGD_ERR_ARG, "bad inpaint arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const ggd_desc& D = c->desc;
+  const int M = n * D.seq_len, d = D.d_model, C = D.d_pose;
+  HIP_TRY(c, hipEventRecord(c->ev_in, (hipStream_t)stream));
+  HIP_TRY(c, hipStreamWaitEvent(s, c->ev_in, 0));
+  HIP_TRY(c, launch_inpaint_input(c->inp_in, poses, masks, M, C, s));
+  GemmArgs g = gemm_args(c->inp0, M, c->inp_in, C + 1, c->inp_h1, d);
+  GEMM(c, PRO_F32, EPI_SILU, g, s);
+  g = gemm_args(c->inp2, M, c->inp_h1, d, c->inp_h2, d);
+  GEMM(c, PRO_F32, EPI_SILU, g, s);
+  g = gemm_args(c->inp4, M, c->inp_h2, d, c->inp_delta, C);
+  GEMM(c, PRO_F32, EPI_F32, g, s);
+  c->inp_on = true;
+  HIP_TRY(c, hipEventRecord(c->ev_out, s));
+  HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
   return GGD_OK;
 }
 

@@ -47,6 +47,8 @@ struct GemmArgs {
   // fp8 weights (GGD_FP8W): non-null = W is OCP e4m3fn bytes [Npad][K] and out column n is
   // scaled by wscale[n] before the bias (per-output-channel dequantization)
   const float* wscale;
+  // PRO_F32: A + a_add elementwise (same layout) -- the inpaint model's x + proj([pose*mask, mask])
+  const float* a_add;
 };
 
 __host__ __device__ __forceinline__ size_t map_row(int m, int len, int stride, int off) {
@@ -205,6 +207,7 @@ hipError_t launch_mb(int mode, void* buf, size_t buf_bytes, int arg, int blocks,
 hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
+hipError_t launch_inpaint_input(float* out, const float* pose, const float* mask, int M, int C, hipStream_t s);
 hipError_t launch_posterior(const PostArgs& a, hipStream_t s);
 hipError_t launch_step_embed(float* out, int T, int d, hipStream_t s);
 hipError_t launch_init_state(float* x, const float* x_T_ncl, uint64_t seed, int64_t clip_offset,

@@ -68,7 +68,10 @@ __device__ __forceinline__ void load_a(ARegs<T, MT, PRO>& R, const GemmArgs& a, 
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int v = tid + i * NTHREADS, r = v / KC, c = v % KC, m = m0 + r, k = kc0 + c;
-      R.v[i] = (m < a.M && k < a.k_valid) ? A[map_row(m, a.a_len, a.a_stride, a.a_off) * a.lda + k] : 0.f;
+      const bool ok = m < a.M && k < a.k_valid;
+      const size_t e = ok ? map_row(m, a.a_len, a.a_stride, a.a_off) * a.lda + k : 0;
+      R.v[i] = ok ? A[e] : 0.f;
+      if (a.a_add) R.v[i] += ok ? a.a_add[e] : 0.f;  // inpaint conditioning: x + proj(pose, mask)
     }
   }
 }
@@ -720,6 +723,22 @@ hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s) 
     hipLaunchKernelGGL(attn_kernel<float>, grid, dim3(NTHREADS), lds, s, a);
   else
     hipLaunchKernelGGL(attn_kernel<bf16_t>, grid, dim3(NTHREADS), lds, s, a);
+  return hipGetLastError();
+}
+
+// Speech2GestureModelInpaint's projection input (models/model.py:160-162):
+// out[m][0..C) = pose[m][c] * mask[m], out[m][C] = mask[m]; rows m = clip * L + frame
+__global__ void inpaint_input_kernel(float* out, const float* pose, const float* mask, int M, int C) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * (C + 1)) return;
+  const int m = idx / (C + 1), c = idx % (C + 1);
+  const float mk = mask[m];
+  out[idx] = c < C ? pose[(size_t)m * C + c] * mk : mk;
+}
+
+hipError_t launch_inpaint_input(float* out, const float* pose, const float* mask, int M, int C, hipStream_t s) {
+  const int total = M * (C + 1);
+  hipLaunchKernelGGL(inpaint_input_kernel, dim3((total + 255) / 256), dim3(256), 0, s, out, pose, mask, M, C);
   return hipGetLastError();
 }
 

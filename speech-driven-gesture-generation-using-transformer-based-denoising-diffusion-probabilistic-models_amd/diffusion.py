@@ -152,12 +152,14 @@ class GaussianSpacedDiffusion(GaussianDiffusion):
         assert isinstance(shape, (tuple, list)) and len(shape) == 3, "shape must be (N, C, L)"
         model_kwargs = dict(model_kwargs or {})
         wav = model_kwargs.pop("wav", None)
+        inp_pose, inp_mask = model_kwargs.pop("inpaint_pose", None), model_kwargs.pop("inpaint_mask", None)
         if model_kwargs:
             raise ValueError(f"unsupported model kwargs {sorted(model_kwargs)}")
         N, C, L = (int(s) for s in shape)
         dev = th.device(device) if device is not None else model.device
         ctx, n = model.prepare(wav, L)
         assert n == N, "wav batch differs from shape[0]"
+        model.condition(ctx, n, L, inp_pose, inp_mask)
         ctx.set_schedule(self.betas, self.timestep_map)
         if seed is None:
             seed = int(th.randint(0, 2 ** 62, (1,)).item())

@@ -107,7 +107,7 @@ def speech_tokens(model_type, z):
     if model_type == "s2g_v2":
         longest = max(a.shape[1] for a in z)
         return th.cat([F.pad(a, (0, 0, longest - a.shape[1], 0)) for a in z], dim=-1).contiguous()
-    if model_type == "default":
+    if model_type in ("default", "inpaint"):  # Speech2GestureModelInpaint inherits the default memory
         return th.cat(list(z), dim=1).contiguous()
     raise ValueError(f"Unsupported model_type {model_type}")
 

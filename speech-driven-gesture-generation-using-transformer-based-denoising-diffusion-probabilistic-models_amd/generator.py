@@ -68,7 +68,13 @@ class Generator:
             else:
                 trans = th.zeros(L, device=device)
             denoise_fn = InpaintDenoise(inpaint_poses, inpaint_masks, trans)
-        out = sample_func(self.model, shape, noise=noise, denoise_fn=denoise_fn, model_kwargs={"wav": wavs},
+        model_kwargs = {"wav": wavs}
+        if self.model.arch["type"] == "inpaint":  # generator.py:244-249
+            assert inpaint_poses is not None and len(inpaint_poses.shape) == 3
+            assert len(inpaint_masks.shape) == 3 and inpaint_masks.size()[:2] == inpaint_poses.size()[:2]
+            model_kwargs["inpaint_pose"] = inpaint_poses.transpose(0, 1)  # -> (T, N, C)
+            model_kwargs["inpaint_mask"] = inpaint_masks.transpose(0, 1)  # -> (T, N, 1)
+        out = sample_func(self.model, shape, noise=noise, denoise_fn=denoise_fn, model_kwargs=model_kwargs,
                           device=device, progress=progress, **kw)
         sample = out["sample"].transpose(1, 2)
         return self.tensor2dtype(sample, return_dtype)

@@ -75,11 +75,11 @@ def _stream_ptr(device):
 
 
 class Speech2GestureModel:
-    """HIP sampler model for Model.type in {'s2g_v2', 'default'} with the one-way decoder."""
+    """HIP sampler model for Model.type in {'s2g_v2', 'default', 'inpaint'} (model_creation.py:133-161)."""
 
     def __init__(self, d_pose, model_params, dtype="bf16", device="cuda"):
         self.arch = arch_from_config(model_params, d_pose)
-        if self.arch["type"] not in ("s2g_v2", "default"):
+        if self.arch["type"] not in ("s2g_v2", "default", "inpaint"):
             raise ValueError(f"Unsupported model_type {self.arch['type']}")
         self.diffusion_steps = int(model_params["Diffusion"]["diffusion_steps"])
         self.dtype = dtype
@@ -157,7 +157,8 @@ class Speech2GestureModel:
             raise RuntimeError("load_state_dict() before use")
         a = self.arch
         desc = native.Desc(
-            model_type=native.MODEL_S2G_V2 if a["type"] == "s2g_v2" else native.MODEL_DEFAULT,
+            model_type={"s2g_v2": native.MODEL_S2G_V2, "default": native.MODEL_DEFAULT,
+                        "inpaint": native.MODEL_INPAINT}[a["type"]],
             decoder_type=native.DEC_ONEWAY if a["decoder"] == "oneway_cross_attention" else native.DEC_TWOWAY,
             d_model=a["d_model"], heads=a["heads"], n_layers=a["n_layers"], d_pose=a["d_pose"],
             seq_len=L, speech_len=Ts, max_batch=max(n, 1), dtype=_DTYPES[self.dtype],
@@ -185,17 +186,36 @@ class Speech2GestureModel:
         self._mem_cache = (key, tok)  # keep tok alive until the ctx has consumed it
         return ctx, n
 
+    def condition(self, ctx, n, L, inpaint_pose=None, inpaint_mask=None):
+        """Speech2GestureModelInpaint (models/model.py:152-166): install proj([pose*mask, mask]) for the
+        next calls.  inpaint_pose (L, N, C), inpaint_mask (L, N, 1) as the reference's model_kwargs."""
+        if self.arch["type"] != "inpaint":
+            if inpaint_pose is not None or inpaint_mask is not None:
+                raise ValueError(f"unsupported model kwargs ['inpaint_mask', 'inpaint_pose'] for type {self.arch['type']}")
+            return
+        if inpaint_pose is None or inpaint_mask is None:
+            raise TypeError("Speech2GestureModelInpaint.myforward() needs inpaint_pose and inpaint_mask")
+        C = self.arch["d_pose"]
+        assert tuple(inpaint_pose.shape) == (L, n, C), f"inpaint_pose must be (L, N, C), got {tuple(inpaint_pose.shape)}"
+        assert tuple(inpaint_mask.shape) == (L, n, 1), f"inpaint_mask must be (L, N, 1), got {tuple(inpaint_mask.shape)}"
+        pose = inpaint_pose.to(self.device, th.float32).transpose(0, 1).contiguous()
+        mask = inpaint_mask.to(self.device, th.float32).reshape(L, n).transpose(0, 1).contiguous()
+        native.check(ctx.h, ctx.lib.ggd_set_inpaint(ctx.h, ctypes.c_void_p(pose.data_ptr()),
+                                                    ctypes.c_void_p(mask.data_ptr()), n, _stream_ptr(self.device)),
+                     "set inpaint")
+
     @th.no_grad()
-    def __call__(self, x_t, t, wav=None, **kwargs):
-        """eps = model(x_t, t, wav=...)  (models/model.py:12-15)."""
+    def __call__(self, x_t, t, wav=None, inpaint_pose=None, inpaint_mask=None, **kwargs):
+        """eps = model(x_t, t, wav=...[, inpaint_pose, inpaint_mask])  (models/model.py:12-15, 152-166)."""
         if kwargs:
-            raise ValueError(f"unsupported model kwargs {sorted(kwargs)} (Speech2GestureModelInpaint is out of scope)")
+            raise ValueError(f"unsupported model kwargs {sorted(kwargs)}")
         assert wav is not None and wav.dim() == 2, "wav (N, T) is required"
         assert x_t.dim() == 3 and x_t.shape[1] == self.arch["d_pose"], f"x_t must be (N, C, L), got {tuple(x_t.shape)}"
         N, C, L = x_t.shape
         assert t.shape == (N,), f"t must be (N,), got {tuple(t.shape)}"
         ctx, n = self.prepare(wav, L)
         assert n == N, "wav batch differs from x_t batch"
+        self.condition(ctx, n, L, inpaint_pose, inpaint_mask)
         x = x_t.to(self.device, th.float32).contiguous()
         tt = t.to(self.device, th.int32).contiguous()
         if int(tt.min()) < 0 or int(tt.max()) >= self.diffusion_steps:

@@ -36,7 +36,7 @@ def create_model(d_pose, model_params, lr=1e-2, weight_decay=None, scheduler_par
     dec = model_params["Decoder"]["type"]
     if dec not in ("oneway_cross_attention", "cross_attention"):
         raise ValueError(f"Unsupported decoder type {dec}.")
-    if model_params["type"] not in ("s2g_v2", "default"):
+    if model_params["type"] not in ("s2g_v2", "default", "inpaint"):
         raise ValueError(f"Unsupported model_type {model_params['type']}")
     model = Speech2GestureModel(d_pose, model_params, dtype=dtype, device=device)
     diffusion = create_diffusion(model_params["Diffusion"], is_training)

@@ -16,14 +16,14 @@ HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_fusedlib.h", "ggd_phases.h", os
 
 GGD_OK, GGD_IGNORED = 0, 1
 GGD_ERR_ARG, GGD_ERR_UNSUPPORTED, GGD_ERR_HIP, GGD_ERR_STATE, GGD_ERR_NAME = -1, -2, -3, -4, -5
-MODEL_S2G_V2, MODEL_DEFAULT = 0, 1
+MODEL_S2G_V2, MODEL_DEFAULT, MODEL_INPAINT = 0, 1, 2
 DEC_ONEWAY, DEC_TWOWAY = 0, 1
 F32, BF16, FP8W = 0, 1, 2   # ggd_dtype (include/ggd.h)
 DDPM, DDIM = 0, 1
 
 EXPORTS = [
     "ggd_create", "ggd_destroy", "ggd_last_error", "ggd_load_weight", "ggd_finalize_weights",
-    "ggd_set_schedule", "ggd_set_memory", "ggd_denoise", "ggd_posterior_step", "ggd_sample",
+    "ggd_set_schedule", "ggd_set_memory", "ggd_set_inpaint", "ggd_denoise", "ggd_posterior_step", "ggd_sample",
     "ggd_set_profiling", "ggd_kernel_time", "ggd_profile_kind", "ggd_diag", "ggd_version",
     "ggd_enc_create", "ggd_enc_destroy", "ggd_enc_last_error", "ggd_enc_load_weight", "ggd_enc_finalize",
     "ggd_enc_lengths", "ggd_enc_run",
@@ -102,6 +102,7 @@ def load():
         "ggd_finalize_weights": (ctypes.c_int, [CTX]),
         "ggd_set_schedule": (ctypes.c_int, [CTX, VP, I32, VP]),
         "ggd_set_memory": (ctypes.c_int, [CTX, VP, I32, I32, I32, VP]),
+        "ggd_set_inpaint": (ctypes.c_int, [CTX, VP, VP, I32, VP]),
         "ggd_denoise": (ctypes.c_int, [CTX, VP, VP, VP, I32, VP]),
         "ggd_posterior_step": (ctypes.c_int, [CTX, I32, F, I32, VP, VP, VP, VP, VP, VP, I32, VP]),
         "ggd_sample": (ctypes.c_int, [CTX, P(SampleArgs), VP]),

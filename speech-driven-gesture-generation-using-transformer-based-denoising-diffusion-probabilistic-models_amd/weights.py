@@ -141,6 +141,10 @@ def parameter_shapes(arch):
     lin(P + "out_layers.1", C, d)
     if arch["type"] == "s2g_v2":
         lin("blend_layer", d, 3 * d)
+    elif arch["type"] == "inpaint":  # models/model.py:135-145: zero-initialised as in GLIDE
+        for name, n_out, n_in in (("proj.0", d, C + 1), ("proj.2", d, d), ("proj.4", C, d)):
+            S[name + ".weight"] = ((n_out, n_in), "zeros")
+            S[name + ".bias"] = ((n_out,), "zeros")
     elif arch["type"] != "default":
         raise ValueError(f"Unsupported model_type {arch['type']}")
     return S

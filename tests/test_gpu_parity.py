@@ -314,3 +314,58 @@ def test_sample_fp8_weights_long_clip(pkg, beat_cfg, setup, setup_fp8):
                                      ref_diffusion.InjectedNoise(x, zs), "ddpm", x_T=x, n_steps=steps)
     assert rel_rms(out["sample"].cpu(), want["sample"]) <= 5e-2
     assert rel_rms(out["eps"].cpu(), want["eps"]) <= 2e-2
+
+
+# ------------------------------------------------------------------------------------------
+# Speech2GestureModelInpaint (Model.type "inpaint", models/model.py:118-166): the seed-pose
+# projection proj([pose * mask, mask]) is added to x_t before the decoder; the HIP context
+# evaluates it once per call (ggd_set_inpaint).  f32 tolerances as the other f32 tests.
+# ------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def setup_inp(pkg, beat_cfg):
+    mp = beat_cfg.Model.to_dict()
+    mp["type"] = "inpaint"
+    arch = pkg.arch_from_config(mp, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=4, perturb=True)   # perturbed: the reference zero-inits proj
+    om = ref_denoiser.OracleModel(sd, oracle_cfg(arch), cache_speech=True)
+    model, diffusion, _, _, _ = pkg.create_model(D_POSE, mp, dtype="f32", device="cuda:0")
+    model.load_state_dict(sd)
+    return model, diffusion, om
+
+
+def _seed_inputs(n, seed_len, seed):
+    g = th.Generator().manual_seed(seed)
+    poses = th.randn(n, L, D_POSE, generator=g)
+    masks = th.ones(n, L, 1)
+    masks[:, seed_len:] = 0
+    return poses, masks
+
+
+def test_inpaint_model_denoise_f32(setup_inp):
+    model, _, om = setup_inp
+    wav, x, t = inputs(3, seed=41)
+    poses, masks = _seed_inputs(3, 10, 42)
+    kw = {"inpaint_pose": poses.transpose(0, 1), "inpaint_mask": masks.transpose(0, 1)}
+    eps = model(x.cuda(), t.cuda(), wav=wav.cuda(), **{k: v.cuda() for k, v in kw.items()}).cpu()
+    ref = om(x, t, wav=wav, **kw)
+    assert (eps - ref).abs().max().item() <= 1e-4
+    # the projection matters: without it the oracle differs
+    assert (om(x, t, wav=wav, inpaint_pose=poses.transpose(0, 1) * 0, inpaint_mask=masks.transpose(0, 1) * 0)
+            - ref).abs().max().item() > 1e-3
+
+
+def test_inpaint_model_generate_sample_f32(pkg, setup_inp):
+    """generate_sample on an inpaint model: model conditioning + x0 replacement + ramp (generator.py:218-296)."""
+    model, diffusion, om = setup_inp
+    gen = pkg.Generator(model, diffusion)
+    n, steps, seed_len, tf = 2, 4, 10, 0.575
+    wav, x, _ = inputs(n, seed=43)
+    poses, masks = _seed_inputs(n, seed_len, 44)
+    zs = th.randn(steps, n, D_POSE, L, generator=th.Generator().manual_seed(45))
+    got = gen.generate_sample((n, D_POSE, L), wav, noise=x, inpaint_poses=poses, inpaint_masks=masks,
+                              sample_alg="ddpm", trans_factor=tf, pose_seed_len=seed_len, device="cuda:0",
+                              step_noise=zs.cuda(), n_steps=steps).cpu()
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    want = ref_diffusion.generate_sample(sch, om, (n, D_POSE, L), wav, ref_diffusion.InjectedNoise(x, zs),
+                                         poses, masks, "ddpm", tf, seed_len, x_T=x, n_steps=steps)
+    assert (got - want).abs().max().item() <= 1e-3
