@@ -274,6 +274,10 @@ def main():
             flop = clip_step * B * T / prof_n   # one launch per chunk of <= 32 clips
             kernel = f"mk_kernel<{args.dtype}> (persistent reverse loop: all {T} denoise steps, 17 phases each)"
             timing = "hipEvent pair around the loop's single launch in the last timed pass"
+        elif prof_kind == 3:  # one workgroup per clip: one launch runs all T steps of the batch
+            flop = clip_step * B * T
+            kernel = f"psk_kernel<{args.dtype}> (one workgroup per clip, all {T} denoise steps in one launch)"
+            timing = "hipEvent pair around the loop's single launch in the last timed pass"
         elif prof_kind == 2:  # generic path: the FFN-up GEMM (LN prologue, ReLU^2 epilogue), per launch
             flop = 2 * B * L * d * 4 * d
             kernel = f"gemm_kernel<{args.dtype}> FFN-up (LN1 prologue + Linear {d}->{4 * d} + ReLU^2, M={B * L})"
@@ -283,7 +287,7 @@ def main():
             kernel = f"kb_kernel<{args.dtype}> (SA out-proj + LN2 + cross-attn Q + conv + cross-attention)"
             timing = "device realtime-clock span of every KB launch of the last timed pass"
         ach = flop / (avg_us * 1e-6) / 1e12
-        tr = pmc_traffic({1: "mk_kernel", 2: "gemm_kernel<unsigned short, 64, 1, 1"}.get(prof_kind, "kb_kernel"),
+        tr = pmc_traffic({1: "mk_kernel", 2: "gemm_kernel<unsigned short, 64, 1, 1", 3: "psk_kernel"}.get(prof_kind, "kb_kernel"),
                          args.workload)
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 6), "traffic": tr and tr["bytes_per_launch"], "traffic_detail": tr, "kernel": kernel, "timing": timing,

@@ -163,7 +163,8 @@ int ggd_set_profiling(ggd_ctx* ctx, int32_t on);
 int ggd_kernel_time(ggd_ctx* ctx, int32_t which, double* avg_us, int64_t* launches);
 /* What the last profiled ggd_sample timed: 0 = kb_kernel launches of the per-phase path,
  * 1 = the persistent loop (mk_kernel: one launch for all denoise steps), 2 = the generic path's
- * FFN-up GEMM (LayerNorm prologue + Linear d -> 4d + ReLU^2, hipEvent pairs per launch). */
+ * FFN-up GEMM (LayerNorm prologue + Linear d -> 4d + ReLU^2, hipEvent pairs per launch), 3 = the
+ * one-workgroup-per-clip loop (psk_kernel: one launch for all steps; chosen for large batches). */
 int ggd_profile_kind(ggd_ctx* ctx);
 
 /* Diagnostics (not part of the reference surface): launch one kernel configuration `iters`
@@ -176,9 +177,9 @@ int ggd_profile_kind(ggd_ctx* ctx);
  * (returns GHz instead of microseconds), 3 / 4 bulk 64 KiB / 16 KiB load per block, 6 clip-group
  * hand-off inside one launch (arg = rounds | variant << 20; avg_us[1..3] = errors, misplaced,
  * timeouts; scripts/handoff_bench.py); what = 6: as
- * 4 with in-kernel phase stamps (avg_us[0..7] = phase ends in us); what = 7: p = {1} routes
- * ggd_sample through the per-step launches instead of the persistent kernel, {0} back (returns 1
- * in *avg_us when the persistent kernel is available); what = 8: persistent-kernel phase stamps of
+ * 4 with in-kernel phase stamps (avg_us[0..7] = phase ends in us); what = 7: p = {0} forces the
+ * one-workgroup-per-clip loop (psk_kernel), {1} never uses it, {2} automatic (the default: used when
+ * the clip-group loop would need >= 4 chunks); returns 1 in *avg_us when psk_kernel is available; what = 8: persistent-kernel phase stamps of
  * iteration 0, p = {1} arm, {2} read (avg_us[0..7]), {0} disarm; what = 9: p = {1} routes
  * ggd_sample through the per-phase launches instead of the persistent loop (ggd_mega.hip), {0}
  * back (returns the loop's clip capacity in *avg_us). */

@@ -86,8 +86,10 @@ struct ggd_ctx {
   FusedLayer* d_layers = nullptr;  // device copy of every layer's FusedLayer (persistent kernel)
   void* arena = nullptr;     // current device arena (dalloc) and its fill level
   size_t arena_off = 0;
-  bool no_persist = true;    // ggd_diag what=7 {0}: use the persistent kernel (still slower than the
-                             // per-step launches on the C2 shape, so it is opt-in for now)
+  int persist_mode = 0;      // ggd_diag what=7: 0 auto, 1 never, 2 always the one-workgroup-per-clip loop.
+                             // Auto: when the clip-group loop would need >= 4 chunks (measured on MI355X,
+                             // scripts/route_compare.py: 385 us/step for any n <= 256 vs 113 us per
+                             // 32-clip chunk)
   unsigned long long* stamps = nullptr;  // ggd_diag what=8: phase stamps of the persistent kernel
   float *out_ln_g = nullptr, *out_ln_b = nullptr;
   std::vector<Layer> layers;
@@ -1311,7 +1313,7 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     return GGD_OK;
   }
   if (what == 7 && np >= 1) {  // p[0] != 0: route ggd_sample through the per-step launches
-    c->no_persist = p[0] != 0;
+    c->persist_mode = p[0] == 0 ? 2 : p[0] == 1 ? 1 : 0;
     *avg_us = c->persist ? 1.0 : 0.0;
     return GGD_OK;
   }
@@ -1631,7 +1633,12 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   HIP_TRY(c, hipStreamWaitEvent(s, c->ev_in, 0));
   HIP_TRY(c, hipMemcpyAsync(c->d_steps, recs.data(), sizeof(StepRec) * T, hipMemcpyHostToDevice, s));
   HIP_TRY(c, launch_init_state(c->x, a->x_T, a->seed, a->clip_offset, a->n, D.d_pose, D.seq_len, s));
-  if (c->persist && !c->no_persist) {
+  bool use_persist = c->persist && c->persist_mode != 1;
+  if (use_persist && c->persist_mode == 0) {
+    const int cap = c->no_mega ? 0 : mega_capacity(D.dtype, D.seq_len);
+    use_persist = cap <= 0 || (a->n + cap - 1) / cap >= 4;
+  }
+  if (use_persist) {
     // ONE launch: a workgroup per clip runs all nsteps iterations (ggd_persist.hip); in
     // profiling mode that launch is the timed kernel
     PersistArgs p{};
@@ -1676,6 +1683,8 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
       HIP_TRY(c, hipEventElapsedTime(&ms, c->prof.ev[0], c->prof.ev[1]));
       c->prof_avg_us = ms * 1000.0;
       c->prof_launches = 1;
+      c->prof_kind = 3;
+      c->span_pending = 0;
     }
     HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));
     HIP_TRY(c, hipEventRecord(c->ev_out, s));

@@ -369,3 +369,59 @@ def test_inpaint_model_generate_sample_f32(pkg, setup_inp):
     want = ref_diffusion.generate_sample(sch, om, (n, D_POSE, L), wav, ref_diffusion.InjectedNoise(x, zs),
                                          poses, masks, "ddpm", tf, seed_len, x_T=x, n_steps=steps)
     assert (got - want).abs().max().item() <= 1e-3
+
+
+# ------------------------------------------------------------------------------------------
+# Route selection of ggd_sample (bf16): the one-workgroup-per-clip loop (psk_kernel) is chosen
+# automatically when the clip-group loop (mk_kernel) would need >= 4 chunks (the C5 shape,
+# 128 clips per GPU); both must agree with the oracle and with each other.
+# ------------------------------------------------------------------------------------------
+def _route(ctx, mode):
+    import ctypes
+    arr = (ctypes.c_int32 * 1)(mode)
+    out = ctypes.c_double()
+    rc = ctx.lib.ggd_diag(ctx.h, 7, arr, 1, 1, ctypes.cast(ctypes.byref(out), ctypes.c_void_p))
+    assert rc == 0
+    return out.value
+
+
+def test_per_clip_loop_matches_oracle_bf16(pkg, beat_cfg, setup):
+    _, sd, om = setup
+    model, diffusion = make_model(pkg, beat_cfg, sd, "bf16")
+    n, steps = 4, 6
+    wav, x, _ = inputs(n, seed=51)
+    zs = th.randn(steps, n, D_POSE, L, generator=th.Generator().manual_seed(52))
+    ctx, _ = model.prepare(wav.cuda(), L)
+    outs = {}
+    try:
+        for name, mode in (("psk", 0), ("mk", 1)):
+            assert _route(ctx, mode) == 1.0   # the per-clip loop is available on this shape
+            outs[name] = diffusion.p_sample_loop(model, (n, D_POSE, L), {"wav": wav.cuda()}, noise=x.cuda(),
+                                                 step_noise=zs.cuda(), n_steps=steps)["sample"].cpu()
+    finally:
+        _route(ctx, 2)
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    want = ref_diffusion.sample_loop(sch, om, (n, D_POSE, L), {"wav": wav}, ref_diffusion.InjectedNoise(x, zs),
+                                     "ddpm", x_T=x, n_steps=steps)["sample"]
+    assert rel_rms(outs["psk"], want) <= 5e-2
+    assert rel_rms(outs["psk"], outs["mk"]) <= 1e-2
+
+
+def test_auto_route_large_batch_ddim_bf16(pkg, beat_cfg, setup):
+    """C5 shape (128 clips, DDIM-50): the automatic route equals the clip-group loop's result."""
+    _, sd, _ = setup
+    model, _ = make_model(pkg, beat_cfg, sd, "bf16")
+    diffusion = pkg.create_diffusion(dict(beat_cfg.Model.Diffusion.to_dict(), timestep_respacing="ddim50"), False)
+    n = 128
+    wav = (th.randn(n, WAV, generator=th.Generator().manual_seed(53)) * 0.1).cuda()
+    ctx, _ = model.prepare(wav, L)
+    run = lambda: diffusion.ddim_sample_loop(model, (n, D_POSE, L), model_kwargs={"wav": wav}, seed=54,
+                                             n_steps=5, extras=False)["sample"].cpu()
+    auto = run()
+    try:
+        _route(ctx, 1)
+        mk = run()
+    finally:
+        _route(ctx, 2)
+    assert bool(th.isfinite(auto).all())
+    assert rel_rms(auto, mk) <= 1e-2
