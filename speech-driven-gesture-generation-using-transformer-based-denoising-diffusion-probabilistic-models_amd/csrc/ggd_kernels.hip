@@ -98,6 +98,58 @@ __device__ __forceinline__ void ln_stats(ARegs<T, MT, PRO_LN>& R, int K) {
   R.rs = 1.0f / sqrtf(q / (float)K + 1e-5f);
 }
 
+// PRO_F32 with a dense A (lda == k_valid, identity row map, one K chunk): the tile's rows are one
+// contiguous, 16-byte aligned span of MT * lda floats, loaded as float4 (all loads issued before the
+// first use) and scattered into the LDS tile; columns k_valid .. KC - 1 are written as zeros.  The
+// emb_x GEMM reads the pose state this way (lda = C = 123: rows are not 16-byte aligned on their
+// own, so the per-element path issued MT * KC / NTHREADS scalar loads per thread).
+template <typename T, int MT>
+__device__ __forceinline__ void stage_f32_span(T* As, const GemmArgs& a, int m0) {
+  constexpr int STR = KC + Tile<T>::PAD, NV = (MT * KC / 4 + NTHREADS - 1) / NTHREADS;
+  const int lda = a.lda, rows = min(MT, a.M - m0), nv = (rows * lda) >> 2;  // whole float4s
+  const float* base = (const float*)a.A + (size_t)m0 * lda;
+  const float* add = a.a_add ? a.a_add + (size_t)m0 * lda : nullptr;
+  float4 v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = min((int)threadIdx.x + i * NTHREADS, max(nv - 1, 0));
+    v[i] = *(const float4*)(base + 4 * j);
+  }
+  if (add) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int j = min((int)threadIdx.x + i * NTHREADS, max(nv - 1, 0));
+      const float4 w = *(const float4*)(add + 4 * j);
+      v[i].x += w.x; v[i].y += w.y; v[i].z += w.z; v[i].w += w.w;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int j = (int)threadIdx.x + i * NTHREADS;
+    if (j >= nv) continue;
+    const float e4[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = 4 * j + q, r = e / lda, c = e - r * lda;
+      As[r * STR + c] = from_f32<T>(e4[q]);
+    }
+  }
+  // the tail that is not a whole float4 (rows * lda % 4), zero padding columns and rows >= rows
+  for (int e = 4 * nv + (int)threadIdx.x; e < rows * lda; e += NTHREADS) {
+    const int r = e / lda, c = e - r * lda;
+    As[r * STR + c] = from_f32<T>(base[e] + (add ? add[e] : 0.f));
+  }
+  const int padc = KC - lda;
+  for (int e = threadIdx.x; e < MT * padc; e += NTHREADS) {
+    const int r = e / padc, c = lda + e % padc;
+    As[r * STR + c] = from_f32<T>(0.f);
+  }
+  for (int e = threadIdx.x; e < (MT - rows) * lda; e += NTHREADS) {
+    const int r = rows + e / lda, c = e % lda;
+    As[r * STR + c] = from_f32<T>(0.f);
+  }
+}
+
 template <typename T, int MT, int PRO>
 __device__ __forceinline__ void store_a(const ARegs<T, MT, PRO>& R, const GemmArgs& a, T* As, int kc0) {
   constexpr int STR = KC + Tile<T>::PAD;
@@ -298,6 +350,9 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs a) {
     if (c > 0) __syncthreads();  // previous chunk's MFMAs are done with the LDS tiles
     if constexpr (PRO == PRO_T) {
       copy_tile<T, MT>(As, (const T*)a.A, a.lda, m0, a.M, c * KC, a.a_len, a.a_stride, a.a_off);
+    } else if (PRO == PRO_F32 && NCH == 1 && a.a_len == 0 && a.lda == a.k_valid && a.lda <= KC &&
+               ((size_t)m0 * a.lda) % 4 == 0) {
+      stage_f32_span<T, MT>(As, a, m0);
     } else {
       ARegs<T, MT, PRO> ra;
       load_a<T, MT, PRO>(ra, a, m0, c * KC);
