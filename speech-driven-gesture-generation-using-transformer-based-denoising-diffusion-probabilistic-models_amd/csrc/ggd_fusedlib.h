@@ -348,8 +348,8 @@ __device__ __forceinline__ ConvW conv_w(const float* w, const float* b, int c) {
 // dst rows (or transposed columns) i < 64 = conv over rows i-1, i, i+1 of the f32 source (row
 // stride ss, column c = tid & 31 of the thread; zero outside [0, rows)); rows >= `rows` are
 // written as zeros, so padded keys / values are finite
-template <typename T, bool TRANS, int NR = 64, int NT = NTHREADS>
-__device__ __forceinline__ void conv_rows(T* dst, int S, const float* src, int ss, int rows, ConvW w,
+template <typename T, bool TRANS, int NR = 64, int NT = NTHREADS, typename SRC = float>
+__device__ __forceinline__ void conv_rows(T* dst, int S, const SRC* src, int ss, int rows, ConvW w,
                                           int tid = ltid()) {
   constexpr int RS = NT / 32, NK = NR / RS;  // row stride between a thread's rows, rows per thread
   static_assert(NR % RS == 0, "rows must split over the thread groups");
@@ -358,9 +358,9 @@ __device__ __forceinline__ void conv_rows(T* dst, int S, const float* src, int s
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const int i = i0 + RS * k;
-    p0[k] = src[min(max(i - 1, 0), rows - 1) * ss + c];
-    p1[k] = src[min(i, rows - 1) * ss + c];
-    p2[k] = src[min(i + 1, rows - 1) * ss + c];
+    p0[k] = to_f32<SRC>(src[min(max(i - 1, 0), rows - 1) * ss + c]);
+    p1[k] = to_f32<SRC>(src[min(i, rows - 1) * ss + c]);
+    p2[k] = to_f32<SRC>(src[min(i + 1, rows - 1) * ss + c]);
   }
 #pragma unroll
   for (int k = 0; k < NK; ++k) {

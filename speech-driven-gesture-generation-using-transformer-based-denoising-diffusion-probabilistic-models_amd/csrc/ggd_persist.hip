@@ -311,9 +311,9 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
         f32x4 acc[RT][2];
         zero_acc(acc);
         pmma<RT, 2, 8>(acc, Ob, SX, 0, fa, lane);
-        if (wave < 2) {  // fa <- cross-attn Q of head 0 (waves 0, 1 only)
-          const int tq[1] = {wave};
-          pload<1, 8>(fa, w.q_ca, 8, tq, 0, lane);
+        {  // fa <- cross-attn Q of every head: wave w owns head w's two column tiles
+          const int tq[2] = {2 * wave, 2 * wave + 1};
+          pload<2, 8>(fa, w.q_ca, 8, tq, 0, lane);
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -350,36 +350,37 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
       };
       static_assert(2 * FLK * 8 == 2 * PK_THREADS, "two 16-byte memory pieces per thread");
       float4 kv0 = kv_load(0, 0), kv1 = kv_load(0, 1);
+      // the cross-attention queries of all 8 heads in one GEMM (wave w: head w's 32 columns), kept
+      // pre-conv in bf16 in the Xn image once every wave is done reading Xn
+      T* Yqb = Xn;
+      {
+        const float bq0 = w.q_ca_b[(2 * wave) * 16 + c16], bq1 = w.q_ca_b[(2 * wave + 1) * 16 + c16];
+        f32x4 acc[RT][2];
+        zero_acc(acc);
+        pmma<RT, 2, 8>(acc, Xn, SX, 0, fa, lane);
+        {  // fa <- the CA out-projection
+          const int to[2] = {2 * wave, 2 * wave + 1};
+          pload<2, 8>(fa, w.o_ca, 8, to, 0, lane);
+        }
+        bar_lds();
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = (2 * wave + j) * 16 + c16;
+          const float bias = j == 0 ? bq0 : bq1;
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Yqb[(rt * 16 + 4 * g4 + r) * SX + col] = from_f32<T>(acc[rt][j][r] + bias);
+        }
+      }
       for (int hd = 0; hd < 8; ++hd) {
         LANE_IDS();
         FSTAMP(6);
-        const float bqc = w.q_ca_b[hd * FDK + (wave & 1) * 16 + c16];
         const ConvW dq = conv_w(w.ca_qw, w.ca_qb, tid & 31), dk = conv_w(w.ca_kw, w.ca_kb, tid & 31),
                     dv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
         if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         FSTAMP(14);
-        {
-          f32x4 acc[RT][1];
-          zero_acc(acc);
-          if (wave < 2) pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
-          FSTAMP(15);
-          if (hd < 7) {
-            if (wave < 2) {
-              const int tq[1] = {2 * (hd + 1) + wave};
-              pload<1, 8>(fa, w.q_ca, 8, tq, 0, lane);
-            }
-          } else {  // fa <- the CA out-projection
-            const int to[2] = {2 * wave, 2 * wave + 1};
-            pload<2, 8>(fa, w.o_ca, 8, to, 0, lane);
-          }
-          if (wave < 2) {
-            const int col = (wave & 1) * 16 + c16;
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) Yq[(rt * 16 + 4 * g4 + r) * SYQ + col] = acc[rt][0][r] + bqc;
-          }
-        }
+        FSTAMP(15);
         FSTAMP(7);
         kv_store(0, kv0);
         kv_store(1, kv1);
@@ -391,7 +392,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
         FSTAMP(9);
         bar_lds();
         FSTAMP(10);
-        conv_rows<T, false, R, NT>((T*)(att_ca + AT::OQ), AT::SQ, Yq, SYQ, L, dq, tid);
+        conv_rows<T, false, R, NT, T>((T*)(att_ca + AT::OQ), AT::SQ, Yqb + hd * FDK, SX, L, dq, tid);
         conv_rows<T, false, FLK, NT>((T*)(att_ca + AT::OK), AT::SQ, raw, FDK, Lk, dk, tid);
         conv_rows<T, true, FLK, NT>((T*)(att_ca + AT::OV), AT::SV, raw + (FLK + 2) * FDK, FDK, Lk, dv, tid);
         FSTAMP(11);
