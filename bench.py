@@ -71,25 +71,26 @@ WORKLOADS = {
 
 
 # HBM-side bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of
-# this same command (scripts/pmc.sh + pmc_summary.py: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950
-# correction of MI355X_MICROARCH.md); PMC cannot run inside the timed region, so the figure is
-# the profile's, keyed by kernel symbol and workload
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01i_pmc_summary.json")
+# this same command (scripts/pmc_all.sh -> scripts/pmc.sh + pmc_summary.py: 2 x FETCH_SIZE +
+# WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), one summary per workload; PMC cannot
+# run inside the timed region, so the figure is the profile's, keyed by kernel symbol and workload
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01n_pmc_{workload}_summary.json")
 
 
 def pmc_traffic(kernel_prefix, workload):
+    path = PMC_SUMMARY.format(workload=workload)
     try:
-        with open(PMC_SUMMARY) as f:
+        with open(path) as f:
             d = json.load(f)
     except OSError:
         return None
-    if d.get("_workload", "c2") != workload:
+    if d.get("_workload") != workload:
         return None
     for k, e in d.items():
         if k.startswith("void ggd::" + kernel_prefix) and "hbm_read_bytes" in e and "hbm_write_bytes" in e:
             return {"bytes_per_launch": e["hbm_read_bytes"] + e["hbm_write_bytes"],
                     "read": e["hbm_read_bytes"], "write": e["hbm_write_bytes"],
-                    "source": os.path.relpath(PMC_SUMMARY, ROOT)}
+                    "source": os.path.relpath(path, ROOT)}
     return None
 
 
@@ -287,7 +288,8 @@ def main():
             kernel = f"kb_kernel<{args.dtype}> (SA out-proj + LN2 + cross-attn Q + conv + cross-attention)"
             timing = "device realtime-clock span of every KB launch of the last timed pass"
         ach = flop / (avg_us * 1e-6) / 1e12
-        tr = pmc_traffic({1: "mk_kernel", 2: "gemm_kernel<unsigned short, 64, 1, 1", 3: "psk_kernel"}.get(prof_kind, "kb_kernel"),
+        tr = pmc_traffic({1: "mk_kernel", 2: "gemm_kernel<unsigned short, 64, 1, 1, 1, true>", 3: "psk_kernel"}.get(
+            prof_kind, "kb_kernel"),
                          args.workload)
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 6), "traffic": tr and tr["bytes_per_launch"], "traffic_detail": tr, "kernel": kernel, "timing": timing,
