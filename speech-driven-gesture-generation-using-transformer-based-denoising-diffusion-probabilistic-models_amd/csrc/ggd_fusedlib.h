@@ -9,6 +9,10 @@
 namespace ggd {
 
 constexpr int FD = 256, FDK = 32, FR = 64, FRT = 4, FLK = 64;  // d_model, d_k, rows, row tiles, max keys
+#ifndef GGD_SCHED_FENCE
+#define GGD_SCHED_FENCE 1
+#endif
+constexpr bool SCHED_FENCE = GGD_SCHED_FENCE != 0;  // A/B switch of the GEMM read/MFMA ordering fence
 constexpr int SH = FD + 4;                                     // f32 residual image row stride
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -246,6 +250,9 @@ struct WGemm {
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) nxt[rt] = *(const bf16x8*)(a0 + rt * 16 * SA + (k + 1) * 32);
         }
+        // keep step k + 1's LDS reads ahead of step k's MFMAs: left alone, the scheduler (under
+        // register pressure) sinks each read next to its MFMA and exposes the LDS latency per step
+        if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -253,6 +260,7 @@ struct WGemm {
             if (j < nj_on)
               acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[rt], __builtin_bit_cast(bf16x8, wb[j][k]),
                                                                    acc[rt][j], 0, 0, 0);
+        if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
         if (k + 1 < KT) {
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) cur[rt] = nxt[rt];

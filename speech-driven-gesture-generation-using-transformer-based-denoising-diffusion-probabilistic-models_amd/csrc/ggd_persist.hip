@@ -80,6 +80,7 @@ __device__ __forceinline__ void pmma_n(f32x4 (&acc)[RT][NJ], const bf16_t* A, in
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) nxt[rt] = *(const bf16x8*)(a0 + rt * 16 * SA + (s + 1) * 32);
     }
+    if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);  // reads of s + 1 stay ahead (WGemm::run)
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -87,6 +88,7 @@ __device__ __forceinline__ void pmma_n(f32x4 (&acc)[RT][NJ], const bf16_t* A, in
         if (j < nj)
           acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[rt], __builtin_bit_cast(bf16x8, f[j * KS + s]),
                                                                acc[rt][j], 0, 0, 0);
+    if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
     if (s + 1 < KS) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) cur[rt] = nxt[rt];
