@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -375,11 +376,139 @@ __global__ void __launch_bounds__(256) enc_head_fc_kernel(const float* __restric
 
 inline unsigned blocks_for(size_t n, int tpb) { return (unsigned)((n + tpb - 1) / tpb); }
 
+// ------------------------------------------------------------------------------------------
+// LDS-tiled implicit-GEMM convolution (bf16 contexts): a workgroup owns a TH x TW block of
+// output pixels of ONE image (128 pixels = 4 waves x 2 row tiles of 16) and NJ x 16 output
+// channels.  Per 32-channel input chunk it stages, once, the input patch the block's taps touch
+// ((TH-1)s+KH rows x (TW-1)s+KW columns, bf16, zeros outside the image) and the chunk's filter
+// taps (NJ*16 x KH*KW x 32 bf16); every tap's A fragment is then an LDS read of the shifted
+// patch position.  enc_conv_kernel fetches each input value from L1/L2 once per tap and each
+// filter fragment once per wave; here both are fetched once per workgroup and chunk.  The
+// accumulation order of an output element is fixed (chunk, tap, 32 channels): batch-invariant.
+// ------------------------------------------------------------------------------------------
+// diagnostics: GGD_ENC_CONV_DIRECT=1 routes bf16 contexts back to enc_conv_kernel (A/B timing)
+static const bool conv_no_lds = std::getenv("GGD_ENC_CONV_DIRECT") != nullptr;
+constexpr int CL_PX = 128;     // output pixels per workgroup
+constexpr int CL_CS = 32 + 8;  // bf16 stride of one patch position / one filter tap in LDS
+
+struct ConvLdsGeom {
+  int TW, TH, PH, PW, taps;
+  size_t patch_bytes, w_bytes;
+};
+__host__ __device__ inline ConvLdsGeom conv_lds_geom(const ConvArgs& a, int TW, int NJ) {
+  ConvLdsGeom g;
+  g.TW = TW;
+  g.TH = CL_PX / TW;
+  g.PH = (g.TH - 1) * a.stride + a.KH;
+  g.PW = (g.TW - 1) * a.stride + a.KW;
+  g.taps = a.KH * a.KW;
+  g.patch_bytes = (size_t)g.PH * g.PW * CL_CS * 2;
+  g.w_bytes = (size_t)NJ * 16 * g.taps * CL_CS * 2;
+  return g;
+}
+
+template <int NJ>
+__global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int TW) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const ConvLdsGeom G = conv_lds_geom(a, TW, NJ);
+  bf16_t* patch = (bf16_t*)smem;
+  bf16_t* wl = (bf16_t*)(smem + G.patch_bytes);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  const int tw_n = (a.Wo + G.TW - 1) / G.TW, th_n = (a.Ho + G.TH - 1) / G.TH, per = tw_n * th_n;
+  const int b = blockIdx.x / per, tix = blockIdx.x - b * per;
+  const int oh0 = (tix / tw_n) * G.TH, ow0 = (tix - (tix / tw_n) * tw_n) * G.TW, n0 = blockIdx.y * (NJ * 16);
+  const int ih0 = oh0 * a.stride - a.pad, iw0 = ow0 * a.stride - a.pad;
+  int pbase[2];  // patch position of tap (0, 0) for this lane's A pixels (row tiles 0, 1)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wave * 32 + i * 16 + r16, ty = q / G.TW, tx = q - ty * G.TW;
+    pbase[i] = ty * a.stride * G.PW + tx * a.stride;
+  }
+  f32x4 acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16_t* W = (const bf16_t*)a.w;
+  const int cch = a.Cin >> 5, npos = G.PH * G.PW;
+  for (int ck = 0; ck < cch; ++ck) {
+    if (ck > 0) __syncthreads();  // the previous chunk's MFMAs are done with the LDS images
+    for (int v = tid; v < npos * 8; v += CONV_TPB) {  // patch: 8 x 4 channels per position
+      const int pos = v >> 3, q4 = v & 7, py = pos / G.PW, px = pos - py * G.PW;
+      const int ih = ih0 + py, iw = iw0 + px;
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
+        x = *(const float4*)(a.in + (((size_t)b * a.H + ih) * a.W + iw) * a.Cin + ck * 32 + q4 * 4);
+      const uint32_t lo = (uint32_t)f2bf(x.x) | ((uint32_t)f2bf(x.y) << 16);
+      const uint32_t hi = (uint32_t)f2bf(x.z) | ((uint32_t)f2bf(x.w) << 16);
+      *(uint2*)(patch + pos * CL_CS + q4 * 4) = make_uint2(lo, hi);
+    }
+    for (int v = tid; v < NJ * 16 * G.taps * 4; v += CONV_TPB) {  // filter taps: 4 x 8 channels
+      const int q8 = v & 3, nt = v >> 2, n = nt / G.taps, tap = nt - n * G.taps;
+      const uint4 u = *(const uint4*)(W + ((size_t)(n0 + n) * G.taps + tap) * a.Cin + ck * 32 + q8 * 8);
+      *(uint4*)(wl + (n * G.taps + tap) * CL_CS + q8 * 8) = u;
+    }
+    __syncthreads();
+    for (int tap = 0; tap < G.taps; ++tap) {
+      const int ky = tap / a.KW, kx = tap - ky * a.KW, toff = ky * G.PW + kx;
+      bf16x8 av[2], bv[NJ];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) av[i] = *(const bf16x8*)(patch + (pbase[i] + toff) * CL_CS + g * 8);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bv[j] = *(const bf16x8*)(wl + ((j * 16 + r16) * G.taps + tap) * CL_CS + g * 8);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue: C/D layout of the 16x16 MFMA -- column = lane & 15, row = 4 (lane >> 4) + r
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int co = n0 + j * 16 + r16;
+    const float bi = a.bias[co], sc = a.s[co], sh = a.t[co];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = wave * 32 + i * 16 + 4 * g + r, ty = q / G.TW, tx = q - ty * G.TW;
+        const int oh = oh0 + ty, ow = ow0 + tx;
+        if (oh >= a.Ho || ow >= a.Wo) continue;
+        const int p = (b * a.Ho + oh) * a.Wo + ow;
+        float v = acc[i][j][r];
+        v = a.mode == CONV_RELU_BN ? fmaxf(v + bi, 0.f) * sc + sh : (v + bi) * sc + sh;
+        if (a.layout == LAYOUT_NHWC) {
+          a.out[(size_t)p * a.Cout_pad + co] = v;
+        } else if (co < a.Cvalid) {
+          a.out[(((size_t)b * a.Wo + ow) * a.Cvalid + co) * a.Ho + oh] = v;
+        }
+      }
+  }
+}
+
 hipError_t launch_conv(int dtype, const ConvArgs& a, hipStream_t s) {
   const int P = a.N * a.Ho * a.Wo;
   const int nj = a.Cout_pad % 64 == 0 ? 4 : 2;
   if (a.Cin % 32 || a.Cout_pad % (nj * 16) || P <= 0) return hipErrorInvalidValue;
   const dim3 grid(blocks_for(P, 128), a.Cout_pad / (nj * 16));
+  if (dtype == GGD_BF16 && !conv_no_lds) {
+    const int TW = a.Wo >= 16 ? 16 : a.Wo >= 8 ? 8 : 4;
+    const ConvLdsGeom G = conv_lds_geom(a, TW, nj);
+    const size_t lds = G.patch_bytes + G.w_bytes;
+    if (lds <= 96 * 1024) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        attr = true;
+      }
+      const int blocks = a.N * ((a.Ho + G.TH - 1) / G.TH) * ((a.Wo + TW - 1) / TW);
+      const dim3 gl(blocks, a.Cout_pad / (nj * 16));
+      if (nj == 4) hipLaunchKernelGGL((enc_conv_lds_kernel<4>), gl, dim3(CONV_TPB), lds, s, a, TW);
+      else hipLaunchKernelGGL((enc_conv_lds_kernel<2>), gl, dim3(CONV_TPB), lds, s, a, TW);
+      return hipGetLastError();
+    }
+  }
   if (dtype == GGD_BF16) {
     if (nj == 4) hipLaunchKernelGGL((enc_conv_kernel<bf16_t, 4>), grid, dim3(CONV_TPB), 0, s, a);
     else hipLaunchKernelGGL((enc_conv_kernel<bf16_t, 2>), grid, dim3(CONV_TPB), 0, s, a);
