@@ -179,7 +179,7 @@ int ggd_profile_kind(ggd_ctx* ctx);
  * timeouts; scripts/handoff_bench.py); what = 6: as
  * 4 with in-kernel phase stamps (avg_us[0..7] = phase ends in us); what = 7: p = {0} forces the
  * one-workgroup-per-clip loop (psk_kernel), {1} never uses it, {2} automatic (the default: used when
- * the clip-group loop would need >= 4 chunks); returns 1 in *avg_us when psk_kernel is available; what = 8: persistent-kernel phase stamps of
+ * the clip-group loop would need >= 3 chunks); returns 1 in *avg_us when psk_kernel is available; what = 8: persistent-kernel phase stamps of
  * iteration 0, p = {1} arm, {2} read (avg_us[0..7]), {0} disarm; what = 9: p = {1} routes
  * ggd_sample through the per-phase launches instead of the persistent loop (ggd_mega.hip), {0}
  * back (returns the loop's clip capacity in *avg_us). */

@@ -87,8 +87,8 @@ struct ggd_ctx {
   void* arena = nullptr;     // current device arena (dalloc) and its fill level
   size_t arena_off = 0;
   int persist_mode = 0;      // ggd_diag what=7: 0 auto, 1 never, 2 always the one-workgroup-per-clip loop.
-                             // Auto: when the clip-group loop would need >= 4 chunks (measured on MI355X,
-                             // scripts/route_compare.py: 385 us/step for any n <= 256 vs 113 us per
+                             // Auto: when the clip-group loop would need >= 3 chunks (measured on MI355X,
+                             // scripts/route_compare.py: 314 us/step for any n <= 256 vs 113 us per
                              // 32-clip chunk)
   unsigned long long* stamps = nullptr;  // ggd_diag what=8: phase stamps of the persistent kernel
   float *out_ln_g = nullptr, *out_ln_b = nullptr;
@@ -1636,7 +1636,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   bool use_persist = c->persist && c->persist_mode != 1;
   if (use_persist && c->persist_mode == 0) {
     const int cap = c->no_mega ? 0 : mega_capacity(D.dtype, D.seq_len);
-    use_persist = cap <= 0 || (a->n + cap - 1) / cap >= 4;
+    use_persist = cap <= 0 || (a->n + cap - 1) / cap >= 3;
   }
   if (use_persist) {
     // ONE launch: a workgroup per clip runs all nsteps iterations (ggd_persist.hip); in

@@ -38,7 +38,14 @@ template <int RT> struct PPlan {
   static constexpr size_t RAW = al16(sizeof(float) * 2 * (FLK + 2) * FDK);
   static constexpr size_t HID = al16(sizeof(bf16_t) * R * SHD);
   static constexpr size_t E = al16(sizeof(float) * R * SE);
-  static constexpr size_t SCR = std::max(std::max(Y + ATT, YQ + RAW + ATT), std::max(HID, E + HID));
+  // attention of a head PAIR at once: two attention images, the second overlaying the first's
+  // 4th P tile (query row tile 3 is always past L <= 48, its wave never touches it)
+  static constexpr int SYB = 192 + 8;                // bf16 pre-conv QKV of a head pair
+  static constexpr size_t YB = al16(sizeof(bf16_t) * R * SYB);
+  static constexpr size_t ATT_B = FAtt<bf16_t, R>::BYTES - sizeof(bf16_t) * 16 * FAtt<bf16_t, R>::SP;
+  static constexpr size_t ATT2 = ATT_B + ATT;
+  static constexpr size_t RAWB = sizeof(bf16_t) * 2 * 2 * FLK * FDK;  // bf16 memory K|V of a head pair
+  static constexpr size_t SCR = std::max(std::max(YB + ATT2, RAWB + ATT2), std::max(HID, E + HID));
   static constexpr size_t OFF_XN = HS, OFF_O = HS + IMG, OFF_ST = HS + 2 * IMG, OFF_S = OFF_ST + ST;
   static constexpr size_t TOTAL = OFF_S + SCR;
 };
@@ -156,11 +163,10 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
   T* Ob = (T*)(smem + PL::OFF_O);
   float2* st = (float2*)(smem + PL::OFF_ST);
   unsigned char* scr = smem + PL::OFF_S;
-  float* Y = (float*)scr;                       // self-attention: QKV of a head pair
-  unsigned char* att_sa = scr + PL::Y;
-  float* Yq = (float*)scr;                      // cross-attention: Q of a head, raw memory K/V
-  float* raw = (float*)(scr + PL::YQ);
-  unsigned char* att_ca = scr + PL::YQ + PL::RAW;
+  T* Yb = (T*)scr;                              // self-attention: bf16 QKV (pre-conv) of a head pair
+  unsigned char* att_sa = scr + PL::YB;         // two attention images (head pair)
+  T* rawb = (T*)scr;                            // cross-attention: bf16 memory K|V of a head pair
+  unsigned char* att_ca = scr + PL::RAWB;
   T* Hd = (T*)scr;                              // FFN chunk
   float* E = (float*)scr;                       // eps (out projection)
   T* Xb = (T*)(scr + PL::E);                    // emb operand
@@ -291,18 +297,20 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-              for (int r = 0; r < 4; ++r) Y[(rt * 16 + 4 * g4 + r) * SY + col] = acc[rt][j][r] + bias;
+              for (int r = 0; r < 4; ++r) Yb[(rt * 16 + 4 * g4 + r) * PL::SYB + col] = from_f32<T>(acc[rt][j][r] + bias);
           }
         }
         bar_lds();
-        for (int hh = 0; hh < 2; ++hh) {
+        {  // both heads of the pair at once: threads 0-255 head 2hp, 256-511 head 2hp + 1
           LANE_IDS();
-          const float* Yh = Y + hh * 96;
-          conv_rows<T, false, R, NT>((T*)(att_sa + AT::OQ), AT::SQ, Yh, SY, L, cq, tid);
-          conv_rows<T, false, FLK, NT>((T*)(att_sa + AT::OK), AT::SQ, Yh + 32, SY, L, ck, tid);
-          conv_rows<T, true, FLK, NT>((T*)(att_sa + AT::OV), AT::SV, Yh + 64, SY, L, cv, tid);
+          const int hh = tid >> 8, t2 = tid & 255;
+          unsigned char* at = att_sa + hh * PL::ATT_B;
+          const T* Yh = Yb + hh * 96;
+          conv_rows<T, false, R, NT / 2, T>((T*)(at + AT::OQ), AT::SQ, Yh, PL::SYB, L, cq, t2);
+          conv_rows<T, false, FLK, NT / 2, T>((T*)(at + AT::OK), AT::SQ, Yh + 32, PL::SYB, L, ck, t2);
+          conv_rows<T, true, FLK, NT / 2, T>((T*)(at + AT::OV), AT::SV, Yh + 64, PL::SYB, L, cv, t2);
           bar_lds();
-          fattn_lds<R>(att_sa, L, L, a.scale, Ob + (2 * hp + hh) * FDK, SX, tid);
+          fattn_lds<R>(at, L, L, a.scale, Ob + (2 * hp + hh) * FDK, SX, t2);
           bar_lds();
         }
       }
@@ -346,12 +354,15 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
         const float* src = r == 0 ? w.kv_step + (size_t)t * 2 * FD : w.kv_mem + ((size_t)b * a.Ts + (r - 1)) * 2 * FD;
         return *(const float4*)(src + half * FD + hd * FDK + q * 4);
       };
-      auto kv_store = [&](int i, float4 val) {
+      // bf16 raw K|V of pair member hh: [half][FLK rows][FDK]
+      auto kv_store = [&](int hh, int i, float4 val) {
         const int v = tid + i * NT, r = v >> 4, half = (v >> 3) & 1, q = v & 7;
-        if (r < Lk) *(float4*)(raw + half * (FLK + 2) * FDK + r * FDK + q * 4) = val;
+        const uint32_t lo = (uint32_t)f2bf(val.x) | ((uint32_t)f2bf(val.y) << 16);
+        const uint32_t hi = (uint32_t)f2bf(val.z) | ((uint32_t)f2bf(val.w) << 16);
+        if (r < Lk) *(uint2*)(rawb + ((hh * 2 + half) * FLK + r) * FDK + q * 4) = make_uint2(lo, hi);
       };
       static_assert(2 * FLK * 8 == 2 * PK_THREADS, "two 16-byte memory pieces per thread");
-      float4 kv0 = kv_load(0, 0), kv1 = kv_load(0, 1);
+      float4 kv0 = kv_load(0, 0), kv1 = kv_load(0, 1), kv2 = kv_load(1, 0), kv3 = kv_load(1, 1);
       // the cross-attention queries of all 8 heads in one GEMM (wave w: head w's 32 columns), kept
       // pre-conv in bf16 in the Xn image once every wave is done reading Xn
       T* Yqb = Xn;
@@ -375,33 +386,31 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
             for (int r = 0; r < 4; ++r) Yqb[(rt * 16 + 4 * g4 + r) * SX + col] = from_f32<T>(acc[rt][j][r] + bias);
         }
       }
-      for (int hd = 0; hd < 8; ++hd) {
+      // head pairs: both heads' conv and attention at once (threads 0-255 head 2hp, 256-511 head
+      // 2hp + 1); the next pair's memory K|V loads fly under this pair's work
+      for (int hp = 0; hp < 4; ++hp) {
         LANE_IDS();
-        FSTAMP(6);
         const ConvW dq = conv_w(w.ca_qw, w.ca_qb, tid & 31), dk = conv_w(w.ca_kw, w.ca_kb, tid & 31),
                     dv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
-        if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        FSTAMP(14);
-        FSTAMP(15);
-        FSTAMP(7);
-        kv_store(0, kv0);
-        kv_store(1, kv1);
-        FSTAMP(8);
-        if (hd < 7) {
-          kv0 = kv_load(hd + 1, 0);
-          kv1 = kv_load(hd + 1, 1);
+        kv_store(0, 0, kv0);
+        kv_store(0, 1, kv1);
+        kv_store(1, 0, kv2);
+        kv_store(1, 1, kv3);
+        if (hp < 3) {
+          kv0 = kv_load(2 * hp + 2, 0);
+          kv1 = kv_load(2 * hp + 2, 1);
+          kv2 = kv_load(2 * hp + 3, 0);
+          kv3 = kv_load(2 * hp + 3, 1);
         }
-        FSTAMP(9);
         bar_lds();
-        FSTAMP(10);
-        conv_rows<T, false, R, NT, T>((T*)(att_ca + AT::OQ), AT::SQ, Yqb + hd * FDK, SX, L, dq, tid);
-        conv_rows<T, false, FLK, NT>((T*)(att_ca + AT::OK), AT::SQ, raw, FDK, Lk, dk, tid);
-        conv_rows<T, true, FLK, NT>((T*)(att_ca + AT::OV), AT::SV, raw + (FLK + 2) * FDK, FDK, Lk, dv, tid);
-        FSTAMP(11);
+        const int hh = tid >> 8, t2 = tid & 255, hd = 2 * hp + hh;
+        unsigned char* at = att_ca + hh * PL::ATT_B;
+        const T* rk = rawb + hh * 2 * FLK * FDK;
+        conv_rows<T, false, R, NT / 2, T>((T*)(at + AT::OQ), AT::SQ, Yqb + hd * FDK, SX, L, dq, t2);
+        conv_rows<T, false, FLK, NT / 2, T>((T*)(at + AT::OK), AT::SQ, rk, FDK, Lk, dk, t2);
+        conv_rows<T, true, FLK, NT / 2, T>((T*)(at + AT::OV), AT::SV, rk + FLK * FDK, FDK, Lk, dv, t2);
         bar_lds();
-        FSTAMP(12);
-        fattn_lds<R>(att_ca, L, Lk, a.scale, Ob + hd * FDK, SX, tid);
-        FSTAMP(13);
+        fattn_lds<R>(at, L, Lk, a.scale, Ob + hd * FDK, SX, t2);
         bar_lds();
       }
       PSTAMP(3);

@@ -373,7 +373,7 @@ def test_inpaint_model_generate_sample_f32(pkg, setup_inp):
 
 # ------------------------------------------------------------------------------------------
 # Route selection of ggd_sample (bf16): the one-workgroup-per-clip loop (psk_kernel) is chosen
-# automatically when the clip-group loop (mk_kernel) would need >= 4 chunks (the C5 shape,
+# automatically when the clip-group loop (mk_kernel) would need >= 3 chunks (the C5 shape,
 # 128 clips per GPU); both must agree with the oracle and with each other.
 # ------------------------------------------------------------------------------------------
 def _route(ctx, mode):
