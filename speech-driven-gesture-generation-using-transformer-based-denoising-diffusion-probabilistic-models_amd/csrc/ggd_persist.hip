@@ -468,6 +468,9 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
             const int to[1] = {wave};
             pload<1, 8>(fa, a.w_out, 8, to, 0, lane);
           }
+          // the chunk image is double-buffered: chunk c + 1 writes the other buffer, so no barrier
+          // is needed behind the FFN-down MFMAs (the next chunk's barrier orders the reuse)
+          T* Hc = Hd + (c & 1) * (PL::HID / sizeof(T));
           {
             const int col = (8 * c + wave) * 16 + c16 - 128 * c;  // column inside the chunk
 #pragma unroll
@@ -475,11 +478,11 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float v = fmaxf(acc[rt][0][r] + bf, 0.f);
-                Hd[(rt * 16 + 4 * g4 + r) * SHD + col] = from_f32<T>(v * v);
+                Hc[(rt * 16 + 4 * g4 + r) * SHD + col] = from_f32<T>(v * v);
               }
           }
           bar_lds();
-          pmma<RT, 2, 4>(accd, Hd, SHD, 0, fb, lane);
+          pmma<RT, 2, 4>(accd, Hc, SHD, 0, fb, lane);
           {
             const int td[2] = {2 * wave, 2 * wave + 1};
             if (c < 7)
@@ -489,8 +492,8 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
             else             // fb <- the next step's emb fragments
               pload<2, 4>(fb, a.w_emb, 4, td, 0, lane);
           }
-          bar_lds();
         }
+        static_assert(2 * PL::HID <= PL::SCR, "double-buffered FFN chunk image");
         const float b20 = w.ff2_b[(2 * wave) * 16 + c16], b21 = w.ff2_b[(2 * wave + 1) * 16 + c16];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
