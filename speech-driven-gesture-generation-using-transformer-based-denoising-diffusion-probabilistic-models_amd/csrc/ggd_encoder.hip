@@ -390,6 +390,9 @@ inline unsigned blocks_for(size_t n, int tpb) { return (unsigned)((n + tpb - 1) 
 static const bool conv_no_lds = std::getenv("GGD_ENC_CONV_DIRECT") != nullptr;
 constexpr int CL_PX = 128;     // output pixels per workgroup
 constexpr int CL_CS = 32 + 8;  // bf16 stride of one patch position / one filter tap in LDS
+constexpr int CL_PMAX = 18;    // patch float4 per thread (npos * 8 <= 18 * 256: 3x3 stride 2, 16-wide tiles)
+constexpr int CL_PMIN = 8;     // ... for the stride-1 shapes (npos <= 256)
+constexpr int CL_TAPS_MAX = 9;
 
 struct ConvLdsGeom {
   int TW, TH, PH, PW, taps;
@@ -407,7 +410,7 @@ __host__ __device__ inline ConvLdsGeom conv_lds_geom(const ConvArgs& a, int TW, 
   return g;
 }
 
-template <int NJ>
+template <int NJ, int PM>
 __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int TW) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const ConvLdsGeom G = conv_lds_geom(a, TW, NJ);
@@ -431,24 +434,62 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int 
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bf16_t* W = (const bf16_t*)a.w;
   const int cch = a.Cin >> 5, npos = G.PH * G.PW;
+  // the next chunk's patch and filter taps are fetched into registers while this chunk's MFMAs
+  // run (PM / WMAX pieces per thread bound them; launch_conv checks the shape fits)
+  constexpr int WMAX = (NJ * 16 * CL_TAPS_MAX * 4 + CONV_TPB - 1) / CONV_TPB;
+  const int np8 = npos * 8, nw = NJ * 16 * G.taps * 4;
+  f32x4 xr[PM];
+  bf16x8 wr[WMAX];  // native vectors (HIP's uint4 struct copies keep the array in scratch)
+  uint32_t okm = 0;  // bit k: patch piece k lies inside the image (else it stages as zero)
+  auto fetch = [&](int ck) __attribute__((always_inline)) {
+    okm = 0;
+#pragma unroll
+    for (int k = 0; k < PM; ++k) {
+      const int v = tid + k * CONV_TPB;
+      {
+        const int vc = min(v, np8 - 1);
+        const int pos = vc >> 3, q4 = vc & 7, py = pos / G.PW, px = pos - py * G.PW;
+        const int ih = ih0 + py, iw = iw0 + px;
+        const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+        const int ihc = min(max(ih, 0), a.H - 1), iwc = min(max(iw, 0), a.W - 1);
+        xr[k] = *(const f32x4*)(a.in + (((size_t)b * a.H + ihc) * a.W + iwc) * a.Cin + ck * 32 + q4 * 4);
+        okm |= (ok && v < np8) ? (1u << k) : 0u;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WMAX; ++k) {
+      const int v = min(tid + k * CONV_TPB, nw - 1);  // clamped: every wr[k] is defined (no scratch)
+      const int q8 = v & 3, nt = v >> 2, n = nt / G.taps, tap = nt - n * G.taps;
+      wr[k] = *(const bf16x8*)(W + ((size_t)(n0 + n) * G.taps + tap) * a.Cin + ck * 32 + q8 * 8);
+    }
+  };
+  auto put = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < PM; ++k) {
+      const int v = tid + k * CONV_TPB;
+      if (v < np8) {
+        const int pos = v >> 3, q4 = v & 7;
+        const bool ok = (okm >> k) & 1u;
+        const uint32_t lo = (uint32_t)f2bf(xr[k].x) | ((uint32_t)f2bf(xr[k].y) << 16);
+        const uint32_t hi = (uint32_t)f2bf(xr[k].z) | ((uint32_t)f2bf(xr[k].w) << 16);
+        *(uint2*)(patch + pos * CL_CS + q4 * 4) = ok ? make_uint2(lo, hi) : make_uint2(0u, 0u);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WMAX; ++k) {
+      const int v = tid + k * CONV_TPB;
+      if (v < nw) {
+        const int q8 = v & 3, nt = v >> 2, n = nt / G.taps, tap = nt - n * G.taps;
+        *(bf16x8*)(wl + (n * G.taps + tap) * CL_CS + q8 * 8) = wr[k];
+      }
+    }
+  };
+  fetch(0);
   for (int ck = 0; ck < cch; ++ck) {
     if (ck > 0) __syncthreads();  // the previous chunk's MFMAs are done with the LDS images
-    for (int v = tid; v < npos * 8; v += CONV_TPB) {  // patch: 8 x 4 channels per position
-      const int pos = v >> 3, q4 = v & 7, py = pos / G.PW, px = pos - py * G.PW;
-      const int ih = ih0 + py, iw = iw0 + px;
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-        x = *(const float4*)(a.in + (((size_t)b * a.H + ih) * a.W + iw) * a.Cin + ck * 32 + q4 * 4);
-      const uint32_t lo = (uint32_t)f2bf(x.x) | ((uint32_t)f2bf(x.y) << 16);
-      const uint32_t hi = (uint32_t)f2bf(x.z) | ((uint32_t)f2bf(x.w) << 16);
-      *(uint2*)(patch + pos * CL_CS + q4 * 4) = make_uint2(lo, hi);
-    }
-    for (int v = tid; v < NJ * 16 * G.taps * 4; v += CONV_TPB) {  // filter taps: 4 x 8 channels
-      const int q8 = v & 3, nt = v >> 2, n = nt / G.taps, tap = nt - n * G.taps;
-      const uint4 u = *(const uint4*)(W + ((size_t)(n0 + n) * G.taps + tap) * a.Cin + ck * 32 + q8 * 8);
-      *(uint4*)(wl + (n * G.taps + tap) * CL_CS + q8 * 8) = u;
-    }
+    put();
     __syncthreads();
+    if (ck + 1 < cch) fetch(ck + 1);
     for (int tap = 0; tap < G.taps; ++tap) {
       const int ky = tap / a.KW, kx = tap - ky * a.KW, toff = ky * G.PW + kx;
       bf16x8 av[2], bv[NJ];
@@ -495,17 +536,22 @@ hipError_t launch_conv(int dtype, const ConvArgs& a, hipStream_t s) {
     const int TW = a.Wo >= 16 ? 16 : a.Wo >= 8 ? 8 : 4;
     const ConvLdsGeom G = conv_lds_geom(a, TW, nj);
     const size_t lds = G.patch_bytes + G.w_bytes;
-    if (lds <= 96 * 1024) {
+    if (lds <= 96 * 1024 && G.PH * G.PW * 8 <= CL_PMAX * CONV_TPB && G.taps <= CL_TAPS_MAX) {
       static bool attr = false;
       if (!attr) {
-        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<4, CL_PMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<2, CL_PMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<4, CL_PMIN>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<2, CL_PMIN>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         attr = true;
       }
       const int blocks = a.N * ((a.Ho + G.TH - 1) / G.TH) * ((a.Wo + TW - 1) / TW);
       const dim3 gl(blocks, a.Cout_pad / (nj * 16));
-      if (nj == 4) hipLaunchKernelGGL((enc_conv_lds_kernel<4>), gl, dim3(CONV_TPB), lds, s, a, TW);
-      else hipLaunchKernelGGL((enc_conv_lds_kernel<2>), gl, dim3(CONV_TPB), lds, s, a, TW);
+      const bool small = G.PH * G.PW * 8 <= CL_PMIN * CONV_TPB;
+      if (nj == 4 && small) hipLaunchKernelGGL((enc_conv_lds_kernel<4, CL_PMIN>), gl, dim3(CONV_TPB), lds, s, a, TW);
+      else if (nj == 4) hipLaunchKernelGGL((enc_conv_lds_kernel<4, CL_PMAX>), gl, dim3(CONV_TPB), lds, s, a, TW);
+      else if (small) hipLaunchKernelGGL((enc_conv_lds_kernel<2, CL_PMIN>), gl, dim3(CONV_TPB), lds, s, a, TW);
+      else hipLaunchKernelGGL((enc_conv_lds_kernel<2, CL_PMAX>), gl, dim3(CONV_TPB), lds, s, a, TW);
       return hipGetLastError();
     }
   }
