@@ -80,6 +80,24 @@ class Generator:
         return self.tensor2dtype(sample, return_dtype)
 
     @th.no_grad()
+    def generate_batches(self, shape: Tuple[int], wav_batches, sample_alg: str = "ddim",
+                         device: str = "cuda", **kw):
+        """generate_sample over independent clip batches, back to back -> list of (N, L, C).
+
+        Serving form of generator.py:218-296 for a queue of batches: batch k+1's speech encoder
+        is issued on a side HIP stream (model.prefetch_speech) before batch k's reverse loop, so
+        the two run at once; outputs equal per-batch generate_sample calls.
+        """
+        wav_batches = [w.to(device) for w in wav_batches]
+        outs = []
+        for k, wav in enumerate(wav_batches):
+            if k + 1 < len(wav_batches):
+                self.model.prefetch_speech(wav_batches[k + 1])
+            shp = (wav.shape[0],) + tuple(shape[1:])
+            outs.append(self.generate_sample(shp, wav, sample_alg=sample_alg, device=device, progress=False, **kw))
+        return outs
+
+    @th.no_grad()
     def generate_sequence(self, wav_seqs, wav_sr, pose_dim, pose_fps, pose_window_len, pose_seed_len,
                           return_dtype="tensor", smooth_trans=True, trans_factor=None, init_poses=None,
                           sample_alg="ddim", batch_size=64, device="cuda", progress=True, **kw):
