@@ -62,12 +62,15 @@ def kb_flop(n, L, Lk, d):
 # BASELINE.json configs as bench workloads (per GPU); C3 is C2 on 8 GPUs (--gpus 8)
 WORKLOADS = {
     "c2": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=1,
-               label="beat-ours C2"),
+               label="beat-ours C2", overlap=False),
     "c4": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=4, dtype="fp8",
-               label="beat-ours C4 long clip (seq_len x4)"),
+               label="beat-ours C4 long clip (seq_len x4)", overlap=False),
     "c5": dict(batch_per_gpu=128, alg="ddim", respacing="ddim50", seq_mult=1,
-               label="beat-ours C5 DDIM-50"),
+               label="beat-ours C5 DDIM-50", overlap=True),
 }
+# overlap: the next pass's speech encoder runs beside this pass's loop (model.prefetch_speech).
+# It pays where the loop leaves CUs idle (C5: psk_kernel, 128 workgroups on 256 CUs, 254.0k ->
+# 286.5k frames/s); C2/C4 loops fill the chip and measured the same or 0.6% slower with it.
 
 
 # HBM-side bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of
@@ -110,8 +113,8 @@ def parse():
     p.add_argument("--graph", action="store_true",
                    help="replay each denoise step as a captured hipGraph (measured slower than eager launches)")
     p.add_argument("--no-profile", action="store_true", help="skip the in-loop kernel events")
-    p.add_argument("--no-overlap", action="store_true",
-                   help="encode each pass's speech inline instead of under the previous pass's loop")
+    p.add_argument("--overlap", default=None, choices=["on", "off"],
+                   help="encode pass k+1's speech beside pass k's loop (default: per workload)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=None,
                    help="denoise steps of the CPU sample (default: ~10 s of oracle work, 40 steps at C2)")
@@ -235,7 +238,7 @@ def main():
     t0 = time.perf_counter()
     prof_us, prof_n = [], 0
     import ctypes
-    overlap = not args.no_overlap
+    overlap = WORKLOADS[args.workload]["overlap"] if args.overlap is None else args.overlap == "on"
     for k in range(args.steps):
         profiled = prof and k == args.steps - 1
         if overlap and k + 1 < args.steps:  # pass k+1's speech encoder runs beside pass k's loop
@@ -319,7 +322,7 @@ def main():
                                   else f"{args.dtype} decoder"),
                    "global_batch": n_total, "seq_len": L, "parallelism": f"dp{world}",
                    "diffusion_steps": T,
-                   "speech_encoder": "inline per pass" if args.no_overlap else
+                   "speech_encoder": "inline per pass" if not overlap else
                    "per pass, pass k+1's beside pass k's loop on a second HIP stream"},
         "roofline": roof,
         "whole_job": {"gflop_per_frame": round(frame_flop / 1e9, 4), "clip_step_mflop": round(clip_step / 1e6, 2),
