@@ -183,6 +183,8 @@ class Speech2GestureModel:
         before the current batch's loop; the call that later samples ``wav_next`` waits on the
         encoder's event instead of encoding again.  The side stream starts after the work
         already queued on the current stream (so ``wav`` is complete), never the other way round.
+        Pass the same device tensor to both calls: a host tensor is copied anew by each call and
+        is not recognised (it is then encoded again; at most 8 unconsumed prefetches are kept).
         """
         wav = wav.to(self.device, th.float32)
         if self._side is None:
@@ -195,6 +197,8 @@ class Speech2GestureModel:
             ev.record(self._side)
         wav.record_stream(self._side)
         self._pending[self._wav_key(wav)] = (tok, ev)
+        while len(self._pending) > 8:  # prefetched but never sampled (e.g. a host wav copied twice)
+            self._pending.pop(next(iter(self._pending)))
 
     def prepare(self, wav, L):
         """Encode ``wav`` once (cached per tensor identity/version) and install the memory."""
