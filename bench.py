@@ -1,23 +1,24 @@
 """Benchmark: generated motion frames/s of the gesture-diffusion sampler (BASELINE.json metric).
 
-One "step" = one full sampling pass over one batch of synthetic BEAT-shaped clips:
-speech encoding (once per clip, a replayed graph) + all T = 1000 DDPM denoise steps (17
-fused kernel launches each, issued eagerly: on ROCm 7.2 a replayed hipGraph of the same
-chain measured 3-10 % slower) + the all-gather of the final poses.  Workload
-(config C2, BASELINE.json configs[1]): beat-ours, 32 clips per GPU, L = 40 frames,
-123 pose channels, 32,000-sample wav windows, bf16 decoder, random-init weights.
+One "step" = one full sampling pass over one batch of synthetic BEAT-shaped clips: the HIP
+speech encoder (once per clip) + all T' denoise steps + the all-gather of the final poses.
+Workloads (BASELINE.json configs; beat-ours, 123 pose channels, random-init weights):
+  c2 (default, the metric's config): 32 clips/GPU, L = 40, 32,000-sample wavs, DDPM T = 1000,
+     bf16 -- one launch of the clip-group persistent loop mk_kernel per pass;
+  c4: 32 clips/GPU, L = 160, DDPM 1000, fp8-e4m3 step weights -- generic per-phase kernels;
+  c5: 128 clips/GPU, L = 40, DDIM-50 -- one launch of the per-clip loop psk_kernel per pass,
+     the next pass's encoder on a second HIP stream beside it (WORKLOADS[...]["overlap"]).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4|c5]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
 
-Prints ONE JSON line on rank 0.  ``roofline`` is measured live inside the timed region:
-during the last timed pass (the same launch sequence, with profiling on) every
-launch of the dominant kernel, kb_kernel (SA out-proj + LN2 + cross-attn Q + conv +
-cross-attention), stamps its own span on the device-wide realtime clock (min start / max
-end over its workgroups, ggd_api.hip ``spans``) — T x n_layers launches per pass.  Its
-algorithmic FLOPs per launch are kb_flop() below.
-``cpu_baseline`` times the CPU oracle (a faithful fp32 restatement that recomputes the
-speech encoder every step, as models/model.py:95-96 does) on a bounded sample.
+Prints ONE JSON line on rank 0.  ``roofline`` is measured live inside the timed region: in the
+last timed pass the library brackets every launch of the dominant kernel with a hipEvent pair
+on the context stream it is launched on (ggd_set_profiling / ggd_kernel_time); FLOPs per launch
+are the algorithmic clip_step_flops() x clips x steps for the loops, 2 M K N for
+the FFN-up GEMM.  ``traffic`` is read from the committed rocprofv3 PMC summary of the same
+command (PMC_SUMMARY).  ``cpu_baseline`` times the CPU oracle (a faithful fp32 restatement that
+recomputes the speech encoder every step, as models/model.py:95-96 does) on a bounded sample.
 """
 import argparse
 import json
