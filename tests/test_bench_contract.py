@@ -1,0 +1,45 @@
+"""bench.py host logic (CPU): workload table vs BASELINE.json, FLOP accounting, PMC lookup."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_default_workload_is_the_metric_config(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert (a.gpus, a.workload, a.batch_per_gpu, a.alg, a.dtype, a.seq_mult) == (1, "c2", 32, "ddpm", "bf16", 1)
+    assert a.respacing == ""
+
+
+def test_workloads_follow_baseline_configs():
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert "frames" in json.dumps(base).lower()
+    w = bench.WORKLOADS
+    assert w["c4"]["seq_mult"] == 4 and w["c4"]["dtype"] == "fp8"
+    assert w["c5"]["alg"] == "ddim" and w["c5"]["respacing"] == "ddim50" and w["c5"]["batch_per_gpu"] == 128
+    assert not w["c2"]["overlap"] and w["c5"]["overlap"]
+
+
+def test_clip_step_flops_hand_count():
+    L, Tm, d, C, layers = 40, 32, 256, 123, 4
+    # per layer: QKV 3d^2, SA out d^2, CA Q d^2, CA out d^2, FFN 2 x 4d^2 (rows L); emb C->d, out d->C
+    gemm = 2 * L * (C * d + d * C + layers * 14 * d * d)
+    attn = layers * 4 * L * (L + Tm) * d
+    conv = layers * 4 * 6 * L * d
+    assert bench.clip_step_flops(L, Tm, d, C, layers) == gemm + attn + conv
+    assert abs(bench.clip_step_flops(L, Tm, d, C, layers) / 1e6 - 311.42) < 0.01
+
+
+@pytest.mark.parametrize("workload,prefix", [("c2", "mk_kernel"), ("c5", "psk_kernel")])
+def test_pmc_traffic_reads_committed_summary(workload, prefix):
+    tr = bench.pmc_traffic(prefix, workload)
+    assert tr is not None and tr["bytes_per_launch"] == tr["read"] + tr["write"] > 0
+    assert os.path.exists(os.path.join(ROOT, tr["source"]))
+    assert bench.pmc_traffic(prefix, "nope") is None
