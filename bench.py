@@ -216,10 +216,11 @@ def main():
     wavs = [th.randn(n_total, wav_len, device=dev, generator=g) * 0.1 for _ in range(n_batches)]
     start, stop = sharding.shard_range(n_total, rank, world)
 
-    def one_pass(wav_all, seed):
+    def one_pass(wav_all, seed, wav_next=None):
         def fn(wav_local, offset):
             out = loop(model, (wav_local.shape[0], d_pose, L), model_kwargs={"wav": wav_local}, seed=seed,
-                       clip_offset=offset, use_graph=args.graph, extras=False)
+                       clip_offset=offset, use_graph=args.graph, extras=False,
+                       prefetch_wav=None if wav_next is None else wav_next[start:stop])
             return out["sample"]
         return sharding.sample_sharded(fn, wav_all, n_total, rank, world, dev)
 
@@ -242,11 +243,12 @@ def main():
     overlap = WORKLOADS[args.workload]["overlap"] if args.overlap is None else args.overlap == "on"
     for k in range(args.steps):
         profiled = prof and k == args.steps - 1
-        if overlap and k + 1 < args.steps:  # pass k+1's speech encoder runs beside pass k's loop
-            model.prefetch_speech(wavs[args.warmup + k + 1][start:stop])
         if profiled:
             lib.ggd_set_profiling(ctx.h, 1)
-        out = one_pass(wavs[args.warmup + k], seed=100 + k)
+        # overlap: pass k+1's speech encoder is issued once pass k's memory is installed and runs
+        # beside pass k's loop on a second HIP stream
+        nxt = wavs[args.warmup + k + 1] if overlap and k + 1 < args.steps else None
+        out = one_pass(wavs[args.warmup + k], seed=100 + k, wav_next=nxt)
         log(f"pass {k} issued")
         if profiled:
             lib.ggd_set_profiling(ctx.h, 0)

@@ -871,7 +871,12 @@ int ggd_create(int device, const ggd_desc* desc, ggd_ctx** out) {
   c->tsize = D.dtype == GGD_F32 ? 4 : 2;
   *out = c;
   HIP_TRY(c, hipSetDevice(device));
-  HIP_TRY(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  {  // the sampler's stream takes the highest priority: a prefetched speech encoder on another
+     // stream (Speech2GestureModel.prefetch_speech) must not hold up the next loop's set-up GEMMs
+    int least = 0, greatest = 0;
+    HIP_TRY(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(c, hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
+  }
   {
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) == hipSuccess && khz > 0)

@@ -148,7 +148,7 @@ class GaussianSpacedDiffusion(GaussianDiffusion):
         return self._loop(native.DDIM, float(eta), model, shape, model_kwargs, noise, denoise_fn, device, **kw)
 
     def _loop(self, alg, eta, model, shape, model_kwargs, noise, denoise_fn, device, step_noise=None,
-              seed=None, clip_offset=0, n_steps=None, use_graph=False, extras=True):
+              seed=None, clip_offset=0, n_steps=None, use_graph=False, extras=True, prefetch_wav=None):
         assert isinstance(shape, (tuple, list)) and len(shape) == 3, "shape must be (N, C, L)"
         model_kwargs = dict(model_kwargs or {})
         wav = model_kwargs.pop("wav", None)
@@ -160,6 +160,10 @@ class GaussianSpacedDiffusion(GaussianDiffusion):
         ctx, n = model.prepare(wav, L)
         assert n == N, "wav batch differs from shape[0]"
         model.condition(ctx, n, L, inp_pose, inp_mask)
+        if prefetch_wav is not None:
+            # the next batch's speech encoder starts once this batch's memory is installed and
+            # runs beside this loop (Speech2GestureModel.prefetch_speech)
+            model.prefetch_speech(prefetch_wav)
         ctx.set_schedule(self.betas, self.timestep_map)
         if seed is None:
             seed = int(th.randint(0, 2 ** 62, (1,)).item())

@@ -85,16 +85,17 @@ class Generator:
         """generate_sample over independent clip batches, back to back -> list of (N, L, C).
 
         Serving form of generator.py:218-296 for a queue of batches: batch k+1's speech encoder
-        is issued on a side HIP stream (model.prefetch_speech) before batch k's reverse loop, so
-        the two run at once; outputs equal per-batch generate_sample calls.
+        is issued on a side HIP stream (model.prefetch_speech) once batch k's speech memory is
+        installed, so it runs beside batch k's reverse loop; outputs equal per-batch
+        generate_sample calls.
         """
         wav_batches = [w.to(device) for w in wav_batches]
         outs = []
         for k, wav in enumerate(wav_batches):
-            if k + 1 < len(wav_batches):
-                self.model.prefetch_speech(wav_batches[k + 1])
+            nxt = wav_batches[k + 1] if k + 1 < len(wav_batches) else None
             shp = (wav.shape[0],) + tuple(shape[1:])
-            outs.append(self.generate_sample(shp, wav, sample_alg=sample_alg, device=device, progress=False, **kw))
+            outs.append(self.generate_sample(shp, wav, sample_alg=sample_alg, device=device, progress=False,
+                                             prefetch_wav=nxt, **kw))
         return outs
 
     @th.no_grad()
