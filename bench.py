@@ -71,7 +71,7 @@ WORKLOADS = {
 }
 # overlap: the next pass's speech encoder runs beside this pass's loop (model.prefetch_speech).
 # It pays where the loop leaves CUs idle (C5: psk_kernel, 128 workgroups on 256 CUs, 254.0k ->
-# 286.5k frames/s); C2/C4 loops fill the chip and measured the same or 0.6% slower with it.
+# 306.5k frames/s); C2/C4 loops fill the chip and measured the same or 0.6% slower with it.
 
 
 # HBM-side bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of
