@@ -48,7 +48,7 @@ constexpr int NFFT = 1024, HOP = 512, NBIN = NFFT / 2 + 1, NMEL = 128;
 constexpr int SPEC_LD = 1088;   // 2 * 513 columns padded to the GEMM's 64-column tiles
 constexpr int POW_LD = 516;     // 513 power bins, rows 16-byte aligned
 constexpr int CONV_TPB = 256;   // 4 waves; a wave owns 32 output pixels
-constexpr int SE_SLICES = 32;   // pixel slices of the SE squeeze's first stage
+constexpr int SE_SLICES = 64;   // pixel slices of the SE squeeze's first stage
 
 // ------------------------------------------------------------------------------------------
 // front end
@@ -267,10 +267,19 @@ __global__ void __launch_bounds__(256) enc_se_sum_kernel(const float* __restrict
   const int stripes = 256 / C, c = tid % C, st = tid / C;
   const int p0 = (int)((long)HW * sl / S), p1 = (int)((long)HW * (sl + 1) / S);
   const float* src = v + (size_t)b * HW * C;
-  float s = 0.f;
-  if (st < stripes)
-    for (int p = p0 + st; p < p1; p += stripes) s += src[(size_t)p * C + c];
-  red[tid] = s;
+  // four independent partial sums keep four loads in flight per thread (fixed order per clip)
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (st < stripes) {
+    int p = p0 + st;
+    for (; p + 3 * stripes < p1; p += 4 * stripes) {
+      s0 += src[(size_t)p * C + c];
+      s1 += src[(size_t)(p + stripes) * C + c];
+      s2 += src[(size_t)(p + 2 * stripes) * C + c];
+      s3 += src[(size_t)(p + 3 * stripes) * C + c];
+    }
+    for (; p < p1; p += stripes) s0 += src[(size_t)p * C + c];
+  }
+  red[tid] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (tid < C) {
     float tot = 0.f;
@@ -994,7 +1003,7 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
           res = r;
         }
         if (rc) return rc;
-        const int S = std::max(1, std::min(SE_SLICES, Ho * Wo / 256));
+        const int S = std::max(1, std::min(SE_SLICES, Ho * Wo / 64));
         hipLaunchKernelGGL(enc_se_sum_kernel, dim3(m, S), dim3(256), 0, s, v, Ho * Wo, B.planes, e->se_part);
         ENC_TRY(e, hipGetLastError());
         hipLaunchKernelGGL(enc_se_kernel, dim3(m), dim3(256), 0, s, e->se_part, S, Ho * Wo, B.planes, B.se_w0,
