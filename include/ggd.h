@@ -12,7 +12,11 @@
  * pointers and sizes only.  Device pointers are HIP device addresses owned by
  * the caller (e.g. the PyTorch caching allocator); `stream` is a hipStream_t
  * (0 = legacy default stream).  The context owns weights, workspaces and
- * captured hipGraphs; nothing is allocated inside the step loop.
+ * captured hipGraphs; nothing is allocated inside the step loop.  Its work runs
+ * on a private non-blocking stream created at the device's highest priority
+ * and is ordered against the caller's `stream` with events in both directions.
+ * Another stream may therefore run beside it, e.g. a speech encoder for the
+ * next batch.
  *
  * Error convention: every call returns 0 (GGD_OK) or a negative ggd_status;
  * ggd_last_error(ctx) returns a message for the last failure on ctx.  The
