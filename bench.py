@@ -9,8 +9,14 @@ Workloads (BASELINE.json configs; beat-ours, 123 pose channels, random-init weig
   c5: 128 clips/GPU, L = 40, DDIM-50 -- one launch of the per-clip loop psk_kernel per pass,
      the next pass's encoder on a second HIP stream beside it (WORKLOADS[...]["overlap"]).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4|c5]
-    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4|c5] [--dtype bf16|f32|fp8]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...  (one rank per GPU, RCCL)
+
+``--gpus N`` (N > 1) started without a launcher spawns the N ranks itself: the parent runs
+``torch.distributed.run`` as a child process before anything touches the GPU and exits with its
+code.  ``--rehearse`` runs the same launch / shard / all-gather / max-over-ranks timing path on
+CPU over gloo, with the CPU oracle as the sampler (a test of the multi-rank plumbing, never a
+measurement: its line says "rehearsal").
 
 Prints ONE JSON line on rank 0.  ``roofline`` is measured live inside the timed region: in the
 last timed pass the library brackets every launch of the dominant kernel with a hipEvent pair
@@ -23,6 +29,9 @@ recomputes the speech encoder every step, as models/model.py:95-96 does) on a bo
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -118,7 +127,11 @@ def parse():
                    help="encode pass k+1's speech beside pass k's loop (default: per workload)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=None,
-                   help="denoise steps of the CPU sample (default: ~10 s of oracle work, 40 steps at C2)")
+                   help="denoise steps of each CPU sample (default: ~4 s of oracle work, 15 steps at C2)")
+    p.add_argument("--cpu-samples", type=int, default=3,
+                   help="timed CPU samples; cpu_baseline reports their median and spread")
+    p.add_argument("--rehearse", action="store_true",
+                   help="CPU/gloo rehearsal of the multi-rank path with the oracle sampler (no GPU, no measurement)")
     a = p.parse_args()
     w = WORKLOADS[a.workload]
     for k in ("batch_per_gpu", "alg", "respacing"):
@@ -128,8 +141,32 @@ def parse():
     if a.dtype is None:
         a.dtype = w.get("dtype", "bf16")
     if a.cpu_steps is None:
-        a.cpu_steps = max(3, round(40 * 32 / (a.batch_per_gpu * a.seq_mult)))
+        a.cpu_steps = max(2, round(15 * 32 / (a.batch_per_gpu * a.seq_mult)))
     return a
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(argv, n, port):
+    """The torch.distributed.run command line that runs this script as ``n`` ranks of one node."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def self_launch(argv, n):
+    """Run this script as ``n`` ranks in a child launcher; returns its exit code.  Called before
+    any HIP call (the parent never initialises the GPU), so the ranks own the devices."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    log(f"spawning {n} ranks: torch.distributed.run")
+    return subprocess.call(launch_command(argv, n, free_port()), env=env)
 
 
 def log(*a):
@@ -139,14 +176,16 @@ def log(*a):
 T_START = time.perf_counter()
 
 
-def cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, n_steps, alg):
-    """Oracle on the host cores: faithful per-step encoder, n_steps denoise steps, extrapolated x T."""
+def cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, n_steps, alg, n_samples=3):
+    """Oracle on the host cores: faithful per-step encoder; ``n_samples`` timed samples of
+    ``n_steps`` denoise steps each, extrapolated x T; the median is the value."""
     from oracle import ref_denoiser, ref_diffusion
-    cores = len(os.sched_getaffinity(0))
+    affinity = sorted(os.sched_getaffinity(0))
+    cores = len(affinity)
     if os.environ.get("OMP_NUM_THREADS"):
         cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))  # the box's CPU share
     th.set_num_threads(cores)
-    log(f"cpu baseline: {cores} threads, B={B}, {n_steps} steps")
+    log(f"cpu baseline: {cores} threads, B={B}, {n_samples} x {n_steps} steps")
     ocfg = {k: arch[k] for k in ("type", "d_model", "decoder", "heads", "n_layers")}
     om = ref_denoiser.OracleModel(sd, ocfg, cache_speech=False)
     g = th.Generator().manual_seed(1)
@@ -155,36 +194,101 @@ def cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, n_steps, alg):
     noise = ref_diffusion.TorchNoise(2)
     ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, alg, n_steps=1)
     log("cpu baseline warm-up step done")
-    t0 = time.perf_counter()
-    ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, alg, n_steps=n_steps)
-    dt = time.perf_counter() - t0
-    per_step = dt / n_steps
+    per = []
+    for _ in range(n_samples):
+        t0 = time.perf_counter()
+        ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, alg, n_steps=n_steps)
+        per.append((time.perf_counter() - t0) / n_steps)
+    per_step = statistics.median(per)
+    fps = [B * L / (p * T) for p in per]
     model_name = ""
     try:
         with open("/proc/cpuinfo") as f:
             model_name = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
     except Exception:
         pass
+    aff = f"{affinity[0]}-{affinity[-1]}" if affinity == list(range(affinity[0], affinity[-1] + 1)) else \
+        ",".join(map(str, affinity))
     return {
-        "value": B * L / (per_step * T),
+        "value": round(B * L / (per_step * T), 4),
         "unit": "frames/s",
         "cores": th.get_num_threads(),
         "kind": "port",
-        "sample": (f"{n_steps} {alg.upper()} denoise steps of B={B} clips (per-step speech encoder, fp32 oracle) "
-                   f"after 1 warm-up, measured {dt:.2f} s = {per_step * 1e3:.0f} ms/step, extrapolated x{T} steps; "
+        "samples": [round(v, 4) for v in fps],
+        "spread": round((max(fps) - min(fps)) / statistics.median(fps), 4),
+        "sample": (f"median of {n_samples} samples, each {n_steps} {alg.upper()} denoise steps of B={B} clips "
+                   f"(per-step speech encoder, fp32 oracle) after 1 warm-up step; ms/step "
+                   f"{', '.join('%.0f' % (p * 1e3) for p in per)}; extrapolated x{T} steps; "
+                   f"{th.get_num_threads()} torch threads, process affinity CPUs {aff} ({len(affinity)}); "
                    f"CPU: {model_name}"),
     }
 
 
+def rehearse(args, rank, world):
+    """--rehearse: the multi-rank path of main() on CPU over gloo, the oracle as the sampler.
+
+    Same launch, barrier + max-over-ranks timing and all-gather as a GPU run; 2 clips per rank,
+    2 DDPM steps of the beat-ours architecture (bounded weight init), noise keyed by global clip id.
+    """
+    import numpy as np
+    import torch.distributed as dist
+    import __graft_entry__ as ge
+    from oracle import ref_denoiser, ref_diffusion
+    th.set_num_threads(1)
+    if world > 1:
+        dist.init_process_group("gloo")
+    pkg = ge.load_package()
+    sharding = __import__(ge.PKG_NAME + ".sharding", fromlist=["x"])
+    cfg = pkg.load_config(args.config)
+    arch = pkg.arch_from_config(cfg.Model, 123)
+    sd = pkg.init_state_dict(arch, seed=0, bounded=True)
+    om = ref_denoiser.OracleModel(sd, {k: arch[k] for k in ("type", "d_model", "decoder", "heads", "n_layers")},
+                                  cache_speech=True)
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    B, L, n_steps = 2, 40, 2
+    n_total = B * world
+    wav_all = th.randn(n_total, 32000, generator=th.Generator().manual_seed(1234)) * 0.1
+
+    def fn(wav_local, offset):  # one clip at a time: a clip's result does not depend on its shard
+        outs = []
+        for j in range(wav_local.shape[0]):
+            noise = ref_diffusion.PhiloxNoise(7, np.array([offset + j]))
+            outs.append(ref_diffusion.sample_loop(sch, om, (1, 123, L), {"wav": wav_local[j:j + 1]}, noise, "ddpm",
+                                                  n_steps=n_steps)["sample"])
+        return th.cat(outs)
+
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    out = sharding.sample_sharded(fn, wav_all, n_total, rank, world, th.device("cpu"))
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = th.tensor([elapsed], dtype=th.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "rehearsal (not a measurement)", "rehearsal": True, "n_gpus": world,
+                          "world": world, "global_batch": n_total, "elapsed_s": elapsed,
+                          "checksum": float(out.double().sum()), "shape": list(out.shape),
+                          "first": out[:, 0, 0].tolist()}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        # one rank per GPU: spawn them before anything touches the GPU, exit with their code
+        raise SystemExit(self_launch(sys.argv[1:], args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and "RANK" in os.environ:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    if world > 1 and "RANK" not in os.environ:
-        raise SystemExit("multi-GPU runs are launched with torch.distributed.run (one rank per GPU)")
+    if args.rehearse:
+        return rehearse(args, rank, world)
     dev = th.device("cuda", local)
     th.cuda.set_device(dev)
     dist = None
@@ -333,7 +437,8 @@ def main():
                       "frac_of_peak": round(value * frame_flop / world / 1e12 / peak, 5)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, args.cpu_steps, args.alg)
+        res["cpu_baseline"] = cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, args.cpu_steps, args.alg,
+                                           args.cpu_samples)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:

@@ -200,18 +200,21 @@ def ddim_sample(sch, model, x, i, model_kwargs, noise, denoise_fn=None, eta=0.0)
 
 
 def sample_loop(sch, model, shape, model_kwargs, noise, alg="ddpm", denoise_fn=None, eta=0.0,
-                x_T=None, n_steps=None):
+                x_T=None, n_steps=None, snapshots=()):
     """p_sample_loop(_progressive) :331-412 / ddim_sample_loop(_progressive) :414-529.
 
     ``n_steps`` truncates the loop after that many iterations (parity tests at
     reduced cost); the iterations run are exactly the reference's first ones.
+    ``snapshots``: iteration counts after which x is recorded in out["snapshots"][k]
+    (the drift curve of a long loop from one oracle run).
     """
     x = x_T if x_T is not None else noise.initial(shape)
     out = None
+    snaps = {}
     idx = list(range(sch.num_timesteps))[::-1]
     if n_steps is not None:
         idx = idx[:n_steps]
-    for i in idx:
+    for k, i in enumerate(idx):
         with th.no_grad():
             if alg == "ddpm":
                 out = p_sample(sch, model, x, i, model_kwargs, noise, denoise_fn)
@@ -220,6 +223,10 @@ def sample_loop(sch, model, shape, model_kwargs, noise, alg="ddpm", denoise_fn=N
             else:
                 raise ValueError(f"Unsupported sample algorithm: {alg}")
         x = out["sample"]
+        if k + 1 in snapshots:
+            snaps[k + 1] = x.clone()
+    if snapshots:
+        out["snapshots"] = snaps
     return out
 
 
@@ -292,3 +299,40 @@ def combine_windows(samples, pose_seed_len, seq_len, smooth_trans):
             x = th.cat([tr, x[:, pose_seed_len:]], dim=1)
         parts.append(x[:, :-pose_seed_len] if i < len(samples) - 1 else x)
     return th.cat(parts, dim=1)[:, :seq_len]
+
+
+def generate_sequence(sch, model, wav_seqs, wav_sr, pose_dim, pose_fps, pose_window_len, pose_seed_len,
+                      make_noise, smooth_trans=True, trans_factor=None, init_poses=None, sample_alg="ddim",
+                      n_steps=None):
+    """Generator.generate_sequence: generator.py:80-195 for ONE batch (batch_size >= N).
+
+    Window k samples wav[:, ws:we] (zero-padded past the end) with its first ``pose_seed_len``
+    frames inpainted from window k-1's tail (window 0: from ``init_poses`` if given, else no
+    inpainting); the windows are joined by combine_windows.  ``make_noise(k)`` gives window k's
+    noise provider.  Where the reference would crash (init_poses None: ``init_poses.to`` at
+    :105 and ``inpaint_poses[...]`` of a None at :148) this follows the evident intent: no
+    seed poses for window 0, zeros elsewhere in the seed-pose buffer from window 1 on.
+    """
+    n, n_wav = wav_seqs.shape
+    seq_len, plan = sequence_plan(n_wav, wav_sr, pose_fps, pose_window_len, pose_seed_len)
+    samples, sample, inpaint_poses = [], None, None
+    for k, (ws, we) in enumerate(plan):
+        wavs = wav_seqs[:, ws:we]
+        masks = th.ones((n, pose_window_len, 1))
+        masks[:, pose_seed_len:] = 0
+        if k == 0:
+            if init_poses is None:
+                inpaint_poses = masks = None
+            else:
+                inpaint_poses = th.zeros((n, pose_window_len, pose_dim))
+                inpaint_poses[:, :pose_seed_len] = init_poses
+        else:
+            if inpaint_poses is None:
+                inpaint_poses = th.zeros((n, pose_window_len, pose_dim))
+            inpaint_poses[:, :pose_seed_len] = sample[:, -pose_seed_len:]
+        if we > n_wav:
+            wavs = th.cat([wavs, th.zeros((n, we - n_wav))], dim=1)
+        sample = generate_sample(sch, model, (n, pose_dim, pose_window_len), wavs, make_noise(k),
+                                 inpaint_poses, masks, sample_alg, trans_factor, pose_seed_len, n_steps=n_steps)
+        samples.append(sample)
+    return combine_windows(samples, pose_seed_len, seq_len, smooth_trans)

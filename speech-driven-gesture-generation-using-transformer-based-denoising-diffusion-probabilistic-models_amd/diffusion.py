@@ -157,6 +157,8 @@ class GaussianSpacedDiffusion(GaussianDiffusion):
             raise ValueError(f"unsupported model kwargs {sorted(model_kwargs)}")
         N, C, L = (int(s) for s in shape)
         dev = th.device(device) if device is not None else model.device
+        if wav is not None:  # one device copy for the whole loop (the per-step path re-keys on it)
+            wav = wav.to(model.device, th.float32)
         ctx, n = model.prepare(wav, L)
         assert n == N, "wav batch differs from shape[0]"
         model.condition(ctx, n, L, inp_pose, inp_mask)

@@ -196,12 +196,21 @@ class Speech2GestureModel:
             ev = th.cuda.Event()
             ev.record(self._side)
         wav.record_stream(self._side)
-        self._pending[self._wav_key(wav)] = (tok, ev)
+        # the entry holds ``wav`` itself: while it is pending, no other tensor can be allocated at
+        # its address, so a key match always means the same tensor (not a reused block)
+        self._pending[self._wav_key(wav)] = (tok, ev, wav)
         while len(self._pending) > 8:  # prefetched but never sampled (e.g. a host wav copied twice)
             self._pending.pop(next(iter(self._pending)))
 
     def prepare(self, wav, L):
-        """Encode ``wav`` once (cached per tensor identity/version) and install the memory."""
+        """Encode ``wav`` once (cached per device tensor identity/version) and install the memory.
+
+        The cache key is the device tensor's address, shape and version; the cache entry keeps
+        that tensor alive, so while it is cached no other tensor can be allocated at the same
+        address and a key match means the same, unmodified tensor.  A host ``wav`` is copied to
+        the device by each call, so each call encodes it afresh (a per-step caller passes the
+        device copy; GaussianSpacedDiffusion._loop does).
+        """
         wav = wav.to(self.device, th.float32)
         n = wav.shape[0]
         Ts = speech_len(self.arch["type"], wav.shape[1])
@@ -211,7 +220,7 @@ class Speech2GestureModel:
             return ctx, n
         pending = self._pending.pop(self._wav_key(wav), None)
         if pending is not None:  # encoded by prefetch_speech on the side stream
-            tok, ev = pending
+            tok, ev, _ = pending
             cur = th.cuda.current_stream(self.device)
             cur.wait_event(ev)
             tok.record_stream(cur)
@@ -223,7 +232,7 @@ class Speech2GestureModel:
         native.check(ctx.h, ctx.lib.ggd_set_memory(ctx.h, ctypes.c_void_p(tok.data_ptr()), n, Ts, tok.shape[2],
                                                    _stream_ptr(self.device)), "set memory")
         ctx.memory_key = key
-        self._mem_cache = (key, tok)  # keep tok alive until the ctx has consumed it
+        self._mem_cache = (key, tok, wav)  # tok: alive until the ctx has consumed it; wav: pins the key
         return ctx, n
 
     def condition(self, ctx, n, L, inpaint_pose=None, inpaint_mask=None):

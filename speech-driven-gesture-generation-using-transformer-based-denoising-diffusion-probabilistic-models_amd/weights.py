@@ -168,9 +168,12 @@ def _mel_fb(n_freqs=513, n_mels=128, sr=16000):
     return th.clamp(th.min(down, up), min=0.0)
 
 
-def init_state_dict(arch, seed=0, perturb=False):
+def init_state_dict(arch, seed=0, perturb=False, bounded=False):
     """Seeded synthetic state_dict.  ``perturb`` randomises LN affines and BN statistics
-    (non-trivial values for parity tests; the benchmark uses the reference init)."""
+    (non-trivial values for parity tests; the benchmark uses the reference init).
+
+    ``bounded`` gives the denoiser a pose skip path so that a 1000-step trajectory stays O(1)
+    (parity tests at full length; see bounded_skip)."""
     g = th.Generator().manual_seed(seed)
     sd = {}
     for name, (shape, init) in parameter_shapes(arch).items():
@@ -212,6 +215,31 @@ def init_state_dict(arch, seed=0, perturb=False):
         if perturb and name.endswith("running_var"):
             t = 0.5 + th.rand(shape, generator=g)
         sd[name] = t.contiguous()
+    if bounded:
+        bounded_skip(sd, arch, seed)
+    return sd
+
+
+def bounded_skip(sd, arch, seed=0, emb_scale=4.0, out_gain=3.0):
+    """Make eps ~ out_gain * x / rms(x) along a random orthonormal pose subspace.
+
+    With reference-init random weights the decoder's output does not depend on x_t (emb_x is
+    swamped by the positional table and the final LayerNorm caps |eps| at ~0.6), so
+    x0 = sqrt(1/abar) x - sqrt(1/abar - 1) eps amplifies x and a 1000-step DDPM trajectory
+    grows to |x| ~ 1e3 (measured: rms 276 after T = 1000).  Here emb_x = emb_scale * Q and
+    out_layers.1 = out_gain * sqrt(C/d) * Q^T for a seeded Q (d x C, orthonormal columns): the
+    pose reaches the output through the residual stream and the final LayerNorm, so eps is a
+    scaled copy of x plus the other paths' contributions.  The reverse update then contracts
+    x whenever |eps| exceeds the posterior's growth (out_gain > 1): rms(x) stays within
+    0.4-1.0 over the whole T = 1000 DDPM loop (oracle, 2 clips).  Every other parameter keeps
+    the reference init, so all kernels see non-trivial operands.
+    """
+    d, C = arch["d_model"], arch["d_pose"]
+    g = th.Generator().manual_seed(1000 + seed)
+    q, _ = th.linalg.qr(th.randn(d, C, generator=g))
+    sd["pose_decoder.emb_x.weight"] = (q * emb_scale).contiguous()
+    sd["pose_decoder.out_layers.1.weight"] = (q.t() * (out_gain * math.sqrt(C / d))).contiguous()
+    sd["pose_decoder.out_layers.1.bias"] = th.zeros(C)
     return sd
 
 

@@ -43,3 +43,35 @@ def test_pmc_traffic_reads_committed_summary(workload, prefix):
     assert tr is not None and tr["bytes_per_launch"] == tr["read"] + tr["write"] > 0
     assert os.path.exists(os.path.join(ROOT, tr["source"]))
     assert bench.pmc_traffic(prefix, "nope") is None
+
+
+def test_launch_command_one_rank_per_gpu():
+    cmd = bench.launch_command(["--gpus", "4", "--steps", "3"], 4, 29555)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd and "--master-port=29555" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    i = cmd.index(os.path.join(ROOT, "bench.py"))
+    assert cmd[i + 1:] == ["--gpus", "4", "--steps", "3"]
+
+
+def _rehearse(n):
+    import subprocess
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("RANK", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--rehearse"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints the only line
+    return json.loads(lines[0])
+
+
+def test_self_launch_rehearsal_matches_single_rank():
+    """bench.py --gpus N spawns N ranks itself (no external torchrun); over gloo with the oracle
+    sampler, the all-gathered clips equal a single rank's bit for bit."""
+    one = _rehearse(1)
+    for n in (2, 3):
+        res = _rehearse(n)
+        assert res["rehearsal"] and res["world"] == n and res["global_batch"] == 2 * n
+        assert res["shape"] == [2 * n, 123, 40]
+        assert res["first"][:2] == one["first"]  # global clips 0, 1: same wav rows, same noise keys

@@ -1,12 +1,15 @@
 """Multi-rank sharding of the clip batch over gloo on CPU, world size 2 and 3.
 
-The sample function stands in for the HIP sampler: a deterministic function of the global clip
-id (as the counter-keyed noise makes the real sampler), so the gathered result must equal the
-single-rank result exactly, in global clip order, for balanced and ragged shards.
+The sampler is the CPU oracle (2 DDPM steps of the beat-ours architecture) with the counter-based
+noise keyed by GLOBAL clip id (oracle/ref_diffusion.PhiloxNoise), as the HIP sampler draws it: the
+gathered result must equal the single-rank result bit for bit, in global clip order, for balanced
+and ragged shards.  Each clip is sampled on its own, so its arithmetic does not depend on how
+many clips share its shard.
 """
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch as th
 import torch.distributed as dist
@@ -23,11 +26,31 @@ def _free_port():
     return p
 
 
-def fake_sample(wav_shard, clip_offset):
-    """(n_local, C, L) output that depends only on (global clip id, that clip's wav)."""
-    n = wav_shard.shape[0]
-    ids = th.arange(clip_offset, clip_offset + n, dtype=th.float32)
-    return (ids[:, None, None] * 1000.0 + wav_shard[:, None, :6].sum(-1, keepdim=True)).expand(n, 5, 6).contiguous()
+_ORACLE = {}
+
+
+def oracle_sample(wav_shard, clip_offset, n_steps=2, seed=11):
+    """(n_local, C, L) poses of the clips [clip_offset, clip_offset + n_local): oracle DDPM steps."""
+    from oracle import ref_denoiser, ref_diffusion
+    import __graft_entry__ as ge
+    if not _ORACLE:
+        pkg = ge.load_package()
+        cfg = pkg.load_config(os.path.join(ROOT, "configs", "beat-ours.json"))
+        arch = pkg.arch_from_config(cfg.Model, 123)
+        sd = pkg.init_state_dict(arch, seed=0, bounded=True)
+        _ORACLE["om"] = ref_denoiser.OracleModel(
+            sd, {k: arch[k] for k in ("type", "d_model", "decoder", "heads", "n_layers")}, cache_speech=True)
+        _ORACLE["sch"] = ref_diffusion.make_schedule("linear", 1000, "")
+    outs = []
+    for j in range(wav_shard.shape[0]):
+        noise = ref_diffusion.PhiloxNoise(seed, np.array([clip_offset + j]))
+        outs.append(ref_diffusion.sample_loop(_ORACLE["sch"], _ORACLE["om"], (1, 123, 40), {"wav": wav_shard[j:j + 1]},
+                                              noise, "ddpm", n_steps=n_steps)["sample"])
+    return th.cat(outs)
+
+
+def _wavs(n_total):
+    return th.randn(n_total, 32000, generator=th.Generator().manual_seed(5)) * 0.1
 
 
 def _worker(rank, world, port, n_total, q):
@@ -37,21 +60,28 @@ def _worker(rank, world, port, n_total, q):
     try:
         import __graft_entry__ as ge
         sharding = __import__(ge.PKG_NAME + ".sharding", fromlist=["x"])
-        g = th.Generator().manual_seed(5)
-        wavs = th.randn(n_total, 32, generator=g)
-        out = sharding.sample_sharded(fake_sample, wavs, n_total, rank, world, th.device("cpu"))
+        th.set_num_threads(1)
+        out = sharding.sample_sharded(oracle_sample, _wavs(n_total), n_total, rank, world, th.device("cpu"))
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_total", [(2, 8), (2, 7), (3, 8)])
-def test_sharded_gather_matches_single_rank(world, n_total):
+@pytest.fixture(scope="module")
+def single_rank():
     import __graft_entry__ as ge
     sharding = __import__(ge.PKG_NAME + ".sharding", fromlist=["x"])
-    g = th.Generator().manual_seed(5)
-    wavs = th.randn(n_total, 32, generator=g)
-    want = sharding.sample_sharded(fake_sample, wavs, n_total, 0, 1, th.device("cpu"))
+    nt = th.get_num_threads()
+    th.set_num_threads(1)  # as the workers: the CPU GEMMs' blocking depends on the thread count
+    try:
+        return sharding.sample_sharded(oracle_sample, _wavs(5), 5, 0, 1, th.device("cpu"))
+    finally:
+        th.set_num_threads(nt)
+
+
+@pytest.mark.parametrize("world,n_total", [(2, 4), (2, 5), (3, 5)])
+def test_sharded_gather_matches_single_rank(single_rank, world, n_total):
+    want = single_rank[:n_total]  # wav rows and noise depend on the global clip id only
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
