@@ -173,8 +173,13 @@ def test_ddim50_full_loop_bf16(pkg, beat_cfg, setup):
 
 
 def test_ddpm_T1000_full_loop_f32(pkg, beat_cfg, setup):
-    """Config C2's sampler over all 1000 DDPM steps (f32 HIP vs f32 oracle, identical noise)."""
-    _, sd, om = setup
+    """Config C2's sampler over all 1000 DDPM steps (f32 HIP vs f32 oracle, identical noise).
+
+    Bounded weights (weights.bounded_skip): the trajectory stays O(1), so BASELINE's 1e-3 is an
+    absolute bound."""
+    arch, _, _ = setup
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True, bounded=True)
+    om = ref_denoiser.OracleModel(sd, oracle_cfg(arch), cache_speech=True)
     model, diffusion = make_model(pkg, beat_cfg, sd, "f32")
     n, seed = 2, 5
     wav, _, _ = inputs(n, seed=51)
@@ -183,10 +188,8 @@ def test_ddpm_T1000_full_loop_f32(pkg, beat_cfg, setup):
     want = ref_diffusion.sample_loop(sch, om, (n, D_POSE, L), {"wav": wav},
                                      ref_diffusion.PhiloxNoise(seed, np.arange(n)), "ddpm")["sample"]
     err = (out - want).abs().max().item()
-    scale = want.abs().max().item()
-    # 1000 chained steps amplify ulp-level differences (libm expf/logf/sinf in the noise, GEMM
-    # summation order): bound the drift relative to the sample's scale, 1e-3 x max(1, max|x|)
-    assert err <= 1e-3 * max(1.0, scale), (err, scale)
+    assert want.abs().max().item() < 5.0
+    assert err <= 1e-3, err
 
 
 def test_full_size_properties_bf16(pkg, beat_cfg, setup):
@@ -222,7 +225,7 @@ def test_counter_noise_values(pkg, beat_cfg, setup):
 def setup_c1(pkg, tedexp_cfg):
     """Config C1: tedexp (legacy schema) -> default model, two-way CrossAttention decoder, d 512, 10 layers."""
     arch = pkg.arch_from_config(tedexp_cfg.Model, 126)
-    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True, bounded=True)
     om = ref_denoiser.OracleModel(sd, oracle_cfg(arch), cache_speech=True)
     g = th.Generator().manual_seed(21)
     wav = th.randn(2, int(16000 * 34 / 15), generator=g) * 0.1
@@ -247,7 +250,8 @@ def test_two_way_denoise_f32(pkg, tedexp_cfg, setup_c1):
     eps = model(x.cuda(), t.cuda(), wav=wav.cuda()).cpu()
     ref = om(x, t, wav=wav)
     err = (eps - ref).abs().max().item()
-    assert err <= 2e-4 * max(1.0, ref.abs().max().item()), err
+    print(f"two-way f32 eps max|diff| {err:.3e}, max|eps| {ref.abs().max().item():.3f}")
+    assert err <= 2e-4, err
 
 
 def test_two_way_denoise_bf16(pkg, tedexp_cfg, setup_c1):
@@ -272,7 +276,11 @@ def test_two_way_sample_respaced_f32(pkg, tedexp_cfg, setup_c1):
                                      "ddpm", x_T=x, n_steps=steps)
     for k in ("sample", "eps", "pred_x_start"):
         err = (out[k].cpu() - want[k]).abs().max().item()
-        assert err <= 1e-3 * max(1.0, want[k].abs().max().item()), (k, err)
+        print(f"two-way f32 {k}: max|diff| {err:.3e}, max|ref| {want[k].abs().max().item():.3f}")
+        # pred_x_start = sqrt(1/abar) x - ... is O(100) at t ~ 1000 (sqrt(1/abar_999) = 157):
+        # its bound scales with that factor; sample and eps are O(1) and bounded absolutely
+        bound = 1e-3 * (157.0 if k == "pred_x_start" else 1.0)
+        assert err <= bound, (k, err)
 
 
 # ------------------------------------------------------------------------------------------
