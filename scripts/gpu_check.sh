@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> cmd...
 MODE=${1:-all}
 step smoke 300 python __graft_entry__.py smoke || exit $?
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread
   rc=$?
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 fi

@@ -1,5 +1,7 @@
-"""Persistent loop placement A/B (GPU box): placement 0 (a clip's 8 workgroups on one XCD) vs 1
-(workgroup part p of every clip on XCD p).  Samples must be bit-identical; prints us/step."""
+"""Persistent loop placement A/B (GPU box): placement 0 (XCD-local clip groups: plain hand-off
+stores, L2 flag barriers), 1 (workgroup part p of every clip on XCD p, write-through) and 2 (a
+clip's 8 workgroups on one XCD, write-through).  Samples must be bit-identical; prints us/step
+and, for placement 0, how many launches ran XCD-local / fell back to write-through."""
 import ctypes
 import os
 import sys
@@ -19,19 +21,20 @@ model, diffusion, _, _, _ = pkg.create_model(123, cfg.Model, dtype="bf16", devic
 model.load_state_dict(pkg.init_state_dict(model.arch, seed=0))
 
 
-def diag(ctx, what, v):
+def diag(ctx, what, v, n_out=1):
     arr = (ctypes.c_int32 * 1)(v)
-    out = ctypes.c_double()
-    native.check(ctx.h, ctx.lib.ggd_diag(ctx.h, what, arr, 1, 1, ctypes.cast(ctypes.byref(out), ctypes.c_void_p)), "diag")
-    return out.value
+    out = (ctypes.c_double * n_out)()
+    native.check(ctx.h, ctx.lib.ggd_diag(ctx.h, what, arr, 1, n_out, ctypes.cast(out, ctypes.c_void_p)), "diag")
+    return list(out) if n_out > 1 else out[0]
 
 
-n, steps = int(sys.argv[1]) if len(sys.argv) > 1 else 32, 1000
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+steps = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
 wav = th.randn(n, 32000, device=dev, generator=th.Generator(device=dev).manual_seed(n)) * 0.1
 ctx, _ = model.prepare(wav, 40)
 res = {}
 for rep in range(2):
-    for place in (0, 1):
+    for place in (0, 1, 2):
         diag(ctx, 12, place)
         f = lambda: diffusion.p_sample_loop(model, (n, 123, 40), model_kwargs={"wav": wav}, seed=11, extras=False,
                                             n_steps=steps)["sample"]
@@ -42,6 +45,7 @@ for rep in range(2):
         th.cuda.synchronize()
         dt = (time.perf_counter() - t0) * 1e3
         res[place] = out.clone()
-        print(f"rep {rep} placement {place}: {dt:8.2f} ms ({dt / steps * 1e3:6.1f} us/step)", flush=True)
-print("identical:", bool(th.equal(res[0], res[1])), flush=True)
+        xl = diag(ctx, 13, 0, 2)
+        print(f"rep {rep} placement {place}: {dt:8.2f} ms ({dt / steps * 1e3:6.1f} us/step) xl/fallback {xl}", flush=True)
+print("identical:", bool(th.equal(res[0], res[1])) and bool(th.equal(res[0], res[2])), flush=True)
 diag(ctx, 12, 0)

@@ -143,7 +143,7 @@ struct ggd_ctx {
 
   // persistent reverse loop (ggd_mega.hip)
   bool no_mega = false;                // ggd_diag what = 9: route sampling through per-phase launches
-  int mega_place = 0;                  // ggd_diag what = 12: persistent-loop workgroup placement
+  int mega_place = 0;                  // ggd_diag what = 12: 0 XCD-local, 1 part per XCD, 2 group per XCD
   FusedArgs* mega_fa = nullptr;        // device [n_layers][4]
   unsigned long long* mega_phase_stamps = nullptr;  // ggd_diag what = 11: layer 1's phases + KE
   FinalArgs* mega_fe = nullptr;
@@ -153,6 +153,7 @@ struct ggd_ctx {
   std::vector<FusedArgs> mega_fa_host;
   FinalArgs mega_fe_host{};
   int mega_status_host = 0;
+  int mega_xl_launches = 0, mega_fallbacks = 0;  // last ggd_sample: XCD-local launches, write-through re-runs
   double wall_mhz = 100.0;             // realtime counter rate (hipDeviceAttributeWallClockRate)
 };
 
@@ -1307,9 +1308,15 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     if (p[0] == 0) c->mega_phase_stamps = nullptr;
     return GGD_OK;
   }
-  if (what == 12 && np >= 1) {  // persistent-loop placement: {0} clip group per XCD, {1} part p on XCD p
-    c->mega_place = p[0] == 1 ? 1 : 0;
+  if (what == 12 && np >= 1) {  // persistent-loop placement: {0} XCD-local clip groups (CP_XL, default),
+                                // {1} part p on XCD p (write-through), {2} clip group per XCD (write-through)
+    c->mega_place = p[0] >= 0 && p[0] <= 2 ? p[0] : 0;
     *avg_us = c->mega_place;
+    return GGD_OK;
+  }
+  if (what == 13) {  // last ggd_sample: [XCD-local launches, write-through re-runs]
+    avg_us[0] = c->mega_xl_launches;
+    if (iters > 1) avg_us[1] = c->mega_fallbacks;
     return GGD_OK;
   }
   if (what == 9 && np >= 1) {  // p[0] != 0: sample through the per-phase launches, not the persistent loop
@@ -1551,7 +1558,7 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
     HIP_TRY(c, dalloc(c, &c->mega_fa, sizeof(FusedArgs) * 4 * NL));
     HIP_TRY(c, dalloc(c, &c->mega_fe, sizeof(FinalArgs)));
     HIP_TRY(c, dalloc(c, &c->mega_ctl, sizeof(unsigned) * MEGA_CTL_WORDS));
-    HIP_TRY(c, dalloc(c, &c->mega_status, sizeof(int)));
+    HIP_TRY(c, dalloc(c, &c->mega_status, sizeof(int) * MEGA_MAX_CHUNKS));
   }
   c->mega_fa_host.assign(4 * NL, FusedArgs{});
   for (int li = 0; li < NL; ++li) {
@@ -1579,26 +1586,47 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
   fe.stamps = c->mega_phase_stamps ? c->mega_phase_stamps + 64 : nullptr;
   HIP_TRY(c, hipMemcpyAsync(c->mega_fa, c->mega_fa_host.data(), sizeof(FusedArgs) * 4 * NL, hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipMemcpyAsync(c->mega_fe, &fe, sizeof(FinalArgs), hipMemcpyHostToDevice, s));
-  HIP_TRY(c, hipMemsetAsync(c->mega_status, 0, sizeof(int), s));
   // batches above the loop's capacity run as consecutive launches of up to `cap` clips each
   const int cap = mega_capacity(D.dtype, D.seq_len);
   const int chunks = (a.n + cap - 1) / cap;
+  if (chunks > MEGA_MAX_CHUNKS) return fail(c, GGD_ERR_ARG, "batch too large for the persistent loop");
+  HIP_TRY(c, hipMemsetAsync(c->mega_status, 0, sizeof(int) * MEGA_MAX_CHUNKS, s));
+  // XCD-local variant first (every clip group on one XCD); a chunk it cannot place (status 3,
+  // nothing ran) is launched again on the write-through path
+  const bool xl = c->mega_place == 0;
   if (c->profiling) {
     c->prof.next = 0;
     int r = prof_mark(c, s);
     if (r) return r;
   }
-  for (int c0 = 0; c0 < a.n; c0 += cap) {
-    MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status, c0 == 0 ? c->mega_stamps : nullptr,
-               c0, c->mega_place};
-    HIP_TRY(c, launch_mega(D.dtype, D.seq_len, m, std::min(cap, a.n - c0), s));
+  for (int c0 = 0, ci = 0; c0 < a.n; c0 += cap, ++ci) {
+    MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + ci,
+               c0 == 0 ? c->mega_stamps : nullptr, c0, c->mega_place == 1 ? 1 : 0};
+    HIP_TRY(c, launch_mega(D.dtype, D.seq_len, m, std::min(cap, a.n - c0), xl, s));
   }
   if (c->profiling) {
     int r = prof_mark(c, s);
     if (r) return r;
   }
-  HIP_TRY(c, hipMemcpyAsync(&c->mega_status_host, c->mega_status, sizeof(int), hipMemcpyDeviceToHost, s));
+  int st[MEGA_MAX_CHUNKS];
+  HIP_TRY(c, hipMemcpyAsync(st, c->mega_status, sizeof(int) * MEGA_MAX_CHUNKS, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
+  c->mega_xl_launches = 0;
+  c->mega_fallbacks = 0;
+  for (int c0 = 0, ci = 0; c0 < a.n; c0 += cap, ++ci) {
+    if (st[ci] != 3) {
+      c->mega_xl_launches += xl ? 1 : 0;
+      continue;
+    }
+    ++c->mega_fallbacks;
+    MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + ci, nullptr, c0, 0};
+    HIP_TRY(c, hipMemsetAsync(c->mega_status + ci, 0, sizeof(int), s));
+    HIP_TRY(c, launch_mega(D.dtype, D.seq_len, m, std::min(cap, a.n - c0), false, s));
+    HIP_TRY(c, hipMemcpyAsync(st + ci, c->mega_status + ci, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  c->mega_status_host = 0;
+  for (int ci = 0; ci < chunks; ++ci) c->mega_status_host = std::max(c->mega_status_host, st[ci]);
   if (c->mega_status_host)
     return fail(c, GGD_ERR_HIP, c->mega_status_host == 2 ? "persistent loop: workgroups were not all resident"
                                                           : "persistent loop: a clip-group barrier timed out");

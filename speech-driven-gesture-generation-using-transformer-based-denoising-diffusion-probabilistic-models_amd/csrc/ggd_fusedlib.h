@@ -80,6 +80,12 @@ __device__ __forceinline__ float4 ld_f4(const float* p) {
 // (device-coherent on any placement; with the group on one XCD both stay in its L2).
 // ------------------------------------------------------------------------------------------
 constexpr int CP_KERNEL = 0, CP_COH = 16;
+// CP_XL (persistent loop, every clip group on ONE XCD, checked at launch): the group shares that
+// XCD's L2, so hand-off stores stay plain (the line stays in L2, which the readers' sc1 loads hit)
+// instead of writing through to the Infinity Cache; loads are still sc1 (past the CU's L1).
+constexpr int CP_XL = 17;
+__host__ __device__ constexpr int cp_load(int cp) { return cp == CP_XL ? CP_COH : cp; }
+__host__ __device__ constexpr int cp_store(int cp) { return cp == CP_XL ? 0 : cp; }
 
 // bounded stores: a raw buffer resource over a clip's output rows; the hardware drops stores
 // past num_records, so padded rows are written without a branch.  (A store under a divergent
@@ -91,13 +97,13 @@ template <int CP = CP_KERNEL> struct OutRowsP {
   __device__ __forceinline__ void put4(uint32_t elem, float4 v) const {  // 4 f32 at elem
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
     const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)(elem * 4), 0, CP);
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)(elem * 4), 0, cp_store(CP));
   }
   template <typename T> __device__ __forceinline__ void put(uint32_t elem, float v) const {
     if constexpr (sizeof(T) == 2)
-      __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, (int)(elem * 2), 0, CP);
+      __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, (int)(elem * 2), 0, cp_store(CP));
     else
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(elem * 4), 0, CP);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(elem * 4), 0, cp_store(CP));
   }
 };
 using OutRows = OutRowsP<CP_KERNEL>;
@@ -109,7 +115,7 @@ __device__ __forceinline__ float ld_f32(const float* base, uint32_t idx) {
     return G(base)[idx];
   } else {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(idx * 4), 0, CP));
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(idx * 4), 0, cp_load(CP)));
   }
 }
 template <int CP>
@@ -121,7 +127,7 @@ __device__ __forceinline__ uint4 ld_16B(const void* base, uint32_t byte_off) {
   } else {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, CP);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, cp_load(CP));
     return make_uint4(v.x, v.y, v.z, v.w);
   }
 }
@@ -151,7 +157,7 @@ __device__ __forceinline__ void glds_rows(void* dst, size_t sd, const void* src,
   for (int p = wave; p < rows * pieces; p += NT / 64) {
     const int r = p / pieces, q = p - r * pieces;
     __builtin_amdgcn_global_load_lds((const void*)((const char*)src + r * ss + q * 1024 + lane * 16),
-                                     (lds_void*)((char*)dst + r * sd + q * 1024), 16, 0, CP);
+                                     (lds_void*)((char*)dst + r * sd + q * 1024), 16, 0, cp_load(CP));
   }
 }
 

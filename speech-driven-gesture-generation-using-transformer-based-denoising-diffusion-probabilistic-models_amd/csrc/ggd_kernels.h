@@ -186,14 +186,16 @@ struct MegaArgs {
   const FinalArgs* fe;   // device: KE args (do_out, do_update)
   int n_layers, k0, n_steps;
   unsigned* ctl;         // control words (MEGA_CTL_WORDS), zeroed before every launch
-  int* status;           // 0 ok, 1 clip-group barrier timed out, 2 workgroups not co-resident
+  int* status;           // 0 ok, 1 clip-group barrier timed out, 2 workgroups not co-resident,
+                         // 3 (XCD-local launch) a clip group could not be placed on one XCD: nothing ran
   unsigned long long* stamps;  // diagnostics: clip 0 / part 0 stamps s_memtime around every barrier
                                // of the first MEGA_STAMP_STEPS iterations ([phase][2]: done, passed)
   int clip0;             // first clip of this launch (batches above the capacity run as chunks)
   int placement;         // 0: a clip's 8 workgroups share one XCD; 1: workgroup part p of every clip on XCD p
 };
 constexpr int MEGA_STAMP_STEPS = 2;
-constexpr int MEGA_CTL_WORDS = 256 + 32 * 16;
+constexpr int MEGA_MAX_CHUNKS = 16;  // status words: one per launch of up to mega_capacity() clips
+constexpr int MEGA_CTL_WORDS = 256 + 32 * 16 + 32 * 32;  // tickets/arrival, group counters, group flag lines
 
 // launchers (return hipError_t of the launch)
 hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s);  // 0 KA, 1 KB, 2 KC, 3 KD
@@ -201,7 +203,8 @@ hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s);
 bool fused_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
 bool persist_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
-hipError_t launch_mega(int dtype, int L, const MegaArgs& a, int n, hipStream_t s);
+// xl: the XCD-local variant (CP_XL, grid padded to whole XCDs; placement 0 only)
+hipError_t launch_mega(int dtype, int L, const MegaArgs& a, int n, bool xl, hipStream_t s);
 int mega_capacity(int dtype, int L);   // clips one launch can hold (all workgroups co-resident)
 hipError_t launch_mb(int mode, void* buf, size_t buf_bytes, int arg, int blocks, hipStream_t s);  // ggd_diag.hip
 hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream_t s);

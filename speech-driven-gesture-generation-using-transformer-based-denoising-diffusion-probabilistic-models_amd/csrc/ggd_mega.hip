@@ -24,7 +24,7 @@
 namespace ggd {
 
 constexpr int MK_SPIN_LIMIT = 1 << 21;   // ~ seconds: only a broken launch ever gets there
-constexpr int MK_ARRIVE = 128, MK_OVF = 144, MK_GROUP = 256;
+constexpr int MK_ARRIVE = 128, MK_OVF = 144, MK_GROUP = 256, MK_FLAGS = 256 + 32 * 16;
 
 __device__ __forceinline__ unsigned mk_load(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -76,46 +76,107 @@ __device__ int mk_role(const MegaArgs& m, int nwg) {
   return ((x + 8 * (s >> 3)) << 3) | (s & 7);
 }
 
+// XCD-local placement (CP_XL): the grid is padded to 8 workgroups per XCD per 8 clip groups, so
+// that XCD x can host every group g with g % 8 == x.  After all workgroups have arrived, every
+// XCD must hold at least its groups' slots; otherwise the whole launch leaves before any work
+// with status 3 and the host runs it again on the write-through path.  Surplus workgroups idle.
+// thread 0: (clip << 3 | part), -2 (idle surplus), or -1 (status set)
+__device__ int mk_role_xl(const MegaArgs& m, int nwg, int G) {
+  unsigned* ctl = m.ctl;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 7;
+  const int t = (int)mk_add(ctl + xcc * 16, 1u);
+  __hip_atomic_fetch_add(ctl + MK_ARRIVE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  for (int spin = 0; __hip_atomic_load(ctl + MK_ARRIVE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg;
+       ++spin) {
+    if (spin > MK_SPIN_LIMIT) {
+      atomicMax(m.status, 2);
+      return -1;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  for (int x = 0; x < 8; ++x)  // every workgroup reads the same final counts: a launch-wide verdict
+    if ((int)mk_load(ctl + x * 16) < mk_slots(x, G, 0)) {
+      atomicMax(m.status, 3);
+      return -1;
+    }
+  if (t >= mk_slots((int)xcc, G, 0)) return -2;
+  return (((int)xcc + 8 * (t >> 3)) << 3) | (t & 7);
+}
+
 // barrier of the clip's 8 workgroups; epoch counts the barriers passed so far (+1).  After the
 // arrival every wave issues `prefetch` (the next phase's weight fragments); the exit barrier does
 // not wait for vector memory, so that stream stays in flight across the wait.
-template <typename F>
-__device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned epoch, int* status, int* s_ok,
-                                        unsigned long long* st, F&& prefetch) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores landed
+// Write-through path (CP_COH): one agent-scope counter per group.  XCD-local path (CP_XL): the
+// group's 8 workgroups share one L2, so each publishes its epoch with a plain store into its own
+// word of the group's flag line (after its waves' stores have reached that L2) and wave 0 polls
+// the 8 words with sc1 loads -- L2 round trips instead of memory-side atomics.
+template <int CPV, typename F>
+__device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part, unsigned epoch, int* status,
+                                        int* s_ok, unsigned long long* st, F&& prefetch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's hand-off stores landed
   __syncthreads();
   if (st && threadIdx.x == 0) st[2 * (epoch - 1)] = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 0) mk_add(ctr, 1u);
-  prefetch();
-  if (threadIdx.x == 0) {
-    const unsigned target = 8u * epoch;
-    int ok = 1;
-    for (int spin = 0; mk_load(ctr) < target; ++spin) {
-      if ((spin & 255) == 255 && (spin > MK_SPIN_LIMIT || __hip_atomic_load(status, __ATOMIC_RELAXED,
-                                                                             __HIP_MEMORY_SCOPE_AGENT))) {
-        atomicMax(status, 1);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+  if constexpr (CPV == CP_XL) {
+    if (threadIdx.x == 0) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(flags, (short)0, 32, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(epoch, r, part * 4, 0, 0);
     }
-    *s_ok = ok;
+  } else {
+    if (threadIdx.x == 0) mk_add(ctr, 1u);
+  }
+  prefetch();
+  if constexpr (CPV == CP_XL) {
+    if (threadIdx.x < 64) {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(flags, (short)0, 32, 0x00020000);
+      const int off = (threadIdx.x & 7) * 4;
+      int ok = 1;
+      for (int spin = 0;; ++spin) {
+        const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
+        if (__ballot(v < epoch) == 0) break;
+        if ((spin & 255) == 255 && (spin > MK_SPIN_LIMIT || __hip_atomic_load(status, __ATOMIC_RELAXED,
+                                                                               __HIP_MEMORY_SCOPE_AGENT))) {
+          if (threadIdx.x == 0) atomicMax(status, 1);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (threadIdx.x == 0) *s_ok = ok;
+    }
+  } else {
+    if (threadIdx.x == 0) {
+      const unsigned target = 8u * epoch;
+      int ok = 1;
+      for (int spin = 0; mk_load(ctr) < target; ++spin) {
+        if ((spin & 255) == 255 && (spin > MK_SPIN_LIMIT || __hip_atomic_load(status, __ATOMIC_RELAXED,
+                                                                               __HIP_MEMORY_SCOPE_AGENT))) {
+          atomicMax(status, 1);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      *s_ok = ok;
+    }
   }
   bar_lds();
   if (st && threadIdx.x == 0) st[2 * (epoch - 1) + 1] = __builtin_amdgcn_s_memtime();
   return *s_ok != 0;
 }
 
-template <typename T, int RT>
-__global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m) {
+template <typename T, int RT, int CPV>
+__global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_role, s_ok;
-  if (threadIdx.x == 0) s_role = mk_role(m, gridDim.x);
+  if (threadIdx.x == 0) s_role = CPV == CP_XL ? mk_role_xl(m, gridDim.x, G) : mk_role(m, gridDim.x);
   __syncthreads();
   const int role = s_role;
   if (role < 0) return;
   const int grp = role >> 3, b = m.clip0 + grp, part = role & 7, lane = ltid() & 63, wave = ltid() >> 6;
   unsigned* ctr = m.ctl + MK_GROUP + grp * 16;
+  unsigned* flags = m.ctl + MK_FLAGS + grp * 32;
   unsigned epoch = 0;
   if (m.stamps && role == 0 && threadIdx.x == 0) m.stamps[2 * 17 * MEGA_STAMP_STEPS] = __builtin_amdgcn_s_memtime();
   // per-phase arguments as constant-address-space objects: field reads are scalar loads
@@ -134,22 +195,22 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m) {
     for (int li = 0; li < NL; ++li) {
       cfa_t f = fa0 + 4 * li;
       asm volatile("" : "+s"(f));  // per-layer arguments are re-read, not held across the loop
-      ka_phase<T, RT, CP_COH>(f[0], part, b, smem, pn);
+      ka_phase<T, RT, CPV>(f[0], part, b, smem, pn);
       KBPre<T, RT> pb(f[1], wave);
-      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st, [&] { pb.load(lane); })) return;
-      kb_phase<T, RT, CP_COH>(f[1], part, b, it, smem, pb);
+      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pb.load(lane); })) return;
+      kb_phase<T, RT, CPV>(f[1], part, b, it, smem, pb);
       KCPre<T, RT> pc(f[2], part, wave);
-      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st, [&] { pc.load(lane); })) return;
-      kc_phase<T, RT, CP_COH>(f[2], part, b, smem, pc);
+      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pc.load(lane); })) return;
+      kc_phase<T, RT, CPV>(f[2], part, b, smem, pc);
       KDPre<T, RT> pd(f[3], part, wave);
-      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st, [&] { pd.load(lane); })) return;
-      kd_phase<T, RT, CP_COH>(f[3], part, b, smem, pd);
+      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pd.load(lane); })) return;
+      kd_phase<T, RT, CPV>(f[3], part, b, smem, pd);
       pn = li + 1 < NL ? ka_pre<T, RT>(f[4], part, wave) : ke_pre<T, RT>(*fe, part);
-      if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); })) return;
+      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); })) return;
     }
-    ke_phase<T, RT, CP_COH>(*fe, part, b, it, smem, pn);
+    ke_phase<T, RT, CPV>(*fe, part, b, it, smem, pn);
     pn = ka_pre<T, RT>(fa0[0], part, wave);
-    if (!mk_sync(ctr, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); })) return;
+    if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); })) return;
   }
 }
 
@@ -165,7 +226,7 @@ template <typename T, int RT>
 static int mk_capacity_t() {
   static int cap = -1;
   if (cap < 0) {
-    (void)hipFuncSetAttribute((const void*)mk_kernel<T, RT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)mk_kernel<T, RT, CP_COH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     // residency from the LDS budget (the occupancy query rejects > 64 KiB of dynamic LDS):
     // one 512-thread workgroup per CU
     int dev = 0, cus = 0, lds_cu = 0;
@@ -186,19 +247,30 @@ int mega_capacity(int dtype, int L) {
   return mk_rt3(L) ? mk_capacity_t<bf16_t, 3>() : mk_capacity_t<bf16_t, 4>();
 }
 
-hipError_t launch_mega(int dtype, int L, const MegaArgs& a, int n, hipStream_t s) {
+template <typename T, int RT>
+static hipError_t launch_mega_t(const MegaArgs& a, int n, bool xl, hipStream_t s) {
+  const int G = n, nwg = xl ? 64 * ((G + 7) / 8) : 8 * G;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)mk_kernel<T, RT, CP_XL>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)mk_kernel<T, RT, CP_COH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();
+    attr = true;
+  }
+  if (xl)
+    hipLaunchKernelGGL((mk_kernel<T, RT, CP_XL>), dim3(nwg), dim3(FT), (mk_lds<T, RT>()), s, a, G);
+  else
+    hipLaunchKernelGGL((mk_kernel<T, RT, CP_COH>), dim3(nwg), dim3(FT), (mk_lds<T, RT>()), s, a, G);
+  return hipGetLastError();
+}
+
+hipError_t launch_mega(int dtype, int L, const MegaArgs& a, int n, bool xl, hipStream_t s) {
   if (n < 1 || n > mega_capacity(dtype, L)) return hipErrorInvalidValue;
-  const dim3 blk(FT), grid(8 * n);
+  if (xl && (a.placement != 0 || 64 * ((n + 7) / 8) > 8 * mega_capacity(dtype, L))) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(a.ctl, 0, sizeof(unsigned) * MEGA_CTL_WORDS, s);
   if (e != hipSuccess) return e;
-  if (dtype == 0) {
-    if (mk_rt3(L)) hipLaunchKernelGGL((mk_kernel<float, 3>), grid, blk, (mk_lds<float, 3>()), s, a);
-    else hipLaunchKernelGGL((mk_kernel<float, 4>), grid, blk, (mk_lds<float, 4>()), s, a);
-  } else {
-    if (mk_rt3(L)) hipLaunchKernelGGL((mk_kernel<bf16_t, 3>), grid, blk, (mk_lds<bf16_t, 3>()), s, a);
-    else hipLaunchKernelGGL((mk_kernel<bf16_t, 4>), grid, blk, (mk_lds<bf16_t, 4>()), s, a);
-  }
-  return hipGetLastError();
+  if (dtype == 0) return mk_rt3(L) ? launch_mega_t<float, 3>(a, n, xl, s) : launch_mega_t<float, 4>(a, n, xl, s);
+  return mk_rt3(L) ? launch_mega_t<bf16_t, 3>(a, n, xl, s) : launch_mega_t<bf16_t, 4>(a, n, xl, s);
 }
 
 }  // namespace ggd

@@ -52,7 +52,7 @@ __device__ __forceinline__ StepRec ld_rec(const StepRec* p) {
 // full rows redundantly anyway -- so only KA / KE gather them and only KD publishes them.
 // (As separate launches, or with f32 images that do not fit beside them, Hs is re-read.)
 template <typename T, int CP> struct Res {
-  static constexpr bool ON = CP == CP_COH && sizeof(T) == 2;
+  static constexpr bool ON = CP != CP_KERNEL && sizeof(T) == 2;
   static constexpr size_t BASE = ON ? Plan<T>::HS : 0;  // start of the phase-private LDS
 };
 

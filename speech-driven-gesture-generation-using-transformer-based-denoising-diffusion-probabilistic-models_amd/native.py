@@ -64,13 +64,16 @@ def build(force=False, verbose=False):
     flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-value", "-Wno-unused-result"]
     objs, procs = [], []
     os.makedirs(os.path.join(PKG_DIR, "build"), exist_ok=True)
+    hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
     for src in SOURCES:  # one hipcc per translation unit, in parallel
         obj = os.path.join(PKG_DIR, "build", src.replace(".hip", ".o"))
+        objs.append(obj)
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(os.path.join(CSRC, src))):
+            continue  # object newer than its source and every header
         cmd = ["hipcc"] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append(subprocess.Popen(cmd, cwd=CSRC))
-        objs.append(obj)
     if any(p.wait() != 0 for p in procs):
         raise RuntimeError("hipcc failed")
     cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", LIB_PATH + ".tmp"]
