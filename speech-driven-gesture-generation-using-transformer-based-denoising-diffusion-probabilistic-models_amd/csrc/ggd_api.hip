@@ -335,9 +335,12 @@ int pack_frag(ggd_ctx* c, FLin& F, const std::vector<const float*>& rows_w, cons
   return GGD_OK;
 }
 
-// rows of the named Linear(s) in the given order; `order` indexes the concatenated rows
+// rows of the named Linear(s) in the given order; `order` indexes the concatenated rows.
+// ln: the LayerNorm in front of this Linear (nn.LayerNorm([d]) of models/nn.py:141-147,212),
+// folded in: LN(x) W^T + b = xhat (W diag(gamma))^T + (b + W beta), xhat = (x - mu) / sigma,
+// so the fused kernels write the bare normalised rows (no per-column affine).  Folded in f64.
 int frag_from(ggd_ctx* c, FLin& F, const std::vector<std::string>& prefixes, int n_each, int k,
-              const std::vector<int>& order) {
+              const std::vector<int>& order, const std::string& ln = "") {
   std::vector<const float*> rw;
   std::vector<float> bias;
   std::vector<const std::vector<float>*> W, B;
@@ -348,10 +351,31 @@ int frag_from(ggd_ctx* c, FLin& F, const std::vector<std::string>& prefixes, int
     W.push_back(w);
     B.push_back(b);
   }
-  for (int r : order) {
-    const int p = r / n_each, i = r % n_each;
-    rw.push_back(W[p]->data() + (size_t)i * k);
-    bias.push_back((*B[p])[i]);
+  const std::vector<float>* g = nullptr;
+  const std::vector<float>* be = nullptr;
+  if (!ln.empty()) {
+    g = get(c, ln + ".weight", (size_t)k);
+    be = get(c, ln + ".bias", (size_t)k);
+    if (!g || !be) return GGD_ERR_NAME;
+  }
+  std::vector<std::vector<float>> folded(g ? order.size() : 0);
+  for (size_t oi = 0; oi < order.size(); ++oi) {
+    const int r = order[oi], p = r / n_each, i = r % n_each;
+    const float* row = W[p]->data() + (size_t)i * k;
+    float bv = (*B[p])[i];
+    if (g) {
+      std::vector<float>& fr = folded[oi];
+      fr.resize(k);
+      double acc = (double)bv;
+      for (int kk = 0; kk < k; ++kk) {
+        fr[kk] = row[kk] * (*g)[kk];
+        acc += (double)row[kk] * (double)(*be)[kk];
+      }
+      row = fr.data();
+      bv = (float)acc;
+    }
+    rw.push_back(row);
+    bias.push_back(bv);
   }
   return pack_frag(c, F, rw, bias, k);
 }
@@ -1052,7 +1076,7 @@ int ggd_finalize_weights(ggd_ctx* c) {
              fused_supported(D.dtype, D.d_model, D.heads, D.seq_len, D.speech_len, D.d_pose);
   if (c->fused) {
     TRY(frag_from(c, c->f_emb, {P + "emb_x"}, d, C, iota_n(d)));
-    TRY(frag_from(c, c->f_out, {P + "out_layers.1"}, C, d, iota_n(C)));
+    TRY(frag_from(c, c->f_out, {P + "out_layers.1"}, C, d, iota_n(C), P + "out_layers.0"));
     std::vector<int> head_major;  // per head h: q rows h*32.., k rows 256 + h*32.., v rows 512 + h*32..
     for (int h = 0; h < D.heads; ++h)
       for (int part = 0; part < 3; ++part)
@@ -1062,11 +1086,11 @@ int ggd_finalize_weights(ggd_ctx* c) {
       const std::string q = P + "layers." + std::to_string(l) + ".";
       const std::string sa = q + "self_attn.", ca = q + "cross_attn.";
       TRY(frag_from(c, Ly.f_qkv, {sa + "query.0.linear", sa + "key.0.linear", sa + "value.0.linear"}, d, d,
-                    head_major));
+                    head_major, q + "norm_self_attn"));
       TRY(frag_from(c, Ly.f_o_sa, {sa + "output"}, d, d, iota_n(d)));
-      TRY(frag_from(c, Ly.f_q_ca, {ca + "query.0.linear"}, d, d, iota_n(d)));
+      TRY(frag_from(c, Ly.f_q_ca, {ca + "query.0.linear"}, d, d, iota_n(d), q + "norm_cross_attn"));
       TRY(frag_from(c, Ly.f_o_ca, {ca + "output"}, d, d, iota_n(d)));
-      TRY(frag_from(c, Ly.f_ff1, {q + "feed_forward.layer1"}, 4 * d, d, iota_n(4 * d)));
+      TRY(frag_from(c, Ly.f_ff1, {q + "feed_forward.layer1"}, 4 * d, d, iota_n(4 * d), q + "norm_ff"));
       TRY(frag_from(c, Ly.f_ff2, {q + "feed_forward.layer2"}, d, 4 * d, iota_n(d)));
     }
   }

@@ -72,6 +72,19 @@ __device__ __forceinline__ float4 ld_f4(const float* p) {
     }                                                                                           \
   } while (0)
 
+// Buffer resource over `bytes` bytes at a wave-uniform base.  The base and the size are passed
+// through readfirstlane so the compiler can PROVE the descriptor uniform: otherwise it wraps
+// every buffer op in a waterfall loop (readfirstlane x4, compare, s_and_saveexec, op, loop) --
+// slow, and ROCm 7.2's register allocator was seen placing a spill store between such a loop
+// and the restore of EXEC (psk_kernel: the store ran with no lanes enabled and a live value of
+// the pose state was lost).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uni_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t v = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
 // ------------------------------------------------------------------------------------------
 // Cache policy of the loads / stores that carry data between decoder phases.  CP_KERNEL (0):
 // the phases are separate launches, the kernel boundary makes their data visible.  CP_COH (sc1):
@@ -93,7 +106,7 @@ __host__ __device__ constexpr int cp_store(int cp) { return cp == CP_XL ? 0 : cp
 template <int CP = CP_KERNEL> struct OutRowsP {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ OutRowsP(void* base, uint32_t bytes)
-      : r(__builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000)) {}
+      : r(uni_rsrc(base, bytes)) {}
   __device__ __forceinline__ void put4(uint32_t elem, float4 v) const {  // 4 f32 at elem
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
     const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
@@ -114,7 +127,7 @@ __device__ __forceinline__ float ld_f32(const float* base, uint32_t idx) {
   if constexpr (CP == CP_KERNEL) {
     return G(base)[idx];
   } else {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r = uni_rsrc(base, 0x7fffffffu);
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(idx * 4), 0, cp_load(CP)));
   }
 }
@@ -125,7 +138,7 @@ __device__ __forceinline__ uint4 ld_16B(const void* base, uint32_t byte_off) {
     const u32x4 v = *G((const u32x4*)((const char*)base + byte_off));
     return make_uint4(v.x, v.y, v.z, v.w);
   } else {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r = uni_rsrc(base, 0x7fffffffu);
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, cp_load(CP));
     return make_uint4(v.x, v.y, v.z, v.w);
@@ -347,6 +360,61 @@ __device__ __forceinline__ void ln_apply(const float* Hs, int L, const float2* s
       *(uint2*)(img + r * SXI + c4) = make_uint2(lo, hi);
     } else {
       *(float4*)(img + r * SXI + c4) = make_float4(y0, y1, y2, y3);
+    }
+  }
+}
+
+// One-pass LayerNorm without the affine (gamma / beta are folded into the consuming Linear at
+// finalize, ggd_api.hip frag_from): row r of the f32 image Hs (stride SH) -> (x - mu) / sigma into
+// the T image (stride SXI).  Each row is held by 8 lanes, 32 values each, in registers: mean,
+// centred variance (two-pass, as torch) and the normalised output need no LDS round trip and no
+// barrier between them.  Rows L .. NR - 1 are written as zeros.
+template <typename T, int NT, int NR, int SXI = Frag<T>::SX>
+__device__ __forceinline__ void ln_rows(const float* Hs, int L, T* img, int tid = ltid()) {
+  constexpr int RPP = NT / 8;  // rows per pass
+  const int j = tid & 7;
+#pragma unroll
+  for (int r0 = 0; r0 < NR; r0 += RPP) {
+    const int r = r0 + (tid >> 3);
+    if (r0 + RPP > NR && r >= NR) break;
+    if (r < L) {
+      float4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = *(const float4*)(Hs + r * SH + (j + 8 * i) * 4);
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+      const float mu = group_sum<8>(s) * (1.0f / (float)FD);
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[i].x -= mu;
+        v[i].y -= mu;
+        v[i].z -= mu;
+        v[i].w -= mu;
+        q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+      }
+      const float rs = __builtin_amdgcn_rsqf(group_sum<8>(q) * (1.0f / (float)FD) + 1e-5f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c4 = (j + 8 * i) * 4;
+        if constexpr (sizeof(T) == 2) {
+          const uint32_t lo = (uint32_t)f2bf(v[i].x * rs) | ((uint32_t)f2bf(v[i].y * rs) << 16);
+          const uint32_t hi = (uint32_t)f2bf(v[i].z * rs) | ((uint32_t)f2bf(v[i].w * rs) << 16);
+          *(uint2*)(img + r * SXI + c4) = make_uint2(lo, hi);
+        } else {
+          *(float4*)(img + r * SXI + c4) = make_float4(v[i].x * rs, v[i].y * rs, v[i].z * rs, v[i].w * rs);
+        }
+      }
+    } else if (r < NR) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c4 = (j + 8 * i) * 4;
+        if constexpr (sizeof(T) == 2)
+          *(uint2*)(img + r * SXI + c4) = make_uint2(0u, 0u);
+        else
+          *(float4*)(img + r * SXI + c4) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   }
 }

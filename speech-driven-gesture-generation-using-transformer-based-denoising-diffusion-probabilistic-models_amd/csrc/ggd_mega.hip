@@ -120,7 +120,7 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
   if (st && threadIdx.x == 0) st[2 * (epoch - 1)] = __builtin_amdgcn_s_memtime();
   if constexpr (CPV == CP_XL) {
     if (threadIdx.x == 0) {
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(flags, (short)0, 32, 0x00020000);
+      const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
       __builtin_amdgcn_raw_buffer_store_b32(epoch, r, part * 4, 0, 0);
     }
   } else {
@@ -129,7 +129,7 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
   prefetch();
   if constexpr (CPV == CP_XL) {
     if (threadIdx.x < 64) {
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(flags, (short)0, 32, 0x00020000);
+      const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
       const int off = (threadIdx.x & 7) * 4;
       int ok = 1;
       for (int spin = 0;; ++spin) {

@@ -58,14 +58,14 @@ __device__ __forceinline__ void pload(uint4 (&f)[N], const void* W, int kt_total
   static_assert(NJ * KS <= N && NJ <= NTL, "fragment buffer / tile list too small");
   // buffer loads: the SGPR resource + scalar byte offset carry the (tile, step) address, so all
   // fragment loads of a wave share ONE vector register (lane * 16) instead of a 64-bit address each
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W), (short)0, 0x7fffffff,
-                                                                       0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = uni_rsrc(W, 0x7fffffffu);
   typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (tiles[j] * kt_total + k0 + s) * 1024, 0);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+          rs, lane * 16, __builtin_amdgcn_readfirstlane((tiles[j] * kt_total + k0 + s) * 1024), 0);
       f[j * KS + s] = make_uint4(v.x, v.y, v.z, v.w);
     }
 }
@@ -266,10 +266,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
       const FusedLayer& w = a.layers[li];
       // ---------------- self-attention block (nn.py:160-162) ----------------
       {
-        const float4 g = *(const float4*)(w.ln1_g + c4), bb = *(const float4*)(w.ln1_b + c4);
-        ln_stats<R, 8>(Hs, L, st, tid);
-        bar_lds();
-        ln_apply<T, NT, R, SX>(Hs, L, st, g, bb, Xn, tid);
+        ln_rows<T, NT, R, SX>(Hs, L, Xn, tid);  // LN1 affine folded into the next Linear
         bar_lds();
       }
       for (int hp = 0; hp < 4; ++hp) {
@@ -341,10 +338,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
       }
       // ---------------- cross-attention block (nn.py:163-167) ----------------
       {
-        const float4 g = *(const float4*)(w.ln2_g + c4), bb = *(const float4*)(w.ln2_b + c4);
-        ln_stats<R, 8>(Hs, L, st, tid);
-        bar_lds();
-        ln_apply<T, NT, R, SX>(Hs, L, st, g, bb, Xn, tid);
+        ln_rows<T, NT, R, SX>(Hs, L, Xn, tid);  // LN2 affine folded into the next Linear
         bar_lds();
       }
       // memory K / V (pre-conv) of a head: row 0 = the step token of t, rows 1.. the cached
@@ -440,10 +434,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
       }
       // ---------------- feed-forward block (nn.py:170-172) ----------------
       {
-        const float4 g = *(const float4*)(w.ln3_g + c4), bb = *(const float4*)(w.ln3_b + c4);
-        ln_stats<R, 8>(Hs, L, st, tid);
-        bar_lds();
-        ln_apply<T, NT, R, SX>(Hs, L, st, g, bb, Xn, tid);
+        ln_rows<T, NT, R, SX>(Hs, L, Xn, tid);  // LN3 affine folded into the next Linear
         bar_lds();
       }
       {
@@ -513,10 +504,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
     PSTAMP(4);
     // ---------------- out_layers + posterior update (nn.py:211-214,228; gaussian_diffusion.py) -------
     {
-      const float4 g = *(const float4*)(a.ln_g + c4), bb = *(const float4*)(a.ln_b + c4);
-      ln_stats<R, 8>(Hs, L, st, tid);
-      bar_lds();
-      ln_apply<T, NT, R, SX>(Hs, L, st, g, bb, Xn, tid);
+      ln_rows<T, NT, R, SX>(Hs, L, Xn, tid);  // out_layers.0 affine folded into out_layers.1
       bar_lds();
     }
     {

@@ -190,7 +190,6 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
   const int nq = wave < 6 ? 1 : 0;
   auto& gm = pre.g;
   const float bias = G(w.qkv_b)[h * 96 + min(wave, 5) * 16 + c16];
-  const float4 lg = ld_f4(w.ln1_g + (tid & 63) * 4), lb = ld_f4(w.ln1_b + (tid & 63) * 4);
   const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
               cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
@@ -207,9 +206,7 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
     bar_lds();
     if (!R::ON) store_rows<CP>(a.h + (size_t)b * L * FD, Hs, L, h);  // the residual rows KB reads
   }
-  ln_stats<RT * 16, 8>(Hs, L, st);
-  bar_lds();
-  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Xn);
+  ln_rows<T, FT, RT * 16>(Hs, L, Xn);
   bar_lds();
   STAMP(1);
   // (kernel path) Hs is dead from here: Y and the attention images overlay it
@@ -270,7 +267,6 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   float bo[2];
   bo[0] = G(w.o_sa_b)[(2 * wave) * 16 + c16];
   bo[1] = G(w.o_sa_b)[(2 * wave + 1) * 16 + c16];
-  const float4 lg = ld_f4(w.ln2_g + (tid & 63) * 4), lb = ld_f4(w.ln2_b + (tid & 63) * 4);
   so.store(Ax, L);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   STAMP(1);
@@ -297,9 +293,7 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   bar_lds();
   STAMP(2);
   if (!R::ON) store_rows<CP>(a.h_out + row0 * FD, Hs, L, h);
-  ln_stats<RT * 16, 8>(Hs, L, st);
-  bar_lds();
-  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Ax);
+  ln_rows<T, FT, RT * 16>(Hs, L, Ax);
   bar_lds();
   STAMP(3);
   // (kernel path) Hs is dead: Yq, raw and the attention images overlay it
@@ -360,7 +354,6 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   float bo[2];
   bo[0] = G(w.o_ca_b)[(2 * wave) * 16 + c16];
   bo[1] = G(w.o_ca_b)[(2 * wave + 1) * 16 + c16];
-  const float4 lg = ld_f4(w.ln3_g + (tid & 63) * 4), lb = ld_f4(w.ln3_b + (tid & 63) * 4);
   so.store(Ax, L);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   STAMP(1);
@@ -372,9 +365,7 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   bar_lds();
   STAMP(2);
   if (!R::ON) store_rows<CP>(a.h_out + row0 * FD, Hs, L, c);
-  ln_stats<RT * 16, 8>(Hs, L, st);
-  bar_lds();
-  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Ax);
+  ln_rows<T, FT, RT * 16>(Hs, L, Ax);
   bar_lds();
   STAMP(3);
   f32x4 acc[RT][1];
@@ -501,7 +492,6 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
 #pragma unroll
   for (int k = 0; k < KT; ++k) go.wb[0][k] = pre.g.wb[0][k];
   const float bo = G(a.b_out)[p * 16 + c16];
-  const float4 lg = ld_f4(a.ln_g + (tid & 63) * 4), lb = ld_f4(a.ln_b + (tid & 63) * 4);
   // the thread's quad: elements e0 + 4 tid .. + 3 (issued now, consumed after the GEMM)
   const bool upd = a.do_update && 4 * tid < ne;
   StepRec rec{};
@@ -530,9 +520,7 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
     }
   }
   __syncthreads();  // LDS-DMA rows and every operand above have landed
-  ln_stats<RT * 16, 8>(Hs, L, st);
-  bar_lds();
-  ln_apply<T, FT, RT * 16>(Hs, L, st, lg, lb, Xn);
+  ln_rows<T, FT, RT * 16>(Hs, L, Xn);
   bar_lds();
   STAMP(1);
   if (wave < RT) {

@@ -61,7 +61,10 @@ def build(force=False, verbose=False):
     """Compile libggd.so for gfx950 with hipcc (cross-compiles without a GPU)."""
     if not force and not is_stale():
         return LIB_PATH
-    flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-value", "-Wno-unused-result"]
+    # -fno-slp-vectorize: no packed-f32 (v_pk_*_f32) code from the SLP vectorizer.  Beside MFMAs it
+    # costs issue slots (MI355X_MICROARCH.md, filler prices), and with it hipcc 7.2 clobbered a live
+    # register of psk_kernel (the per-thread pose state) around the one-pass LayerNorm.
+    flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-fno-slp-vectorize", "-Wno-unused-value", "-Wno-unused-result"]
     objs, procs = [], []
     os.makedirs(os.path.join(PKG_DIR, "build"), exist_ok=True)
     hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
