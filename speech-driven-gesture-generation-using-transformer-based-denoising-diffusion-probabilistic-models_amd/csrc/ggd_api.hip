@@ -114,6 +114,7 @@ struct ggd_ctx {
 
   // memory
   float* kv_mem = nullptr;   // [layers][maxB*Ts][2d]
+  void* kvc = nullptr;       // fused paths: [layers][maxB][heads][KVC_ELEMS] T, convolved step-invariant K | V^T
   float* mem_tmp = nullptr;  // [maxB*Ts][d]
   float* tok_tmp = nullptr;  // [maxB*Ts][d]
   int mem_n = -1;
@@ -511,6 +512,7 @@ FusedLayer fused_layer(ggd_ctx* c, int li) {
   w.ca_vw = Ly.ca_v.w; w.ca_vb = Ly.ca_v.b;
   w.kv_mem = c->kv_mem + (size_t)li * D.max_batch * D.speech_len * 2 * d;
   w.kv_step = c->kv_step + (size_t)li * D.diffusion_steps * 2 * d;
+  w.kvc = c->kvc ? (const char*)c->kvc + c->tsize * (size_t)li * D.max_batch * D.heads * KVC_ELEMS : nullptr;
   return w;
 }
 
@@ -1094,6 +1096,8 @@ int ggd_finalize_weights(ggd_ctx* c) {
       TRY(frag_from(c, Ly.f_ff2, {q + "feed_forward.layer2"}, d, 4 * d, iota_n(d)));
     }
   }
+  if (c->fused)  // convolved step-invariant cross-attention K / V images, filled by ggd_set_memory
+    HIP_TRY(c, dalloc(c, &c->kvc, c->tsize * (size_t)D.n_layers * D.max_batch * D.heads * KVC_ELEMS));
   TRY(build_step_tables(c));
   c->persist = c->fused && persist_supported(D.dtype, D.d_model, D.heads, D.seq_len, D.speech_len, D.d_pose);
   if (c->persist) {
@@ -1168,6 +1172,14 @@ int ggd_set_memory(ggd_ctx* c, const float* tok, int32_t n, int32_t ts, int32_t 
     g = gemm_args(c->layers[l].kv_ca, M, c->mem_tmp, d,
                   c->kv_mem + (size_t)l * D.max_batch * D.speech_len * 2 * d, 2 * d);
     GEMM(c, PRO_F32, EPI_F32, g, s);
+  }
+  if (c->fused) {  // the fused paths read the step-invariant K / V rows convolved, in image order
+    const size_t per_layer = c->tsize * (size_t)D.max_batch * D.heads * KVC_ELEMS;
+    for (int l = 0; l < D.n_layers; ++l) {
+      const Layer& Ly = c->layers[l];
+      HIP_TRY(c, launch_ca_kv_conv(D.dtype == GGD_F32 ? 0 : 1, c->kv_mem + (size_t)l * D.max_batch * D.speech_len * 2 * d,
+                                   Ly.ca_k.w, Ly.ca_k.b, Ly.ca_v.w, Ly.ca_v.b, n, ts, (char*)c->kvc + per_layer * l, s));
+    }
   }
   HIP_TRY(c, hipEventRecord(c->ev_out, s));
   HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
@@ -1479,19 +1491,8 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
       if (it == 1) HIP_TRY(c, hipEventRecord(e0, s));
       if (which < 4) {
         // the layer-0 arguments of launch_fused_layers
-        const Layer& Ly = c->layers[0];
         FusedArgs f{};
-        FusedLayer& w = f.w;
-        w.qkv = Ly.f_qkv.w; w.qkv_b = Ly.f_qkv.b; w.o_sa = Ly.f_o_sa.w; w.o_sa_b = Ly.f_o_sa.b;
-        w.q_ca = Ly.f_q_ca.w; w.q_ca_b = Ly.f_q_ca.b; w.o_ca = Ly.f_o_ca.w; w.o_ca_b = Ly.f_o_ca.b;
-        w.ff1 = Ly.f_ff1.w; w.ff1_b = Ly.f_ff1.b; w.ff2 = Ly.f_ff2.w; w.ff2_b = Ly.f_ff2.b;
-        w.ln1_g = Ly.ln1_g; w.ln1_b = Ly.ln1_b; w.ln2_g = Ly.ln2_g; w.ln2_b = Ly.ln2_b;
-        w.ln3_g = Ly.ln3_g; w.ln3_b = Ly.ln3_b;
-        w.sa_qw = Ly.sa_q.w; w.sa_qb = Ly.sa_q.b; w.sa_kw = Ly.sa_k.w; w.sa_kb = Ly.sa_k.b;
-        w.sa_vw = Ly.sa_v.w; w.sa_vb = Ly.sa_v.b; w.ca_qw = Ly.ca_q.w; w.ca_qb = Ly.ca_q.b;
-        w.ca_kw = Ly.ca_k.w; w.ca_kb = Ly.ca_k.b; w.ca_vw = Ly.ca_v.w; w.ca_vb = Ly.ca_v.b;
-        w.kv_mem = c->kv_mem;
-        w.kv_step = c->kv_step;
+        f.w = fused_layer(c, 0);
         f.L = D.seq_len; f.Ts = D.speech_len;
         f.o_sa = c->att; f.o_ca = c->q; f.hid = c->ffn;
         f.steps = c->d_steps; f.step_counter = c->d_counter;

@@ -44,6 +44,40 @@ __global__ void __launch_bounds__(FT) ke_kernel(FinalArgs a) {
   ke_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, a.do_update ? *a.step_counter : 0, smem, pre);
 }
 
+// Step-invariant cross-attention K / V of every (clip, head) of one layer, convolved and in the
+// attention-image order (KVC_ELEMS, ggd_fusedlib.h): the 3-tap conv of transformer.py:28-44 over
+// the memory rows of nn.py:223 reaches the step token (memory row 0) only from rows 0 and 1, so
+// rows 2 .. Ts are the same in every denoise step; they are convolved here once per clip batch
+// (ggd_set_memory), with conv3's operation order, and rows 0 / 1 are left to the step kernels.
+template <typename T>
+__global__ void __launch_bounds__(256) ca_kv_conv_kernel(const float* kv_mem, const float* kw, const float* kb,
+                                                         const float* vw, const float* vb, int Ts, T* out) {
+  const int h = blockIdx.x, b = blockIdx.y, Lk = 1 + Ts;
+  T* o = out + ((size_t)b * (FD / FDK) + h) * KVC_ELEMS;
+  for (int e = threadIdx.x; e < KVC_ELEMS; e += 256) {
+    const bool isv = e >= FLK * FDK;
+    const int i = isv ? (e - FLK * FDK) % FLK : e / FDK, c = isv ? (e - FLK * FDK) / FLK : e % FDK;
+    float v = 0.f;
+    if (i >= 2 && i < Lk) {
+      const ConvW w = isv ? conv_w(vw, vb, c) : conv_w(kw, kb, c);
+      const float* base = kv_mem + (size_t)b * Ts * 2 * FD + (isv ? FD : 0) + h * FDK + c;  // speech row j at j * 2 FD
+      const float p0 = base[(size_t)(i - 2) * 2 * FD], p1 = base[(size_t)(i - 1) * 2 * FD];
+      const float p2 = i + 1 < Lk ? base[(size_t)i * 2 * FD] : 0.f;
+      v = conv3(w, p0, p1, p2);
+    }
+    o[e] = from_f32<T>(v);
+  }
+}
+
+hipError_t launch_ca_kv_conv(int dtype, const float* kv_mem, const float* kw, const float* kb, const float* vw,
+                             const float* vb, int n, int Ts, void* out, hipStream_t s) {
+  if (n < 1 || Ts < 1 || 1 + Ts > FLK) return hipErrorInvalidValue;
+  const dim3 grid(FD / FDK, n), blk(256);
+  if (dtype == 0) hipLaunchKernelGGL(ca_kv_conv_kernel<float>, grid, blk, 0, s, kv_mem, kw, kb, vw, vb, Ts, (float*)out);
+  else hipLaunchKernelGGL(ca_kv_conv_kernel<bf16_t>, grid, blk, 0, s, kv_mem, kw, kb, vw, vb, Ts, (bf16_t*)out);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------

@@ -426,6 +426,18 @@ struct ConvW { float w0, w1, w2, b; };
 __device__ __forceinline__ ConvW conv_w(const float* w, const float* b, int c) {
   return ConvW{G(w)[c * 3 + 0], G(w)[c * 3 + 1], G(w)[c * 3 + 2], G(b)[c]};
 }
+// one output of the 3-tap conv, in ONE fixed operation order (explicit fmaf chain): the
+// step-invariant cross-attention memory rows are convolved once per clip batch
+// (ca_kv_conv_kernel) with exactly the arithmetic the per-step kernels use for the other rows
+__device__ __forceinline__ float conv3(const ConvW& w, float p0, float p1, float p2) {
+  return fmaf(w.w2, p2, fmaf(w.w1, p1, fmaf(w.w0, p0, w.b)));
+}
+
+// Step-invariant cross-attention K / V of one (layer, clip, head), convolved and in the
+// attention-image element order: K [FLK rows][FDK] then V^T [FDK][FLK keys]; rows / keys 0 and 1
+// (which see the step token through the conv) and >= Lk are zero here -- the per-step kernels
+// fill 0 and 1 (KvFix).  KVC_ELEMS (ggd_kernels.h) elements of T per head.
+static_assert(KVC_ELEMS == 2 * FLK * FDK, "kvc block = K [FLK][FDK] + V^T [FDK][FLK]");
 
 // dst rows (or transposed columns) i < 64 = conv over rows i-1, i, i+1 of the f32 source (row
 // stride ss, column c = tid & 31 of the thread; zero outside [0, rows)); rows >= `rows` are
@@ -447,7 +459,7 @@ __device__ __forceinline__ void conv_rows(T* dst, int S, const SRC* src, int ss,
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
     const int i = i0 + RS * k;
-    const float v = w.b + w.w0 * (i > 0 ? p0[k] : 0.f) + w.w1 * p1[k] + w.w2 * (i + 1 < rows ? p2[k] : 0.f);
+    const float v = conv3(w, i > 0 ? p0[k] : 0.f, p1[k], i + 1 < rows ? p2[k] : 0.f);
     const T o = from_f32<T>(i < rows ? v : 0.f);
     if (TRANS)
       dst[c * S + i] = o;
@@ -507,12 +519,15 @@ __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float 
     s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     att_mma16(s[t], Qm + rt * 16 * A::SQ, A::SQ, Km + t * 16 * A::SQ, A::SQ, 0, lane);
   }
+  // softmax in the base-2 domain: exp(scale s - m) = exp2(scale log2(e) s - m'), one v_exp_f32
+  // per score (and one v_rcp_f32 per row) instead of the range-reduced library expf / division
+  const float sl2 = scale * 1.4426950408889634f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float mx = -INFINITY;
 #pragma unroll
     for (int t = 0; t < LKT; ++t) {
-      const float v = t * 16 + c16 < Lk ? s[t][r] * scale : -INFINITY;
+      const float v = t * 16 + c16 < Lk ? s[t][r] * sl2 : -INFINITY;
       s[t][r] = v;
       mx = fmaxf(mx, v);
     }
@@ -520,12 +535,12 @@ __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float 
     float sum = 0.f;
 #pragma unroll
     for (int t = 0; t < LKT; ++t) {
-      const float p = t * 16 + c16 < Lk ? expf(s[t][r] - mx) : 0.f;
+      const float p = t * 16 + c16 < Lk ? __builtin_amdgcn_exp2f(s[t][r] - mx) : 0.f;
       s[t][r] = p;
       sum += p;
     }
     sum = group_sum<16>(sum);
-    const float inv = 1.0f / sum;
+    const float inv = __builtin_amdgcn_rcpf(sum);
 #pragma unroll
     for (int t = 0; t < LKT; ++t) P[(4 * g4 + r) * A::SP + t * 16 + c16] = from_f32<T>(s[t][r] * inv);
   }
@@ -554,6 +569,67 @@ __device__ __forceinline__ void fattn_any(unsigned char* att, int Lq, int Lk, fl
   else
     fattn<T, 4, FR, false, CP>(att, Lq, Lk, scale, out, ldo);
 }
+
+// Cross-attention K / V^T images of head hd from the precomputed kvc block (KVC_ELEMS of T):
+// load() issues the 16-byte pieces (NT threads, issued early), store() writes them into the
+// attention image `att` (FAtt layout) with its row pads.
+template <typename T, int NT, int QR = FR> struct KvcStage {
+  using A = FAtt<T, QR>;
+  static constexpr int PIECES = KVC_ELEMS * (int)sizeof(T) / 16, NV = (PIECES + NT - 1) / NT, PER_ROW_K = FDK * (int)sizeof(T) / 16,
+                       PER_ROW_V = FLK * (int)sizeof(T) / 16, K_PIECES = FLK * PER_ROW_K;
+  static_assert(PIECES % NT == 0, "whole pieces per thread");
+  uint4 v[NV];
+  __device__ __forceinline__ void load(const T* src, int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+      const u32x4 u = G((const u32x4*)src)[tid + i * NT];
+      v[i] = make_uint4(u.x, u.y, u.z, u.w);
+    }
+  }
+  __device__ __forceinline__ void store(unsigned char* att, int tid) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int q = tid + i * NT;
+      unsigned char* dst;
+      if (q < K_PIECES)
+        dst = att + A::OK + sizeof(T) * ((q / PER_ROW_K) * A::SQ) + 16 * (q % PER_ROW_K);
+      else
+        dst = att + A::OV + sizeof(T) * (((q - K_PIECES) / PER_ROW_V) * A::SV) + 16 * ((q - K_PIECES) % PER_ROW_V);
+      *(uint4*)dst = v[i];
+    }
+  }
+};
+
+// Rows 0 and 1 of the cross-attention K and V of head hd (the rows whose 3-tap conv reads the
+// step token, memory row 0): lane l of the fixing wave handles half l >> 5 (K / V), channel l & 31.
+// m0 = the step token's pre-conv K|V row (kv_step[t]), m1 / m2 = the clip's first two speech rows.
+struct KvFix {
+  float m0, m1, m2;
+  __device__ __forceinline__ void load(const float* kv_step_t, const float* kv_mem_b, int Ts, int hd, int l) {
+    const int half = l >> 5, c = l & 31, col = half * FD + hd * FDK + c;
+    m0 = G(kv_step_t)[col];
+    m1 = G(kv_mem_b)[col];
+    m2 = G(kv_mem_b)[(size_t)min(1, Ts - 1) * 2 * FD + col];
+    if (Ts < 2) m2 = 0.f;
+  }
+  template <typename T, int QR = FR>
+  __device__ __forceinline__ void store(unsigned char* att, const ConvW& ck, const ConvW& cv, int Lk, int l) const {
+    using A = FAtt<T, QR>;
+    const int half = l >> 5, c = l & 31;
+    const ConvW& w = half ? cv : ck;
+    const float r0 = conv3(w, 0.f, m0, Lk > 1 ? m1 : 0.f), r1 = conv3(w, m0, m1, Lk > 2 ? m2 : 0.f);
+    T* K = (T*)(att + A::OK);
+    T* Vt = (T*)(att + A::OV);
+    if (half == 0) {
+      K[0 * A::SQ + c] = from_f32<T>(r0);
+      if (Lk > 1) K[1 * A::SQ + c] = from_f32<T>(r1);
+    } else {
+      Vt[c * A::SV + 0] = from_f32<T>(r0);
+      if (Lk > 1) Vt[c * A::SV + 1] = from_f32<T>(r1);
+    }
+  }
+};
 
 // ------------------------------------------------------------------------------------------
 // LDS plans (bytes; FR = 64 rows everywhere)

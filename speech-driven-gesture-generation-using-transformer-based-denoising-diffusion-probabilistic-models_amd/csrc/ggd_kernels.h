@@ -116,6 +116,8 @@ struct PostArgs {
 };
 
 // Fused per-clip decoder (ggd_fused.hip): fragment-packed weights of one layer.
+constexpr int KVC_ELEMS = 2 * 64 * 32;  // per (clip, head): cross-attn K [64 keys][32] + V^T [32][64 keys]
+
 struct FusedLayer {
   const void *qkv, *o_sa, *q_ca, *o_ca, *ff1, *ff2;  // T fragments [tile][k step][64 lanes][16 B]
   const float *qkv_b, *o_sa_b, *q_ca_b, *o_ca_b, *ff1_b, *ff2_b;
@@ -123,6 +125,7 @@ struct FusedLayer {
   const float *sa_qw, *sa_qb, *sa_kw, *sa_kb, *sa_vw, *sa_vb;
   const float *ca_qw, *ca_qb, *ca_kw, *ca_kb, *ca_vw, *ca_vb;
   const float *kv_mem, *kv_step;
+  const void* kvc;   // [max_batch][heads][KVC_ELEMS] T: step-invariant convolved cross-attn K | V^T images
 };
 
 struct FusedArgs {
@@ -200,6 +203,9 @@ constexpr int MEGA_CTL_WORDS = 256 + 32 * 16 + 32 * 32;  // tickets/arrival, gro
 // launchers (return hipError_t of the launch)
 hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s);  // 0 KA, 1 KB, 2 KC, 3 KD
 hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s);
+// step-invariant convolved cross-attention K | V^T images of one layer (ggd_set_memory; fused paths)
+hipError_t launch_ca_kv_conv(int dtype, const float* kv_mem, const float* kw, const float* kb, const float* vw,
+                             const float* vb, int n, int Ts, void* out, hipStream_t s);
 bool fused_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
 bool persist_supported(int dtype, int d_model, int heads, int L, int Ts, int C);

@@ -165,7 +165,6 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
   unsigned char* scr = smem + PL::OFF_S;
   T* Yb = (T*)scr;                              // self-attention: bf16 QKV (pre-conv) of a head pair
   unsigned char* att_sa = scr + PL::YB;         // two attention images (head pair)
-  T* rawb = (T*)scr;                            // cross-attention: bf16 memory K|V of a head pair
   unsigned char* att_ca = scr + PL::RAWB;
   T* Hd = (T*)scr;                              // FFN chunk
   float* E = (float*)scr;                       // eps (out projection)
@@ -341,22 +340,17 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
         ln_rows<T, NT, R, SX>(Hs, L, Xn, tid);  // LN2 affine folded into the next Linear
         bar_lds();
       }
-      // memory K / V (pre-conv) of a head: row 0 = the step token of t, rows 1.. the cached
-      // speech rows; item v = (row, half, 16-byte piece), rows clamped into [0, Lk)
-      auto kv_load = [&](int hd, int i) -> float4 {
-        const int v = tid + i * NT, r = min(v >> 4, Lk - 1), half = (v >> 3) & 1, q = v & 7;
-        const float* src = r == 0 ? w.kv_step + (size_t)t * 2 * FD : w.kv_mem + ((size_t)b * a.Ts + (r - 1)) * 2 * FD;
-        return *(const float4*)(src + half * FD + hd * FDK + q * 4);
-      };
-      // bf16 raw K|V of pair member hh: [half][FLK rows][FDK]
-      auto kv_store = [&](int hh, int i, float4 val) {
-        const int v = tid + i * NT, r = v >> 4, half = (v >> 3) & 1, q = v & 7;
-        const uint32_t lo = (uint32_t)f2bf(val.x) | ((uint32_t)f2bf(val.y) << 16);
-        const uint32_t hi = (uint32_t)f2bf(val.z) | ((uint32_t)f2bf(val.w) << 16);
-        if (r < Lk) *(uint2*)(rawb + ((hh * 2 + half) * FLK + r) * FDK + q * 4) = make_uint2(lo, hi);
-      };
-      static_assert(2 * FLK * 8 == 2 * PK_THREADS, "two 16-byte memory pieces per thread");
-      float4 kv0 = kv_load(0, 0), kv1 = kv_load(0, 1), kv2 = kv_load(1, 0), kv3 = kv_load(1, 1);
+      // memory K / V of a head pair: the step-invariant rows come convolved and in image order
+      // from the kvc block (set_memory); rows 0 / 1 (the step token's conv reach) are computed by
+      // the last wave of each half.  Threads 0-255 stage head 2hp, 256-511 head 2hp + 1.
+      const T* kvc_b = (const T*)w.kvc + (size_t)b * (FD / FDK) * KVC_ELEMS;
+      const float* kvs_t = w.kv_step + (size_t)t * 2 * FD;
+      const float* kvm_b = w.kv_mem + (size_t)b * a.Ts * 2 * FD;
+      const bool fixer = (wave & 3) == 3;
+      KvcStage<T, NT / 2, R> kvs;
+      KvFix fx;
+      kvs.load(kvc_b + (size_t)(tid >> 8) * KVC_ELEMS, tid & 255);
+      if (fixer) fx.load(kvs_t, kvm_b, a.Ts, tid >> 8, lane);
       // the cross-attention queries of all 8 heads in one GEMM (wave w: head w's 32 columns), kept
       // pre-conv in bf16 in the Xn image once every wave is done reading Xn
       T* Yqb = Xn;
@@ -386,23 +380,16 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
         LANE_IDS();
         const ConvW dq = conv_w(w.ca_qw, w.ca_qb, tid & 31), dk = conv_w(w.ca_kw, w.ca_kb, tid & 31),
                     dv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
-        kv_store(0, 0, kv0);
-        kv_store(0, 1, kv1);
-        kv_store(1, 0, kv2);
-        kv_store(1, 1, kv3);
-        if (hp < 3) {
-          kv0 = kv_load(2 * hp + 2, 0);
-          kv1 = kv_load(2 * hp + 2, 1);
-          kv2 = kv_load(2 * hp + 3, 0);
-          kv3 = kv_load(2 * hp + 3, 1);
-        }
-        bar_lds();
         const int hh = tid >> 8, t2 = tid & 255, hd = 2 * hp + hh;
         unsigned char* at = att_ca + hh * PL::ATT_B;
-        const T* rk = rawb + hh * 2 * FLK * FDK;
+        kvs.store(at, t2);
+        if (hp < 3) kvs.load(kvc_b + (size_t)(hd + 2) * KVC_ELEMS, t2);
+        bar_lds();
         conv_rows<T, false, R, NT / 2, T>((T*)(at + AT::OQ), AT::SQ, Yqb + hd * FDK, SX, L, dq, t2);
-        conv_rows<T, false, FLK, NT / 2, T>((T*)(at + AT::OK), AT::SQ, rk, FDK, Lk, dk, t2);
-        conv_rows<T, true, FLK, NT / 2, T>((T*)(at + AT::OV), AT::SV, rk + FLK * FDK, FDK, Lk, dv, t2);
+        if (fixer) {
+          fx.store<T, R>(at, dk, dv, Lk, lane);
+          if (hp < 3) fx.load(kvs_t, kvm_b, a.Ts, hd + 2, lane);
+        }
         bar_lds();
         fattn_lds<R>(at, L, Lk, a.scale, Ob + hd * FDK, SX, t2);
         bar_lds();

@@ -250,7 +250,6 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   unsigned char* un = pv + PL::IMG + PL::ST;
   float* Hs = R::ON ? (float*)smem : (float*)un;
   float* Yq = (float*)un;
-  float* raw = (float*)(un + PL::YQ);
   unsigned char* att = un + PL::YQ + PL::RAW;
   static_assert(R::BASE + PL::IMG + PL::ST + PL::YQ + PL::RAW + FAtt<T>::BYTES <= 160 * 1024 - 256, "KB LDS");
   const auto& w = a.w;
@@ -277,36 +276,23 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   const float bq = G(w.q_ca_b)[h * FDK + (wave & 1) * 16 + c16];
   const ConvW cq = conv_w(w.ca_qw, w.ca_qb, tid & 31), ck = conv_w(w.ca_kw, w.ca_kb, tid & 31),
               cv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
-  // memory K / V of head h (pre-conv): row 0 = the step token of this clip's t, rows 1.. the
-  // cached speech rows; item v = (row, half, 16-byte piece) with row clamped into [0, Lk)
-  static_assert(2 * FLK * 8 == 2 * FT, "two 16-byte memory pieces per thread");
-  auto kv_load = [&](int i) -> float4 {
-    const int v = tid + i * FT, r = min(v >> 4, Lk - 1), half = (v >> 3) & 1, q = v & 7;
-    const float* src = r == 0 ? w.kv_step + (size_t)t * 2 * FD : w.kv_mem + ((size_t)b * a.Ts + (r - 1)) * 2 * FD;
-    return ld_f4(src + half * FD + h * FDK + q * 4);
-  };
+  // memory K / V of head h: the step-invariant rows come convolved and in image order from the
+  // kvc block (set_memory), rows 0 / 1 (the step token's conv reach) are computed by wave 7
   residual_gemm<T, KT, 2, RT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
-  // issued after the out-projection: t comes from a two-load dependent chain, which must not
-  // stall it; the loads complete under LN2.  Named registers, not an array: an array live
-  // across the LN is demoted to scratch.
-  const float4 kv0 = kv_load(0), kv1 = kv_load(1);
+  // issued after the out-projection: the fix-up rows need t (a two-load dependent chain), which
+  // must not stall it; the loads complete under LN2
+  KvcStage<T, FT> kvs;
+  kvs.load((const T*)w.kvc + ((size_t)b * (FD / FDK) + h) * KVC_ELEMS, tid);
+  KvFix fx;
+  if (wave == FT / 64 - 1) fx.load(w.kv_step + (size_t)t * 2 * FD, w.kv_mem + (size_t)b * a.Ts * 2 * FD, a.Ts, h, lane);
   bar_lds();
   STAMP(2);
   if (!R::ON) store_rows<CP>(a.h_out + row0 * FD, Hs, L, h);
   ln_rows<T, FT, RT * 16>(Hs, L, Ax);
   bar_lds();
   STAMP(3);
-  // (kernel path) Hs is dead: Yq, raw and the attention images overlay it
-  auto kv_store = [&](int i, float4 val) {
-    const int v = tid + i * FT, r = v >> 4, half = (v >> 3) & 1, q = v & 7;
-    if (r < Lk) *(float4*)(raw + half * (FLK + 2) * FDK + (r + 1) * FDK + q * 4) = val;
-  };
-  kv_store(0, kv0);
-  kv_store(1, kv1);
-  if (tid < 2 * 2 * FDK) {  // zero halo rows 0 and Lk + 1 of both halves
-    const int half = tid >> 6, e = tid & 63, r = e < FDK ? 0 : Lk + 1;
-    raw[half * (FLK + 2) * FDK + r * FDK + (e & 31)] = 0.f;
-  }
+  // (kernel path) Hs is dead: Yq and the attention images overlay it
+  kvs.store(att, tid);
   if (wave < 2) {
     f32x4 acc[RT][1];
     gq.run(acc, Ax, Frag<T>::SX, lane);
@@ -319,8 +305,7 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   bar_lds();
   STAMP(4);
   conv_rows<T, false, RT * 16, FT>((T*)(att + AT::OQ), AT::SQ, Yq, SYQ, L, cq);
-  conv_rows<T, false, FLK, FT>((T*)(att + AT::OK), AT::SQ, raw + FDK, FDK, Lk, ck);
-  conv_rows<T, true, FLK, FT>((T*)(att + AT::OV), AT::SV, raw + (FLK + 2) * FDK + FDK, FDK, Lk, cv);
+  if (wave == FT / 64 - 1) fx.store<T>(att, ck, cv, Lk, lane);
   bar_lds();
   STAMP(5);
   fattn_any<T, CP>(att, L, Lk, a.scale, (T*)a.o_ca + row0 * FD + h * FDK, FD);
