@@ -112,6 +112,16 @@ template <int CP = CP_KERNEL> struct OutRowsP {
     const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
     __builtin_amdgcn_raw_buffer_store_b128(u, r, (int)(elem * 4), 0, cp_store(CP));
   }
+  // 4 consecutive values at elem as T: one 8-byte (bf16) or 16-byte (f32) store
+  template <typename T> __device__ __forceinline__ void put4v(uint32_t elem, f32x4 v) const {
+    if constexpr (sizeof(T) == 2) {
+      typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+      const u32x2 u = {(unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16), (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16)};
+      __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)(elem * 2), 0, cp_store(CP));
+    } else {
+      put4(elem, make_float4(v[0], v[1], v[2], v[3]));
+    }
+  }
   template <typename T> __device__ __forceinline__ void put(uint32_t elem, float v) const {
     if constexpr (sizeof(T) == 2)
       __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), r, (int)(elem * 2), 0, cp_store(CP));
@@ -209,17 +219,29 @@ template <typename T, int NT = NTHREADS, int CP = CP_KERNEL> struct ImgStage {
 // MFMA against fragment-packed weights
 // ------------------------------------------------------------------------------------------
 // acc += A[rt*16 .. +16)[k step kf] x fragment wb   (A row-major in LDS, stride SA)
-template <typename T>
+// TR: the product is computed transposed, C^T = W A^T (the fragment-packed weight tile as the
+// MFMA A operand, the activation rows as B -- the same lane maps), so lane (c16, g4) holds the 4
+// CONSECUTIVE output columns 4 g4 .. 4 g4 + 3 of row c16: epilogues move 16 bytes per row tile
+// instead of four scalars.
+template <typename T, bool TR = false>
 __device__ __forceinline__ void mma_aw(f32x4& acc, const T* A, int SA, int rt, int kf, uint4 wb, int lane) {
   const int r16 = lane & 15, g = lane >> 4;
   if constexpr (sizeof(T) == 2) {
     const bf16x8 av = *(const bf16x8*)(A + (rt * 16 + r16) * SA + kf * 32 + g * 8);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, wb), acc, 0, 0, 0);
+    if constexpr (TR)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wb), av, acc, 0, 0, 0);
+    else
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, wb), acc, 0, 0, 0);
   } else {
     const f32x4 av = *(const f32x4*)(A + (rt * 16 + r16) * SA + kf * 16 + g * 4);
     const f32x4 bv = __builtin_bit_cast(f32x4, wb);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+    for (int s = 0; s < 4; ++s) {
+      if constexpr (TR)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(bv[s], av[s], acc, 0, 0, 0);
+      else
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+    }
   }
 }
 
@@ -249,6 +271,7 @@ struct WGemm {
   // fragments of k step k + 1 are read from LDS before the MFMAs of step k issue, so the LDS
   // latency overlaps the matrix work (one wave per SIMD hides nothing on its own).
   // zero = false: accumulate onto the caller's acc (e.g. residual + bias preloaded)
+  template <bool TR = false>
   __device__ __forceinline__ void run(f32x4 (&acc)[RT][NJ], const T* A, int SA, int lane, int nj_on = NJ,
                                       bool zero = true) {
     if (zero) {
@@ -276,9 +299,14 @@ struct WGemm {
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
-            if (j < nj_on)
-              acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[rt], __builtin_bit_cast(bf16x8, wb[j][k]),
-                                                                   acc[rt][j], 0, 0, 0);
+            if (j < nj_on) {
+              if constexpr (TR)
+                acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wb[j][k]), cur[rt],
+                                                                     acc[rt][j], 0, 0, 0);
+              else
+                acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[rt], __builtin_bit_cast(bf16x8, wb[j][k]),
+                                                                     acc[rt][j], 0, 0, 0);
+            }
         if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
         if (k + 1 < KT) {
 #pragma unroll
@@ -295,7 +323,7 @@ struct WGemm {
           for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
-              if (j < nj_on) mma_aw<T>(acc[rt][j], A, SA, rt, g * G + k, wb[j][k], lane);
+              if (j < nj_on) mma_aw<T, TR>(acc[rt][j], A, SA, rt, g * G + k, wb[j][k], lane);
       }
     }
   }
@@ -431,6 +459,53 @@ __device__ __forceinline__ ConvW conv_w(const float* w, const float* b, int c) {
 // (ca_kv_conv_kernel) with exactly the arithmetic the per-step kernels use for the other rows
 __device__ __forceinline__ float conv3(const ConvW& w, float p0, float p1, float p2) {
   return fmaf(w.w2, p2, fmaf(w.w1, p1, fmaf(w.w0, p0, w.b)));
+}
+
+// The 3-tap conv over tokens applied to a transposed GEMM's accumulators (WGemm TR): v[rt][r]
+// is channel 4 g4 + r of token rt 16 + c16 (bias added).  The neighbour tokens are lanes c16 -/+ 1
+// of the same 16-lane DPP row (row_ror 1 / 15); across row tiles, lane 15 of tile rt - 1 /
+// lane 0 of tile rt + 1.  Zero padding outside [0, L); tokens >= L come out zero (as conv_rows).
+template <int RT>
+__device__ __forceinline__ void conv_tokens(f32x4 (&v)[RT], const ConvW (&w)[4], int L, int c16) {
+  constexpr int ROR1 = 0x121, ROR15 = 0x12F;  // dst[l] = src[(l - 1) mod 16] / src[(l + 1) mod 16]
+  f32x4 pr[RT], nx[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pr[rt][r] = dpp_mov<ROR1>(v[rt][r]);
+      nx[rt][r] = dpp_mov<ROR15>(v[rt][r]);
+    }
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int i = rt * 16 + c16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = c16 == 0 ? (rt > 0 ? pr[rt - 1 < 0 ? 0 : rt - 1][r] : 0.f) : pr[rt][r];
+      float n = c16 == 15 ? (rt + 1 < RT ? nx[rt + 1 < RT ? rt + 1 : rt][r] : 0.f) : nx[rt][r];
+      n = i + 1 < L ? n : 0.f;
+      v[rt][r] = i < L ? conv3(w[r], p, v[rt][r], n) : 0.f;
+    }
+  }
+}
+// conv weights of the 4 consecutive channels c0 .. c0 + 3 of a transposed tile's lane
+__device__ __forceinline__ void conv_w4(ConvW (&cw)[4], const float* w, const float* b, int c0) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) cw[r] = conv_w(w, b, c0 + r);
+}
+// store the lane's 4 consecutive channels c0 .. c0 + 3 of token i: row-major image (Q / K: 8 or 16
+// bytes at i S + c0) or transposed (V^T: four scalars at (c0 + r) S + i)
+template <typename T, bool TRANS>
+__device__ __forceinline__ void put_tok4(T* img, int S, int i, int c0, const f32x4& v) {
+  if constexpr (TRANS) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) img[(c0 + r) * S + i] = from_f32<T>(v[r]);
+  } else if constexpr (sizeof(T) == 2) {
+    *(uint2*)(img + i * S + c0) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                             (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+  } else {
+    *(float4*)(img + i * S + c0) = make_float4(v[0], v[1], v[2], v[3]);
+  }
 }
 
 // Step-invariant cross-attention K / V of one (layer, clip, head), convolved and in the

@@ -47,6 +47,8 @@ __device__ __forceinline__ StepRec ld_rec(const StepRec* p) {
   return r;
 }
 
+__device__ __forceinline__ float bias_at(const float4& b, int r) { return r == 0 ? b.x : r == 1 ? b.y : r == 2 ? b.z : b.w; }
+
 // Residual rows resident in LDS (persistent loop, bf16): a workgroup keeps its clip's f32
 // residual rows (Hs, at LDS offset 0) from KA through KB and KC to KD -- KB and KC compute the
 // full rows redundantly anyway -- so only KA / KE gather them and only KD publishes them.
@@ -56,30 +58,31 @@ template <typename T, int CP> struct Res {
   static constexpr size_t BASE = ON ? Plan<T>::HS : 0;  // start of the phase-private LDS
 };
 
-// Hs[i][n] += A[i] . W[n] + bias[n] for all 64 rows; wave w owns the NJ column tiles
-// NJ w .. NJ w + NJ - 1.  The accumulators start from Hs + bias (one batch of LDS reads issued
-// before the MFMAs), so the epilogue is a plain store, not a dependent read-modify-write.
+// Hs[i][n] += A[i] . W[n] + bias[n] for all row tiles; wave w owns the NJ column tiles
+// NJ w .. NJ w + NJ - 1.  Computed transposed (WGemm TR): lane (c16, g4) of tile (rt, j) holds
+// row rt 16 + c16, columns 16 (NJ w + j) + 4 g4 .. + 3, so the accumulators start from one
+// float4 of Hs + bias and the epilogue is one float4 store (no dependent read-modify-write).
 template <typename T, int KT, int NJ, int RT>
 __device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGemm<T, NJ, KT, RT>& g,
-                                              const float (&bias)[NJ], int lane, int wave) {
+                                              const float4 (&bias)[NJ], int lane, int wave) {
   const int c16 = lane & 15, g4 = lane >> 4;
   f32x4 acc[RT][NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int col = (NJ * wave + j) * 16 + c16;
+    const int col = (NJ * wave + j) * 16 + 4 * g4;
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[rt][j][r] = Hs[(rt * 16 + 4 * g4 + r) * SH + col] + bias[j];
+    for (int rt = 0; rt < RT; ++rt) {
+      const float4 h = *(const float4*)(Hs + (rt * 16 + c16) * SH + col);
+      acc[rt][j] = f32x4{h.x + bias[j].x, h.y + bias[j].y, h.z + bias[j].z, h.w + bias[j].w};
+    }
   }
-  g.run(acc, A, SA, lane, NJ, false);
+  g.template run<true>(acc, A, SA, lane, NJ, false);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int col = (NJ * wave + j) * 16 + c16;
+    const int col = (NJ * wave + j) * 16 + 4 * g4;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Hs[(rt * 16 + 4 * g4 + r) * SH + col] = acc[rt][j][r];
+      *(float4*)(Hs + (rt * 16 + c16) * SH + col) = make_float4(acc[rt][j][0], acc[rt][j][1], acc[rt][j][2], acc[rt][j][3]);
   }
 }
 
@@ -172,13 +175,14 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
   glds_rows<FT, CP>(Hs, sizeof(float) * SH, emb ? a.pe : a.h + (size_t)b * L * FD, sizeof(float) * FD, L, 1);
   constexpr int KTE = 128 / Frag<T>::KF, SB = 128 + Frag<T>::PT, NXV = FR * 128 / FT;
   WGemm<T, 2, KTE, RT> ge(a.w_emb, KTE, 0);
-  float be[2], xv[NXV];
+  float4 be[2];
+  float xv[NXV];
   if (emb) {
     ge.tiles[0] = 2 * wave;
     ge.tiles[1] = 2 * wave + 1;
     ge.load(0, lane);
-    be[0] = G(a.b_emb)[(2 * wave) * 16 + c16];
-    be[1] = G(a.b_emb)[(2 * wave + 1) * 16 + c16];
+    be[0] = ld_f4(a.b_emb + (2 * wave) * 16 + 4 * g4);
+    be[1] = ld_f4(a.b_emb + (2 * wave + 1) * 16 + 4 * g4);
     const int C = a.C;
 #pragma unroll
     for (int i = 0; i < NXV; ++i) {
@@ -189,9 +193,12 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
   // QKV of head h: packed as 6 tiles [q0 q1 k0 k1 v0 v1]; waves 0-5 own one tile each
   const int nq = wave < 6 ? 1 : 0;
   auto& gm = pre.g;
-  const float bias = G(w.qkv_b)[h * 96 + min(wave, 5) * 16 + c16];
-  const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
-              cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
+  const float4 bias = ld_f4(w.qkv_b + h * 96 + min(wave, 5) * 16 + 4 * g4);
+  // the conv of the wave's tile (0-1 Q, 2-3 K, 4-5 V): channels c0 .. c0 + 3 of the head
+  const int kind = min(wave, 5) >> 1, c0 = (wave & 1) * 16 + 4 * g4;
+  ConvW cw[4];
+  conv_w4(cw, kind == 0 ? w.sa_qw : kind == 1 ? w.sa_kw : w.sa_vw, kind == 0 ? w.sa_qb : kind == 1 ? w.sa_kb : w.sa_vb,
+          c0);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   if (emb) {
     // Xb = bf16(x) (channels >= C zero; aliases the LN image), Hs = PE + Xb W_emb^T + b
@@ -209,25 +216,33 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
   ln_rows<T, FT, RT * 16>(Hs, L, Xn);
   bar_lds();
   STAMP(1);
-  // (kernel path) Hs is dead from here: Y and the attention images overlay it
+  // (kernel path) Hs is dead from here: the attention images overlay it.  The QKV tile of each
+  // wave is convolved over tokens in registers (conv_tokens) and written straight into the Q, K
+  // (row-major) or V^T image; waves 6-7 zero the V^T keys past the row tiles.
+  using AT = FAtt<T>;
   {
     f32x4 acc[RT][1];
-    gm.run(acc, Xn, Frag<T>::SX, lane, nq);
+    gm.template run<true>(acc, Xn, Frag<T>::SX, lane, nq);
     if (nq) {
-      const int col = wave * 16 + c16;
+      f32x4 v[RT];
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
+        v[rt] = f32x4{acc[rt][0][0] + bias.x, acc[rt][0][1] + bias.y, acc[rt][0][2] + bias.z, acc[rt][0][3] + bias.w};
+      conv_tokens<RT>(v, cw, L, c16);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Y[(rt * 16 + 4 * g4 + r) * SY + col] = acc[rt][0][r] + bias;
+      for (int rt = 0; rt < RT; ++rt) {
+        if (kind == 0) put_tok4<T, false>((T*)(att + AT::OQ), AT::SQ, rt * 16 + c16, c0, v[rt]);
+        else if (kind == 1) put_tok4<T, false>((T*)(att + AT::OK), AT::SQ, rt * 16 + c16, c0, v[rt]);
+        else put_tok4<T, true>((T*)(att + AT::OV), AT::SV, rt * 16 + c16, c0, v[rt]);
+      }
+    } else if constexpr (RT * 16 < FLK) {
+      constexpr int NK = FLK - RT * 16;
+      T* Vt = (T*)(att + AT::OV);
+      for (int e = tid - 6 * 64; e < FDK * NK; e += 2 * 64) Vt[(e / NK) * AT::SV + RT * 16 + e % NK] = from_f32<T>(0.f);
     }
   }
   bar_lds();
   STAMP(2);
-  using AT = FAtt<T>;
-  conv_rows<T, false, RT * 16, FT>((T*)(att + AT::OQ), AT::SQ, Y, SY, L, cq);
-  conv_rows<T, false, FLK, FT>((T*)(att + AT::OK), AT::SQ, Y + 32, SY, L, ck);
-  conv_rows<T, true, FLK, FT>((T*)(att + AT::OV), AT::SV, Y + 64, SY, L, cv);
-  bar_lds();
   STAMP(3);
   fattn_any<T, CP>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
   STAMP_END(4);
@@ -263,9 +278,9 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   ImgStage<T, FT, CP> so;
   so.load(Ax, (const T*)a.o_sa + row0 * FD, L);
   auto& go = pre.go;
-  float bo[2];
-  bo[0] = G(w.o_sa_b)[(2 * wave) * 16 + c16];
-  bo[1] = G(w.o_sa_b)[(2 * wave + 1) * 16 + c16];
+  float4 bo[2];
+  bo[0] = ld_f4(w.o_sa_b + (2 * wave) * 16 + 4 * g4);
+  bo[1] = ld_f4(w.o_sa_b + (2 * wave + 1) * 16 + 4 * g4);
   so.store(Ax, L);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   STAMP(1);
@@ -273,9 +288,11 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   WGemm<T, 1, KT, RT> gq(w.q_ca, KT, 0);
   gq.tiles[0] = 2 * h + (wave & 1);
   if (wave < 2) gq.load(0, lane);
-  const float bq = G(w.q_ca_b)[h * FDK + (wave & 1) * 16 + c16];
-  const ConvW cq = conv_w(w.ca_qw, w.ca_qb, tid & 31), ck = conv_w(w.ca_kw, w.ca_kb, tid & 31),
-              cv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
+  const float4 bq = ld_f4(w.q_ca_b + h * FDK + (wave & 1) * 16 + 4 * g4);
+  const int cq0 = (wave & 1) * 16 + 4 * g4;  // the query channels of the lane (waves 0-1)
+  ConvW cq[4];
+  conv_w4(cq, w.ca_qw, w.ca_qb, cq0);
+  const ConvW ck = conv_w(w.ca_kw, w.ca_kb, tid & 31), cv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
   // memory K / V of head h: the step-invariant rows come convolved and in image order from the
   // kvc block (set_memory), rows 0 / 1 (the step token's conv reach) are computed by wave 7
   residual_gemm<T, KT, 2, RT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
@@ -289,22 +306,27 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   STAMP(2);
   if (!R::ON) store_rows<CP>(a.h_out + row0 * FD, Hs, L, h);
   ln_rows<T, FT, RT * 16>(Hs, L, Ax);
+  // resident rows: the attention images do not overlay Hs, so the memory K / V pieces (loads in
+  // flight since the out-projection) are staged before LN2's barrier and the step-token rows fixed
+  // right after it
+  if constexpr (R::ON) kvs.store(att, tid);
   bar_lds();
   STAMP(3);
-  // (kernel path) Hs is dead: Yq and the attention images overlay it
-  kvs.store(att, tid);
-  if (wave < 2) {
+  // (kernel path) Hs is dead: the attention images overlay it
+  if constexpr (!R::ON) kvs.store(att, tid);
+  if (wave < 2) {  // the head's query, convolved over tokens in registers, into the Q image
     f32x4 acc[RT][1];
-    gq.run(acc, Ax, Frag<T>::SX, lane);
-    const int col = wave * 16 + c16;
+    gq.template run<true>(acc, Ax, Frag<T>::SX, lane);
+    f32x4 v[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
+      v[rt] = f32x4{acc[rt][0][0] + bq.x, acc[rt][0][1] + bq.y, acc[rt][0][2] + bq.z, acc[rt][0][3] + bq.w};
+    conv_tokens<RT>(v, cq, L, c16);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Yq[(rt * 16 + 4 * g4 + r) * SYQ + col] = acc[rt][0][r] + bq;
+    for (int rt = 0; rt < RT; ++rt) put_tok4<T, false>((T*)(att + AT::OQ), AT::SQ, rt * 16 + c16, cq0, v[rt]);
   }
-  bar_lds();
+  if constexpr (!R::ON) bar_lds();  // every staged piece has landed before the fix-up overwrites some
   STAMP(4);
-  conv_rows<T, false, RT * 16, FT>((T*)(att + AT::OQ), AT::SQ, Yq, SYQ, L, cq);
   if (wave == FT / 64 - 1) fx.store<T>(att, ck, cv, Lk, lane);
   bar_lds();
   STAMP(5);
@@ -336,16 +358,16 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   ImgStage<T, FT, CP> so;
   so.load(Ax, (const T*)a.o_ca + row0 * FD, L);
   auto& go = pre.go;
-  float bo[2];
-  bo[0] = G(w.o_ca_b)[(2 * wave) * 16 + c16];
-  bo[1] = G(w.o_ca_b)[(2 * wave + 1) * 16 + c16];
+  float4 bo[2];
+  bo[0] = ld_f4(w.o_ca_b + (2 * wave) * 16 + 4 * g4);
+  bo[1] = ld_f4(w.o_ca_b + (2 * wave + 1) * 16 + 4 * g4);
   so.store(Ax, L);
   __syncthreads();  // LDS-DMA rows and every operand above have landed
   STAMP(1);
   WGemm<T, 1, KT, RT> gf(w.ff1, KT, 0);  // in flight across the out-projection
   gf.tiles[0] = 8 * c + wave;
   gf.load(0, lane);
-  const float bf = G(w.ff1_b)[(8 * c + wave) * 16 + c16];
+  const float4 bf = ld_f4(w.ff1_b + (8 * c + wave) * 16 + 4 * g4);
   residual_gemm<T, KT, 2, RT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
   bar_lds();
   STAMP(2);
@@ -354,16 +376,15 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   bar_lds();
   STAMP(3);
   f32x4 acc[RT][1];
-  gf.run(acc, Ax, Frag<T>::SX, lane);
+  gf.template run<true>(acc, Ax, Frag<T>::SX, lane);
   const OutRowsP<CP> out((T*)a.hid + row0 * (4 * FD), (uint32_t)(sizeof(T) * L * 4 * FD));
-  const int col = (8 * c + wave) * 16 + c16;
+  const int col = (8 * c + wave) * 16 + 4 * g4;
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = fmaxf(acc[rt][0][r] + bf, 0.f);
-      out.template put<T>((uint32_t)((rt * 16 + 4 * g4 + r) * (4 * FD) + col), v * v);
-    }
+  for (int rt = 0; rt < RT; ++rt) {
+    const float v0 = fmaxf(acc[rt][0][0] + bf.x, 0.f), v1 = fmaxf(acc[rt][0][1] + bf.y, 0.f);
+    const float v2 = fmaxf(acc[rt][0][2] + bf.z, 0.f), v3 = fmaxf(acc[rt][0][3] + bf.w, 0.f);
+    out.template put4v<T>((uint32_t)((rt * 16 + c16) * (4 * FD) + col), f32x4{v0 * v0, v1 * v1, v2 * v2, v3 * v3});
+  }
   STAMP_END(4);
 }
 
@@ -382,26 +403,24 @@ __device__ __forceinline__ void kd_phase(const FA& a, int c, int b, unsigned cha
   T* Hd = (T*)smem;
   const auto& w = a.w;
   const size_t row0 = (size_t)b * L;
-  const int col = tile * 16 + c16;
+  const int col = tile * 16 + 4 * g4;  // transposed product: row rt 16 + c16, columns col .. col + 3
   const int h = c;  // STAMP uses (h, b)
 
   STAMP(0);
-  float res[RT][4];
+  float4 res[RT];
   if constexpr (Res<T, CP>::ON) {  // the residual rows KC left in LDS; then the image may overlay them
     const float* Hs = (const float*)smem;
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) res[rt][r] = Hs[min(rt * 16 + 4 * g4 + r, L - 1) * SH + col];
+    for (int rt = 0; rt < RT; ++rt) res[rt] = *(const float4*)(Hs + min(rt * 16 + c16, L - 1) * SH + col);
     bar_lds();
   } else {
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        res[rt][r] = ld_f32<CP>(a.h, (uint32_t)((row0 + min(rt * 16 + 4 * g4 + r, L - 1)) * FD + col));
+    for (int rt = 0; rt < RT; ++rt) {
+      const uint4 u = ld_16B<CP>(a.h, (uint32_t)(sizeof(float) * ((row0 + min(rt * 16 + c16, L - 1)) * FD + col)));
+      res[rt] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+    }
   }
-  const float bias = G(w.ff2_b)[col];
+  const float4 bias = ld_f4(w.ff2_b + col);
   f32x4 acc[RT][1];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) acc[rt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -414,14 +433,14 @@ __device__ __forceinline__ void kd_phase(const FA& a, int c, int b, unsigned cha
     if constexpr (KDPre<T, RT>::ONE_PASS) {
       __syncthreads();
       STAMP(1);
-      pre.gd.run(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
+      pre.gd.template run<true>(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
     } else {
       WGemm<T, 1, KTW, RT> gd(w.ff2, KTT, p * (KP / Frag<T>::KF) + kq * KTW);
       gd.tiles[0] = tile;
       gd.load(0, lane);
       __syncthreads();
       if (p == 0) STAMP(1);
-      gd.run(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
+      gd.template run<true>(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
     }
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) acc[rt][0] += part[rt][0];
@@ -440,10 +459,11 @@ __device__ __forceinline__ void kd_phase(const FA& a, int c, int b, unsigned cha
       const f32x4 o1 = red[((0 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
       const f32x4 o2 = red[((1 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
       const f32x4 o3 = red[((2 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
+      f32x4 y;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        out.template put<float>((uint32_t)((rt * 16 + 4 * g4 + r) * FD + col),
-                       res[rt][r] + ((((acc[rt][0][r] + o1[r]) + o2[r]) + o3[r]) + bias));
+      for (int r = 0; r < 4; ++r) y[r] = (((acc[rt][0][r] + o1[r]) + o2[r]) + o3[r]) + bias_at(bias, r);
+      out.put4((uint32_t)((rt * 16 + c16) * FD + col),
+               make_float4(res[rt].x + y[0], res[rt].y + y[1], res[rt].z + y[2], res[rt].w + y[3]));
     }
   }
   STAMP_END(3);
@@ -476,7 +496,7 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
   go.tiles[0] = p;
 #pragma unroll
   for (int k = 0; k < KT; ++k) go.wb[0][k] = pre.g.wb[0][k];
-  const float bo = G(a.b_out)[p * 16 + c16];
+  const float4 bo = ld_f4(a.b_out + p * 16 + 4 * g4);
   // the thread's quad: elements e0 + 4 tid .. + 3 (issued now, consumed after the GEMM)
   const bool upd = a.do_update && 4 * tid < ne;
   StepRec rec{};
@@ -510,9 +530,9 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
   STAMP(1);
   if (wave < RT) {
     f32x4 acc[1][1];
-    go.run(acc, Xn + wave * 16 * Frag<T>::SX, Frag<T>::SX, lane);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) E[(wave * 16 + 4 * g4 + r) * SE + c16] = acc[0][0][r] + bo;
+    go.template run<true>(acc, Xn + wave * 16 * Frag<T>::SX, Frag<T>::SX, lane);
+    *(float4*)(E + (wave * 16 + c16) * SE + 4 * g4) =
+        make_float4(acc[0][0][0] + bo.x, acc[0][0][1] + bo.y, acc[0][0][2] + bo.z, acc[0][0][3] + bo.w);
   }
   bar_lds();
   STAMP(2);
