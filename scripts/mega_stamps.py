@@ -51,8 +51,8 @@ diag(10, [0])
 diag(11, [1])
 diffusion.p_sample_loop(model, (32, 123, 40), model_kwargs={"wav": wav}, seed=1, extras=False, n_steps=3)
 t = diag(11, [2], 80)
-labels = {0: "KA ln|gemm|conv|attn", 1: "KB load|oproj|ln2|qgemm+kv|conv|attn", 2: "KC load|oproj|ln3|ffn1",
-          3: "KD load|gemm|reduce", 4: "KE ln+out|stage|upd"}
+labels = {0: "KA ln|qkv+conv|-|attn", 1: "KB load|oproj|ln2|q+conv|fix|attn", 2: "KC load|oproj|ln3|ffn1|ffn2",
+          3: "KD sum|-|store", 4: "KE ln+out|stage|upd"}
 for j in range(5):
     v = [round(x, 2) for x in t[16 * j + 1:16 * j + 8] if x >= 0]
     print(f"{labels[j]:40s} {v}", flush=True)

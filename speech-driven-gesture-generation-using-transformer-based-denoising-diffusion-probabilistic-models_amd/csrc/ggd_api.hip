@@ -115,6 +115,7 @@ struct ggd_ctx {
   // memory
   float* kv_mem = nullptr;   // [layers][maxB*Ts][2d]
   void* kvc = nullptr;       // fused paths: [layers][maxB][heads][KVC_ELEMS] T, convolved step-invariant K | V^T
+  float* ffp = nullptr;      // fused paths: FFN-down partial sums per hidden chunk [maxB][8][L][d]
   float* mem_tmp = nullptr;  // [maxB*Ts][d]
   float* tok_tmp = nullptr;  // [maxB*Ts][d]
   int mem_n = -1;
@@ -526,6 +527,7 @@ FusedArgs fused_args(ggd_ctx* c, int li, const int* t_clip) {
   f.o_sa = c->att;
   f.o_ca = c->q;
   f.hid = c->ffn;
+  f.ffp = c->ffp;
   f.t_clip = t_clip;
   f.steps = c->d_steps;
   f.step_counter = c->d_counter;
@@ -1096,8 +1098,10 @@ int ggd_finalize_weights(ggd_ctx* c) {
       TRY(frag_from(c, Ly.f_ff2, {q + "feed_forward.layer2"}, d, 4 * d, iota_n(d)));
     }
   }
-  if (c->fused)  // convolved step-invariant cross-attention K / V images, filled by ggd_set_memory
+  if (c->fused) {  // convolved step-invariant cross-attention K / V images, filled by ggd_set_memory
     HIP_TRY(c, dalloc(c, &c->kvc, c->tsize * (size_t)D.n_layers * D.max_batch * D.heads * KVC_ELEMS));
+    HIP_TRY(c, dalloc(c, &c->ffp, sizeof(float) * (size_t)D.max_batch * 8 * D.seq_len * D.d_model));
+  }
   TRY(build_step_tables(c));
   c->persist = c->fused && persist_supported(D.dtype, D.d_model, D.heads, D.seq_len, D.speech_len, D.d_pose);
   if (c->persist) {
@@ -1494,7 +1498,7 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
         FusedArgs f{};
         f.w = fused_layer(c, 0);
         f.L = D.seq_len; f.Ts = D.speech_len;
-        f.o_sa = c->att; f.o_ca = c->q; f.hid = c->ffn;
+        f.o_sa = c->att; f.o_ca = c->q; f.hid = c->ffn; f.ffp = c->ffp;
         f.steps = c->d_steps; f.step_counter = c->d_counter;
         f.scale = 1.0f / std::sqrt((float)(d / D.heads));
         f.h = c->h; f.h_out = c->h2;

@@ -137,17 +137,10 @@ template <typename T, int RT> struct KCPre {  // CA out-projection (the FFN-up t
   }
   __device__ __forceinline__ void load(int lane) { go.load(0, lane); }
 };
-template <typename T, int RT> struct KDPre {  // FFN-down: column tile (w & 1), K quarter (w >> 1)
-  static constexpr int KP = Plan<T>::KP, KTT = 4 * FD / Frag<T>::KF, KTW = KP / Frag<T>::KF / 4;
-  static constexpr bool ONE_PASS = KP == 4 * FD;  // bf16: the whole K in one image
-  WGemm<T, 1, KTW, RT> gd;
+template <typename T, int RT> struct KDPre {  // the FFN-down column reduce streams no weights
   template <typename FA>
-  __device__ __forceinline__ KDPre(const FA& a, int c, int wave) : gd(a.w.ff2, KTT, (wave >> 1) * KTW) {
-    gd.tiles[0] = 2 * c + (wave & 1);
-  }
-  __device__ __forceinline__ void load(int lane) {
-    if (ONE_PASS) gd.load(0, lane);
-  }
+  __device__ __forceinline__ KDPre(const FA&, int, int) {}
+  __device__ __forceinline__ void load(int) {}
 };
 
 // ------------------------------------------------------------------------------------------
@@ -336,7 +329,9 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
 }
 
 // ------------------------------------------------------------------------------------------
-// KC: CA out-proj + residual + LN3 + FFN-up chunk (128 hidden) + ReLU^2   grid (8 chunks, clips)
+// KC: CA out-proj + residual + LN3 + FFN-up chunk c (128 hidden) + ReLU^2 + that chunk's share of
+// FFN-down (hidden chunk x W2[:, chunk]^T, all 256 output columns): an f32 partial sum per chunk,
+// reduced by KD.  The hidden chunk never leaves LDS.                  grid (8 chunks, clips)
 // ------------------------------------------------------------------------------------------
 template <typename T, int RT, int CP, typename FA>
 __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned char* smem, KCPre<T, RT>& pre) {
@@ -369,103 +364,88 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   gf.load(0, lane);
   const float4 bf = ld_f4(w.ff1_b + (8 * c + wave) * 16 + 4 * g4);
   residual_gemm<T, KT, 2, RT>(Hs, Ax, Frag<T>::SX, go, bo, lane, wave);
+  // FFN-down fragments of the chunk (k steps c KC .. c KC + KC - 1, column tiles 2w, 2w + 1): in
+  // flight across LN3 and FFN-up, in the registers the out-projection has just released
+  constexpr int KC = 128 / Frag<T>::KF, KTT = 4 * FD / Frag<T>::KF, SHC = 128 + Frag<T>::PT;
+  WGemm<T, 2, KC, RT> gd(w.ff2, KTT, c * KC);
+  gd.tiles[0] = 2 * wave;
+  gd.tiles[1] = 2 * wave + 1;
+  gd.load(0, lane);
   bar_lds();
   STAMP(2);
   if (!R::ON) store_rows<CP>(a.h_out + row0 * FD, Hs, L, c);
   ln_rows<T, FT, RT * 16>(Hs, L, Ax);
   bar_lds();
   STAMP(3);
-  f32x4 acc[RT][1];
-  gf.template run<true>(acc, Ax, Frag<T>::SX, lane);
-  const OutRowsP<CP> out((T*)a.hid + row0 * (4 * FD), (uint32_t)(sizeof(T) * L * 4 * FD));
-  const int col = (8 * c + wave) * 16 + 4 * g4;
+  // hidden chunk image (overlays the dead Hs on the kernel path; beside the resident rows otherwise)
+  T* Hc = (T*)(pv + PL::IMG + PL::ST);
+  {
+    f32x4 acc[RT][1];
+    gf.template run<true>(acc, Ax, Frag<T>::SX, lane);
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt) {
-    const float v0 = fmaxf(acc[rt][0][0] + bf.x, 0.f), v1 = fmaxf(acc[rt][0][1] + bf.y, 0.f);
-    const float v2 = fmaxf(acc[rt][0][2] + bf.z, 0.f), v3 = fmaxf(acc[rt][0][3] + bf.w, 0.f);
-    out.template put4v<T>((uint32_t)((rt * 16 + c16) * (4 * FD) + col), f32x4{v0 * v0, v1 * v1, v2 * v2, v3 * v3});
+    for (int rt = 0; rt < RT; ++rt) {
+      const float v0 = fmaxf(acc[rt][0][0] + bf.x, 0.f), v1 = fmaxf(acc[rt][0][1] + bf.y, 0.f);
+      const float v2 = fmaxf(acc[rt][0][2] + bf.z, 0.f), v3 = fmaxf(acc[rt][0][3] + bf.w, 0.f);
+      put_tok4<T, false>(Hc, SHC, rt * 16 + c16, wave * 16 + 4 * g4, f32x4{v0 * v0, v1 * v1, v2 * v2, v3 * v3});
+    }
   }
-  STAMP_END(4);
+  bar_lds();
+  STAMP(4);
+  {
+    f32x4 acc[RT][2];
+    gd.template run<true>(acc, Hc, SHC, lane);
+    const OutRowsP<CP> out(a.ffp + ((size_t)b * 8 + c) * L * FD, (uint32_t)(sizeof(float) * L * FD));
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+        out.put4((uint32_t)((rt * 16 + c16) * FD + (2 * wave + j) * 16 + 4 * g4),
+                 make_float4(acc[rt][j][0], acc[rt][j][1], acc[rt][j][2], acc[rt][j][3]));
+  }
+  STAMP_END(5);
 }
 
 // ------------------------------------------------------------------------------------------
-// KD: FFN-down (K = 1024) of 32 output columns + residual, in place     grid (8 chunks, clips)
-// wave w: column tile (w & 1), K quarter (w >> 1); the four partial sums meet through LDS and
-// are added in a fixed order (deterministic).
+// KD: columns [32 p, 32 p + 32) of h += sum over the 8 chunks of KC's FFN-down partials + b2, in
+// place.  Thread (row tid / 8, column quad tid % 8): 8 partial float4 in flight, added in chunk
+// order (deterministic).                                          grid (8 column chunks, clips)
 // ------------------------------------------------------------------------------------------
 template <typename T, int RT, int CP, typename FA>
-__device__ __forceinline__ void kd_phase(const FA& a, int c, int b, unsigned char* smem, KDPre<T, RT>& pre) {
-  using PL = Plan<T>;
-  constexpr int KP = PL::KP, NP = 4 * FD / KP, SA = KP + Frag<T>::PT;
-  constexpr int KTT = 4 * FD / Frag<T>::KF, KTW = KP / Frag<T>::KF / 4;  // k steps: total, per wave per pass
-  const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
-  const int L = a.L, c16 = lane & 15, g4 = lane >> 4, tile = 2 * c + (wave & 1), kq = wave >> 1;
-  T* Hd = (T*)smem;
+__device__ __forceinline__ void kd_phase(const FA& a, int p, int b, unsigned char* smem, KDPre<T, RT>& pre) {
+  (void)pre;
+  const int tid = ltid(), L = a.L;
+  const int row = min(tid >> 3, L - 1), col = 32 * p + 4 * (tid & 7);  // rows >= L: clamped loads, dropped store
   const auto& w = a.w;
   const size_t row0 = (size_t)b * L;
-  const int col = tile * 16 + 4 * g4;  // transposed product: row rt 16 + c16, columns col .. col + 3
-  const int h = c;  // STAMP uses (h, b)
+  const int h = p;  // STAMP uses (h, b)
 
   STAMP(0);
-  float4 res[RT];
-  if constexpr (Res<T, CP>::ON) {  // the residual rows KC left in LDS; then the image may overlay them
-    const float* Hs = (const float*)smem;
+  float4 part[8];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) res[rt] = *(const float4*)(Hs + min(rt * 16 + c16, L - 1) * SH + col);
-    bar_lds();
+  for (int c = 0; c < 8; ++c) {
+    const uint4 u = ld_16B<CP>(a.ffp, (uint32_t)(sizeof(float) * ((((size_t)b * 8 + c) * L + row) * FD + col)));
+    part[c] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+  }
+  float4 res;
+  if constexpr (Res<T, CP>::ON) {  // the residual rows KC left in LDS
+    res = *(const float4*)((const float*)smem + row * SH + col);
   } else {
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const uint4 u = ld_16B<CP>(a.h, (uint32_t)(sizeof(float) * ((row0 + min(rt * 16 + c16, L - 1)) * FD + col)));
-      res[rt] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
-    }
+    const uint4 u = ld_16B<CP>(a.h, (uint32_t)(sizeof(float) * ((row0 + row) * FD + col)));
+    res = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
   }
   const float4 bias = ld_f4(w.ff2_b + col);
-  f32x4 acc[RT][1];
+  float4 y = part[0];
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt) acc[rt][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int p = 0; p < NP; ++p) {
-    if (p > 0) __syncthreads();  // the previous pass' image is consumed
-    glds_rows<FT, CP>(Hd, sizeof(T) * SA, (const T*)a.hid + row0 * (4 * FD) + p * KP, sizeof(T) * 4 * FD, L,
-                  (int)(sizeof(T) * KP / 1024));
-    f32x4 part[RT][1];
-    if constexpr (KDPre<T, RT>::ONE_PASS) {
-      __syncthreads();
-      STAMP(1);
-      pre.gd.template run<true>(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
-    } else {
-      WGemm<T, 1, KTW, RT> gd(w.ff2, KTT, p * (KP / Frag<T>::KF) + kq * KTW);
-      gd.tiles[0] = tile;
-      gd.load(0, lane);
-      __syncthreads();
-      if (p == 0) STAMP(1);
-      gd.template run<true>(part, Hd + kq * KTW * Frag<T>::KF, SA, lane);
-    }
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc[rt][0] += part[rt][0];
+  for (int c = 1; c < 8; ++c) {
+    y.x += part[c].x;
+    y.y += part[c].y;
+    y.z += part[c].z;
+    y.w += part[c].w;
   }
-  bar_lds();
-  STAMP(2);
-  f32x4* red = (f32x4*)smem;  // [3 quarters][2 tiles][RT][64 lanes]
-  if (kq > 0)
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) red[(((kq - 1) * 2 + (wave & 1)) * RT + rt) * 64 + lane] = acc[rt][0];
-  bar_lds();
-  if (kq == 0) {
-    const OutRowsP<CP> out(a.h + row0 * FD, (uint32_t)(sizeof(float) * L * FD));
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const f32x4 o1 = red[((0 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
-      const f32x4 o2 = red[((1 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
-      const f32x4 o3 = red[((2 * 2 + (wave & 1)) * RT + rt) * 64 + lane];
-      f32x4 y;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) y[r] = (((acc[rt][0][r] + o1[r]) + o2[r]) + o3[r]) + bias_at(bias, r);
-      out.put4((uint32_t)((rt * 16 + c16) * FD + col),
-               make_float4(res[rt].x + y[0], res[rt].y + y[1], res[rt].z + y[2], res[rt].w + y[3]));
-    }
-  }
+  STAMP(1);
+  const OutRowsP<CP> out(a.h + row0 * FD, (uint32_t)(sizeof(float) * L * FD));
+  out.put4((uint32_t)((tid >> 3) * FD + col),
+           make_float4(res.x + (y.x + bias.x), res.y + (y.y + bias.y), res.z + (y.z + bias.z), res.w + (y.w + bias.w)));
   STAMP_END(3);
 }
 
