@@ -53,19 +53,22 @@ template <typename T>
 __global__ void __launch_bounds__(256) ca_kv_conv_kernel(const float* kv_mem, const float* kw, const float* kb,
                                                          const float* vw, const float* vb, int Ts, T* out) {
   const int h = blockIdx.x, b = blockIdx.y, Lk = 1 + Ts;
-  T* o = out + ((size_t)b * (FD / FDK) + h) * KVC_ELEMS;
-  for (int e = threadIdx.x; e < KVC_ELEMS; e += 256) {
-    const bool isv = e >= FLK * FDK;
-    const int i = isv ? (e - FLK * FDK) % FLK : e / FDK, c = isv ? (e - FLK * FDK) / FLK : e % FDK;
-    float v = 0.f;
+  T* K = out + ((size_t)b * (FD / FDK) + h) * KVC_ELEMS;
+  T* Vt = K + FLK * FDK;
+  const int c = threadIdx.x & 31;  // channel fastest: the memory rows are read coalesced
+  const ConvW wk = conv_w(kw, kb, c), wv = conv_w(vw, vb, c);
+  const float* base = kv_mem + (size_t)b * Ts * 2 * FD + h * FDK + c;  // speech row j at j 2 FD (K), + FD (V)
+  for (int i = threadIdx.x >> 5; i < FLK; i += 256 / 32) {
+    float k = 0.f, v = 0.f;
     if (i >= 2 && i < Lk) {
-      const ConvW w = isv ? conv_w(vw, vb, c) : conv_w(kw, kb, c);
-      const float* base = kv_mem + (size_t)b * Ts * 2 * FD + (isv ? FD : 0) + h * FDK + c;  // speech row j at j * 2 FD
-      const float p0 = base[(size_t)(i - 2) * 2 * FD], p1 = base[(size_t)(i - 1) * 2 * FD];
-      const float p2 = i + 1 < Lk ? base[(size_t)i * 2 * FD] : 0.f;
-      v = conv3(w, p0, p1, p2);
+      const float* p0 = base + (size_t)(i - 2) * 2 * FD;
+      const float* p1 = p0 + 2 * FD;
+      const bool nx = i + 1 < Lk;
+      k = conv3(wk, p0[0], p1[0], nx ? p1[2 * FD] : 0.f);
+      v = conv3(wv, p0[FD], p1[FD], nx ? p1[3 * FD] : 0.f);
     }
-    o[e] = from_f32<T>(v);
+    K[i * FDK + c] = from_f32<T>(k);
+    Vt[c * FLK + i] = from_f32<T>(v);
   }
 }
 
