@@ -87,7 +87,7 @@ WORKLOADS = {
 # this same command (scripts/pmc_all.sh -> scripts/pmc.sh + pmc_summary.py: 2 x FETCH_SIZE +
 # WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), one summary per workload; PMC cannot
 # run inside the timed region, so the figure is the profile's, keyed by kernel symbol and workload
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01p_pmc_{workload}_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02a_pmc_{workload}_summary.json")
 
 
 def pmc_traffic(kernel_prefix, workload):
