@@ -6,8 +6,8 @@ Workloads (BASELINE.json configs; beat-ours, 123 pose channels, random-init weig
   c2 (default, the metric's config): 32 clips/GPU, L = 40, 32,000-sample wavs, DDPM T = 1000,
      bf16 -- one launch of the clip-group persistent loop mk_kernel per pass;
   c4: 32 clips/GPU, L = 160, DDPM 1000, fp8-e4m3 step weights -- generic per-phase kernels;
-  c5: 128 clips/GPU, L = 40, DDIM-50 -- one launch of the per-clip loop psk_kernel per pass,
-     the next pass's encoder on a second HIP stream beside it (WORKLOADS[...]["overlap"]).
+  c5: 128 clips/GPU, L = 40, DDIM-50 -- one launch of the clip-pair loop (psk_kernel, two
+     workgroups per clip) per pass; the encoder runs inline (WORKLOADS[...]["overlap"]).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c4|c5] [--dtype bf16|f32|fp8]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...  (one rank per GPU, RCCL)
@@ -21,8 +21,8 @@ measurement: its line says "rehearsal").
 Prints ONE JSON line on rank 0.  ``roofline`` is measured live inside the timed region: in the
 last timed pass the library brackets every launch of the dominant kernel with a hipEvent pair
 on the context stream it is launched on (ggd_set_profiling / ggd_kernel_time); FLOPs per launch
-are the algorithmic clip_step_flops() x clips x steps for the loops, 2 M K N for
-the FFN-up GEMM.  ``traffic`` is read from the committed rocprofv3 PMC summary of the same
+are the algorithmic clip_step_flops() x clips x steps for the loops, attn_flop()
+for the generic path's attention launches (C4).  ``traffic`` is read from the committed rocprofv3 PMC summary of the same
 command (PMC_SUMMARY).  ``cpu_baseline`` times the CPU oracle (a faithful fp32 restatement that
 recomputes the speech encoder every step, as models/model.py:95-96 does) on a bounded sample.
 """
@@ -69,6 +69,12 @@ def kb_flop(n, L, Lk, d):
     return n * (4 * L * d * d + 4 * L * Lk * d + 6 * L * d + 12 * Lk * d)
 
 
+def attn_flop(n, L, Lk, d):
+    """Algorithmic FLOPs of one attn_q_kernel launch over n clips: QK^T and PV 4*L*Lk*d, the 3-tap
+    conv 6 FLOP per output on Q (L x d) and on K, V (Lk x d each)."""
+    return n * (4 * L * Lk * d + 6 * L * d + 12 * Lk * d)
+
+
 # BASELINE.json configs as bench workloads (per GPU); C3 is C2 on 8 GPUs (--gpus 8)
 WORKLOADS = {
     "c2": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=1,
@@ -76,11 +82,12 @@ WORKLOADS = {
     "c4": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=4, dtype="fp8",
                label="beat-ours C4 long clip (seq_len x4)", overlap=False),
     "c5": dict(batch_per_gpu=128, alg="ddim", respacing="ddim50", seq_mult=1,
-               label="beat-ours C5 DDIM-50", overlap=True),
+               label="beat-ours C5 DDIM-50", overlap=False),
 }
 # overlap: the next pass's speech encoder runs beside this pass's loop (model.prefetch_speech).
-# It pays where the loop leaves CUs idle (C5: psk_kernel, 128 workgroups on 256 CUs, 254.0k ->
-# 306.5k frames/s); C2/C4 loops fill the chip and measured the same or 0.6% slower with it.
+# It paid while the C5 loop left CUs idle (one workgroup per clip on 128 of 256 CUs: 254.0k ->
+# 306.5k frames/s); the clip-pair loop fills the chip, and C5 measured 364.1k with it vs 388.7k
+# without (r02b); C2/C4 loops fill the chip and measured the same or 0.6% slower with it.
 
 
 # HBM-side bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of
@@ -394,16 +401,23 @@ def main():
             flop = clip_step * B * T
             kernel = f"psk_kernel<{args.dtype}> (one workgroup per clip, all {T} denoise steps in one launch)"
             timing = "hipEvent pair around the loop's single launch in the last timed pass"
-        elif prof_kind == 2:  # generic path: the FFN-up GEMM (LN prologue, ReLU^2 epilogue), per launch
-            flop = 2 * B * L * d * 4 * d
-            kernel = f"gemm_kernel<{args.dtype}> FFN-up (LN1 prologue + Linear {d}->{4 * d} + ReLU^2, M={B * L})"
-            timing = "hipEvent pair around every FFN-up launch of the last timed pass (context stream)"
+        elif prof_kind == 4:  # clip pairs: one launch (per 128 clips) runs all T steps of the batch
+            flop = clip_step * B * T
+            kernel = (f"psk_kernel<{args.dtype}, pair> (two workgroups per clip, all {T} denoise steps in one launch"
+                      " per <= 128 clips)")
+            timing = "hipEvent pair around the loop's launches in the last timed pass"
+        elif prof_kind == 2:  # generic path: the attention launches (self and cross, the top rocprof row)
+            flop = (attn_flop(B, L, L, d) + attn_flop(B, L, Tm, d)) / 2
+            kernel = (f"attn_q_kernel<{args.dtype}> (self- and cross-attention with the 3-tap convs, one workgroup per"
+                      f" head x clip x 64-query block; the largest time share of the C4 step)")
+            timing = "hipEvent pair around every attention launch of the last timed pass (context stream)"
         else:
             flop = kb_flop(B, L, Tm, d)
             kernel = f"kb_kernel<{args.dtype}> (SA out-proj + LN2 + cross-attn Q + conv + cross-attention)"
             timing = "device realtime-clock span of every KB launch of the last timed pass"
         ach = flop / (avg_us * 1e-6) / 1e12
-        tr = pmc_traffic({1: "mk_kernel", 2: "gemm_kernel<unsigned short, 64, 1, 1, 1, true>", 3: "psk_kernel"}.get(
+        tr = pmc_traffic({1: "mk_kernel", 2: "attn_q_kernel", 3: "psk_kernel<3, false>",
+                          4: "psk_kernel<3, true>"}.get(
             prof_kind, "kb_kernel"),
                          args.workload)
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",

@@ -168,7 +168,8 @@ int ggd_kernel_time(ggd_ctx* ctx, int32_t which, double* avg_us, int64_t* launch
 /* What the last profiled ggd_sample timed: 0 = kb_kernel launches of the per-phase path,
  * 1 = the persistent loop (mk_kernel: one launch for all denoise steps), 2 = the generic path's
  * FFN-up GEMM (LayerNorm prologue + Linear d -> 4d + ReLU^2, hipEvent pairs per launch), 3 = the
- * one-workgroup-per-clip loop (psk_kernel: one launch for all steps; chosen for large batches). */
+ * one-workgroup-per-clip loop (psk_kernel: one launch for all steps; chosen for large batches), 4 = the
+ * clip-pair loop (psk_kernel with two workgroups per clip: one launch per <= 128 clips). */
 int ggd_profile_kind(ggd_ctx* ctx);
 
 /* Diagnostics (not part of the reference surface): launch one kernel configuration `iters`

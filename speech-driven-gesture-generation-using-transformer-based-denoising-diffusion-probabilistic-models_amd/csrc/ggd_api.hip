@@ -91,6 +91,12 @@ struct ggd_ctx {
                              // scripts/route_compare.py: 314 us/step for any n <= 256 vs 113 us per
                              // 32-clip chunk)
   unsigned long long* stamps = nullptr;  // ggd_diag what=8: phase stamps of the persistent kernel
+  int pair_mode = 0;         // ggd_diag what=14: 0 auto, 1 never, 2 always two workgroups per clip
+  unsigned* pair_ctl = nullptr;           // clip-pair loop: control words, status, hand-off slots
+  int* pair_status = nullptr;
+  unsigned char* pair_xbuf = nullptr;
+  int pair_launches = 0;                  // last ggd_sample: clip-pair launches (0: one workgroup per clip)
+  int pair_force_coh = 0;                 // ggd_diag what=14 p[1]: write-through hand-offs on any placement
   float *out_ln_g = nullptr, *out_ln_b = nullptr;
   std::vector<Layer> layers;
   float* pe = nullptr;       // [pe_len][d]
@@ -160,6 +166,9 @@ struct ggd_ctx {
 };
 
 namespace {
+
+// clip-pair step time / one-workgroup-per-clip step time (ggd_persist.hip), measured on MI355X
+constexpr double PAIR_STEP_RATIO = 0.68;  // 172 / 253 us per DDIM step at 128 clips (r02b)
 
 int fail(ggd_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -709,7 +718,9 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     at.heads = D.heads;
     at.d = d;
     at.scale = 1.0f / std::sqrt((float)dk);
+    if (c->profiling && sampling) { int r = prof_mark(c, s); if (r) return r; }
     HIP_TRY(c, launch_attention(D.dtype, at, n, s));
+    if (c->profiling && sampling) { int r = prof_mark(c, s); if (r) return r; }
 
     g = gemm_args(Ly.o_sa, M, c->att, d, c->h, d);
     GEMM(c, PRO_T, EPI_RESID, g, s);
@@ -732,7 +743,9 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     at.cw_k = Ly.ca_k.w; at.cb_k = Ly.ca_k.b;
     at.cw_v = Ly.ca_v.w; at.cb_v = Ly.ca_v.b;
     at.Lk = 1 + D.speech_len;
+    if (c->profiling && sampling) { int r = prof_mark(c, s); if (r) return r; }
     HIP_TRY(c, launch_attention(D.dtype, at, n, s));
+    if (c->profiling && sampling) { int r = prof_mark(c, s); if (r) return r; }
 
     g = gemm_args(Ly.o_ca, M, c->att, d, c->h, d);
     GEMM(c, PRO_T, EPI_RESID, g, s);
@@ -741,10 +754,7 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     g = gemm_args(Ly.ff1, M, c->h, d, c->ffn, 4 * d);
     g.ln_g = Ly.ln3_g;
     g.ln_b = Ly.ln3_b;
-    const bool prof = c->profiling && sampling;
-    if (prof) { int r = prof_mark(c, s); if (r) return r; }
     GEMM(c, PRO_LN, EPI_RELU2, g, s);
-    if (prof) { int r = prof_mark(c, s); if (r) return r; }
 
     g = gemm_args(Ly.ff2, M, c->ffn, 4 * d, c->h, d);
     GEMM(c, PRO_T, EPI_RESID, g, s);
@@ -1354,6 +1364,16 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     *avg_us = c->mega_place;
     return GGD_OK;
   }
+  if (what == 14 && np >= 1) {  // clip pairs: {0} auto, {1} never, {2} always (persistent per-clip route)
+    c->pair_mode = p[0] >= 0 && p[0] <= 2 ? p[0] : 0;
+    c->pair_force_coh = np >= 2 && p[1] != 0;
+    *avg_us = c->pair_launches;
+    return GGD_OK;
+  }
+  if (what == 15) {  // last ggd_sample: clip-pair launches
+    *avg_us = c->pair_launches;
+    return GGD_OK;
+  }
   if (what == 13) {  // last ggd_sample: [XCD-local launches, write-through re-runs]
     avg_us[0] = c->mega_xl_launches;
     if (iters > 1) avg_us[1] = c->mega_fallbacks;
@@ -1731,12 +1751,50 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
     p.extras = a->extras;
     p.scale = 1.0f / std::sqrt((float)(D.d_model / D.heads));
     p.stamps = c->stamps;
+    // clip pairs (two workgroups per clip) when the one-workgroup loop would leave CUs idle:
+    // chunks of <= pcap clips, each filling the chip, vs rounds of 2 pcap clips at one per CU
+    // (a pair step measured PAIR_STEP_RATIO x the one-workgroup step)
+    const int pcap = persist_pair_capacity();
+    bool pair = c->pair_mode == 2 && pcap > 0;
+    if (c->pair_mode == 0 && pcap > 0) {
+      const int chunks = (a->n + pcap - 1) / pcap, rounds = (a->n + 2 * pcap - 1) / (2 * pcap);
+      pair = chunks * PAIR_STEP_RATIO < rounds;
+    }
+    c->pair_launches = 0;
+    if (pair) {
+      if (!c->pair_ctl) {
+        HIP_TRY(c, dalloc(c, &c->pair_ctl, sizeof(unsigned) * PAIR_CTL_WORDS));
+        HIP_TRY(c, dalloc(c, &c->pair_status, sizeof(int)));
+        HIP_TRY(c, dalloc(c, &c->pair_xbuf, (size_t)PAIR_MAX * 4 * PAIR_SLOT_BYTES));
+      }
+      p.ctl = c->pair_ctl;
+      p.status = c->pair_status;
+      p.xbuf = c->pair_xbuf;
+      p.force_coh = c->pair_force_coh;
+      HIP_TRY(c, hipMemsetAsync(c->pair_status, 0, sizeof(int), s));
+    }
     if (c->profiling) {
       c->prof.next = 0;
       int r = prof_mark(c, s);
       if (r) return r;
     }
-    HIP_TRY(c, launch_persist(p, s));
+    if (pair) {
+      for (int c0 = 0; c0 < a->n; c0 += pcap) {  // chunks share the control words: stream-ordered
+        p.clip0 = c0;
+        HIP_TRY(c, launch_persist_pair(p, std::min(pcap, a->n - c0), s));
+        ++c->pair_launches;
+      }
+    } else {
+      HIP_TRY(c, launch_persist(p, s));
+    }
+    if (pair) {
+      int st = 0;
+      HIP_TRY(c, hipMemcpyAsync(&st, c->pair_status, sizeof(int), hipMemcpyDeviceToHost, s));
+      HIP_TRY(c, hipStreamSynchronize(s));
+      if (st)
+        return fail(c, GGD_ERR_HIP, st == 2 ? "clip-pair loop: workgroups were not all resident"
+                                            : "clip-pair loop: a pair barrier timed out");
+    }
     if (c->profiling) {
       int r = prof_mark(c, s);
       if (r) return r;
@@ -1745,7 +1803,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
       HIP_TRY(c, hipEventElapsedTime(&ms, c->prof.ev[0], c->prof.ev[1]));
       c->prof_avg_us = ms * 1000.0;
       c->prof_launches = 1;
-      c->prof_kind = 3;
+      c->prof_kind = pair ? 4 : 3;
       c->span_pending = 0;
     }
     HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));

@@ -179,7 +179,16 @@ struct PersistArgs {
   float* extras;               // (6, N, C, L) of the last iteration, or null
   float scale;
   unsigned long long* stamps;  // diagnostics: workgroup 0 stamps phase boundaries of iteration 0
+  // clip pairs (launch_persist_pair): two workgroups per clip, each half the heads and FFN chunks
+  unsigned* ctl;               // PAIR_CTL_WORDS control words, zeroed before every launch
+  int* status;                 // 0 ok, 1 a pair barrier timed out, 2 workgroups not co-resident
+  unsigned char* xbuf;         // hand-off slots [pairs][2 parts][2 epochs][PAIR_SLOT_BYTES]
+  int clip0;                   // first clip of this launch (batches above the capacity run as chunks)
+  int force_coh;               // diagnostics: take the write-through placement even when XCD-local fits
 };
+constexpr int PAIR_MAX = 128;                              // clip pairs per launch (ctl words)
+constexpr int PAIR_CTL_WORDS = 256 + PAIR_MAX * 32;        // tickets / arrival, one flag line per pair
+constexpr size_t PAIR_SLOT_BYTES = 48 * 256 * 4;           // f32 [48 rows][256] FFN-down partial
 
 // Persistent reverse loop (ggd_mega.hip): ONE launch of 8 workgroups per clip runs iterations
 // k0 .. k0 + n_steps - 1; the phases of ggd_phases.h meet at clip-group barriers instead of
@@ -209,6 +218,10 @@ hipError_t launch_ca_kv_conv(int dtype, const float* kv_mem, const float* kw, co
                              const float* vb, int n, int Ts, void* out, hipStream_t s);
 bool fused_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
+// clip pairs: clips [a.clip0, a.clip0 + pairs) with two co-resident workgroups each (pairs <=
+// persist_pair_capacity()); a.ctl must hold PAIR_CTL_WORDS words (zeroed here)
+hipError_t launch_persist_pair(const PersistArgs& a, int pairs, hipStream_t s);
+int persist_pair_capacity();
 bool persist_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
 // xl: the XCD-local variant (CP_XL, grid padded to whole XCDs; placement 0 only)
 hipError_t launch_mega(int dtype, int L, const MegaArgs& a, int n, bool xl, hipStream_t s);

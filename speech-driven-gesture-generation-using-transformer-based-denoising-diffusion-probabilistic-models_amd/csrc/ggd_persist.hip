@@ -149,9 +149,141 @@ __device__ __forceinline__ void fattn_lds(unsigned char* att, int Lq, int Lk, fl
 
 constexpr int PK_THREADS = 512;  // 8 waves: two per SIMD, so one wave's LDS / L2 waits overlap the other's MFMAs
 
-template <int RT>
-__global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
+// ------------------------------------------------------------------------------------------
+// Clip pairs.  With fewer clips than CUs (C5: 128 clips per GPU on 256 CUs) one workgroup per
+// clip leaves half the chip idle, so a clip can be split over TWO workgroups: part p runs the
+// attention of heads 4p .. 4p + 3 and FFN chunks 4p .. 4p + 3 (1024 / 128 = 8 chunks).  The
+// partners meet three times per layer: after self-attention and after cross-attention each
+// hands its four heads' outputs (bf16, L x 128) to the other, which then runs the full
+// out-projection itself (a redundant 256 x 256 GEMM is cheaper than a second hand-off and keeps
+// the residual bit-identical to the one-workgroup loop); after the FFN each hands its f32
+// FFN-down partial (L x 256) and both add part 0's + part 1's.  Every other step-loop value
+// (embedding, LayerNorms, out-projection, posterior update with its counter noise) is computed
+// identically by both, so both hold the same pose state and part 0 alone writes it.
+//
+// Placement: a workgroup takes a ticket on its XCD; when every XCD holds its pairs' slots, the
+// partners share an L2 and hand-offs are plain stores + sc1 loads (as ggd_mega.hip's CP_XL);
+// otherwise every workgroup takes pair blockIdx.x / 2 and hand-off stores write through (sc1).
+// All waits are bounded: a timed-out barrier sets `status` and its workgroups leave.
+// ------------------------------------------------------------------------------------------
+constexpr int PP_SPIN_LIMIT = 1 << 21;
+constexpr int PP_ARRIVE = 128, PP_FLAGS = 256;
+
+__device__ __forceinline__ int pp_slots(int x, int P) { return x < P ? 2 * ((P - 1 - x) / 8 + 1) : 0; }
+
+// thread 0: (pair << 2) | (xl << 1) | part, -2 (idle surplus) or -1 (status set)
+__device__ int pp_role(const PersistArgs& a, int nwg, int P) {
+  unsigned* ctl = a.ctl;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 7;
+  const int t = (int)__hip_atomic_fetch_add(ctl + xcc * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(ctl + PP_ARRIVE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  for (int spin = 0; __hip_atomic_load(ctl + PP_ARRIVE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg;
+       ++spin) {
+    if (spin > PP_SPIN_LIMIT) {
+      atomicMax(a.status, 2);
+      return -1;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  bool xl = !a.force_coh;  // every workgroup reads the same final counts: one verdict per launch
+  for (int x = 0; x < 8; ++x)
+    if ((int)__hip_atomic_load(ctl + x * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pp_slots(x, P)) xl = false;
+  if (xl) {
+    if (t >= pp_slots((int)xcc, P)) return -2;
+    return (((int)xcc + 8 * (t >> 1)) << 2) | 2 | (t & 1);
+  }
+  const int pair = (int)blockIdx.x >> 1;
+  return pair < P ? (pair << 2) | ((int)blockIdx.x & 1) : -2;
+}
+
+// barrier of a clip's two workgroups: every wave's hand-off stores have landed (vmcnt(0)), then
+// thread 0 publishes `epoch` in its word of the pair's flag line and wave 0 polls the partner's
+__device__ __forceinline__ bool pp_sync(unsigned* flags, int part, unsigned epoch, bool xl, int* status, int* s_ok) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 8u);
+  if (threadIdx.x == 0) {
+    if (xl)
+      __builtin_amdgcn_raw_buffer_store_b32(epoch, r, part * 4, 0, 0);
+    else
+      __hip_atomic_store(flags + part, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x < 64) {
+    int ok = 1;
+    for (int spin = 0;; ++spin) {
+      const unsigned v = xl ? __builtin_amdgcn_raw_buffer_load_b32(r, (part ^ 1) * 4, 0, CP_COH)
+                            : __hip_atomic_load(flags + (part ^ 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v >= epoch) break;
+      if ((spin & 255) == 255 &&
+          (spin > PP_SPIN_LIMIT || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        if (threadIdx.x == 0) atomicMax(status, 1);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (threadIdx.x == 0) *s_ok = ok;
+  }
+  bar_lds();
+  return *s_ok != 0;
+}
+
+typedef __attribute__((ext_vector_type(4))) unsigned int pp_u32x4;
+__device__ __forceinline__ void pp_put16(const __amdgpu_buffer_rsrc_t& r, int off, pp_u32x4 v, bool xl) {
+  if (xl)
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, CP_COH);
+}
+
+// this part's four heads of the attention output (Ob columns 128 part ..) -> its hand-off slot
+template <int R, int SX>
+__device__ __forceinline__ void pp_put_heads(const bf16_t* Ob, int part, unsigned char* slot, int L, bool xl, int tid) {
+  constexpr int NI = (R * 16 + PK_THREADS - 1) / PK_THREADS;
+  const __amdgpu_buffer_rsrc_t r = uni_rsrc(slot, (uint32_t)PAIR_SLOT_BYTES);
+#pragma unroll
+  for (int k = 0; k < NI; ++k) {
+    const int i = tid + k * PK_THREADS, row = i >> 4, c = i & 15;
+    if (row < L) pp_put16(r, i * 16, *(const pp_u32x4*)(Ob + row * SX + 128 * part + c * 8), xl);
+  }
+}
+// the partner's four heads from its slot -> Ob columns 128 (part ^ 1) ..
+template <int R, int SX>
+__device__ __forceinline__ void pp_get_heads(bf16_t* Ob, int part, const unsigned char* slot, int L, int tid) {
+  constexpr int NI = (R * 16 + PK_THREADS - 1) / PK_THREADS;
+  const __amdgpu_buffer_rsrc_t r = uni_rsrc(slot, (uint32_t)PAIR_SLOT_BYTES);
+  pp_u32x4 v[NI];
+#pragma unroll
+  for (int k = 0; k < NI; ++k) {
+    const int i = tid + k * PK_THREADS;
+    if ((i >> 4) < L) v[k] = __builtin_amdgcn_raw_buffer_load_b128(r, i * 16, 0, CP_COH);
+  }
+#pragma unroll
+  for (int k = 0; k < NI; ++k) {
+    const int i = tid + k * PK_THREADS, row = i >> 4, c = i & 15;
+    if (row < L) *(pp_u32x4*)(Ob + row * SX + 128 * (part ^ 1) + c * 8) = v[k];
+  }
+}
+
+// the two partners swap their heads' attention outputs (Ob columns 128 part .. <-> 128 (part ^ 1) ..)
+template <int R, int SX>
+__device__ __forceinline__ bool pp_swap_heads(bf16_t* Ob, int part, unsigned char* xb, unsigned& ep, unsigned* flags,
+                                              bool xl, int* status, int* s_ok, int L, int tid) {
+  ++ep;
+  const size_t sl = (size_t)(ep & 1) * PAIR_SLOT_BYTES;
+  pp_put_heads<R, SX>(Ob, part, xb + (size_t)part * 2 * PAIR_SLOT_BYTES + sl, L, xl, tid);
+  if (!pp_sync(flags, part, ep, xl, status, s_ok)) return false;
+  pp_get_heads<R, SX>(Ob, part, xb + (size_t)(part ^ 1) * 2 * PAIR_SLOT_BYTES + sl, L, tid);
+  bar_lds();
+  return true;
+}
+
+template <int RT, bool PAIR>
+__global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int s_role, s_ok;
   using PL = PPlan<RT>;
   using T = bf16_t;
   using AT = FAtt<T, PL::R>;
@@ -170,7 +302,27 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
   float* E = (float*)scr;                       // eps (out projection)
   T* Xb = (T*)(scr + PL::E);                    // emb operand
 
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, c16 = lane & 15, g4 = lane >> 4;
+  // clip b; PAIR: this workgroup's part (heads 4 part .., FFN chunks 4 part ..), its pair's flag
+  // line and hand-off slots [part][epoch & 1]
+  int b = blockIdx.x, part = 0;
+  bool xl = false;
+  unsigned* flags = nullptr;
+  unsigned char* xb = nullptr;
+  unsigned ep = 0;
+  if constexpr (PAIR) {
+    if (threadIdx.x == 0) s_role = pp_role(a, gridDim.x, P);
+    __syncthreads();
+    const int role = __builtin_amdgcn_readfirstlane(s_role);
+    if (role < 0) return;
+    b = a.clip0 + (role >> 2);
+    part = role & 1;
+    xl = (role & 2) != 0;
+    flags = a.ctl + PP_FLAGS + (role >> 2) * 32;
+    xb = a.xbuf + (size_t)(role >> 2) * 4 * PAIR_SLOT_BYTES;
+  }
+  constexpr int HP = PAIR ? 2 : 4, NC = PAIR ? 4 : 8;  // head pairs, FFN chunks of this workgroup
+  const int hp0 = PAIR ? 2 * part : 0, c0f = PAIR ? 4 * part : 0, qoff = 12 * hp0;
+  const int tid = threadIdx.x, lane = tid & 63, c16 = lane & 15, g4 = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: tile indices live in SGPRs
   const int Lk = 1 + a.Ts;
   const size_t row0 = (size_t)b * a.L;
@@ -200,7 +352,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
   {
     const int te[2] = {2 * wave, 2 * wave + 1};
     pload<2, 4>(fb, a.w_emb, 4, te, 0, lane);
-    const int tq[2] = {tq0, tq1};
+    const int tq[2] = {qoff + tq0, qoff + tq1};
     if (nq == 2) pload<2, 8>(fa, a.layers[0].qkv, 8, tq, 0, lane);
     else pload<1, 8>(fa, a.layers[0].qkv, 8, tq, 0, lane);
   }
@@ -246,7 +398,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
       pmma<RT, 2, 4>(acc, Xb, SHD, 0, fb, lane);
       {  // fb <- layer 0's first FFN-down chunk
         const int td[2] = {2 * wave, 2 * wave + 1};
-        pload<2, 4>(fb, a.layers[0].ff2, 32, td, 0, lane);
+        pload<2, 4>(fb, a.layers[0].ff2, 32, td, 4 * c0f, lane);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -268,8 +420,9 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
         ln_rows<T, NT, R, SX>(Hs, L, Xn, tid);  // LN1 affine folded into the next Linear
         bar_lds();
       }
-      for (int hp = 0; hp < 4; ++hp) {
+      for (int hi = 0; hi < HP; ++hi) {
         LANE_IDS();
+        const int hp = hp0 + hi;
         const float bq0 = w.qkv_b[hp * 192 + tq0 * 16 + c16], bq1 = w.qkv_b[hp * 192 + tq1 * 16 + c16];
         const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
                     cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
@@ -277,7 +430,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
           f32x4 acc[RT][2];
           zero_acc(acc);
           pmma_n<RT, 2, 8>(acc, Xn, SX, 0, fa, nq, lane);
-          if (hp < 3) {  // refill: the next head pair, or the SA out-projection
+          if (hi < HP - 1) {  // refill: the next head pair, or the SA out-projection
             const int tq[2] = {12 * (hp + 1) + tq0, 12 * (hp + 1) + tq1};
             if (nq == 2) pload<2, 8>(fa, w.qkv, 8, tq, 0, lane);
             else pload<1, 8>(fa, w.qkv, 8, tq, 0, lane);
@@ -311,13 +464,18 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
         }
       }
       PSTAMP(2);
+      if constexpr (PAIR)
+        if (!pp_swap_heads<R, SX>(Ob, part, xb, ep, flags, xl, a.status, &s_ok, L, tid)) return;
       // SA out-projection + residual
       {
         const float bo0 = w.o_sa_b[(2 * wave) * 16 + c16], bo1 = w.o_sa_b[(2 * wave + 1) * 16 + c16];
         f32x4 acc[RT][2];
         zero_acc(acc);
         pmma<RT, 2, 8>(acc, Ob, SX, 0, fa, lane);
-        {  // fa <- cross-attn Q of every head: wave w owns head w's two column tiles
+        if constexpr (PAIR) {  // fa <- cross-attn Q of this part's heads: wave w owns column tile 8 part + w
+          const int tq[1] = {8 * part + wave};
+          pload<1, 8>(fa, w.q_ca, 8, tq, 0, lane);
+        } else {  // fa <- cross-attn Q of every head: wave w owns head w's two column tiles
           const int tq[2] = {2 * wave, 2 * wave + 1};
           pload<2, 8>(fa, w.q_ca, 8, tq, 0, lane);
         }
@@ -349,24 +507,27 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
       const bool fixer = (wave & 3) == 3;
       KvcStage<T, NT / 2, R> kvs;
       KvFix fx;
-      kvs.load(kvc_b + (size_t)(tid >> 8) * KVC_ELEMS, tid & 255);
-      if (fixer) fx.load(kvs_t, kvm_b, a.Ts, tid >> 8, lane);
+      kvs.load(kvc_b + (size_t)(2 * hp0 + (tid >> 8)) * KVC_ELEMS, tid & 255);
+      if (fixer) fx.load(kvs_t, kvm_b, a.Ts, 2 * hp0 + (tid >> 8), lane);
       // the cross-attention queries of all 8 heads in one GEMM (wave w: head w's 32 columns), kept
       // pre-conv in bf16 in the Xn image once every wave is done reading Xn
       T* Yqb = Xn;
       {
-        const float bq0 = w.q_ca_b[(2 * wave) * 16 + c16], bq1 = w.q_ca_b[(2 * wave + 1) * 16 + c16];
-        f32x4 acc[RT][2];
+        // PAIR: the part's 4 heads, wave w one column tile (8 part + w)
+        constexpr int NQJ = PAIR ? 1 : 2;
+        const int qt0 = PAIR ? 8 * part + wave : 2 * wave;
+        const float bq0 = w.q_ca_b[qt0 * 16 + c16], bq1 = w.q_ca_b[(qt0 + 1) * 16 + c16];
+        f32x4 acc[RT][NQJ];
         zero_acc(acc);
-        pmma<RT, 2, 8>(acc, Xn, SX, 0, fa, lane);
+        pmma<RT, NQJ, 8>(acc, Xn, SX, 0, fa, lane);
         {  // fa <- the CA out-projection
           const int to[2] = {2 * wave, 2 * wave + 1};
           pload<2, 8>(fa, w.o_ca, 8, to, 0, lane);
         }
         bar_lds();
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int col = (2 * wave + j) * 16 + c16;
+        for (int j = 0; j < NQJ; ++j) {
+          const int col = (qt0 + j) * 16 + c16;
           const float bias = j == 0 ? bq0 : bq1;
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt)
@@ -376,33 +537,36 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
       }
       // head pairs: both heads' conv and attention at once (threads 0-255 head 2hp, 256-511 head
       // 2hp + 1); the next pair's memory K|V loads fly under this pair's work
-      for (int hp = 0; hp < 4; ++hp) {
+      for (int hi = 0; hi < HP; ++hi) {
         LANE_IDS();
+        const int hp = hp0 + hi;
         const ConvW dq = conv_w(w.ca_qw, w.ca_qb, tid & 31), dk = conv_w(w.ca_kw, w.ca_kb, tid & 31),
                     dv = conv_w(w.ca_vw, w.ca_vb, tid & 31);
         const int hh = tid >> 8, t2 = tid & 255, hd = 2 * hp + hh;
         unsigned char* at = att_ca + hh * PL::ATT_B;
         kvs.store(at, t2);
-        if (hp < 3) kvs.load(kvc_b + (size_t)(hd + 2) * KVC_ELEMS, t2);
+        if (hi < HP - 1) kvs.load(kvc_b + (size_t)(hd + 2) * KVC_ELEMS, t2);
         bar_lds();
         conv_rows<T, false, R, NT / 2, T>((T*)(at + AT::OQ), AT::SQ, Yqb + hd * FDK, SX, L, dq, t2);
         if (fixer) {
           fx.store<T, R>(at, dk, dv, Lk, lane);
-          if (hp < 3) fx.load(kvs_t, kvm_b, a.Ts, hd + 2, lane);
+          if (hi < HP - 1) fx.load(kvs_t, kvm_b, a.Ts, hd + 2, lane);
         }
         bar_lds();
         fattn_lds<R>(at, L, Lk, a.scale, Ob + hd * FDK, SX, t2);
         bar_lds();
       }
       PSTAMP(3);
+      if constexpr (PAIR)
+        if (!pp_swap_heads<R, SX>(Ob, part, xb, ep, flags, xl, a.status, &s_ok, L, tid)) return;
       // CA out-projection + residual
       {
         const float bo0 = w.o_ca_b[(2 * wave) * 16 + c16], bo1 = w.o_ca_b[(2 * wave + 1) * 16 + c16];
         f32x4 acc[RT][2];
         zero_acc(acc);
         pmma<RT, 2, 8>(acc, Ob, SX, 0, fa, lane);
-        {  // fa <- FFN-up chunk 0 (fb already holds FFN-down chunk 0)
-          const int tf[1] = {wave};
+        {  // fa <- FFN-up chunk c0f (fb already holds FFN-down chunk c0f)
+          const int tf[1] = {8 * c0f + wave};
           pload<1, 8>(fa, w.ff1, 8, tf, 0, lane);
         }
 #pragma unroll
@@ -429,17 +593,18 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
         const FusedLayer& wn = a.layers[last ? li : li + 1];
         f32x4 accd[RT][2];
         zero_acc(accd);
-        for (int c = 0; c < 8; ++c) {
+        for (int ci = 0; ci < NC; ++ci) {
           LANE_IDS();
+          const int c = c0f + ci;
           const float bf = w.ff1_b[(8 * c + wave) * 16 + c16];
           f32x4 acc[RT][1];
           zero_acc(acc);
-                    pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
-          if (c < 7) {
+          pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
+          if (ci < NC - 1) {
             const int tf[1] = {8 * (c + 1) + wave};
             pload<1, 8>(fa, w.ff1, 8, tf, 0, lane);
           } else if (!last) {  // fa <- the next layer's first QKV pair
-            const int tq[2] = {tq0, tq1};
+            const int tq[2] = {qoff + tq0, qoff + tq1};
             if (nq == 2) pload<2, 8>(fa, wn.qkv, 8, tq, 0, lane);
             else pload<1, 8>(fa, wn.qkv, 8, tq, 0, lane);
           } else {             // fa <- the output projection
@@ -463,15 +628,39 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
           pmma<RT, 2, 4>(accd, Hc, SHD, 0, fb, lane);
           {
             const int td[2] = {2 * wave, 2 * wave + 1};
-            if (c < 7)
+            if (ci < NC - 1)
               pload<2, 4>(fb, w.ff2, 32, td, 4 * (c + 1), lane);
             else if (!last)  // fb <- the next layer's first FFN-down chunk
-              pload<2, 4>(fb, wn.ff2, 32, td, 0, lane);
+              pload<2, 4>(fb, wn.ff2, 32, td, 4 * c0f, lane);
             else             // fb <- the next step's emb fragments
               pload<2, 4>(fb, a.w_emb, 4, td, 0, lane);
           }
         }
         static_assert(2 * PL::HID <= PL::SCR, "double-buffered FFN chunk image");
+        if constexpr (PAIR) {  // FFN-down partials of the two halves of K: both add part 0's + part 1's
+          ++ep;
+          const size_t sl = (size_t)(ep & 1) * PAIR_SLOT_BYTES;
+          {
+            const __amdgpu_buffer_rsrc_t r = uni_rsrc(xb + (size_t)part * 2 * PAIR_SLOT_BYTES + sl, (uint32_t)PAIR_SLOT_BYTES);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+              for (int j = 0; j < 2; ++j)
+                pp_put16(r, (((wave * RT + rt) * 2 + j) * 64 + lane) * 16, __builtin_bit_cast(pp_u32x4, accd[rt][j]), xl);
+          }
+          if (!pp_sync(flags, part, ep, xl, a.status, &s_ok)) return;
+          const __amdgpu_buffer_rsrc_t r = uni_rsrc(xb + (size_t)(part ^ 1) * 2 * PAIR_SLOT_BYTES + sl, (uint32_t)PAIR_SLOT_BYTES);
+          pp_u32x4 o[RT][2];
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              o[rt][j] = __builtin_amdgcn_raw_buffer_load_b128(r, (((wave * RT + rt) * 2 + j) * 64 + lane) * 16, 0, CP_COH);
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) accd[rt][j] += __builtin_bit_cast(f32x4, o[rt][j]);  // commutative: same bits in both
+        }
         const float b20 = w.ff2_b[(2 * wave) * 16 + c16], b21 = w.ff2_b[(2 * wave + 1) * 16 + c16];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -500,7 +689,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
       zero_acc(acc);
       pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
       {  // fa <- layer 0's first QKV pair (next step)
-        const int tq[2] = {tq0, tq1};
+        const int tq[2] = {qoff + tq0, qoff + tq1};
         if (nq == 2) pload<2, 8>(fa, a.layers[0].qkv, 8, tq, 0, lane);
         else pload<1, 8>(fa, a.layers[0].qkv, 8, tq, 0, lane);
       }
@@ -515,7 +704,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
       const size_t plane = (size_t)a.n * LC;
       const float* nz = a.noise ? a.noise + (size_t)(a.k0 + k) * plane + (size_t)b * LC : nullptr;
       const bool inp = a.inp_mask != nullptr;
-      const bool ex = a.extras != nullptr && k + 1 == a.n_steps;
+      const bool ex = a.extras != nullptr && k + 1 == a.n_steps && part == 0;
 #pragma unroll
       for (int j = 0; j < NQ; ++j) {
         const int q = tid + NT * j;
@@ -554,7 +743,8 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a) {
     bar_lds();  // E is dead before the next step's Xb zero fill (same scratch)
     PSTAMP(5);
   }
-  // final state -> the internal (L, C) layout
+  // final state -> the internal (L, C) layout (PAIR: both parts hold it; part 0 writes)
+  if (part != 0) return;
   const int L = a.L, C = a.C, LC = L * C;
 #pragma unroll
   for (int j = 0; j < NQ; ++j) {
@@ -575,20 +765,52 @@ bool persist_supported(int dtype, int d_model, int heads, int L, int Ts, int C) 
          C >= 1 && C <= 128;
 }
 
-hipError_t launch_persist(const PersistArgs& a, hipStream_t s) {
-  if (!persist_attrs_done) {
-    (void)hipFuncSetAttribute((const void*)psk_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)psk_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)psk_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    persist_attrs_done = true;
-  }
+static void persist_attrs() {
+  if (persist_attrs_done) return;
+#define GGD_PSK_ATTR(rt, pr) \
+  (void)hipFuncSetAttribute((const void*)psk_kernel<rt, pr>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
+  GGD_PSK_ATTR(1, false); GGD_PSK_ATTR(2, false); GGD_PSK_ATTR(3, false);
+  GGD_PSK_ATTR(1, true); GGD_PSK_ATTR(2, true); GGD_PSK_ATTR(3, true);
+#undef GGD_PSK_ATTR
+  (void)hipGetLastError();
+  persist_attrs_done = true;
+}
+
+template <bool PAIR>
+static hipError_t launch_psk(const PersistArgs& a, int P, dim3 grid, hipStream_t s) {
   const int rt = (a.L + 15) / 16;
-  const dim3 grid(a.n), blk(PK_THREADS);
-  if (rt == 1) hipLaunchKernelGGL(psk_kernel<1>, grid, blk, PPlan<1>::TOTAL, s, a);
-  else if (rt == 2) hipLaunchKernelGGL(psk_kernel<2>, grid, blk, PPlan<2>::TOTAL, s, a);
-  else if (rt == 3) hipLaunchKernelGGL(psk_kernel<3>, grid, blk, PPlan<3>::TOTAL, s, a);
+  const dim3 blk(PK_THREADS);
+  if (rt == 1) hipLaunchKernelGGL((psk_kernel<1, PAIR>), grid, blk, PPlan<1>::TOTAL, s, a, P);
+  else if (rt == 2) hipLaunchKernelGGL((psk_kernel<2, PAIR>), grid, blk, PPlan<2>::TOTAL, s, a, P);
+  else if (rt == 3) hipLaunchKernelGGL((psk_kernel<3, PAIR>), grid, blk, PPlan<3>::TOTAL, s, a, P);
   else return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+hipError_t launch_persist(const PersistArgs& a, hipStream_t s) {
+  persist_attrs();
+  return launch_psk<false>(a, a.n, dim3(a.n), s);
+}
+
+// pairs per launch: the grid (16 workgroups per 8 pairs, one per CU) must be co-resident
+int persist_pair_capacity() {
+  static int cap = -1;
+  if (cap < 0) {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetLastError();
+    cap = std::min(PAIR_MAX, 8 * (cus / 16));
+  }
+  return cap;
+}
+
+hipError_t launch_persist_pair(const PersistArgs& a, int pairs, hipStream_t s) {
+  if (pairs < 1 || pairs > persist_pair_capacity() || !a.ctl || !a.status || !a.xbuf) return hipErrorInvalidValue;
+  persist_attrs();
+  hipError_t e = hipMemsetAsync(a.ctl, 0, sizeof(unsigned) * PAIR_CTL_WORDS, s);
+  if (e != hipSuccess) return e;
+  return launch_psk<true>(a, pairs, dim3(16 * ((pairs + 7) / 8)), s);
 }
 
 }  // namespace ggd

@@ -8,7 +8,7 @@ UNSCALED on the final x:
 
   C2  bf16, 32 clips, DDPM T = 1000 (clip-group persistent loop): rel-RMS <= 5e-2 on clips 0, 1, 31
   C2  f32,  32 clips, DDPM T = 1000:                               max|diff| <= 1e-3 on clips 0, 31
-  C5  bf16, 128 clips, DDIM-50 (one-workgroup-per-clip loop):      rel-RMS <= 5e-2 on clips 0, 64, 127
+  C5  bf16, 128 clips, DDIM-50 (clip-pair loop, 2 workgroups/clip): rel-RMS <= 5e-2 on clips 0, 64, 127
   C4  fp8 step weights, 32 clips x L 160, DDPM T = 1000:           rel-RMS <= 5e-2 on clips 0, 31,
       against the oracle run on the same e4m3-dequantized weights (oracle/fp8.py)
 

@@ -433,3 +433,76 @@ def test_auto_route_large_batch_ddim_bf16(pkg, beat_cfg, setup):
         _route(ctx, 2)
     assert bool(th.isfinite(auto).all())
     assert rel_rms(auto, mk) <= 1e-2
+
+
+# ------------------------------------------------------------------------------------------
+# Clip pairs (ggd_persist.hip, PAIR): two workgroups per clip, each half the heads and FFN
+# chunks, meeting three times per layer.  Checked against the oracle, against the
+# one-workgroup-per-clip loop, on uneven pair counts per XCD (surplus workgroups idle), across
+# two launches (> 128 clips) and on the write-through placement.
+# ------------------------------------------------------------------------------------------
+def _pair(ctx, mode, coh=0):
+    import ctypes
+    arr = (ctypes.c_int32 * 2)(mode, coh)
+    out = ctypes.c_double()
+    rc = ctx.lib.ggd_diag(ctx.h, 14, arr, 2, 1, ctypes.cast(ctypes.byref(out), ctypes.c_void_p))
+    assert rc == 0
+
+
+def _pair_launches(ctx):
+    import ctypes
+    out = ctypes.c_double()
+    arr = (ctypes.c_int32 * 1)(0)
+    assert ctx.lib.ggd_diag(ctx.h, 15, arr, 0, 1, ctypes.cast(ctypes.byref(out), ctypes.c_void_p)) == 0
+    return int(out.value)
+
+
+def test_clip_pair_loop_matches_oracle_bf16(pkg, beat_cfg, setup):
+    _, sd, om = setup
+    model, diffusion = make_model(pkg, beat_cfg, sd, "bf16")
+    n, steps = 4, 6
+    wav, x, _ = inputs(n, seed=61)
+    zs = th.randn(steps, n, D_POSE, L, generator=th.Generator().manual_seed(62))
+    ctx, _ = model.prepare(wav.cuda(), L)
+    outs = {}
+    run = lambda: diffusion.p_sample_loop(model, (n, D_POSE, L), {"wav": wav.cuda()}, noise=x.cuda(),
+                                          step_noise=zs.cuda(), n_steps=steps)["sample"].cpu()
+    try:
+        _route(ctx, 0)                       # the per-clip loops
+        for name, mode, coh in (("pair", 2, 0), ("pair_wt", 2, 1), ("psk", 1, 0)):
+            _pair(ctx, mode, coh)
+            outs[name] = run()
+            assert _pair_launches(ctx) == (1 if mode == 2 else 0), name
+    finally:
+        _pair(ctx, 0)
+        _route(ctx, 2)
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    want = ref_diffusion.sample_loop(sch, om, (n, D_POSE, L), {"wav": wav}, ref_diffusion.InjectedNoise(x, zs),
+                                     "ddpm", x_T=x, n_steps=steps)["sample"]
+    assert rel_rms(outs["pair"], want) <= 5e-2
+    assert rel_rms(outs["pair"], outs["psk"]) <= 1e-2
+    assert th.equal(outs["pair"], outs["pair_wt"])   # placement changes where bytes live, not the arithmetic
+
+
+@pytest.mark.parametrize("n", [100, 130])
+def test_clip_pair_batches_ddim_bf16(pkg, beat_cfg, setup, n):
+    """100 clips: pairs spread unevenly over the XCDs; 130: two launches (128 + 2 pairs)."""
+    _, sd, _ = setup
+    model, _ = make_model(pkg, beat_cfg, sd, "bf16")
+    diffusion = pkg.create_diffusion(dict(beat_cfg.Model.Diffusion.to_dict(), timestep_respacing="ddim50"), False)
+    wav = (th.randn(n, WAV, generator=th.Generator().manual_seed(63)) * 0.1).cuda()
+    ctx, _ = model.prepare(wav, L)
+    run = lambda: diffusion.ddim_sample_loop(model, (n, D_POSE, L), model_kwargs={"wav": wav}, seed=64,
+                                             n_steps=5, extras=False)["sample"].cpu()
+    try:
+        _route(ctx, 0)
+        _pair(ctx, 2)
+        pair = run()
+        assert _pair_launches(ctx) == (n + 127) // 128
+        _pair(ctx, 1)
+        psk = run()
+    finally:
+        _pair(ctx, 0)
+        _route(ctx, 2)
+    assert bool(th.isfinite(pair).all())
+    assert rel_rms(pair, psk) <= 1e-2
