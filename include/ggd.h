@@ -172,7 +172,31 @@ int ggd_kernel_time(ggd_ctx* ctx, int32_t which, double* avg_us, int64_t* launch
  * clip-pair loop (psk_kernel with two workgroups per clip: one launch per <= 128 clips). */
 int ggd_profile_kind(ggd_ctx* ctx);
 
-/* Diagnostics (not part of the reference surface): launch one kernel configuration `iters`
+/* Route selection of ggd_sample (not part of the reference surface: the reference has one
+ * path).  Every route computes the same model; the knobs exist for A/B measurements and for
+ * the tests that compare routes.  Defaults (all 0) pick the fastest measured route per shape. */
+enum {
+  GGD_ROUTE_PER_CLIP = 0,            /* 0 auto, 1 never, 2 always: the per-clip persistent loops
+                                        (one workgroup or a clip pair per clip, ggd_persist.hip) */
+  GGD_ROUTE_PAIR = 1,                /* per-clip loops: 0 auto, 1 never, 2 always two workgroups per clip */
+  GGD_ROUTE_PAIR_WRITE_THROUGH = 2,  /* 1: clip-pair hand-offs written through on any placement */
+  GGD_ROUTE_PHASE_LAUNCHES = 3,      /* 1: per-phase launches instead of the clip-group loop (ggd_mega.hip) */
+  GGD_ROUTE_PLACEMENT = 4            /* clip-group loop: 0 XCD-local, 1 part p on XCD p, 2 group per XCD */
+};
+int ggd_set_route(ggd_ctx* ctx, int32_t knob, int32_t value);
+enum {
+  GGD_INFO_PER_CLIP_AVAILABLE = 0,   /* 1 when the per-clip loops support this shape / dtype */
+  GGD_INFO_LOOP_CAPACITY = 1,        /* clips per launch of the clip-group loop (0: unavailable) */
+  GGD_INFO_PAIR_LAUNCHES = 2,        /* last ggd_sample: clip-pair launches (0: another route) */
+  GGD_INFO_XL_LAUNCHES = 3,          /* last ggd_sample: XCD-local clip-group launches */
+  GGD_INFO_WT_RERUNS = 4             /* last ggd_sample: clip-group launches re-run write-through */
+};
+int ggd_route_info(ggd_ctx* ctx, int32_t what, double* out);
+
+/* ggd_diag (microbenchmarks, phase stamps, calibration kernels) is exported by the separate
+ * diagnostics library libggd_diag.so only (built from the same sources with -DGGD_DIAG plus
+ * ggd_diag.hip; scripts/ load it with GGD_DIAG=1), never by the product libggd.so.  It launches
+ * one kernel configuration `iters`
  * times back to back on the ctx stream and return the average microseconds per launch
  * (hipEvents).  what = 0: GEMM, p = {pro, epi, M, N, K, force_mt, no_xcd_remap};
  * what = 1: attention, p = {cross, n[, no_qsplit]}; what = 2: one full denoise step (eager launches),
@@ -187,8 +211,12 @@ int ggd_profile_kind(ggd_ctx* ctx);
  * the clip-group loop would need >= 3 chunks); returns 1 in *avg_us when psk_kernel is available; what = 8: persistent-kernel phase stamps of
  * iteration 0, p = {1} arm, {2} read (avg_us[0..7]), {0} disarm; what = 9: p = {1} routes
  * ggd_sample through the per-phase launches instead of the persistent loop (ggd_mega.hip), {0}
- * back (returns the loop's clip capacity in *avg_us). */
+ * back (returns the loop's clip capacity in *avg_us); what = 10 / 11: clip-group loop barrier / phase
+ * stamps; what = 12 / 14: as GGD_ROUTE_PLACEMENT / GGD_ROUTE_PAIR (p[1]: write-through);
+ * what = 13 / 15: as ggd_route_info. */
+#ifdef GGD_DIAG
 int ggd_diag(ggd_ctx* ctx, int32_t what, const int32_t* p, int32_t np, int32_t iters, double* avg_us);
+#endif
 
 /* ------------------------------------------------------------------------------------
  * Speech encoder: HA2GSpeechEncoder (models/modules/ha2g/speech_encoder.py:9-61 ->

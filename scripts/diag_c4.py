@@ -1,5 +1,7 @@
 """C4-shape (L = 160, 128,000-sample wav) kernel latencies via ggd_diag on the generic path:
 attention (query-split vs one workgroup per head) and one full denoise step (eager launches)."""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
 import os
 import sys

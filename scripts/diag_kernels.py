@@ -1,4 +1,6 @@
 """Per-kernel latency table via ggd_diag (back-to-back launches, hipEvents on the ctx stream)."""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
 import os
 import sys

@@ -4,6 +4,8 @@ ggd_diag what=5 mode 6 (csrc/ggd_diag.hip mb_xcdsync_kernel): 256 workgroups of 
 groups of 8; each round every member writes kb KiB and gathers all 8 slices of its group.
 Cost per round = slope of the launch time over the number of rounds.
 """
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
 import os
 import sys

@@ -1,4 +1,6 @@
 """One persistent-loop sample and one per-phase sample of 200 steps (for rocprofv3 --pmc)."""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
 import os
 import sys

@@ -1,4 +1,6 @@
 """Persistent reverse loop (ggd_mega.hip) vs the per-phase launches: identical samples, time (GPU box)."""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
 import os
 import sys

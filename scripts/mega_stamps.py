@@ -1,4 +1,6 @@
 """Per-phase time inside the persistent loop: body vs clip-group barrier (GPU box)."""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
 import os
 import sys

@@ -1,4 +1,6 @@
 """Where a bench pass spends its time: encoder, memory install, sampling loop (GPU box)."""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import os
 import sys
 import time

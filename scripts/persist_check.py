@@ -1,4 +1,6 @@
 """Persistent per-clip sampler vs the per-step launch path: agreement and speed (bf16, C2 shape)."""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
 import os
 import sys

@@ -2,6 +2,8 @@
 stores, L2 flag barriers), 1 (workgroup part p of every clip on XCD p, write-through) and 2 (a
 clip's 8 workgroups on one XCD, write-through).  Samples must be bit-identical; prints us/step
 and, for placement 0, how many launches ran XCD-local / fell back to write-through."""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
 import os
 import sys

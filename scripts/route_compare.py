@@ -1,6 +1,8 @@
 """Sampling time per denoise step on the three fused routes (GPU box): the persistent clip-group
 loop (mk_kernel, 8 workgroups per clip), the one-workgroup-per-clip loop (psk_kernel) and the
 per-phase launches, for several batch sizes; plus the bf16 agreement of the routes' samples."""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
 import os
 import sys

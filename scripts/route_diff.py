@@ -1,4 +1,6 @@
 """psk_kernel vs mk_kernel after k steps on the same inputs (GPU box): where do they differ?"""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
 import os
 import sys

@@ -1324,6 +1324,46 @@ int ggd_kernel_time(ggd_ctx* c, int32_t which, double* avg_us, int64_t* launches
   return GGD_OK;
 }
 
+int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
+  if (!c) return GGD_ERR_ARG;
+  switch (knob) {
+    case GGD_ROUTE_PER_CLIP:  // 0 auto, 1 never, 2 always the one-workgroup / clip-pair loops
+      if (value < 0 || value > 2) break;
+      c->persist_mode = value;
+      return GGD_OK;
+    case GGD_ROUTE_PAIR:      // 0 auto, 1 never, 2 always two workgroups per clip (per-clip loops)
+      if (value < 0 || value > 2) break;
+      c->pair_mode = value;
+      return GGD_OK;
+    case GGD_ROUTE_PAIR_WRITE_THROUGH:
+      c->pair_force_coh = value != 0;
+      return GGD_OK;
+    case GGD_ROUTE_PHASE_LAUNCHES:  // 1: per-phase launches instead of the persistent clip-group loop
+      c->no_mega = value != 0;
+      return GGD_OK;
+    case GGD_ROUTE_PLACEMENT:       // clip-group loop: 0 XCD-local, 1 part p on XCD p, 2 group per XCD
+      if (value < 0 || value > 2) break;
+      c->mega_place = value;
+      return GGD_OK;
+    default:
+      break;
+  }
+  return fail(c, GGD_ERR_ARG, "unknown route knob or value");
+}
+
+int ggd_route_info(ggd_ctx* c, int32_t what, double* out) {
+  if (!c || !out) return GGD_ERR_ARG;
+  switch (what) {
+    case GGD_INFO_PER_CLIP_AVAILABLE: *out = c->persist ? 1.0 : 0.0; return GGD_OK;
+    case GGD_INFO_LOOP_CAPACITY: *out = c->fused ? (double)mega_capacity(c->desc.dtype, c->desc.seq_len) : 0.0; return GGD_OK;
+    case GGD_INFO_PAIR_LAUNCHES: *out = c->pair_launches; return GGD_OK;
+    case GGD_INFO_XL_LAUNCHES: *out = c->mega_xl_launches; return GGD_OK;
+    case GGD_INFO_WT_RERUNS: *out = c->mega_fallbacks; return GGD_OK;
+    default: return fail(c, GGD_ERR_ARG, "unknown route info");
+  }
+}
+
+#ifdef GGD_DIAG
 int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t iters, double* avg_us) {
   if (!c || !p || !avg_us || iters <= 0) return fail(c, GGD_ERR_ARG, "bad argument");
   HIP_TRY(c, hipSetDevice(c->device));
@@ -1592,6 +1632,8 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
   (void)hipEventDestroy(e1);
   return rc;
 }
+
+#endif  // GGD_DIAG
 
 }  // extern "C"
 

@@ -3,6 +3,10 @@
 The library is built in-tree (``build()``; ``__graft_entry__.build()`` calls it) so
 the ``.so`` travels with the repository snapshot to the GPU box.  There is no
 fallback: if the library is missing, ``load()`` raises.
+
+``libggd_diag.so`` is the same library built with -DGGD_DIAG plus ggd_diag.hip: it adds the
+``ggd_diag`` microbenchmarks / phase stamps used by scripts/ (``GGD_DIAG=1`` loads it instead).
+The product library never exports them.
 """
 import ctypes
 import os
@@ -10,8 +14,11 @@ import subprocess
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
-LIB_PATH = os.path.join(PKG_DIR, "libggd.so")
-SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_diag.hip", "ggd_encoder.hip", "ggd_api.hip"]
+PRODUCT_LIB = os.path.join(PKG_DIR, "libggd.so")
+DIAG_LIB = os.path.join(PKG_DIR, "libggd_diag.so")
+LIB_PATH = DIAG_LIB if os.environ.get("GGD_DIAG") == "1" else PRODUCT_LIB
+SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_encoder.hip", "ggd_api.hip"]
+DIAG_SOURCES = ["ggd_diag.hip"]   # + ggd_api.hip again with -DGGD_DIAG
 HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_fusedlib.h", "ggd_phases.h", os.path.join("..", "..", "include", "ggd.h")]
 
 GGD_OK, GGD_IGNORED = 0, 1
@@ -24,7 +31,7 @@ DDPM, DDIM = 0, 1
 EXPORTS = [
     "ggd_create", "ggd_destroy", "ggd_last_error", "ggd_load_weight", "ggd_finalize_weights",
     "ggd_set_schedule", "ggd_set_memory", "ggd_set_inpaint", "ggd_denoise", "ggd_posterior_step", "ggd_sample",
-    "ggd_set_profiling", "ggd_kernel_time", "ggd_profile_kind", "ggd_diag", "ggd_version",
+    "ggd_set_profiling", "ggd_kernel_time", "ggd_profile_kind", "ggd_set_route", "ggd_route_info", "ggd_version",
     "ggd_enc_create", "ggd_enc_destroy", "ggd_enc_last_error", "ggd_enc_load_weight", "ggd_enc_finalize",
     "ggd_enc_lengths", "ggd_enc_run",
 ]
@@ -47,14 +54,17 @@ class SampleArgs(ctypes.Structure):
 
 
 def _sources():
-    return [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
+    return [os.path.join(CSRC, s) for s in SOURCES + DIAG_SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
 
 
 def is_stale():
-    if not os.path.exists(LIB_PATH):
-        return True
-    t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(p) > t for p in _sources())
+    for lib in (PRODUCT_LIB, DIAG_LIB):
+        if not os.path.exists(lib):
+            return True
+        t = os.path.getmtime(lib)
+        if any(os.path.getmtime(p) > t for p in _sources()):
+            return True
+    return False
 
 
 def build(force=False, verbose=False):
@@ -65,24 +75,29 @@ def build(force=False, verbose=False):
     # costs issue slots (MI355X_MICROARCH.md, filler prices), and with it hipcc 7.2 clobbered a live
     # register of psk_kernel (the per-thread pose state) around the one-pass LayerNorm.
     flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-fno-slp-vectorize", "-Wno-unused-value", "-Wno-unused-result"]
-    objs, procs = [], []
     os.makedirs(os.path.join(PKG_DIR, "build"), exist_ok=True)
     hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
-    for src in SOURCES:  # one hipcc per translation unit, in parallel
-        obj = os.path.join(PKG_DIR, "build", src.replace(".hip", ".o"))
-        objs.append(obj)
+    units = [(src, src.replace(".hip", ".o"), []) for src in SOURCES + DIAG_SOURCES]
+    units.append(("ggd_api.hip", "ggd_api_diag.o", ["-DGGD_DIAG"]))
+    procs = []
+    for src, obj_name, extra in units:  # one hipcc per translation unit, in parallel
+        obj = os.path.join(PKG_DIR, "build", obj_name)
         if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(os.path.join(CSRC, src))):
             continue  # object newer than its source and every header
-        cmd = ["hipcc"] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = ["hipcc"] + flags + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append(subprocess.Popen(cmd, cwd=CSRC))
     if any(p.wait() != 0 for p in procs):
         raise RuntimeError("hipcc failed")
-    cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", LIB_PATH + ".tmp"]
-    subprocess.run(cmd, check=True, cwd=CSRC)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    obj = lambda n: os.path.join(PKG_DIR, "build", n)
+    product = [obj(s.replace(".hip", ".o")) for s in SOURCES]
+    diag = [o for o in product if not o.endswith("ggd_api.o")] + [obj("ggd_api_diag.o"), obj("ggd_diag.o")]
+    for lib, objs in ((PRODUCT_LIB, product), (DIAG_LIB, diag)):
+        cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", lib + ".tmp"]
+        subprocess.run(cmd, check=True, cwd=CSRC)
+        os.replace(lib + ".tmp", lib)
+    return PRODUCT_LIB
 
 
 _lib = None
@@ -115,7 +130,8 @@ def load():
         "ggd_set_profiling": (ctypes.c_int, [CTX, I32]),
         "ggd_kernel_time": (ctypes.c_int, [CTX, I32, P(ctypes.c_double), P(I64)]),
         "ggd_profile_kind": (ctypes.c_int, [CTX]),
-        "ggd_diag": (ctypes.c_int, [CTX, I32, VP, I32, I32, VP]),
+        "ggd_set_route": (ctypes.c_int, [CTX, I32, I32]),
+        "ggd_route_info": (ctypes.c_int, [CTX, I32, VP]),
         "ggd_version": (ctypes.c_char_p, []),
         "ggd_enc_create": (ctypes.c_int, [ctypes.c_int, I32, I32, I32, I32, P(CTX)]),
         "ggd_enc_destroy": (ctypes.c_int, [CTX]),
@@ -125,6 +141,8 @@ def load():
         "ggd_enc_lengths": (ctypes.c_int, [CTX, P(I32), P(I32), P(I32)]),
         "ggd_enc_run": (ctypes.c_int, [CTX, VP, I32, VP, VP, VP, VP]),
     }
+    if LIB_PATH == DIAG_LIB:
+        sig["ggd_diag"] = (ctypes.c_int, [CTX, I32, VP, I32, I32, VP])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res

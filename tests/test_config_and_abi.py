@@ -90,8 +90,12 @@ def test_inpaint_denoise_matches_reference_formula(pkg):
     assert th.equal(got, want)
 
 
-def _header_symbols():
+def _header_symbols(diag=False):
+    """Function declarations of include/ggd.h (comments stripped); the GGD_DIAG block only with diag."""
     txt = open(os.path.join(ROOT, "include", "ggd.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    if not diag:
+        txt = re.sub(r"#ifdef GGD_DIAG.*?#endif", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(ggd_[a-z_]+)\s*\(", txt)))
 
 
@@ -106,6 +110,19 @@ def test_library_loads_and_exports_every_header_symbol(pkg):
         assert hasattr(lib, s), s
     assert set(syms) == set(native.EXPORTS)
     assert lib.ggd_version().decode().startswith("ggd")
+
+
+def test_diagnostics_stay_out_of_the_product_library(pkg):
+    """ggd_diag (microbenchmarks, stamps) is exported by libggd_diag.so only."""
+    import ctypes
+    native = importlib.import_module(pkg.__name__ + ".native")
+    if native.is_stale():
+        native.build()
+    assert "ggd_diag" in _header_symbols(diag=True) and "ggd_diag" not in _header_symbols()
+    assert not hasattr(ctypes.CDLL(native.PRODUCT_LIB), "ggd_diag")
+    diag = ctypes.CDLL(native.DIAG_LIB)
+    for s in _header_symbols(diag=True):
+        assert hasattr(diag, s), s
 
 
 def test_abi_struct_layouts_match_header(pkg):

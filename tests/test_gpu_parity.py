@@ -384,13 +384,21 @@ def test_inpaint_model_generate_sample_f32(pkg, setup_inp):
 # automatically when the clip-group loop (mk_kernel) would need >= 3 chunks (the C5 shape,
 # 128 clips per GPU); both must agree with the oracle and with each other.
 # ------------------------------------------------------------------------------------------
-def _route(ctx, mode):
+ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_PAIR_WT = 0, 1, 2            # include/ggd.h GGD_ROUTE_*
+INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES = 0, 2              # include/ggd.h GGD_INFO_*
+
+
+def _info(ctx, what):
     import ctypes
-    arr = (ctypes.c_int32 * 1)(mode)
     out = ctypes.c_double()
-    rc = ctx.lib.ggd_diag(ctx.h, 7, arr, 1, 1, ctypes.cast(ctypes.byref(out), ctypes.c_void_p))
-    assert rc == 0
+    assert ctx.lib.ggd_route_info(ctx.h, what, ctypes.cast(ctypes.byref(out), ctypes.c_void_p)) == 0
     return out.value
+
+
+def _route(ctx, mode):
+    """mode 0: always the per-clip loops, 1: never, 2: automatic; returns 1.0 when they fit the shape."""
+    assert ctx.lib.ggd_set_route(ctx.h, ROUTE_PER_CLIP, {0: 2, 1: 1, 2: 0}[mode]) == 0
+    return _info(ctx, INFO_PER_CLIP_AVAILABLE)
 
 
 def test_per_clip_loop_matches_oracle_bf16(pkg, beat_cfg, setup):
@@ -442,19 +450,12 @@ def test_auto_route_large_batch_ddim_bf16(pkg, beat_cfg, setup):
 # two launches (> 128 clips) and on the write-through placement.
 # ------------------------------------------------------------------------------------------
 def _pair(ctx, mode, coh=0):
-    import ctypes
-    arr = (ctypes.c_int32 * 2)(mode, coh)
-    out = ctypes.c_double()
-    rc = ctx.lib.ggd_diag(ctx.h, 14, arr, 2, 1, ctypes.cast(ctypes.byref(out), ctypes.c_void_p))
-    assert rc == 0
+    assert ctx.lib.ggd_set_route(ctx.h, ROUTE_PAIR, mode) == 0
+    assert ctx.lib.ggd_set_route(ctx.h, ROUTE_PAIR_WT, coh) == 0
 
 
 def _pair_launches(ctx):
-    import ctypes
-    out = ctypes.c_double()
-    arr = (ctypes.c_int32 * 1)(0)
-    assert ctx.lib.ggd_diag(ctx.h, 15, arr, 0, 1, ctypes.cast(ctypes.byref(out), ctypes.c_void_p)) == 0
-    return int(out.value)
+    return int(_info(ctx, INFO_PAIR_LAUNCHES))
 
 
 def test_clip_pair_loop_matches_oracle_bf16(pkg, beat_cfg, setup):
