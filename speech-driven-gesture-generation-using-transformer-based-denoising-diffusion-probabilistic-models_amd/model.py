@@ -108,7 +108,8 @@ class Speech2GestureModel:
 
     def train(self, mode=True):
         if mode:
-            raise ValueError("training is out of scope for the HIP sampler (SURVEY.md 8f rank 3)")
+            raise ValueError("the HIP sampler model is inference-only: train through "
+                             "create_model(..., is_training=True) -> training.TrainableModel")
         return self
 
     def state_dict(self):

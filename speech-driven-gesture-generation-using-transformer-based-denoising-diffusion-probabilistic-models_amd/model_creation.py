@@ -21,12 +21,25 @@ def create_model(d_pose, model_params, lr=1e-2, weight_decay=None, scheduler_par
                  dtype="bf16", device="cuda"):
     """model_creation.py:51-191 -> (model, diffusion, optimizer, schedule_sampler, lr_scheduler).
 
-    Inference scope: optimizer, schedule_sampler and lr_scheduler are None (training
-    is SURVEY.md 8f rank 3).  Legacy {"type","args"} model params (tedexp) are
-    adapted to the flat schema first.
+    Inference (is_training False): the HIP sampler model; optimizer, schedule_sampler and
+    lr_scheduler are None.  Training: a training.TrainableModel (reference init, seed 0) with
+    AdamW, the uniform schedule sampler and the configured lr schedule (SURVEY.md 8f rank 3;
+    s2g_v2 + one-way decoder, speech encoder frozen).  Legacy {"type","args"} model params
+    (tedexp) are adapted to the flat schema first.
     """
     if is_training:
-        raise ValueError("training is out of scope for the HIP sampler (SURVEY.md 8f rank 3)")
+        from . import training
+        from .weights import arch_from_config, init_state_dict
+        if not isinstance(model_params, JsonConfig):
+            model_params = JsonConfig(dict(model_params))
+        if is_legacy_schema(model_params):
+            model_params = adapt_legacy({"Model": model_params.to_dict()}).Model
+        arch = arch_from_config(model_params, d_pose)
+        model = training.TrainableModel(arch, init_state_dict(arch, seed=0), device=device)
+        diffusion = create_diffusion(model_params["Diffusion"], True)
+        optimizer = training.AdamW(model, lr=lr, weight_decay=weight_decay)
+        sp = scheduler_params.to_dict() if isinstance(scheduler_params, JsonConfig) else scheduler_params
+        return model, diffusion, optimizer, training.UniformSampler(diffusion), training.LRScheduler(optimizer, sp)
     if not isinstance(model_params, JsonConfig):
         model_params = JsonConfig(dict(model_params))
     if is_legacy_schema(model_params):

@@ -17,9 +17,11 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 PRODUCT_LIB = os.path.join(PKG_DIR, "libggd.so")
 DIAG_LIB = os.path.join(PKG_DIR, "libggd_diag.so")
 LIB_PATH = DIAG_LIB if os.environ.get("GGD_DIAG") == "1" else PRODUCT_LIB
-SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_encoder.hip", "ggd_api.hip"]
+SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_encoder.hip", "ggd_train.hip",
+           "ggd_api.hip"]
 DIAG_SOURCES = ["ggd_diag.hip"]   # + ggd_api.hip again with -DGGD_DIAG
-HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_fusedlib.h", "ggd_phases.h", os.path.join("..", "..", "include", "ggd.h")]
+HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_fusedlib.h", "ggd_phases.h", os.path.join("..", "..", "include", "ggd.h"),
+           os.path.join("..", "..", "include", "ggd_train.h")]
 
 GGD_OK, GGD_IGNORED = 0, 1
 GGD_ERR_ARG, GGD_ERR_UNSUPPORTED, GGD_ERR_HIP, GGD_ERR_STATE, GGD_ERR_NAME = -1, -2, -3, -4, -5
@@ -34,6 +36,10 @@ EXPORTS = [
     "ggd_set_profiling", "ggd_kernel_time", "ggd_profile_kind", "ggd_set_route", "ggd_route_info", "ggd_version",
     "ggd_enc_create", "ggd_enc_destroy", "ggd_enc_last_error", "ggd_enc_load_weight", "ggd_enc_finalize",
     "ggd_enc_lengths", "ggd_enc_run",
+    # training path (include/ggd_train.h)
+    "ggd_tr_gemm", "ggd_tr_colsum", "ggd_tr_layernorm_fwd", "ggd_tr_layernorm_bwd", "ggd_tr_seqconv_fwd",
+    "ggd_tr_seqconv_bwd", "ggd_tr_attention_fwd", "ggd_tr_attention_bwd", "ggd_tr_elementwise", "ggd_tr_q_sample",
+    "ggd_tr_mse", "ggd_tr_sumsq", "ggd_tr_sumsq_blocks", "ggd_tr_adamw", "ggd_tr_scale",
 ]
 
 
@@ -140,6 +146,22 @@ def load():
         "ggd_enc_finalize": (ctypes.c_int, [CTX]),
         "ggd_enc_lengths": (ctypes.c_int, [CTX, P(I32), P(I32), P(I32)]),
         "ggd_enc_run": (ctypes.c_int, [CTX, VP, I32, VP, VP, VP, VP]),
+        "ggd_tr_gemm": (ctypes.c_int, [I32, I32, I32, I32, I32, F, VP, I32, VP, I32, F, VP, I32, VP, VP]),
+        "ggd_tr_colsum": (ctypes.c_int, [I32, I32, VP, I32, VP, F, VP]),
+        "ggd_tr_layernorm_fwd": (ctypes.c_int, [I32, I32, VP, VP, VP, F, VP, VP, VP, VP]),
+        "ggd_tr_layernorm_bwd": (ctypes.c_int, [I32, I32, VP, VP, VP, VP, VP, VP, VP, VP, VP]),
+        "ggd_tr_seqconv_fwd": (ctypes.c_int, [I32, I32, I32, I32, VP, I32, VP, VP, VP, I32, VP]),
+        "ggd_tr_seqconv_bwd": (ctypes.c_int, [I32, I32, I32, I32, VP, I32, VP, VP, I32, VP, I32, VP, VP, VP]),
+        "ggd_tr_attention_fwd": (ctypes.c_int, [I32, I32, I32, I32, I32, F, VP, I32, VP, VP, I32, VP, I32, VP]),
+        "ggd_tr_attention_bwd": (ctypes.c_int, [I32, I32, I32, I32, I32, F, VP, I32, VP, VP, I32, VP, I32, VP, VP,
+                                                VP, VP]),
+        "ggd_tr_elementwise": (ctypes.c_int, [I32, I64, VP, VP, VP, VP]),
+        "ggd_tr_q_sample": (ctypes.c_int, [I32, I32, VP, VP, VP, VP, VP, VP]),
+        "ggd_tr_mse": (ctypes.c_int, [I32, I32, VP, VP, VP, VP, F, VP]),
+        "ggd_tr_sumsq": (ctypes.c_int, [I64, VP, VP, VP, VP]),
+        "ggd_tr_sumsq_blocks": (ctypes.c_int, []),
+        "ggd_tr_adamw": (ctypes.c_int, [I64, VP, VP, VP, VP, F, F, F, F, F, I64, F, VP]),
+        "ggd_tr_scale": (ctypes.c_int, [I64, VP, F, VP]),
     }
     if LIB_PATH == DIAG_LIB:
         sig["ggd_diag"] = (ctypes.c_int, [CTX, I32, VP, I32, I32, VP])

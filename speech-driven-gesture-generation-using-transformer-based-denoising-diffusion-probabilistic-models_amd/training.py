@@ -1,0 +1,614 @@
+"""Training path: loss, backward, AdamW and the gradient all-reduce.
+
+Mirrors the reference's training step (models/trainer.py:131-248):
+  Trainer._compute_loss: x_start = poses^T, noise ~ N(0, 1), t ~ UniformSampler (resample.py:60-68),
+      diffusion.training_losses (gaussian_diffusion.py:531-569) -> mse per clip -> mean
+  Trainer._train_step: zero_grad, backward, compute_grad_norm (trainer.py:341-349), optional
+      clip_grad_norm_ / clip_grad_value_, optimizer.step (AdamW, model_creation.py:176-178),
+      lr_scheduler.step (lr_scheduler.py: ConstantLR / NoamLR "noamxf" / NoamDecayLR "noam")
+  DDP (trainer.py:83, utils/pytorch_ddp.py:18): gradients averaged over ranks by an all-reduce.
+
+Every arithmetic op of the decoder's forward and backward is a hand-written HIP kernel behind
+include/ggd_train.h (csrc/ggd_train.hip), wrapped here in torch.autograd.Function objects: torch
+contributes the chain rule (with its gradient-accumulation adds where one tensor feeds several
+ops) and a few copies (transposes, concatenations, padding).  Parameters live in ONE flat f32 buffer (each parameter a view of it), gradients in a
+second flat buffer (each parameter's .grad a view; autograd accumulates into it in place), so
+the all-reduce is one RCCL call per bucket and AdamW is one HIP launch over the whole model.
+
+Scope: the s2g_v2 model with the one-way decoder (the beat-ours configuration): step encoder,
+blend layer, decoder.  The HA2G speech encoder runs frozen (eval mode, the HIP inference
+encoder) and its parameters are not updated -- the reference also trains it, with BatchNorm in
+train mode; that backward is not built.
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch as th
+import torch.nn.functional as F
+
+from . import native
+from .weights import parameter_shapes
+
+EW_RELU2, EW_RELU2_BWD, EW_SILU, EW_SILU_BWD, EW_ADD = 0, 1, 2, 3, 4   # include/ggd_train.h
+
+
+def _lib():
+    return native.load()
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _s(t):
+    return ctypes.c_void_p(th.cuda.current_stream(t.device).cuda_stream)
+
+
+def _ok(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (ggd_train status {rc})")
+
+
+def gemm(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, alpha=1.0, beta=0.0, bias=None):
+    _ok(_lib().ggd_tr_gemm(ta, tb, M, N, K, alpha, _p(A), lda, _p(B), ldb, beta, _p(C), ldc, _p(bias), _s(C)), "gemm")
+
+
+# ------------------------------------------------------------------------------------------
+# autograd Functions over the HIP kernels
+# ------------------------------------------------------------------------------------------
+class _Linear(th.autograd.Function):
+    """nn.Linear (F.linear): y = x W^T + b; dX = dY W, dW = dY^T X, db = colsum dY."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        M, K = x.shape
+        N = w.shape[0]
+        y = x.new_empty(M, N)
+        gemm(0, 1, M, N, K, x, K, w, K, y, N, bias=b)
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        M, K = x.shape
+        N = w.shape[0]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = x.new_empty(M, K)
+            gemm(0, 0, M, K, N, dy, N, w, K, dx, K)
+        if ctx.needs_input_grad[1]:
+            dw = w.new_empty(N, K)
+            gemm(1, 0, N, K, M, dy, N, x, K, dw, K)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = w.new_empty(N)
+            _ok(_lib().ggd_tr_colsum(M, N, _p(dy), N, _p(db), 0.0, _s(dy)), "colsum")
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    shape = x.shape
+    y = _Linear.apply(x.reshape(-1, shape[-1]).contiguous(), w, b)
+    return y.reshape(*shape[:-1], w.shape[0])
+
+
+class _LayerNorm(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, eps):
+        rows, d = x.shape
+        y = th.empty_like(x)
+        mean = x.new_empty(rows)
+        rstd = x.new_empty(rows)
+        _ok(_lib().ggd_tr_layernorm_fwd(rows, d, _p(x), _p(g), _p(b), eps, _p(y), _p(mean), _p(rstd), _s(x)), "ln fwd")
+        ctx.save_for_backward(x, g, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, g, mean, rstd = ctx.saved_tensors
+        dy = dy.contiguous()
+        rows, d = x.shape
+        dx = th.empty_like(x)
+        dg = th.empty_like(g)
+        db = th.empty_like(g)
+        _ok(_lib().ggd_tr_layernorm_bwd(rows, d, _p(x), _p(g), _p(mean), _p(rstd), _p(dy), _p(dx), _p(dg), _p(db),
+                                        _s(x)), "ln bwd")
+        return dx, dg, db, None
+
+
+def layer_norm(x, g, b, eps=1e-5):
+    shape = x.shape
+    return _LayerNorm.apply(x.reshape(-1, shape[-1]).contiguous(), g, b, eps).reshape(shape)
+
+
+class _SeqConv(th.autograd.Function):
+    """SpatialDepthWiseConv over frames of (n, L, H dk) token matrices."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, heads):
+        n, L, W = x.shape
+        dk = W // heads
+        y = th.empty_like(x)
+        w3 = w.reshape(dk, 3)
+        _ok(_lib().ggd_tr_seqconv_fwd(n, L, heads, dk, _p(x), W, _p(w3), _p(b), _p(y), W, _s(x)), "conv fwd")
+        ctx.save_for_backward(x, w)
+        ctx.heads = heads
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        n, L, W = x.shape
+        H = ctx.heads
+        dk = W // H
+        dx = th.empty_like(x)
+        dw = th.empty_like(w)
+        db = w.new_empty(dk)
+        _ok(_lib().ggd_tr_seqconv_bwd(n, L, H, dk, _p(x), W, _p(w.reshape(dk, 3)), _p(dy), W, _p(dx), W, _p(dw), _p(db),
+                                      _s(x)), "conv bwd")
+        return dx, dw, db, None
+
+
+class _Attention(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, heads, scale):
+        n, Lq, W = q.shape
+        Lk = k.shape[1]
+        dk = W // heads
+        o = th.empty_like(q)
+        _ok(_lib().ggd_tr_attention_fwd(n, heads, Lq, Lk, dk, scale, _p(q), W, _p(k), _p(v), W, _p(o), W, _s(q)),
+            "attention fwd")
+        ctx.save_for_backward(q, k, v)
+        ctx.heads, ctx.scale = heads, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v = ctx.saved_tensors
+        do = do.contiguous()
+        n, Lq, W = q.shape
+        Lk = k.shape[1]
+        H = ctx.heads
+        dq, dk_, dv = th.empty_like(q), th.empty_like(k), th.empty_like(v)
+        _ok(_lib().ggd_tr_attention_bwd(n, H, Lq, Lk, W // H, ctx.scale, _p(q), W, _p(k), _p(v), W, _p(do), W, _p(dq),
+                                        _p(dk_), _p(dv), _s(q)), "attention bwd")
+        return dq, dk_, dv, None, None
+
+
+def _ew(op, a, b=None):
+    out = th.empty_like(a)
+    _ok(_lib().ggd_tr_elementwise(op, a.numel(), _p(a), _p(b), _p(out), _s(a)), "elementwise")
+    return out
+
+
+class _Act(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, fwd_op, bwd_op):
+        x = x.contiguous()
+        ctx.save_for_backward(x)
+        ctx.bwd_op = bwd_op
+        return _ew(fwd_op, x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return _ew(ctx.bwd_op, x, dy.contiguous()), None, None
+
+
+def squared_relu(x):
+    """SquaredReLU (transformer.py:8-16)."""
+    return _Act.apply(x, EW_RELU2, EW_RELU2_BWD)
+
+
+def silu(x):
+    return _Act.apply(x, EW_SILU, EW_SILU_BWD)
+
+
+class _Add(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        return _ew(EW_ADD, a.contiguous(), b.contiguous())
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, dy
+
+
+def add(a, b):
+    return _Add.apply(a, b)
+
+
+# ------------------------------------------------------------------------------------------
+# the trainable model
+# ------------------------------------------------------------------------------------------
+def positional_table(d, max_len):
+    """PositionalEncoding table (transformer.py:157-166), [max_len][d]."""
+    pos = th.arange(0, max_len, dtype=th.float32)[:, None]
+    freq = th.exp(th.arange(0, d, 2, dtype=th.float32) * -(math.log(10000.0) / d))
+    tab = th.zeros(max_len, d)
+    tab[:, 0::2] = th.sin(pos * freq)
+    tab[:, 1::2] = th.cos(pos * freq)
+    return tab
+
+
+def step_embedding(t, dim, max_period=10000):
+    """diffusion_step_embedding (nn.py:17-35): [cos | sin] of t f_k, f_k = exp(-ln(1e4) k / (dim / 2))."""
+    half = dim // 2
+    freqs = th.exp(-math.log(max_period) * th.arange(0, half, dtype=th.float32, device=t.device) / half)
+    arg = t[:, None].float() * freqs[None]
+    return th.cat([th.cos(arg), th.sin(arg)], dim=-1)
+
+
+def _trainable(arch):
+    """Parameter names the training path updates (reference state_dict order): everything of the
+    s2g_v2 model except the speech encoder (frozen) and non-float buffers."""
+    shapes = parameter_shapes(arch)
+    return [(k, shape) for k, (shape, init) in shapes.items()
+            if not k.startswith("speech_encoder.") and init != "int0"]
+
+
+class TrainableModel:
+    """The s2g_v2 + one-way-decoder denoiser (models/model.py:76-117, nn.py:177-228) with its
+    trainable parameters in one flat f32 device buffer under the reference's state_dict names."""
+
+    def __init__(self, arch, sd, device="cuda"):
+        if arch["type"] != "s2g_v2" or arch["decoder"] != "oneway_cross_attention":
+            raise ValueError("the training path covers s2g_v2 with the one-way decoder (beat-ours)")
+        self.arch = arch
+        self.device = th.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("the training path runs on a GPU device only (no CPU fallback)")
+        names = _trainable(arch)
+        total = sum(int(np.prod(s)) for _, s in names)
+        self.flat = th.zeros(total, device=self.device)
+        self.flat_grad = th.zeros(total, device=self.device)
+        self.params = {}
+        off = 0
+        for k, shape in names:
+            n = int(np.prod(shape))
+            p = th.nn.Parameter(self.flat[off:off + n].view(shape))
+            p.grad = self.flat_grad[off:off + n].view(shape)
+            self.params[k] = p
+            off += n
+        self.load_state_dict(sd)
+        self._pe = {}
+        self._enc_sd = {k: v for k, v in sd.items() if k.startswith("speech_encoder.")}
+        self._encoder = None
+
+    def speech_encoder(self):
+        """The frozen HA2G encoder (HIP, f32, eval mode) on this model's encoder weights."""
+        if self._encoder is None:
+            from .encoder import SpeechEncoder
+            self._encoder = SpeechEncoder(self._enc_sd, self.device, dtype="f32", d_model=self.arch["d_model"])
+        return self._encoder
+
+    # -- state ---------------------------------------------------------------------------------
+    def load_state_dict(self, sd, strict=False):
+        missing = [k for k in self.params if k not in sd]
+        if strict and missing:
+            raise RuntimeError(f"missing keys {missing[:5]}")
+        with th.no_grad():
+            for k, p in self.params.items():
+                if k in sd:
+                    p.copy_(sd[k].to(p.device, th.float32).reshape(p.shape))
+        return missing
+
+    def state_dict(self):
+        return {k: p.detach().clone() for k, p in self.params.items()}
+
+    def named_parameters(self):
+        return iter(self.params.items())
+
+    def parameters(self):
+        return iter(self.params.values())
+
+    def zero_grad(self):
+        self.flat_grad.zero_()
+
+    def _pe_rows(self, n, L):
+        key = (n, L)
+        if key not in self._pe:
+            tab = positional_table(self.arch["d_model"], L).to(self.device)
+            self._pe[key] = tab[None].expand(n, L, -1).contiguous()
+        return self._pe[key]
+
+    # -- forward (model.py:81-117 + nn.py:216-228), token-major (N, L, d) ----------------------
+    def _mdha(self, pre, q_in, kv_in):
+        P, H = self.params, self.arch["heads"]
+        d = self.arch["d_model"]
+
+        def heads(x, w):
+            y = linear(x, P[f"{pre}.{w}.0.linear.weight"], P[f"{pre}.{w}.0.linear.bias"])
+            return _SeqConv.apply(y.contiguous(), P[f"{pre}.{w}.1.conv.weight"], P[f"{pre}.{w}.1.conv.bias"], H)
+
+        q, k, v = heads(q_in, "query"), heads(kv_in, "key"), heads(kv_in, "value")
+        o = _Attention.apply(q, k, v, H, 1.0 / math.sqrt(d // H))
+        return linear(o, P[f"{pre}.output.weight"], P[f"{pre}.output.bias"])
+
+    def __call__(self, x_t, t, z):
+        """x_t (N, C, L), t (N,) int64 original timesteps, z = (z_low, z_mid, z_high) speech tokens
+        (N, T_i, d) from the frozen encoder -> eps (N, C, L)."""
+        P, a = self.params, self.arch
+        d = a["d_model"]
+        N, C, L = x_t.shape
+        # memory: [step token; blend(left-padded levels)] (model.py:91-106)
+        e = step_embedding(t.to(self.device), d)
+        s = linear(silu(linear(e, P["diffusion_step_encoder.proj.0.weight"], P["diffusion_step_encoder.proj.0.bias"])),
+                   P["diffusion_step_encoder.proj.2.weight"], P["diffusion_step_encoder.proj.2.bias"])
+        longest = max(zi.shape[1] for zi in z)
+        zz = th.cat([F.pad(zi, (0, 0, longest - zi.shape[1], 0)) for zi in z], dim=-1)
+        sp = linear(zz, P["blend_layer.weight"], P["blend_layer.bias"])
+        mem = th.cat([s[:, None], sp], dim=1)
+        Tm = mem.shape[1]
+        pre = "pose_decoder."
+        m = add(linear(mem, P[pre + "emb_mem.weight"], P[pre + "emb_mem.bias"]), self._pe_rows(N, Tm))
+        h = add(linear(x_t.transpose(1, 2).contiguous(), P[pre + "emb_x.weight"], P[pre + "emb_x.bias"]),
+                self._pe_rows(N, L))
+        for i in range(a["n_layers"]):
+            q = pre + f"layers.{i}."
+            u = layer_norm(h, P[q + "norm_self_attn.weight"], P[q + "norm_self_attn.bias"])
+            h = add(h, self._mdha(q + "self_attn", u, u))
+            u = layer_norm(h, P[q + "norm_cross_attn.weight"], P[q + "norm_cross_attn.bias"])
+            h = add(h, self._mdha(q + "cross_attn", u, m))
+            u = layer_norm(h, P[q + "norm_ff.weight"], P[q + "norm_ff.bias"])
+            f = squared_relu(linear(u, P[q + "feed_forward.layer1.weight"], P[q + "feed_forward.layer1.bias"]))
+            h = add(h, linear(f, P[q + "feed_forward.layer2.weight"], P[q + "feed_forward.layer2.bias"]))
+        u = layer_norm(h, P[pre + "out_layers.0.weight"], P[pre + "out_layers.0.bias"])
+        y = linear(u, P[pre + "out_layers.1.weight"], P[pre + "out_layers.1.bias"])
+        return y.transpose(1, 2)
+
+
+# ------------------------------------------------------------------------------------------
+# loss (gaussian_diffusion.py:531-569)
+# ------------------------------------------------------------------------------------------
+class _DiffusionMSE(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, eps, noise):
+        eps = eps.contiguous()
+        n = eps.shape[0]
+        per = eps[0].numel()
+        mse = eps.new_empty(n)
+        d = th.empty_like(eps)
+        _ok(_lib().ggd_tr_mse(n, per, _p(eps), _p(noise), _p(mse), _p(d), 1.0, _s(eps)), "mse")
+        ctx.save_for_backward(d)
+        return mse
+
+    @staticmethod
+    def backward(ctx, dmse):
+        (d,) = ctx.saved_tensors
+        n = d.shape[0]
+        out = th.empty_like(d)
+        zero = d.new_zeros(n)  # out = dmse[clip] d (the q_sample kernel with coefficients (dmse, 0))
+        _ok(_lib().ggd_tr_q_sample(n, d[0].numel(), _p(d), _p(d), _p(dmse.contiguous()), _p(zero), _p(out), _s(d)),
+            "mse bwd")
+        return out, None
+
+
+def q_sample(diffusion, x_start, t, noise):
+    """gaussian_diffusion.py:188-205 with the fp64 tables cast to f32 per clip (_extract_into_tensor)."""
+    idx = t.cpu().numpy()
+    ca = th.from_numpy(diffusion.sqrt_alphas_cumprod[idx]).float().to(x_start.device)
+    cb = th.from_numpy(diffusion.sqrt_one_minus_alphas_cumprod[idx]).float().to(x_start.device)
+    xt = th.empty_like(x_start)
+    n = x_start.shape[0]
+    _ok(_lib().ggd_tr_q_sample(n, x_start[0].numel(), _p(x_start), _p(noise), _p(ca), _p(cb), _p(xt), _s(xt)),
+        "q_sample")
+    return xt
+
+
+def training_losses(diffusion, model, x_start, t, model_kwargs, noise=None):
+    """GaussianDiffusion.training_losses (gaussian_diffusion.py:531-569): returns mse (N,) with the
+    autograd graph to the parameters, and eps / x_t / pred_x_start / model_mean (detached)."""
+    x_start = x_start.contiguous().float()
+    if noise is None:
+        noise = th.randn_like(x_start)
+    noise = noise.contiguous().float()
+    x_t = q_sample(diffusion, x_start, t, noise)
+    eps = model(x_t, t, model_kwargs["speech_tokens"])
+    assert eps.shape == noise.shape == x_start.shape
+    mse = _DiffusionMSE.apply(eps, noise)
+    with th.no_grad():
+        idx = t.cpu().numpy()
+        ext = lambda arr: th.from_numpy(arr[idx]).float().to(x_t.device).reshape(-1, 1, 1)
+        e = eps.detach()
+        x0 = ext(diffusion.sqrt_recip_alphas_cumprod) * x_t - ext(diffusion.sqrt_recipm1_alphas_cumprod) * e
+        mean = ext(diffusion.posterior_mean_coef1) * x0 + ext(diffusion.posterior_mean_coef2) * x_t
+    return {"mse": mse, "eps": e, "x_t": x_t, "pred_x_start": x0, "model_mean": mean}
+
+
+# ------------------------------------------------------------------------------------------
+# optimizer, schedules, sampler
+# ------------------------------------------------------------------------------------------
+class AdamW:
+    """torch.optim.AdamW (betas 0.9 / 0.999, eps 1e-8, model_creation.py:176-178) over the flat
+    parameter buffer: ONE HIP launch per step."""
+
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        self.model = model
+        self.lr, self.betas, self.eps = float(lr), betas, float(eps)
+        self.weight_decay = 0.0 if weight_decay is None else float(weight_decay)
+        self.param_groups = [{"lr": self.lr, "initial_lr": self.lr}]
+        self.exp_avg = th.zeros_like(model.flat)
+        self.exp_avg_sq = th.zeros_like(model.flat)
+        self.step_count = 0
+
+    def zero_grad(self):
+        self.model.zero_grad()
+
+    def step(self, grad_scale=1.0):
+        self.step_count += 1
+        f = self.model.flat
+        _ok(_lib().ggd_tr_adamw(f.numel(), _p(f), _p(self.model.flat_grad), _p(self.exp_avg), _p(self.exp_avg_sq),
+                                float(self.param_groups[0]["lr"]), self.betas[0], self.betas[1], self.eps,
+                                self.weight_decay, self.step_count, float(grad_scale), _s(f)), "adamw")
+
+    def state_dict(self):
+        return {"step": self.step_count, "exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone(),
+                "param_groups": [dict(g) for g in self.param_groups]}
+
+    def load_state_dict(self, st):
+        self.step_count = int(st["step"])
+        self.exp_avg.copy_(st["exp_avg"])
+        self.exp_avg_sq.copy_(st["exp_avg_sq"])
+        self.param_groups = [dict(g) for g in st["param_groups"]]
+
+
+def parse_steps(s):
+    """model_creation.py parse_steps: '4k' -> 4000, '200k' -> 200000."""
+    s = str(s)
+    return int(float(s[:-1]) * 1000) if s.endswith("k") else int(s)
+
+
+class LRScheduler:
+    """lr_scheduler.py: ConstantLR ('const'), NoamLR ('noamxf'), NoamDecayLR ('noam'), with
+    _LRScheduler's step counting (last_epoch starts at 0 and get_lr runs at construction)."""
+
+    def __init__(self, optimizer, params=None):
+        self.opt = optimizer
+        self.type = (params or {}).get("type", "const")
+        if self.type not in ("const", "noam", "noamxf"):
+            raise ValueError("Unsupport lr_scheduler type.")
+        self.warmup = float(parse_steps(params["warmup_steps"])) if self.type != "const" else 0.0
+        self.d_model = float(params["d_model"]) if self.type == "noamxf" else 0.0
+        self.minimum = (params or {}).get("minimum")
+        self.base_lr = optimizer.param_groups[0]["initial_lr"]
+        self.last_epoch = 0
+        self._apply()
+
+    def get_lr(self):
+        if self.type == "const":
+            return self.base_lr
+        if self.type == "noamxf":
+            cur = self.last_epoch + 1
+            return self.base_lr * self.d_model ** -0.5 * min(cur ** -0.5, cur * self.warmup ** -1.5)
+        last = max(1, self.last_epoch)
+        lr = self.base_lr * self.warmup ** 0.5 * min(last ** -0.5, last * self.warmup ** -1.5)
+        if self.minimum is not None and last > self.warmup and lr < self.minimum:
+            lr = self.minimum
+        return lr
+
+    def _apply(self):
+        self.opt.param_groups[0]["lr"] = self.get_lr()
+
+    def step(self):
+        self.last_epoch += 1
+        self._apply()
+
+    def get_last_lr(self):
+        return [self.opt.param_groups[0]["lr"]]
+
+    def state_dict(self):
+        return {"last_epoch": self.last_epoch}
+
+    def load_state_dict(self, st):
+        self.last_epoch = int(st["last_epoch"])
+        self._apply()
+
+
+class UniformSampler:
+    """resample.py:60-68 + ScheduleSampler.sample (:37-58): uniform t, unit weights."""
+
+    def __init__(self, diffusion):
+        self.num_timesteps = diffusion.num_timesteps
+
+    def sample(self, batch_size, device, rng=np.random):
+        idx = rng.choice(self.num_timesteps, size=(batch_size,))
+        return th.from_numpy(idx).long().to(device), th.ones(batch_size, device=device)
+
+
+# ------------------------------------------------------------------------------------------
+# gradient all-reduce (DDP in kind) and the train step
+# ------------------------------------------------------------------------------------------
+BUCKET_ELEMS = 8 << 20   # 32 MiB of f32 per all-reduce: a handful of large collectives over xGMI
+
+
+def allreduce_gradients(flat_grad, group=None):
+    """Average the flat gradient over the ranks of `group` (DDP's averaging, trainer.py:83):
+    bucketed all_reduce (RCCL over xGMI on GPUs, gloo on CPU)."""
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return flat_grad
+    world = dist.get_world_size(group)
+    if world == 1:
+        return flat_grad
+    for o in range(0, flat_grad.numel(), BUCKET_ELEMS):
+        b = flat_grad[o:o + BUCKET_ELEMS]
+        dist.all_reduce(b, group=group)
+    flat_grad.div_(world)
+    return flat_grad
+
+
+def grad_norm(model):
+    """compute_grad_norm (trainer.py:341-349): the 2-norm of all gradients (HIP reduction)."""
+    g = model.flat_grad
+    lib = _lib()
+    part = g.new_empty(lib.ggd_tr_sumsq_blocks())
+    out = g.new_empty(1)
+    _ok(lib.ggd_tr_sumsq(g.numel(), _p(g), _p(part), _p(out), _s(g)), "sumsq")
+    return float(out.item()) ** 0.5
+
+
+class Trainer:
+    """The reference Trainer's step (trainer.py:131-248) on one rank; world > 1 averages the
+    gradients with allreduce_gradients (torch.distributed must be initialised by the caller,
+    backend 'nccl' = RCCL on ROCm)."""
+
+    def __init__(self, model, diffusion, speech_encoder, lr=1e-3, weight_decay=None, scheduler_params=None,
+                 grad_norm_clip_value=None, grad_clip_value=None, loss_params=None, seed=0):
+        if grad_clip_value is not None:
+            raise ValueError("clip_grad_value_ is not built (beat-ours sets neither clip)")
+        if loss_params:
+            raise ValueError("extra losses (speed_loss, ...) are not built; beat-ours uses none")
+        self.model = model
+        self.diffusion = diffusion
+        self.encoder = speech_encoder if speech_encoder is not None else (lambda wav: model.speech_encoder()(wav))
+        self.optimizer = AdamW(model, lr=lr, weight_decay=weight_decay)
+        self.lr_scheduler = LRScheduler(self.optimizer, scheduler_params)
+        self.schedule_sampler = UniformSampler(diffusion)
+        self.grad_norm_clip_value = grad_norm_clip_value
+        self.rng = np.random.RandomState(seed)
+        self.train_step = 0
+
+    def _compute_loss(self, batch, noise=None, t=None):
+        poses = batch["pose"].to(self.model.device)          # (N, T, C)
+        z = batch.get("speech_tokens")
+        if z is None:
+            z = self.encoder(batch["wav"])                   # frozen HA2G encoder (eval mode)
+        x_start = poses.transpose(1, 2)
+        if noise is None:
+            noise = th.randn_like(x_start)
+        if t is None:
+            t, _ = self.schedule_sampler.sample(poses.shape[0], self.model.device, self.rng)
+        out = training_losses(self.diffusion, self.model, x_start, t, {"speech_tokens": z}, noise=noise)
+        loss = out["mse"].mean()
+        return {"loss": loss, "denoise": loss}
+
+    def step(self, batch, noise=None, t=None):
+        """zero_grad -> loss -> backward -> all-reduce -> grad norm -> clip -> AdamW -> lr step."""
+        self.optimizer.zero_grad()
+        terms = self._compute_loss(batch, noise=noise, t=t)
+        terms["loss"].backward()
+        allreduce_gradients(self.model.flat_grad)
+        gn = grad_norm(self.model)
+        scale = 1.0
+        if self.grad_norm_clip_value is not None:   # clip_grad_norm_: coef = max_norm / (norm + 1e-6), <= 1
+            scale = min(1.0, float(self.grad_norm_clip_value) / (gn + 1e-6))
+        self.optimizer.step(grad_scale=scale)
+        self.lr_scheduler.step()
+        self.train_step += 1
+        return {"loss": float(terms["loss"].item()), "grad_norm": gn, "lr": self.lr_scheduler.get_last_lr()[0]}
+
+    # -- checkpoints in the reference's dict layout (trainer.py:200-224) ------------------------
+    def checkpoint(self):
+        return {"model_state_dict": self.model.state_dict(), "optimizer_state_dict": self.optimizer.state_dict(),
+                "lr_scheduler_state_dict": self.lr_scheduler.state_dict(), "train_step": self.train_step}
+
+    def load_checkpoint(self, ck):
+        self.model.load_state_dict(ck["model_state_dict"])
+        self.optimizer.load_state_dict(ck["optimizer_state_dict"])
+        self.lr_scheduler.load_state_dict(ck["lr_scheduler_state_dict"])
+        self.train_step = int(ck["train_step"])

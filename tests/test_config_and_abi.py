@@ -47,8 +47,10 @@ def test_create_model_surface(pkg, beat_cfg, tedexp_cfg):
     assert model2.arch["decoder"] == "cross_attention"
     with pytest.raises(ValueError):
         pkg.create_model(123, dict(beat_cfg.Model.to_dict(), type="unet"))
-    with pytest.raises(ValueError):
-        pkg.create_model(123, beat_cfg.Model, is_training=True)
+    with pytest.raises(ValueError):   # the training path runs on the GPU only (no CPU fallback)
+        pkg.create_model(123, beat_cfg.Model, is_training=True, device="cpu")
+    with pytest.raises(ValueError):   # and covers s2g_v2 + the one-way decoder
+        pkg.create_model(126, tedexp_cfg.Model, is_training=True, device="cuda")
 
 
 def test_load_state_dict_checks_names_and_shapes(pkg, beat_cfg):
@@ -92,7 +94,7 @@ def test_inpaint_denoise_matches_reference_formula(pkg):
 
 def _header_symbols(diag=False):
     """Function declarations of include/ggd.h (comments stripped); the GGD_DIAG block only with diag."""
-    txt = open(os.path.join(ROOT, "include", "ggd.h")).read()
+    txt = "".join(open(os.path.join(ROOT, "include", h)).read() for h in ("ggd.h", "ggd_train.h"))
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     if not diag:
         txt = re.sub(r"#ifdef GGD_DIAG.*?#endif", "", txt, flags=re.S)

@@ -1,0 +1,243 @@
+"""Training path on the GPU (…_amd/training.py over include/ggd_train.h) against torch / the oracle.
+
+Op level: every HIP forward / backward kernel against torch's own CPU autograd of the same op
+(f32; max|diff| <= 1e-4 relative to the operand scale).  Model level: one training step's loss
+and the gradients of every trainable parameter against torch autograd through the CPU oracle's
+restated model (oracle/ref_denoiser.denoise, gaussian_diffusion.py:531-569's mse) on identical
+x_start / t / noise and identical frozen speech tokens: loss rel <= 1e-5, each gradient
+max|diff| <= 2e-3 x max|grad|.  Optimizer: AdamW against torch.optim.AdamW; two Trainer steps
+(noamxf schedule) against the oracle step with torch.optim.AdamW.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch as th
+import torch.nn.functional as F
+
+from oracle import ref_denoiser
+from tests.conftest import oracle_cfg
+
+pytestmark = pytest.mark.gpu
+
+D_POSE, L, WAV = 123, 40, 32000
+
+
+@pytest.fixture(scope="module")
+def tr(pkg):
+    import importlib
+    return importlib.import_module(pkg.__name__ + ".training")
+
+
+def close(got, want, tol=1e-4):
+    got, want = got.detach().cpu(), want.detach().cpu()
+    scale = max(1.0, want.abs().max().item())
+    err = (got - want).abs().max().item()
+    assert err <= tol * scale, (err, scale)
+
+
+@pytest.mark.parametrize("shape", [(77, 45, 133), (96, 130, 3000)])   # the second one runs split-K
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
+def test_gemm_variants(tr, ta, tb, shape):
+    g = th.Generator().manual_seed(ta * 2 + tb)
+    M, N, K = shape
+    A = th.randn(K, M, generator=g) if ta else th.randn(M, K, generator=g)
+    B = th.randn(N, K, generator=g) if tb else th.randn(K, N, generator=g)
+    C = th.randn(M, N, generator=g)
+    bias = th.randn(N, generator=g)
+    want = 0.5 * ((A.t() if ta else A) @ (B.t() if tb else B)) + 0.25 * C + bias
+    Cd = C.cuda()
+    tr.gemm(ta, tb, M, N, K, A.cuda(), M if ta else K, B.cuda(), K if tb else N, Cd, N, alpha=0.5, beta=0.25,
+            bias=bias.cuda())
+    close(Cd, want, 1e-5)
+
+
+def test_linear_layernorm_act_backward(tr):
+    g = th.Generator().manual_seed(3)
+    x = th.randn(5, 7, 96, generator=g)
+    w = th.randn(160, 96, generator=g) * 0.1
+    b = th.randn(160, generator=g)
+    lg, lb = th.randn(160, generator=g), th.randn(160, generator=g)
+    dy = th.randn(5, 7, 160, generator=g)
+
+    def run(lin, ln, act, tensors):
+        xx, ww, bb, gg, bt = [t.clone().requires_grad_(True) for t in tensors]
+        y = act(ln(lin(xx, ww, bb), gg, bt))
+        y.backward(dy.to(xx.device))
+        return [y] + [t.grad for t in (xx, ww, bb, gg, bt)]
+
+    for act_hip, act_ref in ((tr.squared_relu, lambda u: F.relu(u) ** 2), (tr.silu, F.silu)):
+        got = run(tr.linear, tr.layer_norm, act_hip, [t.cuda() for t in (x, w, b, lg, lb)])
+        want = run(F.linear, lambda u, a, c: F.layer_norm(u, (160,), a, c, 1e-5), act_ref, [x, w, b, lg, lb])
+        for a, c in zip(got, want):
+            close(a, c, 1e-4)
+
+
+def test_seqconv_and_attention_backward(tr):
+    g = th.Generator().manual_seed(4)
+    n, Lq, Lk, H, dk = 3, 40, 32, 8, 32
+    q = th.randn(n, Lq, H * dk, generator=g)
+    k = th.randn(n, Lk, H * dk, generator=g)
+    v = th.randn(n, Lk, H * dk, generator=g)
+    w = th.randn(dk, 1, 3, generator=g)
+    bc = th.randn(dk, generator=g)
+    do = th.randn(n, Lq, H * dk, generator=g)
+    scale = 1 / math.sqrt(dk)
+
+    def conv_ref(x, w_, b_):  # transformer.py:28-44: padding 2, crop 1 each side
+        y = x.reshape(n, -1, H, dk).permute(0, 2, 3, 1).reshape(n * H, dk, -1)
+        y = F.conv1d(y, w_, b_, padding=2, groups=dk)[:, :, 1:-1]
+        return y.reshape(n, H, dk, -1).permute(0, 3, 1, 2).reshape(n, -1, H * dk)
+
+    def attn_ref(q_, k_, v_):
+        qh, kh, vh = (t.reshape(n, -1, H, dk).transpose(1, 2) for t in (q_, k_, v_))
+        p = th.softmax(qh @ kh.transpose(-1, -2) * scale, dim=-1)
+        return (p @ vh).transpose(1, 2).reshape(n, -1, H * dk)
+
+    def run(conv, attn, dev):
+        ts = [t.to(dev).clone().requires_grad_(True) for t in (q, k, v, w, bc)]
+        qq, kk, vv, ww, bb = ts
+        o = attn(conv(qq, ww, bb), kk, vv)
+        o.backward(do.to(dev))
+        return [o] + [t.grad for t in ts]
+
+    got = run(lambda x, w_, b_: tr._SeqConv.apply(x, w_, b_, H), lambda a, b_, c: tr._Attention.apply(a, b_, c, H, scale),
+              "cuda")
+    want = run(conv_ref, attn_ref, "cpu")
+    for a, c in zip(got, want):
+        close(a, c, 1e-4)
+
+
+def test_adamw_matches_torch(tr, pkg, beat_cfg):
+    arch = pkg.arch_from_config(beat_cfg.Model, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=0)
+    model = tr.TrainableModel(arch, sd, "cuda")
+    ref = model.flat.detach().cpu().clone().requires_grad_(True)
+    opt_ref = th.optim.AdamW([ref], lr=3e-3, weight_decay=0.01)
+    opt = tr.AdamW(model, lr=3e-3, weight_decay=0.01)
+    g = th.Generator().manual_seed(5)
+    for _ in range(3):
+        grad = th.randn(ref.shape, generator=g) * 1e-2
+        ref.grad = grad.clone()
+        opt_ref.step()
+        model.flat_grad.copy_(grad)
+        opt.step()
+    close(model.flat, ref, 2e-6)
+    gn = tr.grad_norm(model)
+    want = grad.double().norm().item()   # f64: a long f32 CPU reduction drifts by ~1e-4
+    assert abs(gn - want) <= 1e-5 * want, (gn, want)
+
+
+@pytest.fixture(scope="module")
+def train_setup(pkg, beat_cfg, tr):
+    arch = pkg.arch_from_config(beat_cfg.Model, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    enc_model, diffusion, _, _, _ = pkg.create_model(D_POSE, beat_cfg.Model, dtype="f32", device="cuda:0")
+    enc_model.load_state_dict(sd)
+    diffusion = pkg.create_diffusion(beat_cfg.Model.Diffusion.to_dict(), True)
+    n = 3
+    g = th.Generator().manual_seed(7)
+    wav = th.randn(n, WAV, generator=g) * 0.1
+    z = enc_model.encoder()(wav.cuda())
+    return arch, sd, diffusion, n, g, z
+
+
+def _oracle_loss(arch, sd_ref, diffusion, x0, t, noise, z_cpu):
+    idx = t.numpy()
+    ca = th.from_numpy(diffusion.sqrt_alphas_cumprod[idx]).float().reshape(-1, 1, 1)
+    cb = th.from_numpy(diffusion.sqrt_one_minus_alphas_cumprod[idx]).float().reshape(-1, 1, 1)
+    x_t = ca * x0 + cb * noise
+    cfg = oracle_cfg(arch)
+    speech = ref_denoiser.speech_memory(sd_ref, cfg, z_cpu)
+    eps = ref_denoiser.denoise(sd_ref, cfg, x_t, t, speech=speech)
+    return ((eps - noise) ** 2).mean(dim=(1, 2)).mean()
+
+
+def test_training_step_gradients_match_oracle(tr, train_setup):
+    arch, sd, diffusion, n, g, z = train_setup
+    model = tr.TrainableModel(arch, sd, "cuda")
+    x0 = th.randn(n, D_POSE, L, generator=g)
+    t = th.tensor([999, 417, 3])
+    noise = th.randn(n, D_POSE, L, generator=g)
+    model.zero_grad()
+    out = tr.training_losses(diffusion, model, x0.cuda(), t.cuda(), {"speech_tokens": z}, noise=noise.cuda())
+    loss = out["mse"].mean()
+    loss.backward()
+    names = list(model.params)
+    sd_ref = {k: v.detach().float().clone() for k, v in sd.items()}
+    for k in names:
+        sd_ref[k].requires_grad_(True)
+    want = _oracle_loss(arch, sd_ref, diffusion, x0, t, noise, tuple(a.cpu() for a in z))
+    want.backward()
+    assert abs(loss.item() - want.item()) <= 1e-5 * want.item(), (loss.item(), want.item())
+    # The key conv biases get an exactly-zero gradient (softmax over keys is invariant to a bias
+    # added to every key): both sides hold rounding noise there, so every error is measured
+    # against max(max|grad| of the tensor, 1e-4 x the largest gradient of the model).
+    floor = 1e-4 * max(sd_ref[k].grad.abs().max().item() for k in names)
+    worst = []
+    for k in names:
+        gg, gr = model.params[k].grad.cpu(), sd_ref[k].grad
+        assert gr is not None, k
+        s = max(gr.abs().max().item(), floor)
+        e = (gg - gr).abs().max().item() / s
+        worst.append((e, k, gr.abs().max().item()))
+    worst.sort(reverse=True)
+    print("\nworst gradient errors (max|diff| / scale, tensor, max|grad|):", worst[:6])
+    for k in names:
+        if k.endswith("key.1.conv.bias"):
+            assert sd_ref[k].grad.abs().max().item() <= 1e-3 * floor / 1e-4
+    assert worst[0][0] <= 2e-3, worst[:6]
+
+
+def test_trainer_steps_match_torch_adamw(tr, train_setup):
+    arch, sd, diffusion, n, g, z = train_setup
+    sched = {"type": "noamxf", "warmup_steps": "4k", "d_model": 256}
+    model = tr.TrainableModel(arch, sd, "cuda")
+    trainer = tr.Trainer(model, diffusion, speech_encoder=None, lr=1.0, weight_decay=0.0, scheduler_params=sched)
+    names = list(model.params)
+    sd_ref = {k: v.detach().float().clone() for k, v in sd.items()}
+    params = [sd_ref[k].requires_grad_(True) for k in names]
+    opt = th.optim.AdamW(params, lr=1.0, weight_decay=0.0)
+    noam = lambda step: 256 ** -0.5 * min((step + 1) ** -0.5, (step + 1) * 4000 ** -1.5)   # lr_scheduler.py NoamLR
+    z_cpu = tuple(a.cpu() for a in z)
+    for step in range(2):
+        x0 = th.randn(n, D_POSE, L, generator=g)
+        t = th.randint(0, 1000, (n,), generator=g)
+        noise = th.randn(n, D_POSE, L, generator=g)
+        res = trainer.step({"pose": x0.transpose(1, 2).cuda(), "speech_tokens": z}, noise=noise.cuda(), t=t.cuda())
+        for grp in opt.param_groups:
+            grp["lr"] = noam(step)
+        opt.zero_grad()
+        loss = _oracle_loss(arch, sd_ref, diffusion, x0, t, noise, z_cpu)
+        loss.backward()
+        opt.step()
+        assert abs(res["loss"] - loss.item()) <= 1e-4 * loss.item()
+        assert abs(res["lr"] - noam(step + 1)) <= 1e-12
+    got = th.cat([model.params[k].detach().cpu().reshape(-1) for k in names])
+    want = th.cat([sd_ref[k].detach().reshape(-1) for k in names])
+    start = th.cat([sd[k].float().reshape(-1) for k in names])
+    d_got, d_want = got - start, want - start
+    rel = ((d_got - d_want).norm() / d_want.norm()).item()
+    assert rel <= 2e-2, rel   # AdamW's m / sqrt(v) amplifies f32 summation-order noise where g ~ 0
+    ck = trainer.checkpoint()
+    assert set(ck) >= {"model_state_dict", "optimizer_state_dict", "lr_scheduler_state_dict", "train_step"}
+
+
+def test_create_model_training_surface(pkg, beat_cfg, tr):
+    """create_model(is_training=True) returns the reference's 5-tuple (model_creation.py:51-191)."""
+    model, diffusion, opt, sampler, sched = pkg.create_model(
+        D_POSE, beat_cfg.Model, lr=1.0, weight_decay=0.0, is_training=True, device="cuda:0",
+        scheduler_params={"type": "noamxf", "warmup_steps": "4k", "d_model": 256})
+    assert isinstance(model, tr.TrainableModel) and isinstance(opt, tr.AdamW)
+    assert diffusion.num_timesteps == 1000 and sampler.num_timesteps == 1000
+    assert sched.get_last_lr()[0] == pytest.approx(256 ** -0.5 * 4000 ** -1.5)
+    n_train = sum(p.numel() for p in model.parameters())
+    assert n_train == model.flat.numel()
+    wav = th.randn(2, WAV, generator=th.Generator().manual_seed(9)) * 0.1
+    trainer = tr.Trainer(model, diffusion, None, lr=1.0, weight_decay=0.0,
+                         scheduler_params={"type": "noamxf", "warmup_steps": "4k", "d_model": 256})
+    poses = th.randn(2, L, D_POSE, generator=th.Generator().manual_seed(10))
+    before = model.flat.clone()
+    res = trainer.step({"pose": poses.cuda(), "wav": wav.cuda()})   # speech tokens from the frozen HIP encoder
+    assert np.isfinite(res["loss"]) and res["grad_norm"] > 0
+    assert not th.equal(before, model.flat)
