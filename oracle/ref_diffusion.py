@@ -7,6 +7,8 @@ Test infrastructure only (see oracle/__init__.py).  Restates
 fp64 numpy schedule tables, fp32 torch tensor math, exactly the reference's
 operation order (the HIP update kernel is checked bit-for-bit against it).
 """
+import math
+
 import numpy as np
 import torch as th
 
@@ -336,3 +338,60 @@ def generate_sequence(sch, model, wav_seqs, wav_sr, pose_dim, pose_fps, pose_win
                                  inpaint_poses, masks, sample_alg, trans_factor, pose_seed_len, n_steps=n_steps)
         samples.append(sample)
     return combine_windows(samples, pose_seed_len, seq_len, smooth_trans)
+
+
+# ----------------------------------------------------------------------------
+# variational bound in bits per dim: gaussian_diffusion.py:571-678 + losses.py
+# ----------------------------------------------------------------------------
+
+def normal_kl(mean1, logvar1, mean2, logvar2):
+    """losses.py normal_kl."""
+    logvar1 = logvar1 if isinstance(logvar1, th.Tensor) else th.tensor(logvar1)
+    logvar2 = logvar2 if isinstance(logvar2, th.Tensor) else th.tensor(logvar2)
+    return 0.5 * (-1.0 + logvar2 - logvar1 + th.exp(logvar1 - logvar2) + ((mean1 - mean2) ** 2) * th.exp(-logvar2))
+
+
+def continuous_gaussian_log_likelihood(x, means, log_scales):
+    """losses.py continuous_gaussian_log_likelihood (log N(x; mean, exp(log_scale)^2) in nats, no
+    -log(scale) term, as the reference writes it)."""
+    c = (x - means) * th.exp(-log_scales)
+    return (-c ** 2 / 2) - th.log(th.sqrt(2 * th.tensor(math.pi)))
+
+
+def mean_flat(x):
+    return x.mean(dim=list(range(1, x.dim())))
+
+
+def calc_bpd_loop(sch, model, x_start, model_kwargs, noises):
+    """calc_bpd_loop (gaussian_diffusion.py:624-678) with the per-t noise given as noises[k] for the
+    k-th iteration (t = T' - 1 - k), in place of th.randn_like."""
+    n = x_start.shape[0]
+    shape = x_start.shape
+    vb, xmse, mse = [], [], []
+    for k, i in enumerate(list(range(sch.num_timesteps))[::-1]):
+        it = th.full((n,), i, dtype=th.long)
+        noise = noises[k]
+        ac = np.asarray(sch.alphas_cumprod)
+        x_t = _ext(np.sqrt(ac), it, shape) * x_start + _ext(np.sqrt(1.0 - ac), it, shape) * noise
+        # _vb_terms_bpd (:575-606)
+        true_mean = (_ext(sch.posterior_mean_coef1, it, shape) * x_start
+                     + _ext(sch.posterior_mean_coef2, it, shape) * x_t)
+        true_logvar = _ext(sch.posterior_log_variance_clipped, it, shape)
+        out = p_mean_variance(sch, model, x_t, i, model_kwargs)
+        kl = mean_flat(normal_kl(true_mean, true_logvar, out["mean"], out["log_variance"])) / math.log(2.0)
+        nll = -continuous_gaussian_log_likelihood(x_start, out["mean"], 0.5 * out["log_variance"])
+        nll = mean_flat(nll) / math.log(2.0)
+        vb.append(th.where(it == 0, nll, kl))
+        xmse.append(mean_flat((out["pred_x_start"] - x_start) ** 2))
+        # _predict_eps_from_xstart (:294-298)
+        eps = ((_ext(sch.sqrt_recip_alphas_cumprod, it, shape) * x_t - out["pred_x_start"])
+               / _ext(sch.sqrt_recipm1_alphas_cumprod, it, shape))
+        mse.append(mean_flat((eps - noise) ** 2))
+    vb, xmse, mse = th.stack(vb, 1), th.stack(xmse, 1), th.stack(mse, 1)
+    # _prior_bpd (:608-622): q(x_T | x_0) against N(0, 1)
+    last = th.full((n,), sch.num_timesteps - 1, dtype=th.long)
+    ac = np.asarray(sch.alphas_cumprod)
+    qm = _ext(np.sqrt(ac), last, shape) * x_start
+    qlv = _ext(np.log(1.0 - ac), last, shape)
+    prior = mean_flat(normal_kl(qm, qlv, th.zeros(()), th.zeros(()))) / math.log(2.0)
+    return {"total_bpd": vb.sum(dim=1) + prior, "prior_bpd": prior, "vb": vb, "x_start_mse": xmse, "mse": mse}

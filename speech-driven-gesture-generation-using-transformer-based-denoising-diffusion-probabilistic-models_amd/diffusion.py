@@ -229,3 +229,50 @@ class GaussianSpacedDiffusion(GaussianDiffusion):
                    "eps": eps, "pred_x_start": x0, "raw_x_start": raw}
             x = xn
         return out
+
+    # ------------------------------------------------------------------ variational bound
+    def _ext(self, arr, i, like):
+        """_extract_into_tensor (gaussian_diffusion.py:681-694): fp64 table value -> f32 per clip."""
+        return th.tensor(float(arr[i]), dtype=th.float32, device=like.device)
+
+    def calc_bpd_loop(self, model, x_start, model_kwargs, noise=None, seed=None):
+        """gaussian_diffusion.py:624-678 (bits per dim over every kept step t = T' - 1 .. 0, with the
+        _vb_terms_bpd terms of :575-606 and the prior term of :608-622).  The model runs on the HIP
+        denoiser (one ggd_denoise per t for the whole batch); the per-t noise is noise[k] for the
+        k-th iteration when given ((T', N, C, L)), else drawn on the device in loop order."""
+        x_start = x_start.float()
+        dev = x_start.device
+        N = x_start.shape[0]
+        dims = list(range(1, x_start.dim()))
+        g = th.Generator(device=dev).manual_seed(seed if seed is not None else 0) if noise is None else None
+        log2 = math.log(2.0)
+        vb, xmse, mse = [], [], []
+        for k, i in enumerate(list(range(self.num_timesteps))[::-1]):
+            z = noise[k].to(dev).float() if noise is not None else th.randn(x_start.shape, device=dev, generator=g)
+            x_t = self._ext(self.sqrt_alphas_cumprod, i, x_start) * x_start + \
+                self._ext(self.sqrt_one_minus_alphas_cumprod, i, x_start) * z
+            t = th.full((N,), self.timestep_map[i], dtype=th.long, device=dev)
+            eps = model(x_t, t, **model_kwargs).float()
+            x0 = self._ext(self.sqrt_recip_alphas_cumprod, i, x_start) * x_t - \
+                self._ext(self.sqrt_recipm1_alphas_cumprod, i, x_start) * eps
+            c1, c2 = self._ext(self.posterior_mean_coef1, i, x_start), self._ext(self.posterior_mean_coef2, i, x_start)
+            model_mean = c1 * x0 + c2 * x_t
+            true_mean = c1 * x_start + c2 * x_t
+            logv = self._ext(self.posterior_log_variance_clipped, i, x_start)
+            if i == 0:   # decoder NLL: -log N(x_0; model mean, exp(logv)) (losses.py)
+                c = (x_start - model_mean) * th.exp(-0.5 * logv)
+                term = -((-c ** 2 / 2) - math.log(math.sqrt(2 * math.pi)))
+            else:        # KL(q(x_{t-1} | x_t, x_0) || p(x_{t-1} | x_t)), equal fixed variances
+                term = 0.5 * (-1.0 + logv - logv + th.exp(logv - logv) + (true_mean - model_mean) ** 2 * th.exp(-logv))
+            vb.append(term.mean(dim=dims) / log2)
+            xmse.append(((x0 - x_start) ** 2).mean(dim=dims))
+            e2 = (self._ext(self.sqrt_recip_alphas_cumprod, i, x_start) * x_t - x0) / \
+                self._ext(self.sqrt_recipm1_alphas_cumprod, i, x_start)
+            mse.append(((e2 - z) ** 2).mean(dim=dims))
+        vb, xmse, mse = th.stack(vb, 1), th.stack(xmse, 1), th.stack(mse, 1)
+        last = self.num_timesteps - 1
+        qm = self._ext(self.sqrt_alphas_cumprod, last, x_start) * x_start
+        qlv = self._ext(self.log_one_minus_alphas_cumprod, last, x_start)
+        prior = (0.5 * (-1.0 - qlv + th.exp(qlv) + qm ** 2)).mean(dim=dims) / log2
+        return {"total_bpd": vb.sum(dim=1) + prior, "prior_bpd": prior, "vb": vb, "x_start_mse": xmse, "mse": mse}
+

@@ -44,6 +44,21 @@ class Generator:
         return np.sum(timings) / repetitions, np.std(timings)
 
     @th.no_grad()
+    def eval_bpd(self, poses, wavs, pose_seed_len=None, noise=None, seed=None):
+        """generator.py:197-216: the variational bound of poses (N, T, C) given wavs (N, T_wav),
+        diffusion.calc_bpd_loop on x_start = poses^T; the inpaint model conditions on the first
+        pose_seed_len frames."""
+        poses = poses.to(self.model.device, th.float32)
+        model_kwargs = {"wav": wavs.to(self.model.device, th.float32)}
+        if getattr(self.model, "arch", {}).get("type") == "inpaint":
+            assert pose_seed_len is not None, "Provide pose_seed_len for inpaint model."
+            masks = th.ones_like(poses)[:, :, :1]
+            masks[:, pose_seed_len:] = 0
+            model_kwargs["inpaint_pose"] = poses.clone().transpose(0, 1)
+            model_kwargs["inpaint_mask"] = masks.transpose(0, 1)
+        return self.diffusion.calc_bpd_loop(self.model, poses.transpose(1, 2), model_kwargs, noise=noise, seed=seed)
+
+    @th.no_grad()
     def generate_sample(self, shape: Tuple[int], wavs: th.Tensor, noise: th.Tensor = None,
                         inpaint_poses: th.Tensor = None, inpaint_masks: th.Tensor = None,
                         sample_alg: str = "ddim", trans_factor: float = None, pose_seed_len: int = None,

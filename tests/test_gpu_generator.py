@@ -138,3 +138,31 @@ def test_eval_infer_time_ddim(pkg, beat_cfg, setup):
     assert np.isfinite(mean_ms) and mean_ms > 0 and std_ms >= 0
     with pytest.raises(ValueError):
         gen.eval_infer_time_ddim((1, D_POSE, L), {"wav": wav}, sample_alg="bogus", repetitions=1)
+
+
+def test_eval_bpd_matches_oracle_f32(pkg, beat_cfg):
+    """Generator.eval_bpd -> calc_bpd_loop (generator.py:197-216, gaussian_diffusion.py:571-678) on the
+    HIP denoiser (f32) against the oracle restatement, identical per-t noise; respaced to 20 steps
+    so the oracle finishes in seconds.  Tolerance: total / prior bpd and every vb / mse term rel <= 1e-3."""
+    from oracle import ref_denoiser, ref_diffusion
+    from tests.conftest import oracle_cfg
+    arch = pkg.arch_from_config(beat_cfg.Model, 123)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    model, _, _, _, _ = pkg.create_model(123, beat_cfg.Model, dtype="f32", device="cuda:0")
+    model.load_state_dict(sd)
+    diffusion = pkg.create_diffusion(dict(beat_cfg.Model.Diffusion.to_dict(), timestep_respacing="20"), False)
+    gen = pkg.Generator(model, diffusion)
+    g = th.Generator().manual_seed(31)
+    n = 2
+    poses = th.randn(n, 40, 123, generator=g) * 0.5
+    wavs = th.randn(n, 32000, generator=g) * 0.1
+    noise = th.randn(diffusion.num_timesteps, n, 123, 40, generator=g)
+    got = gen.eval_bpd(poses.cuda(), wavs.cuda(), noise=noise.cuda())
+    om = ref_denoiser.OracleModel(sd, oracle_cfg(arch), cache_speech=True)
+    sch = ref_diffusion.make_schedule("linear", 1000, "20")
+    want = ref_diffusion.calc_bpd_loop(sch, om, poses.transpose(1, 2), {"wav": wavs}, noise)
+    for k in ("total_bpd", "prior_bpd", "vb", "x_start_mse", "mse"):
+        a, b = got[k].cpu(), want[k]
+        assert a.shape == b.shape, k
+        err = ((a - b).abs() - 1e-3 * b.abs() - 1e-5 * b.abs().max()).max().item()
+        assert err <= 0, (k, (a - b).abs().max().item(), b.abs().max().item())

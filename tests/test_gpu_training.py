@@ -241,3 +241,27 @@ def test_create_model_training_surface(pkg, beat_cfg, tr):
     res = trainer.step({"pose": poses.cuda(), "wav": wav.cuda()})   # speech tokens from the frozen HIP encoder
     assert np.isfinite(res["loss"]) and res["grad_norm"] > 0
     assert not th.equal(before, model.flat)
+
+
+def test_checkpoint_roundtrip_resumes_identically(pkg, beat_cfg, tr, train_setup, tmp_path):
+    """formats.save_checkpoint (trainer.py:200-212 layout) -> load_checkpoint -> Trainer.load_checkpoint:
+    the resumed trainer's next step equals the uninterrupted one bit for bit."""
+    import importlib
+    fm = importlib.import_module(pkg.__name__ + ".formats")
+    arch, sd, diffusion, n, g, z = train_setup
+    sched = {"type": "noamxf", "warmup_steps": "4k", "d_model": 256}
+    mk = lambda: tr.Trainer(tr.TrainableModel(arch, sd, "cuda"), diffusion, None, lr=1.0, weight_decay=0.0,
+                            scheduler_params=sched)
+    a = mk()
+    gg = th.Generator().manual_seed(21)
+    batches = [({"pose": th.randn(n, L, D_POSE, generator=gg).cuda(), "speech_tokens": z},
+                th.randn(n, D_POSE, L, generator=gg).cuda(), th.randint(0, 1000, (n,), generator=gg).cuda())
+               for _ in range(2)]
+    a.step(batches[0][0], noise=batches[0][1], t=batches[0][2])
+    path = tmp_path / "chkpt_gpu0_seed0.pt"
+    fm.save_checkpoint(str(path), a)
+    b = mk()
+    b.load_checkpoint(fm.load_checkpoint(str(path), map_location="cuda:0"))
+    ra = a.step(batches[1][0], noise=batches[1][1], t=batches[1][2])
+    rb = b.step(batches[1][0], noise=batches[1][1], t=batches[1][2])
+    assert ra == rb and th.equal(a.model.flat, b.model.flat)
