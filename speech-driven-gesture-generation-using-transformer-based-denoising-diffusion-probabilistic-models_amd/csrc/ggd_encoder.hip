@@ -4,10 +4,9 @@
 // Runs ONCE per clip (the reference recomputes it inside every denoise step, model.py:95-96;
 // in eval mode it is a pure function of the clip's audio).  Pipeline per chunk of clips:
 //
-//   frames   pre-emphasis (ha2g/model/utils.py:22-38) + centre reflect pad + framing  -> f32 [n*F][1024]
-//   DFT      frames x [cos | -sin] basis with the Hann window folded in (f32 MFMA GEMM,
-//            launch_gemm)                                                            -> f32 [n*F][1088]
-//   power    re^2 + im^2                                                              -> f32 [n*F][516]
+//   STFT     one workgroup per frame: pre-emphasis (ha2g/model/utils.py:22-38) + centre reflect
+//            pad + Hann window, 1024-point radix-2 FFT in LDS (f64-exact twiddles),
+//            power re^2 + im^2 of the 513 one-sided bins                             -> f32 [n*F][516]
 //   mel      power x HTK filterbank (f32 MFMA GEMM)                                   -> f32 [n*F][128]
 //   inorm    +1e-6, InstanceNorm1d(128) over frames (speech_encoder.py:28,57-58)     -> f32 [n][128][F]
 //   conv1    3x3 1->32 + bias, ReLU, BN (ResNetSE34V2.py:118-126) on VALU             -> f32 NHWC [n][128][F][32]
@@ -45,7 +44,6 @@ using namespace ggd;
 namespace {
 
 constexpr int NFFT = 1024, HOP = 512, NBIN = NFFT / 2 + 1, NMEL = 128;
-constexpr int SPEC_LD = 1088;   // 2 * 513 columns padded to the GEMM's 64-column tiles
 constexpr int POW_LD = 516;     // 513 power bins, rows 16-byte aligned
 constexpr int CONV_TPB = 256;   // 4 waves; a wave owns 32 output pixels
 constexpr int SE_SLICES = 64;   // pixel slices of the SE squeeze's first stage
@@ -53,32 +51,43 @@ constexpr int SE_SLICES = 64;   // pixel slices of the SE squeeze's first stage
 // ------------------------------------------------------------------------------------------
 // front end
 // ------------------------------------------------------------------------------------------
-__global__ void enc_frames_kernel(const float* __restrict__ wav, float* __restrict__ frames, int n, int Tw, int F,
-                                  float coef) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x, total = (size_t)n * F * NFFT;
-  if (idx >= total) return;
-  const int k = (int)(idx % NFFT), f = (int)((idx / NFFT) % F), b = (int)(idx / ((size_t)NFFT * F));
-  // centre reflect padding of n_fft / 2 (torch.stft center=True, pad_mode='reflect')
-  int src = f * HOP + k - NFFT / 2;
-  if (src < 0) src = -src;
-  if (src >= Tw) src = 2 * (Tw - 1) - src;
-  // pre-emphasis y[j] = x[j] - c x[j - 1], reflect-padded on the left: y[0] = x[0] - c x[1]
+// Power spectrum of frame (clip b, frame f): torch.stft(n_fft 1024, hop 512, Hann window,
+// center=True, pad_mode='reflect', onesided) |X_k|^2 (speech_encoder.py:18-26).  The frame is loaded
+// in bit-reversed order, then 10 radix-2 decimation-in-time stages run in LDS (512 butterflies
+// per stage over 256 threads); tw[t] = exp(-2 pi i t / 1024), t < 512, rounded once from f64.
+__global__ void __launch_bounds__(256) enc_stft_power_kernel(const float* __restrict__ wav, const float* __restrict__ window,
+                                                             const float2* __restrict__ tw, float* __restrict__ pw, int Tw,
+                                                             int F, float coef) {
+  __shared__ float2 a[NFFT];
+  const int fr = blockIdx.x, b = fr / F, f = fr - b * F;
   const float* x = wav + (size_t)b * Tw;
-  const int prev = src == 0 ? 1 : src - 1;
-  frames[idx] = x[src] - coef * x[prev];
-}
-
-__global__ void enc_power_kernel(const float* __restrict__ spec, float* __restrict__ pw, int M) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)M * POW_LD) return;
-  const int f = (int)(idx % POW_LD);
-  const size_t m = idx / POW_LD;
-  float v = 0.f;
-  if (f < NBIN) {
-    const float re = spec[m * SPEC_LD + f], im = spec[m * SPEC_LD + NBIN + f];
-    v = re * re + im * im;
+  for (int k = threadIdx.x; k < NFFT; k += blockDim.x) {
+    // centre reflect padding of n_fft / 2 (torch.stft center=True, pad_mode='reflect')
+    int src = f * HOP + k - NFFT / 2;
+    if (src < 0) src = -src;
+    if (src >= Tw) src = 2 * (Tw - 1) - src;
+    // pre-emphasis y[j] = x[j] - c x[j - 1], reflect-padded on the left: y[0] = x[0] - c x[1]
+    const int prev = src == 0 ? 1 : src - 1;
+    a[__brev((unsigned)k) >> 22] = make_float2((x[src] - coef * x[prev]) * window[k], 0.f);
   }
-  pw[idx] = v;
+  __syncthreads();
+#pragma unroll 1
+  for (int st = 1; st <= 10; ++st) {
+    const int half = 1 << (st - 1), stride = NFFT >> st;
+    for (int j = threadIdx.x; j < NFFT / 2; j += blockDim.x) {
+      const int pos = j & (half - 1), i1 = ((j >> (st - 1)) << st) + pos, i2 = i1 + half;
+      const float2 w = tw[pos * stride], u = a[i1], v = a[i2];
+      const float2 t = make_float2(v.x * w.x - v.y * w.y, v.x * w.y + v.y * w.x);
+      a[i1] = make_float2(u.x + t.x, u.y + t.y);
+      a[i2] = make_float2(u.x - t.x, u.y - t.y);
+    }
+    __syncthreads();
+  }
+  for (int k = threadIdx.x; k < POW_LD; k += blockDim.x) {
+    float p = 0.f;
+    if (k < NBIN) p = a[k].x * a[k].x + a[k].y * a[k].y;
+    pw[(size_t)fr * POW_LD + k] = p;
+  }
 }
 
 // +1e-6, instance norm over frames per (clip, mel bin) -> image [n][128][F]; one workgroup per clip
@@ -605,14 +614,14 @@ struct ggd_enc {
   std::vector<void*> allocs;
   bool finalized = false;
   // weights
-  float *basis = nullptr, *fbT = nullptr, *zeros = nullptr;
+  float *window = nullptr, *twiddle = nullptr, *fbT = nullptr, *zeros = nullptr;
   float coef = 0.97f;
   float *c1_w = nullptr, *c1_b = nullptr, *c1_s = nullptr, *c1_t = nullptr;
   std::vector<EBlock> blocks;
   EHead head[3];
   float *proj_w = nullptr, *proj_b = nullptr;
   // workspaces (chunk clips)
-  float *frames = nullptr, *spec = nullptr, *pw = nullptr, *mel = nullptr, *img = nullptr;
+  float *pw = nullptr, *mel = nullptr, *img = nullptr;
   float *buf[4] = {}, *feat[3] = {}, *se_y = nullptr, *se_part = nullptr, *hbuf = nullptr, *sbuf = nullptr;
 };
 
@@ -842,20 +851,20 @@ int ggd_enc_finalize(ggd_enc* e) {
   NEED(PFX + "wav2spec.1.mel_scale.fb", (size_t)NBIN * NMEL, fb);
   NEED(PFX + "wav2spec.0.flipped_filter", 2, pre);
   e->coef = -(*pre)[0];
-  // DFT basis (rows = output columns of the GEMM): [cos | -sin](2 pi k f / n_fft) * window[k]
-  std::vector<float> basis((size_t)SPEC_LD * NFFT, 0.f);
-  for (int f = 0; f < NBIN; ++f)
-    for (int k = 0; k < NFFT; ++k) {
-      const double ang = 2.0 * M_PI * (double)((long)k * f % NFFT) / NFFT;
-      basis[(size_t)f * NFFT + k] = (float)(std::cos(ang) * (*win)[k]);
-      basis[(size_t)(NBIN + f) * NFFT + k] = (float)(-std::sin(ang) * (*win)[k]);
-    }
-  ENC_TRY(e, upload(e, &e->basis, basis));
+  // FFT twiddles exp(-2 pi i t / n_fft), t < n_fft / 2, as (re, im) pairs
+  std::vector<float> tw((size_t)NFFT, 0.f);
+  for (int t = 0; t < NFFT / 2; ++t) {
+    const double ang = 2.0 * M_PI * (double)t / NFFT;
+    tw[2 * t] = (float)std::cos(ang);
+    tw[2 * t + 1] = (float)(-std::sin(ang));
+  }
+  ENC_TRY(e, upload(e, &e->twiddle, tw));
+  ENC_TRY(e, upload(e, &e->window, *win));
   std::vector<float> fbT((size_t)NMEL * 768, 0.f);
   for (int m = 0; m < NMEL; ++m)
     for (int f = 0; f < NBIN; ++f) fbT[(size_t)m * 768 + f] = (*fb)[(size_t)f * NMEL + m];
   ENC_TRY(e, upload(e, &e->fbT, fbT));
-  ENC_TRY(e, upload(e, &e->zeros, std::vector<float>(SPEC_LD, 0.f)));
+  ENC_TRY(e, upload(e, &e->zeros, std::vector<float>(NMEL, 0.f)));
 
   // conv1 + bn1
   {
@@ -914,8 +923,6 @@ int ggd_enc_finalize(ggd_enc* e) {
   }
   // workspaces for one chunk of clips
   const size_t n = e->chunk, F = e->F;
-  ENC_TRY(e, ealloc(e, &e->frames, sizeof(float) * n * F * NFFT));
-  ENC_TRY(e, ealloc(e, &e->spec, sizeof(float) * n * F * SPEC_LD));
   ENC_TRY(e, ealloc(e, &e->pw, sizeof(float) * n * F * POW_LD));
   ENC_TRY(e, ealloc(e, &e->mel, sizeof(float) * n * F * NMEL));
   ENC_TRY(e, ealloc(e, &e->img, sizeof(float) * n * F * NMEL));
@@ -946,27 +953,13 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
   for (int c0 = 0; c0 < n; c0 += e->chunk) {
     const int m = std::min(e->chunk, n - c0);
     const float* w = wav + (size_t)c0 * e->wav_len;
-    // front end
-    const size_t nf = (size_t)m * F * NFFT;
-    hipLaunchKernelGGL(enc_frames_kernel, dim3(blocks_for(nf, 256)), dim3(256), 0, s, w, e->frames, m, e->wav_len, F,
-                       e->coef);
+    // front end: STFT power, then the mel GEMM
+    hipLaunchKernelGGL(enc_stft_power_kernel, dim3(m * F), dim3(256), 0, s, w, e->window, (const float2*)e->twiddle,
+                       e->pw, e->wav_len, F, e->coef);
     ENC_TRY(e, hipGetLastError());
     GemmArgs g{};
     g.M = m * F;
-    g.N = SPEC_LD;
-    g.K = NFFT;
-    g.k_valid = NFFT;
-    g.A = e->frames;
-    g.lda = NFFT;
-    g.W = e->basis;
     g.bias = e->zeros;
-    g.out = e->spec;
-    g.ldo = SPEC_LD;
-    g.n_valid = SPEC_LD;
-    ENC_TRY(e, launch_gemm(GGD_F32, PRO_F32, EPI_F32, g, s));
-    hipLaunchKernelGGL(enc_power_kernel, dim3(blocks_for((size_t)m * F * POW_LD, 256)), dim3(256), 0, s, e->spec,
-                       e->pw, m * F);
-    ENC_TRY(e, hipGetLastError());
     g.N = NMEL;
     g.K = 768;
     g.k_valid = NBIN;
