@@ -251,6 +251,11 @@ int ggd_enc_lengths(const ggd_enc* enc, int32_t* t_low, int32_t* t_mid, int32_t*
 int ggd_enc_run(ggd_enc* enc, const float* wav, int32_t n, float* z_low, float* z_mid, float* z_high,
                 void* stream);
 
+/* The encoder's front end only: wav (N, wav_len) -> the InstanceNorm'd mel image img (N, 128, F)
+ * f32 (pre-emphasis, STFT power, mel, +1e-6, InstanceNorm1d: speech_encoder.py:18-34,53-58), the
+ * parameter-free input of the SE-ResNet that the training path differentiates through. */
+int ggd_enc_frontend(ggd_enc* enc, const float* wav, int32_t n, float* img, void* stream);
+
 /* Library version string. */
 const char* ggd_version(void);
 

@@ -58,7 +58,11 @@ enum {
   GGD_EW_RELU2_BWD = 1,  /* out = b 2 relu(a)        (a: pre-activation, b: upstream gradient) */
   GGD_EW_SILU = 2,       /* out = a sigmoid(a) */
   GGD_EW_SILU_BWD = 3,   /* out = b (s + a s (1 - s)), s = sigmoid(a) */
-  GGD_EW_ADD = 4         /* out = a + b */
+  GGD_EW_ADD = 4,        /* out = a + b */
+  GGD_EW_RELU = 5,       /* out = relu(a)                (ResNetSE34V2.py:119, ResNetBlocks.py:24,34) */
+  GGD_EW_RELU_BWD = 6,   /* out = a > 0 ? b : 0           (a: pre-activation) */
+  GGD_EW_SIGMOID = 7,    /* out = sigmoid(a)              (SELayer, ResNetBlocks.py:88) */
+  GGD_EW_SIGMOID_BWD = 8 /* out = b a (1 - a)             (a: the sigmoid OUTPUT) */
 };
 int ggd_tr_elementwise(int op, int64_t n, const float* a, const float* b, float* out, void* stream);
 
@@ -81,6 +85,34 @@ int ggd_tr_adamw(int64_t n, float* p, const float* g, float* m, float* v, float 
                  float weight_decay, int64_t step, float grad_scale, void* stream);
 /* x *= s (clip_grad_norm_ applied in place). */
 int ggd_tr_scale(int64_t n, float* x, float s, void* stream);
+
+/* ---- speech-encoder training (HA2G SE-ResNet34, ha2g/model/ResNetSE34V2.py:118-188,
+ * ResNetBlocks.py:7-96) on NHWC activations: rows = pixels (n, h, w), channels innermost ---- */
+
+/* nn.Conv2d as im2col + ggd_tr_gemm: col[(n, oh, ow)][(ky, kx, c)] (zeros outside the image);
+ * col2im is its adjoint (a gather: each input pixel sums the entries copied from it). */
+int ggd_tr_im2col(int N, int H, int W, int C, int KH, int KW, int stride, int pad, const float* x, float* col,
+                  void* stream);
+int ggd_tr_col2im(int N, int H, int W, int C, int KH, int KW, int stride, int pad, const float* dcol, float* dx,
+                  void* stream);
+/* nn.BatchNorm2d in train mode over P = N H W rows (batch statistics, biased variance in the
+ * normalisation, eps); var_unbiased (nullable) receives the variance for the running-stat
+ * update.  Backward gives dx, dgamma, dbeta. */
+int ggd_tr_batchnorm_fwd(int P, int C, const float* x, const float* g, const float* b, float eps, float* y, float* mean,
+                         float* rstd, float* var_unbiased, void* stream);
+int ggd_tr_batchnorm_bwd(int P, int C, const float* x, const float* g, const float* mean, const float* rstd,
+                         const float* dy, float* dx, float* dg, float* db, void* stream);
+/* SELayer pieces (ResNetBlocks.py:81-96): out[n][c] = scale sum_p x[n][p][c] (y[n][p][c]);
+ * channel_scale: out[n][p][c] = x[n][p][c] s[n][c] (+ add[n][c]; x null: add broadcast only). */
+int ggd_tr_image_channel_sum(int N, int HW, int C, const float* x, const float* y, float scale, float* out,
+                             void* stream);
+int ggd_tr_channel_scale(int N, int HW, int C, const float* x, const float* s, const float* add, float* out,
+                         void* stream);
+/* nn.PixelShuffle(r) (ResNetSE34V2.py:169,179) on NHWC: src [N][H][W][C r^2] -> dst [N][H r][W r][C];
+ * backward = 1 moves dst-shaped gradients back to the src shape. */
+int ggd_tr_pixel_shuffle(int N, int H, int W, int C, int r, const float* src, float* dst, int backward, void* stream);
+/* head flatten (ResNetSE34V2.py:161-165): NHWC [N][H][W][C] -> rows (n, w) x features (c H + h). */
+int ggd_tr_head_flatten(int N, int H, int W, int C, const float* src, float* dst, int backward, void* stream);
 
 #ifdef __cplusplus
 }

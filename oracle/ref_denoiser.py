@@ -213,8 +213,11 @@ def mel_power_spectrogram(wav, window, fb, n_fft=1024, hop=512):
     return th.matmul(power.transpose(-1, -2), fb).transpose(-1, -2)
 
 
-def _bn(sd, name, x):
-    """BatchNorm2d in eval mode (running stats, eps 1e-5): main.py:116 calls model.eval()."""
+def _bn(sd, name, x, train=False):
+    """BatchNorm2d (eps 1e-5): eval mode uses the running stats (main.py:116 calls model.eval());
+    train mode (trainer.py:229 model.train()) normalises with the batch statistics."""
+    if train:
+        return F.batch_norm(x, None, None, sd[name + ".weight"], sd[name + ".bias"], True, 0.0, 1e-5)
     return F.batch_norm(x, sd[name + ".running_mean"], sd[name + ".running_var"],
                         sd[name + ".weight"], sd[name + ".bias"], False, 0.0, 1e-5)
 
@@ -223,35 +226,36 @@ def _conv(sd, name, x, stride=1, padding=0):
     return F.conv2d(x, sd[name + ".weight"], sd.get(name + ".bias"), stride=stride, padding=padding)
 
 
-def _se_block(sd, name, x, stride):
+def _se_block(sd, name, x, stride, train=False):
     """SEBasicBlock.forward: ha2g/model/ResNetBlocks.py:21-37 (ReLU before BN after conv1)."""
     out = _conv(sd, name + ".conv1", x, stride=stride, padding=1)
-    out = _bn(sd, name + ".bn1", F.relu(out))
-    out = _bn(sd, name + ".bn2", _conv(sd, name + ".conv2", out, padding=1))
+    out = _bn(sd, name + ".bn1", F.relu(out), train)
+    out = _bn(sd, name + ".bn2", _conv(sd, name + ".conv2", out, padding=1), train)
     # SELayer: ResNetBlocks.py:81-96
     y = out.mean(dim=(2, 3))
     y = F.relu(_lin(sd, name + ".se.fc.0", y))
     y = th.sigmoid(_lin(sd, name + ".se.fc.2", y))
     out = out * y[:, :, None, None]
     if (name + ".downsample.0.weight") in sd:
-        res = _bn(sd, name + ".downsample.1", _conv(sd, name + ".downsample.0", x, stride=stride))
+        res = _bn(sd, name + ".downsample.1", _conv(sd, name + ".downsample.0", x, stride=stride), train)
     else:
         res = x
     return F.relu(out + res)
 
 
-def _head(sd, feat, conv, bn, fc, shuffle):
+def _head(sd, feat, conv, bn, fc, shuffle, train=False):
     """Low/mid/high heads: ResNetSE34V2.py:157-188 (PixelShuffle, conv, ReLU, BN, flatten c*H, Linear)."""
     if shuffle > 1:
         feat = F.pixel_shuffle(feat, shuffle)
-    feat = _bn(sd, bn, F.relu(_conv(sd, conv, feat)))
+    feat = _bn(sd, bn, F.relu(_conv(sd, conv, feat)), train)
     n, c, hgt, w = feat.shape
     feat = feat.reshape(n, c * hgt, w).transpose(1, 2)
     return _lin(sd, fc, feat)
 
 
-def speech_encoder(sd, wav):
-    """HA2GSpeechEncoder.forward: speech_encoder.py:37-61 -> (z_low, z_mid, z_high), each (N, T_i, d)."""
+def speech_encoder(sd, wav, train=False):
+    """HA2GSpeechEncoder.forward: speech_encoder.py:37-61 -> (z_low, z_mid, z_high), each (N, T_i, d).
+    train: BatchNorm on batch statistics (the training step's mode); the front end has no state."""
     p = "speech_encoder."
     x = pre_emphasis(wav)
     x = mel_power_spectrogram(x, sd[p + "wav2spec.1.spectrogram.window"], sd[p + "wav2spec.1.mel_scale.fb"])
@@ -260,15 +264,15 @@ def speech_encoder(sd, wav):
     # Hierarchical_WavEncoder / ResNetSE.forward: hierarchy_net.py:16-19, ResNetSE34V2.py:118-188
     r = p + "wav_encoder.feat_extractor."
     x = x[:, None]
-    x = _bn(sd, r + "bn1", F.relu(_conv(sd, r + "conv1", x, padding=1)))
+    x = _bn(sd, r + "bn1", F.relu(_conv(sd, r + "conv1", x, padding=1)), train)
     feats = []
     for li, (nblk, stride) in enumerate(zip((3, 4, 6, 3), (1, 2, 2, 2))):
         for bi in range(nblk):
-            x = _se_block(sd, r + f"layer{li + 1}.{bi}", x, stride if bi == 0 else 1)
+            x = _se_block(sd, r + f"layer{li + 1}.{bi}", x, stride if bi == 0 else 1, train)
         feats.append(x)
-    low = _head(sd, feats[1], r + "conv_low", r + "bn_low", r + "fc_low", 1)
-    mid = _head(sd, feats[2], r + "conv_mid", r + "bn_mid", r + "fc_mid", 2)
-    high = _head(sd, feats[3], r + "conv_high", r + "bn_high", r + "fc_high", 4)
+    low = _head(sd, feats[1], r + "conv_low", r + "bn_low", r + "fc_low", 1, train)
+    mid = _head(sd, feats[2], r + "conv_mid", r + "bn_mid", r + "fc_mid", 2, train)
+    high = _head(sd, feats[3], r + "conv_high", r + "bn_high", r + "fc_high", 4, train)
     proj = p + "wav_proj_layer"
     return _lin(sd, proj, low), _lin(sd, proj, mid), _lin(sd, proj, high)
 

@@ -1,0 +1,44 @@
+"""Step-phase stamps of the per-clip loops (psk_kernel, one workgroup or a clip pair per clip) at the
+C5 shape: workgroup 0's s_memtime at the PSTAMP points of iteration 0 (emb, SA/CA of the last layer,
+all layers, step end), in microseconds from the step start."""
+import os as _os
+_os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
+import ctypes
+import os
+import sys
+
+import torch as th
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+pkg = ge.load_package()
+native = __import__(ge.PKG_NAME + ".native", fromlist=["x"])
+cfg = pkg.load_config(os.path.join(ROOT, "configs", "beat-ours.json"))
+model, _, _, _, _ = pkg.create_model(123, cfg.Model, dtype="bf16", device="cuda:0")
+model.load_state_dict(pkg.init_state_dict(model.arch, seed=0))
+diffusion = pkg.create_diffusion(dict(cfg.Model.Diffusion.to_dict(), timestep_respacing="ddim50"), False)
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+wav = th.randn(B, 32000, device="cuda") * 0.1
+ctx, _ = model.prepare(wav, 40)
+
+
+def diag(what, vals, n_out=17):
+    arr = (ctypes.c_int32 * len(vals))(*vals)
+    res = (ctypes.c_double * n_out)()
+    native.check(ctx.h, ctx.lib.ggd_diag(ctx.h, what, arr, len(vals), 1, ctypes.cast(res, ctypes.c_void_p)), "diag")
+    return list(res)
+
+
+names = ["emb", "L3 SA", "L3 CA", "layers", "step"]
+for label, pair in (("one workgroup per clip", 1), ("clip pair", 2)):
+    diag(7, [0])            # the per-clip loops
+    diag(14, [pair, 0])
+    for rep in range(3):
+        diag(8, [1])
+        diffusion.ddim_sample_loop(model, (B, 123, 40), model_kwargs={"wav": wav}, seed=1, n_steps=3, extras=False)
+        t = diag(8, [2])
+        print(f"{label:24s} rep {rep}: " + "  ".join(f"{n} {t[i]:7.2f}" for i, n in enumerate(names)), flush=True)
+diag(14, [0, 0])
+diag(7, [2])

@@ -943,6 +943,37 @@ int ggd_enc_finalize(ggd_enc* e) {
   return GGD_OK;
 }
 
+int ggd_enc_frontend(ggd_enc* e, const float* wav, int32_t n, float* img, void* stream) {
+  if (!e || !wav || !img) return efail(e, GGD_ERR_ARG, "null argument");
+  if (!e->finalized) return efail(e, GGD_ERR_STATE, "encoder weights not finalized");
+  if (n <= 0 || n > e->max_batch) return efail(e, GGD_ERR_ARG, "batch outside [1, max_batch]");
+  ENC_TRY(e, hipSetDevice(e->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int F = e->F;
+  for (int c0 = 0; c0 < n; c0 += e->chunk) {
+    const int m = std::min(e->chunk, n - c0);
+    hipLaunchKernelGGL(enc_stft_power_kernel, dim3(m * F), dim3(256), 0, s, wav + (size_t)c0 * e->wav_len, e->window,
+                       (const float2*)e->twiddle, e->pw, e->wav_len, F, e->coef);
+    ENC_TRY(e, hipGetLastError());
+    GemmArgs g{};
+    g.M = m * F;
+    g.bias = e->zeros;
+    g.N = NMEL;
+    g.K = 768;
+    g.k_valid = NBIN;
+    g.A = e->pw;
+    g.lda = POW_LD;
+    g.W = e->fbT;
+    g.out = e->mel;
+    g.ldo = NMEL;
+    g.n_valid = NMEL;
+    ENC_TRY(e, launch_gemm(GGD_F32, PRO_F32, EPI_F32, g, s));
+    hipLaunchKernelGGL(enc_inorm_kernel, dim3(m), dim3(NMEL), 0, s, e->mel, img + (size_t)c0 * NMEL * F, F);
+    ENC_TRY(e, hipGetLastError());
+  }
+  return GGD_OK;
+}
+
 int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_mid, float* z_high, void* stream) {
   if (!e || !wav || !z_low || !z_mid || !z_high) return efail(e, GGD_ERR_ARG, "null argument");
   if (!e->finalized) return efail(e, GGD_ERR_STATE, "encoder weights not finalized");

@@ -408,6 +408,10 @@ __global__ void ew_kernel(int op, int64_t n, const float* __restrict__ a, const 
     case GGD_EW_RELU2_BWD: r = b[i] * 2.f * fmaxf(x, 0.f); break;
     case GGD_EW_SILU: r = x / (1.f + expf(-x)); break;
     case GGD_EW_SILU_BWD: { const float s = 1.f / (1.f + expf(-x)); r = b[i] * (s + x * s * (1.f - s)); break; }
+    case GGD_EW_RELU: r = fmaxf(x, 0.f); break;
+    case GGD_EW_RELU_BWD: r = x > 0.f ? b[i] : 0.f; break;
+    case GGD_EW_SIGMOID: r = 1.f / (1.f + expf(-x)); break;
+    case GGD_EW_SIGMOID_BWD: r = b[i] * x * (1.f - x); break;   // a: the sigmoid OUTPUT
     default: r = x + b[i]; break;  // GGD_EW_ADD
   }
   out[i] = r;
@@ -492,6 +496,178 @@ __global__ void adamw_kernel(int64_t n, float* p, const float* __restrict__ g, f
 __global__ void scale_kernel(int64_t n, float* x, float s) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] *= s;
+}
+
+// ------------------------------------------------------------------------------------------
+// speech-encoder training ops, NHWC activations (rows = pixels (n, h, w), channels innermost)
+// ------------------------------------------------------------------------------------------
+// im2col: col[(n, oh, ow)][(ky, kx, c)] = x[n][oh s - pad + ky][ow s - pad + kx][c], 0 outside
+__global__ void im2col_kernel(const float* __restrict__ x, int N, int H, int W, int C, int KH, int KW, int st, int pad,
+                              int Ho, int Wo, float* __restrict__ col) {
+  const int64_t total = (int64_t)N * Ho * Wo * KH * KW * C;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int c = (int)(e % C);
+  int64_t t = e / C;
+  const int kx = (int)(t % KW);
+  t /= KW;
+  const int ky = (int)(t % KH);
+  const int64_t p = t / KH;
+  const int ow = (int)(p % Wo), oh = (int)((p / Wo) % Ho), n = (int)(p / ((int64_t)Wo * Ho));
+  const int ih = oh * st - pad + ky, iw = ow * st - pad + kx;
+  col[e] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? x[(((int64_t)n * H + ih) * W + iw) * C + c] : 0.f;
+}
+
+// col2im as a gather: dx[n][ih][iw][c] = sum of the col entries that im2col copied from it
+__global__ void col2im_kernel(const float* __restrict__ dcol, int N, int H, int W, int C, int KH, int KW, int st,
+                              int pad, int Ho, int Wo, float* __restrict__ dx) {
+  const int64_t total = (int64_t)N * H * W * C;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int c = (int)(e % C);
+  const int64_t q = e / C;
+  const int iw = (int)(q % W), ih = (int)((q / W) % H), n = (int)(q / ((int64_t)W * H));
+  float s = 0.f;
+  for (int ky = 0; ky < KH; ++ky) {
+    const int ty = ih + pad - ky;
+    if (ty < 0 || ty % st) continue;
+    const int oh = ty / st;
+    if (oh >= Ho) continue;
+    for (int kx = 0; kx < KW; ++kx) {
+      const int tx = iw + pad - kx;
+      if (tx < 0 || tx % st) continue;
+      const int ow = tx / st;
+      if (ow >= Wo) continue;
+      s += dcol[((((int64_t)n * Ho + oh) * Wo + ow) * KH * KW + ky * KW + kx) * C + c];
+    }
+  }
+  dx[e] = s;
+}
+
+// per-channel column statistics over P rows of C channels, two fixed-order stages (RS-row slices):
+//   mode 0: sum x;  mode 1: sum (x - mean[c])^2;  mode 2: sum dy and sum dy (x - mean[c]) rstd[c]
+__global__ void chan_partial_kernel(int P, int C, int mode, const float* __restrict__ X, const float* __restrict__ DY,
+                                    const float* __restrict__ mean, const float* __restrict__ rstd, float* part,
+                                    float* part2) {
+  __shared__ float red[2][4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * RS, r1 = min(P, r0 + RS);
+  float s = 0.f, s2 = 0.f;
+  if (c < C) {
+    const float mu = mode ? mean[c] : 0.f, rs = mode == 2 ? rstd[c] : 0.f;
+    for (int r = r0 + ph; r < r1; r += 4) {
+      const float v = X[(size_t)r * C + c];
+      if (mode == 0) {
+        s += v;
+      } else if (mode == 1) {
+        s += (v - mu) * (v - mu);
+      } else {
+        const float g = DY[(size_t)r * C + c];
+        s += g;
+        s2 += g * (v - mu) * rs;
+      }
+    }
+  }
+  red[0][ph][threadIdx.x & 63] = s;
+  red[1][ph][threadIdx.x & 63] = s2;
+  __syncthreads();
+  if (ph == 0 && c < C) {
+    const int l = threadIdx.x;
+    part[(size_t)blockIdx.y * C + c] = ((red[0][0][l] + red[0][1][l]) + red[0][2][l]) + red[0][3][l];
+    if (mode == 2) part2[(size_t)blockIdx.y * C + c] = ((red[1][0][l] + red[1][1][l]) + red[1][2][l]) + red[1][3][l];
+  }
+}
+// out[c] = scale sum_z part[z][c]; mode 1 (variance) also gives rstd and the unbiased variance
+__global__ void chan_final_kernel(int C, int S, const float* __restrict__ part, float scale, float* out, float* rstd,
+                                  float* var_unbiased, float eps, float unbias) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int z = 0; z < S; ++z) s += part[(size_t)z * C + c];
+  s *= scale;
+  out[c] = s;
+  if (rstd) rstd[c] = 1.0f / sqrtf(s + eps);
+  if (var_unbiased) var_unbiased[c] = s * unbias;
+}
+// y = (x - mean) rstd g + b per channel
+__global__ void bn_apply_kernel(int64_t n, int C, const float* __restrict__ x, const float* __restrict__ mean,
+                                const float* __restrict__ rstd, const float* __restrict__ g, const float* __restrict__ b,
+                                float* y) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int c = (int)(e % C);
+  y[e] = (x[e] - mean[c]) * rstd[c] * g[c] + b[c];
+}
+// dx = g rstd (dy - dbeta / P - xhat dgamma / P)
+__global__ void bn_bwd_apply_kernel(int64_t n, int C, int P, const float* __restrict__ x, const float* __restrict__ dy,
+                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                    const float* __restrict__ g, const float* __restrict__ dbeta,
+                                    const float* __restrict__ dgamma, float* dx) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int c = (int)(e % C);
+  const float xh = (x[e] - mean[c]) * rstd[c];
+  dx[e] = g[c] * rstd[c] * (dy[e] - dbeta[c] / P - xh * dgamma[c] / P);
+}
+
+// per-image channel means: out[n][c] = scale sum_p X[n][p][c] (Y: X Y), one block per (image, 64 channels)
+__global__ void img_chan_sum_kernel(int HW, int C, const float* __restrict__ X, const float* __restrict__ Y, float scale,
+                                    float* out) {
+  __shared__ float red[4][64];
+  const int n = blockIdx.y, c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < C)
+    for (int p = ph; p < HW; p += 4) {
+      const size_t i = ((size_t)n * HW + p) * C + c;
+      s += Y ? X[i] * Y[i] : X[i];
+    }
+  red[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph == 0 && c < C) {
+    const int l = threadIdx.x;
+    out[(size_t)n * C + c] = (((red[0][l] + red[1][l]) + red[2][l]) + red[3][l]) * scale;
+  }
+}
+// out[n][p][c] = X[n][p][c] s[n][c] (+ add[n][c] when add is set)
+__global__ void chan_scale_kernel(int64_t total, int HW, int C, const float* __restrict__ X, const float* __restrict__ s,
+                                  const float* __restrict__ add, float* out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int c = (int)(e % C);
+  const int64_t n = e / ((int64_t)HW * C);
+  const float v = X ? X[e] * s[n * C + c] : 0.f;
+  out[e] = add ? v + add[n * C + c] : v;
+}
+
+// PixelShuffle(r) on NHWC (torch.nn.PixelShuffle channel order c r^2 + i r + j):
+// out[n][h r + i][w r + j][c] = in[n][h][w][c r^2 + i r + j]; dir 1 moves gradients back
+__global__ void shuffle_kernel(int N, int H, int W, int C, int r, const float* __restrict__ src, float* __restrict__ dst,
+                               int dir) {
+  const int64_t total = (int64_t)N * H * r * W * r * C;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int c = (int)(e % C);
+  const int64_t q = e / C;
+  const int wo = (int)(q % (W * r)), ho = (int)((q / (W * r)) % (H * r)), n = (int)(q / ((int64_t)W * r * H * r));
+  const int h = ho / r, i = ho - h * r, w = wo / r, j = wo - w * r;
+  const int64_t in_i = (((int64_t)n * H + h) * W + w) * (C * r * r) + c * r * r + i * r + j;
+  if (dir == 0) dst[e] = src[in_i];
+  else dst[in_i] = src[e];
+}
+
+// head flatten (ResNetSE34V2.py:161-165): rows (n, w), features c H + h from NHWC x[n][h][w][c];
+// dir 1 moves gradients back
+__global__ void head_flat_kernel(int N, int H, int W, int C, const float* __restrict__ src, float* __restrict__ dst,
+                                 int dir) {
+  const int64_t total = (int64_t)N * H * W * C;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int c = (int)(e % C);
+  const int64_t q = e / C;
+  const int w = (int)(q % W), h = (int)((q / W) % H), n = (int)(q / ((int64_t)W * H));
+  const int64_t row_i = ((int64_t)n * W + w) * (C * H) + c * H + h;
+  if (dir == 0) dst[row_i] = src[e];
+  else dst[e] = src[row_i];
 }
 
 inline unsigned blocks_for(int64_t n, int per = TT) { return (unsigned)((n + per - 1) / per); }
@@ -636,8 +812,9 @@ int ggd_tr_attention_bwd(int n, int H, int Lq, int Lk, int dk, float scale, cons
 }
 
 int ggd_tr_elementwise(int op, int64_t n, const float* a, const float* b, float* out, void* stream) {
-  if (n < 0 || !a || !out || op < 0 || op > GGD_EW_ADD) return -1;
-  if ((op == GGD_EW_RELU2_BWD || op == GGD_EW_SILU_BWD || op == GGD_EW_ADD) && !b) return -1;
+  if (n < 0 || !a || !out || op < 0 || op > GGD_EW_SIGMOID_BWD) return -1;
+  if ((op == GGD_EW_RELU2_BWD || op == GGD_EW_SILU_BWD || op == GGD_EW_ADD || op == GGD_EW_RELU_BWD ||
+       op == GGD_EW_SIGMOID_BWD) && !b) return -1;
   if (n == 0) return 0;
   hipLaunchKernelGGL(ew_kernel, dim3(blocks_for(n)), dim3(TT), 0, (hipStream_t)stream, op, n, a, b, out);
   return rc(hipGetLastError());
@@ -687,5 +864,97 @@ int ggd_tr_scale(int64_t n, float* x, float s, void* stream) {
 }
 
 int ggd_tr_sumsq_blocks(void) { return SUMSQ_BLOCKS; }
+
+int ggd_tr_im2col(int N, int H, int W, int C, int KH, int KW, int stride, int pad, const float* x, float* col,
+                  void* stream) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || KH <= 0 || KW <= 0 || stride <= 0 || pad < 0 || !x || !col) return -1;
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  if (Ho <= 0 || Wo <= 0) return -2;
+  const int64_t total = (int64_t)N * Ho * Wo * KH * KW * C;
+  hipLaunchKernelGGL(im2col_kernel, dim3(blocks_for(total)), dim3(TT), 0, (hipStream_t)stream, x, N, H, W, C, KH, KW,
+                     stride, pad, Ho, Wo, col);
+  return rc(hipGetLastError());
+}
+
+int ggd_tr_col2im(int N, int H, int W, int C, int KH, int KW, int stride, int pad, const float* dcol, float* dx,
+                  void* stream) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || KH <= 0 || KW <= 0 || stride <= 0 || pad < 0 || !dcol || !dx) return -1;
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  if (Ho <= 0 || Wo <= 0) return -2;
+  const int64_t total = (int64_t)N * H * W * C;
+  hipLaunchKernelGGL(col2im_kernel, dim3(blocks_for(total)), dim3(TT), 0, (hipStream_t)stream, dcol, N, H, W, C, KH, KW,
+                     stride, pad, Ho, Wo, dx);
+  return rc(hipGetLastError());
+}
+
+int ggd_tr_batchnorm_fwd(int P, int C, const float* x, const float* g, const float* b, float eps, float* y, float* mean,
+                         float* rstd, float* var_unbiased, void* stream) {
+  if (P <= 1 || C <= 0 || !x || !g || !b || !y || !mean || !rstd) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  const int S = (P + RS - 1) / RS;
+  float* ws = workspace(sizeof(float) * ((size_t)S * C + C));
+  if (!ws) return -3;
+  float* var = ws + (size_t)S * C;
+  const dim3 gp((C + 63) / 64, S);
+  hipLaunchKernelGGL(chan_partial_kernel, gp, dim3(256), 0, s, P, C, 0, x, nullptr, nullptr, nullptr, ws, nullptr);
+  hipLaunchKernelGGL(chan_final_kernel, dim3(blocks_for(C)), dim3(TT), 0, s, C, S, ws, 1.0f / P, mean, nullptr, nullptr,
+                     0.f, 0.f);
+  hipLaunchKernelGGL(chan_partial_kernel, gp, dim3(256), 0, s, P, C, 1, x, nullptr, mean, nullptr, ws, nullptr);
+  hipLaunchKernelGGL(chan_final_kernel, dim3(blocks_for(C)), dim3(TT), 0, s, C, S, ws, 1.0f / P, var, rstd, var_unbiased,
+                     eps, (float)P / (float)(P - 1));
+  const int64_t n = (int64_t)P * C;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(blocks_for(n)), dim3(TT), 0, s, n, C, x, mean, rstd, g, b, y);
+  return rc(hipGetLastError());
+}
+
+int ggd_tr_batchnorm_bwd(int P, int C, const float* x, const float* g, const float* mean, const float* rstd,
+                         const float* dy, float* dx, float* dg, float* db, void* stream) {
+  if (P <= 1 || C <= 0 || !x || !g || !mean || !rstd || !dy || !dx || !dg || !db) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  const int S = (P + RS - 1) / RS;
+  float* ws = workspace(sizeof(float) * (size_t)S * C * 2);
+  if (!ws) return -3;
+  hipLaunchKernelGGL(chan_partial_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, P, C, 2, x, dy, mean, rstd, ws,
+                     ws + (size_t)S * C);
+  hipLaunchKernelGGL(chan_final_kernel, dim3(blocks_for(C)), dim3(TT), 0, s, C, S, ws, 1.0f, db, nullptr, nullptr, 0.f, 0.f);
+  hipLaunchKernelGGL(chan_final_kernel, dim3(blocks_for(C)), dim3(TT), 0, s, C, S, ws + (size_t)S * C, 1.0f, dg, nullptr,
+                     nullptr, 0.f, 0.f);
+  const int64_t n = (int64_t)P * C;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks_for(n)), dim3(TT), 0, s, n, C, P, x, dy, mean, rstd, g, db, dg, dx);
+  return rc(hipGetLastError());
+}
+
+int ggd_tr_image_channel_sum(int N, int HW, int C, const float* x, const float* y, float scale, float* out,
+                             void* stream) {
+  if (N <= 0 || HW <= 0 || C <= 0 || !x || !out) return -1;
+  hipLaunchKernelGGL(img_chan_sum_kernel, dim3((C + 63) / 64, N), dim3(256), 0, (hipStream_t)stream, HW, C, x, y, scale,
+                     out);
+  return rc(hipGetLastError());
+}
+
+int ggd_tr_channel_scale(int N, int HW, int C, const float* x, const float* s, const float* add, float* out,
+                         void* stream) {
+  if (N <= 0 || HW <= 0 || C <= 0 || (!x && !add) || (x && !s) || !out) return -1;
+  const int64_t total = (int64_t)N * HW * C;
+  hipLaunchKernelGGL(chan_scale_kernel, dim3(blocks_for(total)), dim3(TT), 0, (hipStream_t)stream, total, HW, C, x, s,
+                     add, out);
+  return rc(hipGetLastError());
+}
+
+int ggd_tr_pixel_shuffle(int N, int H, int W, int C, int r, const float* src, float* dst, int backward, void* stream) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || r <= 0 || !src || !dst) return -1;
+  const int64_t total = (int64_t)N * H * r * W * r * C;
+  hipLaunchKernelGGL(shuffle_kernel, dim3(blocks_for(total)), dim3(TT), 0, (hipStream_t)stream, N, H, W, C, r, src, dst,
+                     backward ? 1 : 0);
+  return rc(hipGetLastError());
+}
+
+int ggd_tr_head_flatten(int N, int H, int W, int C, const float* src, float* dst, int backward, void* stream) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || !src || !dst) return -1;
+  const int64_t total = (int64_t)N * H * W * C;
+  hipLaunchKernelGGL(head_flat_kernel, dim3(blocks_for(total)), dim3(TT), 0, (hipStream_t)stream, N, H, W, C, src, dst,
+                     backward ? 1 : 0);
+  return rc(hipGetLastError());
+}
 
 }  // extern "C"

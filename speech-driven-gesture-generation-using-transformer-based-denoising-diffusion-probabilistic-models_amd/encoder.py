@@ -85,6 +85,23 @@ class SpeechEncoder:
                      "encode", "ggd_enc_last_error")
         return tuple(z)
 
+    @th.no_grad()
+    def frontend(self, wav):
+        """wav (N, T) f32 -> the InstanceNorm'd mel image (N, 128, F) (ggd_enc_frontend): the input of
+        the SE-ResNet, parameter-free, for the training path."""
+        wav = wav.to(self.device, th.float32).contiguous()
+        n, tw = wav.shape
+        h = self._context(tw)
+        F_ = 1 + tw // 512
+        img = th.empty(n, 128, F_, device=self.device)
+        stream = ctypes.c_void_p(th.cuda.current_stream(self.device).cuda_stream)
+        for c0 in range(0, n, self.max_batch):
+            m = min(self.max_batch, n - c0)
+            native.check(h, self.lib.ggd_enc_frontend(h, ctypes.c_void_p(wav[c0:].data_ptr()), m,
+                                                      ctypes.c_void_p(img[c0:].data_ptr()), stream),
+                         "frontend", "ggd_enc_last_error")
+        return img
+
     def close(self):
         for h in self._ctx.values():
             self.lib.ggd_enc_destroy(h)

@@ -18,13 +18,13 @@ def create_diffusion(diffusion_params, is_training):
 
 
 def create_model(d_pose, model_params, lr=1e-2, weight_decay=None, scheduler_params=None, is_training=False,
-                 dtype="bf16", device="cuda"):
+                 dtype="bf16", device="cuda", train_encoder=True):
     """model_creation.py:51-191 -> (model, diffusion, optimizer, schedule_sampler, lr_scheduler).
 
     Inference (is_training False): the HIP sampler model; optimizer, schedule_sampler and
-    lr_scheduler are None.  Training: a training.TrainableModel (reference init, seed 0) with
-    AdamW, the uniform schedule sampler and the configured lr schedule (SURVEY.md 8f rank 3;
-    s2g_v2 + one-way decoder, speech encoder frozen).  Legacy {"type","args"} model params
+    lr_scheduler are None.  Training: a training.TrainableModel (reference init, seed 0; the HA2G
+    encoder trained in train mode unless train_encoder=False) with AdamW, the uniform schedule
+    sampler and the configured lr schedule (s2g_v2 + one-way decoder).  Legacy {"type","args"} model params
     (tedexp) are adapted to the flat schema first.
     """
     if is_training:
@@ -35,7 +35,7 @@ def create_model(d_pose, model_params, lr=1e-2, weight_decay=None, scheduler_par
         if is_legacy_schema(model_params):
             model_params = adapt_legacy({"Model": model_params.to_dict()}).Model
         arch = arch_from_config(model_params, d_pose)
-        model = training.TrainableModel(arch, init_state_dict(arch, seed=0), device=device)
+        model = training.TrainableModel(arch, init_state_dict(arch, seed=0), device=device, train_encoder=train_encoder)
         diffusion = create_diffusion(model_params["Diffusion"], True)
         optimizer = training.AdamW(model, lr=lr, weight_decay=weight_decay)
         sp = scheduler_params.to_dict() if isinstance(scheduler_params, JsonConfig) else scheduler_params

@@ -31,6 +31,7 @@ from . import native
 from .weights import parameter_shapes
 
 EW_RELU2, EW_RELU2_BWD, EW_SILU, EW_SILU_BWD, EW_ADD = 0, 1, 2, 3, 4   # include/ggd_train.h
+EW_RELU, EW_RELU_BWD, EW_SIGMOID, EW_SIGMOID_BWD = 5, 6, 7, 8
 
 
 def _lib():
@@ -222,6 +223,182 @@ def add(a, b):
     return _Add.apply(a, b)
 
 
+def relu(x):
+    return _Act.apply(x, EW_RELU, EW_RELU_BWD)
+
+
+class _Sigmoid(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = _ew(EW_SIGMOID, x.contiguous())
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return _ew(EW_SIGMOID_BWD, y, dy.contiguous())
+
+
+# ------------------------------------------------------------------------------------------
+# speech-encoder ops on NHWC activations (N, H, W, C): H = mel axis, W = frames
+# ------------------------------------------------------------------------------------------
+class _Conv2d(th.autograd.Function):
+    """nn.Conv2d = im2col + GEMM against the [Cout][(ky, kx, c)] filter matrix; backward: dW = dY^T col,
+    db = colsum dY, dcol = dY W, dX = col2im(dcol).  col is recomputed in backward (memory)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        Co, Ci, KH, KW = w.shape
+        assert Ci == C
+        Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+        K, P = KH * KW * C, N * Ho * Wo
+        wp = w.permute(0, 2, 3, 1).contiguous().reshape(Co, K)
+        col = x.new_empty(P, K)
+        lib = _lib()
+        _ok(lib.ggd_tr_im2col(N, H, W, C, KH, KW, stride, pad, _p(x), _p(col), _s(x)), "im2col")
+        y = x.new_empty(P, Co)
+        gemm(0, 1, P, Co, K, col, K, wp, K, y, Co, bias=b)
+        ctx.save_for_backward(x, wp)
+        ctx.geo = (N, H, W, C, Co, KH, KW, stride, pad, Ho, Wo, b is not None)
+        return y.view(N, Ho, Wo, Co)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wp = ctx.saved_tensors
+        N, H, W, C, Co, KH, KW, stride, pad, Ho, Wo, has_b = ctx.geo
+        K, P = KH * KW * C, N * Ho * Wo
+        dy = dy.contiguous().view(P, Co)
+        lib = _lib()
+        col = x.new_empty(P, K)
+        _ok(lib.ggd_tr_im2col(N, H, W, C, KH, KW, stride, pad, _p(x), _p(col), _s(x)), "im2col")
+        dwp = wp.new_empty(Co, K)
+        gemm(1, 0, Co, K, P, dy, Co, col, K, dwp, K)
+        dw = dwp.view(Co, KH, KW, C).permute(0, 3, 1, 2).contiguous()
+        db = None
+        if has_b:
+            db = wp.new_empty(Co)
+            _ok(lib.ggd_tr_colsum(P, Co, _p(dy), Co, _p(db), 0.0, _s(dy)), "colsum")
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dcol = col  # reuse the buffer
+            gemm(0, 0, P, K, Co, dy, Co, wp, K, dcol, K)
+            dx = th.empty_like(x)
+            _ok(lib.ggd_tr_col2im(N, H, W, C, KH, KW, stride, pad, _p(dcol), _p(dx), _s(x)), "col2im")
+        return dx, dw, db, None, None
+
+
+class _BatchNorm2d(th.autograd.Function):
+    """nn.BatchNorm2d in train mode (batch statistics over N H W, eps 1e-5); `stats` receives the
+    batch mean and unbiased variance for the running-stat update."""
+
+    @staticmethod
+    def forward(ctx, x, g, b, stats):
+        N, H, W, C = x.shape
+        P = N * H * W
+        y = th.empty_like(x)
+        mean, rstd, var_u = x.new_empty(C), x.new_empty(C), x.new_empty(C)
+        _ok(_lib().ggd_tr_batchnorm_fwd(P, C, _p(x), _p(g), _p(b), 1e-5, _p(y), _p(mean), _p(rstd), _p(var_u), _s(x)),
+            "bn fwd")
+        stats.append((mean, var_u))
+        ctx.save_for_backward(x, g, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, g, mean, rstd = ctx.saved_tensors
+        N, H, W, C = x.shape
+        dx, dg, db = th.empty_like(x), th.empty_like(g), th.empty_like(g)
+        _ok(_lib().ggd_tr_batchnorm_bwd(N * H * W, C, _p(x), _p(g), _p(mean), _p(rstd), _p(dy.contiguous()), _p(dx),
+                                        _p(dg), _p(db), _s(x)), "bn bwd")
+        return dx, dg, db, None
+
+
+class _ChanMean(th.autograd.Function):
+    """AdaptiveAvgPool2d(1): (N, H, W, C) -> (N, C)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, H, W, C = x.shape
+        out = x.new_empty(N, C)
+        _ok(_lib().ggd_tr_image_channel_sum(N, H * W, C, _p(x), None, 1.0 / (H * W), _p(out), _s(x)), "pool")
+        ctx.shape = x.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C = ctx.shape
+        lib = _lib()
+        d = dy.contiguous().clone()
+        _ok(lib.ggd_tr_scale(d.numel(), _p(d), 1.0 / (H * W), _s(d)), "scale")
+        dx = d.new_empty(N, H, W, C)
+        _ok(lib.ggd_tr_channel_scale(N, H * W, C, None, None, _p(d), _p(dx), _s(d)), "broadcast")
+        return dx
+
+
+class _ChanScale(th.autograd.Function):
+    """SELayer's x * y[:, :, None, None] on NHWC: (N, H, W, C) x (N, C)."""
+
+    @staticmethod
+    def forward(ctx, x, sc):
+        N, H, W, C = x.shape
+        out = th.empty_like(x)
+        _ok(_lib().ggd_tr_channel_scale(N, H * W, C, _p(x), _p(sc), None, _p(out), _s(x)), "chan scale")
+        ctx.save_for_backward(x, sc)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, sc = ctx.saved_tensors
+        N, H, W, C = x.shape
+        dy = dy.contiguous()
+        lib = _lib()
+        dx = th.empty_like(x)
+        _ok(lib.ggd_tr_channel_scale(N, H * W, C, _p(dy), _p(sc), None, _p(dx), _s(x)), "chan scale bwd")
+        ds = sc.new_empty(N, C)
+        _ok(lib.ggd_tr_image_channel_sum(N, H * W, C, _p(dy), _p(x), 1.0, _p(ds), _s(x)), "chan scale ds")
+        return dx, ds
+
+
+class _PixelShuffle(th.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r):
+        N, H, W, Cr = x.shape
+        C = Cr // (r * r)
+        y = x.new_empty(N, H * r, W * r, C)
+        _ok(_lib().ggd_tr_pixel_shuffle(N, H, W, C, r, _p(x), _p(y), 0, _s(x)), "shuffle")
+        ctx.geo = (N, H, W, C, r)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C, r = ctx.geo
+        dx = dy.new_empty(N, H, W, C * r * r)
+        _ok(_lib().ggd_tr_pixel_shuffle(N, H, W, C, r, _p(dy.contiguous()), _p(dx), 1, _s(dy)), "shuffle bwd")
+        return dx, None
+
+
+class _HeadFlatten(th.autograd.Function):
+    """NHWC (N, H, W, C) -> (N, W, C H): the reference's feat.reshape(N, -1, W).transpose(1, 2)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, H, W, C = x.shape
+        y = x.new_empty(N, W, C * H)
+        _ok(_lib().ggd_tr_head_flatten(N, H, W, C, _p(x), _p(y), 0, _s(x)), "flatten")
+        ctx.geo = (N, H, W, C)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C = ctx.geo
+        dx = dy.new_empty(N, H, W, C)
+        _ok(_lib().ggd_tr_head_flatten(N, H, W, C, _p(dy.contiguous()), _p(dx), 1, _s(dy)), "flatten bwd")
+        return dx
+
+
 # ------------------------------------------------------------------------------------------
 # the trainable model
 # ------------------------------------------------------------------------------------------
@@ -243,26 +420,38 @@ def step_embedding(t, dim, max_period=10000):
     return th.cat([th.cos(arg), th.sin(arg)], dim=-1)
 
 
-def _trainable(arch):
-    """Parameter names the training path updates (reference state_dict order): everything of the
-    s2g_v2 model except the speech encoder (frozen) and non-float buffers."""
+_ENC_BUFFERS = (".running_mean", ".running_var", ".num_batches_tracked", "wav2spec.0.flipped_filter",
+                "wav2spec.1.spectrogram.window", "wav2spec.1.mel_scale.fb")
+
+
+def _trainable(arch, train_encoder=False):
+    """Parameter names the training path updates (reference state_dict order): the decoder, step
+    encoder and blend layer, plus the speech encoder's parameters when it is trained (its BN running
+    statistics and front-end constants are buffers, never parameters)."""
     shapes = parameter_shapes(arch)
-    return [(k, shape) for k, (shape, init) in shapes.items()
-            if not k.startswith("speech_encoder.") and init != "int0"]
+    out = []
+    for k, (shape, init) in shapes.items():
+        if init == "int0" or k.endswith(_ENC_BUFFERS):
+            continue
+        if k.startswith("speech_encoder.") and not train_encoder:
+            continue
+        out.append((k, shape))
+    return out
 
 
 class TrainableModel:
     """The s2g_v2 + one-way-decoder denoiser (models/model.py:76-117, nn.py:177-228) with its
     trainable parameters in one flat f32 device buffer under the reference's state_dict names."""
 
-    def __init__(self, arch, sd, device="cuda"):
+    def __init__(self, arch, sd, device="cuda", train_encoder=False):
         if arch["type"] != "s2g_v2" or arch["decoder"] != "oneway_cross_attention":
             raise ValueError("the training path covers s2g_v2 with the one-way decoder (beat-ours)")
         self.arch = arch
         self.device = th.device(device)
         if self.device.type != "cuda":
             raise ValueError("the training path runs on a GPU device only (no CPU fallback)")
-        names = _trainable(arch)
+        self.train_encoder = bool(train_encoder)
+        names = _trainable(arch, self.train_encoder)
         total = sum(int(np.prod(s)) for _, s in names)
         self.flat = th.zeros(total, device=self.device)
         self.flat_grad = th.zeros(total, device=self.device)
@@ -278,6 +467,9 @@ class TrainableModel:
         self._pe = {}
         self._enc_sd = {k: v for k, v in sd.items() if k.startswith("speech_encoder.")}
         self._encoder = None
+        # BatchNorm running statistics of the trained encoder (buffers, updated in train mode)
+        self.buffers = {k: v.detach().to(self.device).clone() for k, v in sd.items()
+                        if k.startswith("speech_encoder.") and k.endswith(_ENC_BUFFERS[:3])} if self.train_encoder else {}
 
     def speech_encoder(self):
         """The frozen HA2G encoder (HIP, f32, eval mode) on this model's encoder weights."""
@@ -295,10 +487,15 @@ class TrainableModel:
             for k, p in self.params.items():
                 if k in sd:
                     p.copy_(sd[k].to(p.device, th.float32).reshape(p.shape))
+            for k, b in getattr(self, "buffers", {}).items():
+                if k in sd:
+                    b.copy_(sd[k].to(b.device, b.dtype).reshape(b.shape))
         return missing
 
     def state_dict(self):
-        return {k: p.detach().clone() for k, p in self.params.items()}
+        sd = {k: p.detach().clone() for k, p in self.params.items()}
+        sd.update({k: v.clone() for k, v in self.buffers.items()})
+        return sd
 
     def named_parameters(self):
         return iter(self.params.items())
@@ -329,9 +526,63 @@ class TrainableModel:
         o = _Attention.apply(q, k, v, H, 1.0 / math.sqrt(d // H))
         return linear(o, P[f"{pre}.output.weight"], P[f"{pre}.output.bias"])
 
-    def __call__(self, x_t, t, z):
-        """x_t (N, C, L), t (N,) int64 original timesteps, z = (z_low, z_mid, z_high) speech tokens
-        (N, T_i, d) from the frozen encoder -> eps (N, C, L)."""
+    # -- the HA2G encoder in train mode (ResNetSE34V2.py:118-188), NHWC ---------------------------
+    def _bn(self, name, x):
+        stats = []
+        y = _BatchNorm2d.apply(x, self.params[name + ".weight"], self.params[name + ".bias"], stats)
+        mean, var_u = stats[0]
+        with th.no_grad():   # nn.BatchNorm2d momentum 0.1 running-stat update
+            self.buffers[name + ".running_mean"].mul_(0.9).add_(0.1 * mean)
+            self.buffers[name + ".running_var"].mul_(0.9).add_(0.1 * var_u)
+            self.buffers[name + ".num_batches_tracked"].add_(1)
+        return y
+
+    def _conv(self, name, x, stride=1, pad=0):
+        return _Conv2d.apply(x, self.params[name + ".weight"], self.params.get(name + ".bias"), stride, pad)
+
+    def _se_block(self, name, x, stride):
+        """SEBasicBlock (ResNetBlocks.py:21-37): conv, ReLU, BN, conv, BN, SE, + residual, ReLU."""
+        P = self.params
+        out = self._bn(name + ".bn1", relu(self._conv(name + ".conv1", x, stride, 1)))
+        out = self._bn(name + ".bn2", self._conv(name + ".conv2", out, 1, 1))
+        y = relu(linear(_ChanMean.apply(out), P[name + ".se.fc.0.weight"], P[name + ".se.fc.0.bias"]))
+        y = _Sigmoid.apply(linear(y, P[name + ".se.fc.2.weight"], P[name + ".se.fc.2.bias"]))
+        out = _ChanScale.apply(out, y)
+        if (name + ".downsample.0.weight") in P:
+            res = self._bn(name + ".downsample.1", self._conv(name + ".downsample.0", x, stride, 0))
+        else:
+            res = x
+        return relu(add(out, res))
+
+    def encode(self, wav):
+        """HA2GSpeechEncoder.forward (speech_encoder.py:37-61) with the SE-ResNet in train mode:
+        (z_low, z_mid, z_high) with the autograd graph to the encoder's parameters."""
+        P = self.params
+        img = self.speech_encoder().frontend(wav)                     # (N, 128, F), parameter-free
+        r = "speech_encoder.wav_encoder.feat_extractor."
+        x = img[..., None]                                           # NHWC, C = 1
+        x = self._bn(r + "bn1", relu(self._conv(r + "conv1", x, 1, 1)))
+        feats = []
+        for li, (nblk, stride) in enumerate(zip((3, 4, 6, 3), (1, 2, 2, 2))):
+            for bi in range(nblk):
+                x = self._se_block(r + f"layer{li + 1}.{bi}", x, stride if bi == 0 else 1)
+            feats.append(x)
+        proj_w, proj_b = P["speech_encoder.wav_proj_layer.weight"], P["speech_encoder.wav_proj_layer.bias"]
+        out = []
+        for feat, hn, shuf in ((feats[1], "low", 1), (feats[2], "mid", 2), (feats[3], "high", 4)):
+            if shuf > 1:
+                feat = _PixelShuffle.apply(feat.contiguous(), shuf)
+            h = self._bn(r + "bn_" + hn, relu(self._conv(r + "conv_" + hn, feat, 1, 0)))
+            h = linear(_HeadFlatten.apply(h.contiguous()), P[r + f"fc_{hn}.weight"], P[r + f"fc_{hn}.bias"])
+            out.append(linear(h, proj_w, proj_b))
+        return tuple(out)
+
+    def __call__(self, x_t, t, z=None, wav=None):
+        """x_t (N, C, L), t (N,) int64 original timesteps -> eps (N, C, L).  Speech: z = (z_low, z_mid,
+        z_high) tokens (N, T_i, d) from the frozen encoder, or wav (N, T_wav) encoded here (through the
+        trained encoder when train_encoder, else the frozen HIP encoder)."""
+        if z is None:
+            z = self.encode(wav) if self.train_encoder else self.speech_encoder()(wav)
         P, a = self.params, self.arch
         d = a["d_model"]
         N, C, L = x_t.shape
@@ -408,7 +659,7 @@ def training_losses(diffusion, model, x_start, t, model_kwargs, noise=None):
         noise = th.randn_like(x_start)
     noise = noise.contiguous().float()
     x_t = q_sample(diffusion, x_start, t, noise)
-    eps = model(x_t, t, model_kwargs["speech_tokens"])
+    eps = model(x_t, t, z=model_kwargs.get("speech_tokens"), wav=model_kwargs.get("wav"))
     assert eps.shape == noise.shape == x_start.shape
     mse = _DiffusionMSE.apply(eps, noise)
     with th.no_grad():
@@ -576,14 +827,17 @@ class Trainer:
     def _compute_loss(self, batch, noise=None, t=None):
         poses = batch["pose"].to(self.model.device)          # (N, T, C)
         z = batch.get("speech_tokens")
-        if z is None:
-            z = self.encoder(batch["wav"])                   # frozen HA2G encoder (eval mode)
+        kw = {"speech_tokens": z}
+        if z is None and self.model.train_encoder:
+            kw = {"wav": batch["wav"]}                       # encoded with grad (train-mode SE-ResNet)
+        elif z is None:
+            kw = {"speech_tokens": self.encoder(batch["wav"])}   # frozen HA2G encoder (eval mode)
         x_start = poses.transpose(1, 2)
         if noise is None:
             noise = th.randn_like(x_start)
         if t is None:
             t, _ = self.schedule_sampler.sample(poses.shape[0], self.model.device, self.rng)
-        out = training_losses(self.diffusion, self.model, x_start, t, {"speech_tokens": z}, noise=noise)
+        out = training_losses(self.diffusion, self.model, x_start, t, kw, noise=noise)
         loss = out["mse"].mean()
         return {"loss": loss, "denoise": loss}
 

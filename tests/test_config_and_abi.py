@@ -98,7 +98,7 @@ def _header_symbols(diag=False):
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     if not diag:
         txt = re.sub(r"#ifdef GGD_DIAG.*?#endif", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(ggd_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(ggd_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_library_loads_and_exports_every_header_symbol(pkg):

@@ -265,3 +265,117 @@ def test_checkpoint_roundtrip_resumes_identically(pkg, beat_cfg, tr, train_setup
     ra = a.step(batches[1][0], noise=batches[1][1], t=batches[1][2])
     rb = b.step(batches[1][0], noise=batches[1][1], t=batches[1][2])
     assert ra == rb and th.equal(a.model.flat, b.model.flat)
+
+
+# ------------------------------------------------------------------------------------------
+# speech-encoder training (train-mode SE-ResNet34 on NHWC activations)
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("cin,cout,k,stride,pad,bias", [(1, 32, 3, 1, 1, True), (32, 64, 3, 2, 1, False),
+                                                         (32, 64, 1, 2, 0, False), (64, 64, 2, 1, 0, True)])
+def test_conv2d_nhwc_matches_torch(tr, cin, cout, k, stride, pad, bias):
+    g = th.Generator().manual_seed(cin + cout + k)
+    x = th.randn(3, 17, 13, cin, generator=g)                         # NHWC
+    w = th.randn(cout, cin, k, k, generator=g) * 0.2
+    b = th.randn(cout, generator=g) if bias else None
+    dy_shape = (3, (17 + 2 * pad - k) // stride + 1, (13 + 2 * pad - k) // stride + 1, cout)
+    dy = th.randn(*dy_shape, generator=g)
+
+    def ref(xx, ww, bb):
+        return F.conv2d(xx.permute(0, 3, 1, 2), ww, bb, stride=stride, padding=pad).permute(0, 2, 3, 1)
+
+    def run(fn, dev):
+        ts = [t.to(dev).clone().requires_grad_(True) if t is not None else None for t in (x, w, b)]
+        y = fn(*ts)
+        y.backward(dy.to(dev))
+        return [y] + [t.grad for t in ts if t is not None]
+
+    got = run(lambda a, c, d: tr._Conv2d.apply(a, c, d, stride, pad), "cuda")
+    want = run(ref, "cpu")
+    for a, c in zip(got, want):
+        close(a, c, 2e-5)
+
+
+def test_batchnorm_se_shuffle_flatten_match_torch(tr):
+    g = th.Generator().manual_seed(12)
+    x = th.randn(3, 8, 6, 32, generator=g) * 2 + 1
+    gam, bet = th.randn(32, generator=g), th.randn(32, generator=g)
+    sc = th.rand(3, 32, generator=g)
+    dy = th.randn(3, 16, 12, 8, generator=g)
+
+    def ref(xx, gg, bb, ss):
+        y = F.batch_norm(xx.permute(0, 3, 1, 2), None, None, gg, bb, True, 0.0, 1e-5)
+        pooled = y.mean(dim=(2, 3))
+        y = y * th.sigmoid(ss + pooled)[:, :, None, None]
+        y = F.pixel_shuffle(F.relu(y), 2)                                  # (3, 8, 16, 12)
+        return y.permute(0, 2, 3, 1)
+
+    def hip(xx, gg, bb, ss):
+        y = tr._BatchNorm2d.apply(xx, gg, bb, [])
+        pooled = tr._ChanMean.apply(y)
+        y = tr._ChanScale.apply(y, tr._Sigmoid.apply(tr.add(ss, pooled)))
+        return tr._PixelShuffle.apply(tr.relu(y).contiguous(), 2)
+
+    def run(fn, dev):
+        ts = [t.to(dev).clone().requires_grad_(True) for t in (x, gam, bet, sc)]
+        y = fn(*ts)
+        y.backward(dy.to(dev))
+        return [y] + [t.grad for t in ts]
+
+    for a, c in zip(run(hip, "cuda"), run(ref, "cpu")):
+        close(a, c, 1e-4)
+    h = th.randn(2, 5, 7, 3, generator=g)
+    flat = tr._HeadFlatten.apply(h.cuda()).cpu()
+    assert th.equal(flat, h.permute(0, 3, 1, 2).reshape(2, 15, 7).transpose(1, 2))   # ResNetSE34V2.py:161-163
+
+
+@pytest.fixture(scope="module")
+def enc_setup(pkg, beat_cfg, tr):
+    arch = pkg.arch_from_config(beat_cfg.Model, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    diffusion = pkg.create_diffusion(beat_cfg.Model.Diffusion.to_dict(), True)
+    wav = th.randn(3, WAV, generator=th.Generator().manual_seed(17)) * 0.1
+    return arch, sd, diffusion, wav
+
+
+def test_encoder_training_gradients_match_oracle(tr, enc_setup):
+    """Full training step with the HA2G encoder trained (BatchNorm on batch statistics): loss, speech
+    tokens and every parameter gradient (encoder included) vs torch autograd through the oracle with
+    train-mode BN; the running statistics follow nn.BatchNorm2d's momentum-0.1 update."""
+    arch, sd, diffusion, wav = enc_setup
+    model = tr.TrainableModel(arch, sd, "cuda", train_encoder=True)
+    n = wav.shape[0]
+    g = th.Generator().manual_seed(18)
+    x0 = th.randn(n, D_POSE, L, generator=g)
+    t = th.tensor([911, 250, 7])
+    noise = th.randn(n, D_POSE, L, generator=g)
+    model.zero_grad()
+    out = tr.training_losses(diffusion, model, x0.cuda(), t.cuda(), {"wav": wav.cuda()}, noise=noise.cuda())
+    loss = out["mse"].mean()
+    loss.backward()
+    names = list(model.params)
+    assert any(k.startswith("speech_encoder.") for k in names)
+    sd_ref = {k: v.detach().float().clone() for k, v in sd.items()}
+    for k in names:
+        sd_ref[k].requires_grad_(True)
+    z_ref = ref_denoiser.speech_encoder(sd_ref, wav, train=True)
+    want = _oracle_loss(arch, sd_ref, diffusion, x0, t, noise, z_ref)
+    want.backward()
+    assert abs(loss.item() - want.item()) <= 1e-4 * want.item(), (loss.item(), want.item())
+    floor = 1e-4 * max(sd_ref[k].grad.abs().max().item() for k in names)
+    worst = []
+    for k in names:
+        gg, gr = model.params[k].grad.cpu(), sd_ref[k].grad
+        s = max(gr.abs().max().item(), floor)
+        worst.append(((gg - gr).abs().max().item() / s, k))
+    worst.sort(reverse=True)
+    print("\nworst gradient errors with the encoder trained:", worst[:6])
+    assert worst[0][0] <= 5e-3, worst[:6]
+    # running statistics of the first BN: 0.9 init + 0.1 batch stats of relu(conv1(img))
+    img = model.speech_encoder().frontend(wav.cuda()).cpu()
+    r = "speech_encoder.wav_encoder.feat_extractor."
+    a = F.relu(F.conv2d(img[:, None], sd[r + "conv1.weight"].float(), sd[r + "conv1.bias"].float(), padding=1))
+    rm = 0.9 * sd[r + "bn1.running_mean"] + 0.1 * a.mean(dim=(0, 2, 3))
+    rv = 0.9 * sd[r + "bn1.running_var"] + 0.1 * a.var(dim=(0, 2, 3), unbiased=True)
+    close(model.buffers[r + "bn1.running_mean"], rm, 1e-4)
+    close(model.buffers[r + "bn1.running_var"], rv, 1e-4)
+    assert int(model.buffers[r + "bn1.num_batches_tracked"]) == int(sd[r + "bn1.num_batches_tracked"]) + 1
