@@ -261,9 +261,16 @@ def speech_encoder(sd, wav, train=False):
     x = mel_power_spectrogram(x, sd[p + "wav2spec.1.spectrogram.window"], sd[p + "wav2spec.1.mel_scale.fb"])
     x = x + 1e-6
     x = F.instance_norm(x, eps=1e-5)  # InstanceNorm1d(128), no affine, per-instance stats
-    # Hierarchical_WavEncoder / ResNetSE.forward: hierarchy_net.py:16-19, ResNetSE34V2.py:118-188
+    return speech_encoder_from_image(sd, x, train)
+
+
+def speech_encoder_from_image(sd, img, train=False):
+    """The SE-ResNet + heads + projection of speech_encoder() from the InstanceNorm'd mel image
+    (N, 128, F) (Hierarchical_WavEncoder / ResNetSE.forward: hierarchy_net.py:16-19,
+    ResNetSE34V2.py:118-188, speech_encoder.py:59-61)."""
+    p = "speech_encoder."
     r = p + "wav_encoder.feat_extractor."
-    x = x[:, None]
+    x = img[:, None]
     x = _bn(sd, r + "bn1", F.relu(_conv(sd, r + "conv1", x, padding=1)), train)
     feats = []
     for li, (nblk, stride) in enumerate(zip((3, 4, 6, 3), (1, 2, 2, 2))):

@@ -548,10 +548,10 @@ __global__ void col2im_kernel(const float* __restrict__ dcol, int N, int H, int 
 //   mode 0: sum x;  mode 1: sum (x - mean[c])^2;  mode 2: sum dy and sum dy (x - mean[c]) rstd[c]
 __global__ void chan_partial_kernel(int P, int C, int mode, const float* __restrict__ X, const float* __restrict__ DY,
                                     const float* __restrict__ mean, const float* __restrict__ rstd, float* part,
-                                    float* part2) {
+                                    float* part2, int rs) {
   __shared__ float red[2][4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
-  const int r0 = blockIdx.y * RS, r1 = min(P, r0 + RS);
+  const int r0 = blockIdx.y * rs, r1 = min(P, r0 + rs);
   float s = 0.f, s2 = 0.f;
   if (c < C) {
     const float mu = mode ? mean[c] : 0.f, rs = mode == 2 ? rstd[c] : 0.f;
@@ -577,14 +577,21 @@ __global__ void chan_partial_kernel(int P, int C, int mode, const float* __restr
     if (mode == 2) part2[(size_t)blockIdx.y * C + c] = ((red[1][0][l] + red[1][1][l]) + red[1][2][l]) + red[1][3][l];
   }
 }
-// out[c] = scale sum_z part[z][c]; mode 1 (variance) also gives rstd and the unbiased variance
-__global__ void chan_final_kernel(int C, int S, const float* __restrict__ part, float scale, float* out, float* rstd,
-                                  float* var_unbiased, float eps, float unbias) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int z = 0; z < S; ++z) s += part[(size_t)z * C + c];
-  s *= scale;
+// out[c] = scale sum_z part[z][c] (S <= 256): one block per channel, one slice per thread, LDS
+// tree in a fixed order; also rstd and the unbiased variance when asked (mode-1 partials)
+__global__ void __launch_bounds__(256) chan_final_kernel(int C, int S, const float* __restrict__ part, float scale,
+                                                         float* out, float* rstd, float* var_unbiased, float eps,
+                                                         float unbias) {
+  __shared__ float red[256];
+  const int c = blockIdx.x, z = threadIdx.x;
+  red[z] = z < S ? part[(size_t)z * C + c] : 0.f;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (z < o) red[z] += red[z + o];
+    __syncthreads();
+  }
+  if (z) return;
+  const float s = red[0] * scale;
   out[c] = s;
   if (rstd) rstd[c] = 1.0f / sqrtf(s + eps);
   if (var_unbiased) var_unbiased[c] = s * unbias;
@@ -610,14 +617,16 @@ __global__ void bn_bwd_apply_kernel(int64_t n, int C, int P, const float* __rest
   dx[e] = g[c] * rstd[c] * (dy[e] - dbeta[c] / P - xh * dgamma[c] / P);
 }
 
-// per-image channel means: out[n][c] = scale sum_p X[n][p][c] (Y: X Y), one block per (image, 64 channels)
-__global__ void img_chan_sum_kernel(int HW, int C, const float* __restrict__ X, const float* __restrict__ Y, float scale,
-                                    float* out) {
+// per-image channel sums: part[z][n][c] = sum over pixel slice z of X[n][p][c] (Y: X Y); block
+// (channel block, image, slice), 4 pixel phases per block; img_chan_final adds the slices x scale
+__global__ void img_chan_sum_kernel(int HW, int C, int ps, const float* __restrict__ X, const float* __restrict__ Y,
+                                    float* part) {
   __shared__ float red[4][64];
-  const int n = blockIdx.y, c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  const int n = blockIdx.y, z = blockIdx.z, c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  const int p0 = z * ps, p1 = min(HW, p0 + ps);
   float s = 0.f;
   if (c < C)
-    for (int p = ph; p < HW; p += 4) {
+    for (int p = p0 + ph; p < p1; p += 4) {
       const size_t i = ((size_t)n * HW + p) * C + c;
       s += Y ? X[i] * Y[i] : X[i];
     }
@@ -625,8 +634,15 @@ __global__ void img_chan_sum_kernel(int HW, int C, const float* __restrict__ X, 
   __syncthreads();
   if (ph == 0 && c < C) {
     const int l = threadIdx.x;
-    out[(size_t)n * C + c] = (((red[0][l] + red[1][l]) + red[2][l]) + red[3][l]) * scale;
+    part[((size_t)z * gridDim.y + n) * C + c] = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
   }
+}
+__global__ void img_chan_final_kernel(int NC, int S, const float* __restrict__ part, float scale, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= NC) return;
+  float s = 0.f;
+  for (int z = 0; z < S; ++z) s += part[(size_t)z * NC + i];
+  out[i] = s * scale;
 }
 // out[n][p][c] = X[n][p][c] s[n][c] (+ add[n][c] when add is set)
 __global__ void chan_scale_kernel(int64_t total, int HW, int C, const float* __restrict__ X, const float* __restrict__ s,
@@ -685,6 +701,10 @@ float* workspace(size_t bytes) {
   g_ws_bytes = bytes;
   return g_ws;
 }
+
+// row slices of the per-channel reductions: at most 256 (the final stage loops over them), each
+// at least RS rows
+int chan_slices(int P) { return std::max(1, std::min(256, (P + RS - 1) / RS)); }
 
 // column sums of X (and the LayerNorm dgamma sums when X2 is set) into out / out2
 int colsums(int M, int N, const float* X, int ldx, const float* X2, const float* mean, const float* rstd, float* out,
@@ -891,16 +911,16 @@ int ggd_tr_batchnorm_fwd(int P, int C, const float* x, const float* g, const flo
                          float* rstd, float* var_unbiased, void* stream) {
   if (P <= 1 || C <= 0 || !x || !g || !b || !y || !mean || !rstd) return -1;
   hipStream_t s = (hipStream_t)stream;
-  const int S = (P + RS - 1) / RS;
+  const int S = chan_slices(P), rs = (P + S - 1) / S;
   float* ws = workspace(sizeof(float) * ((size_t)S * C + C));
   if (!ws) return -3;
   float* var = ws + (size_t)S * C;
   const dim3 gp((C + 63) / 64, S);
-  hipLaunchKernelGGL(chan_partial_kernel, gp, dim3(256), 0, s, P, C, 0, x, nullptr, nullptr, nullptr, ws, nullptr);
-  hipLaunchKernelGGL(chan_final_kernel, dim3(blocks_for(C)), dim3(TT), 0, s, C, S, ws, 1.0f / P, mean, nullptr, nullptr,
+  hipLaunchKernelGGL(chan_partial_kernel, gp, dim3(256), 0, s, P, C, 0, x, nullptr, nullptr, nullptr, ws, nullptr, rs);
+  hipLaunchKernelGGL(chan_final_kernel, dim3(C), dim3(256), 0, s, C, S, ws, 1.0f / P, mean, nullptr, nullptr,
                      0.f, 0.f);
-  hipLaunchKernelGGL(chan_partial_kernel, gp, dim3(256), 0, s, P, C, 1, x, nullptr, mean, nullptr, ws, nullptr);
-  hipLaunchKernelGGL(chan_final_kernel, dim3(blocks_for(C)), dim3(TT), 0, s, C, S, ws, 1.0f / P, var, rstd, var_unbiased,
+  hipLaunchKernelGGL(chan_partial_kernel, gp, dim3(256), 0, s, P, C, 1, x, nullptr, mean, nullptr, ws, nullptr, rs);
+  hipLaunchKernelGGL(chan_final_kernel, dim3(C), dim3(256), 0, s, C, S, ws, 1.0f / P, var, rstd, var_unbiased,
                      eps, (float)P / (float)(P - 1));
   const int64_t n = (int64_t)P * C;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(blocks_for(n)), dim3(TT), 0, s, n, C, x, mean, rstd, g, b, y);
@@ -911,13 +931,13 @@ int ggd_tr_batchnorm_bwd(int P, int C, const float* x, const float* g, const flo
                          const float* dy, float* dx, float* dg, float* db, void* stream) {
   if (P <= 1 || C <= 0 || !x || !g || !mean || !rstd || !dy || !dx || !dg || !db) return -1;
   hipStream_t s = (hipStream_t)stream;
-  const int S = (P + RS - 1) / RS;
+  const int S = chan_slices(P), rs = (P + S - 1) / S;
   float* ws = workspace(sizeof(float) * (size_t)S * C * 2);
   if (!ws) return -3;
   hipLaunchKernelGGL(chan_partial_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, P, C, 2, x, dy, mean, rstd, ws,
-                     ws + (size_t)S * C);
-  hipLaunchKernelGGL(chan_final_kernel, dim3(blocks_for(C)), dim3(TT), 0, s, C, S, ws, 1.0f, db, nullptr, nullptr, 0.f, 0.f);
-  hipLaunchKernelGGL(chan_final_kernel, dim3(blocks_for(C)), dim3(TT), 0, s, C, S, ws + (size_t)S * C, 1.0f, dg, nullptr,
+                     ws + (size_t)S * C, rs);
+  hipLaunchKernelGGL(chan_final_kernel, dim3(C), dim3(256), 0, s, C, S, ws, 1.0f, db, nullptr, nullptr, 0.f, 0.f);
+  hipLaunchKernelGGL(chan_final_kernel, dim3(C), dim3(256), 0, s, C, S, ws + (size_t)S * C, 1.0f, dg, nullptr,
                      nullptr, 0.f, 0.f);
   const int64_t n = (int64_t)P * C;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks_for(n)), dim3(TT), 0, s, n, C, P, x, dy, mean, rstd, g, db, dg, dx);
@@ -927,8 +947,12 @@ int ggd_tr_batchnorm_bwd(int P, int C, const float* x, const float* g, const flo
 int ggd_tr_image_channel_sum(int N, int HW, int C, const float* x, const float* y, float scale, float* out,
                              void* stream) {
   if (N <= 0 || HW <= 0 || C <= 0 || !x || !out) return -1;
-  hipLaunchKernelGGL(img_chan_sum_kernel, dim3((C + 63) / 64, N), dim3(256), 0, (hipStream_t)stream, HW, C, x, y, scale,
-                     out);
+  hipStream_t s = (hipStream_t)stream;
+  const int S = std::max(1, std::min(64, HW / 256)), ps = (HW + S - 1) / S;
+  float* ws = workspace(sizeof(float) * (size_t)S * N * C);
+  if (!ws) return -3;
+  hipLaunchKernelGGL(img_chan_sum_kernel, dim3((C + 63) / 64, N, S), dim3(256), 0, s, HW, C, ps, x, y, ws);
+  hipLaunchKernelGGL(img_chan_final_kernel, dim3(blocks_for((int64_t)N * C)), dim3(TT), 0, s, N * C, S, ws, scale, out);
   return rc(hipGetLastError());
 }
 

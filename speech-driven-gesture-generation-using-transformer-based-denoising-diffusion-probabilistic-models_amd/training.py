@@ -554,11 +554,13 @@ class TrainableModel:
             res = x
         return relu(add(out, res))
 
-    def encode(self, wav):
+    def encode(self, wav=None, img=None):
         """HA2GSpeechEncoder.forward (speech_encoder.py:37-61) with the SE-ResNet in train mode:
-        (z_low, z_mid, z_high) with the autograd graph to the encoder's parameters."""
+        (z_low, z_mid, z_high) with the autograd graph to the encoder's parameters.  img: the
+        front end's InstanceNorm'd mel image (N, 128, F) when already computed."""
         P = self.params
-        img = self.speech_encoder().frontend(wav)                     # (N, 128, F), parameter-free
+        if img is None:
+            img = self.speech_encoder().frontend(wav)                 # (N, 128, F), parameter-free
         r = "speech_encoder.wav_encoder.feat_extractor."
         x = img[..., None]                                           # NHWC, C = 1
         x = self._bn(r + "bn1", relu(self._conv(r + "conv1", x, 1, 1)))

@@ -338,9 +338,58 @@ def enc_setup(pkg, beat_cfg, tr):
 
 
 def test_encoder_training_gradients_match_oracle(tr, enc_setup):
-    """Full training step with the HA2G encoder trained (BatchNorm on batch statistics): loss, speech
-    tokens and every parameter gradient (encoder included) vs torch autograd through the oracle with
-    train-mode BN; the running statistics follow nn.BatchNorm2d's momentum-0.1 update."""
+    """The HA2G encoder in train mode (BatchNorm on batch statistics) from the same front-end image:
+    speech tokens and every encoder parameter gradient of L = sum_l <z_l, R_l> against torch autograd
+    through the oracle.  Deep train-mode BN chains amplify f32 summation-order differences, so the
+    yardstick is an f64 oracle run: our error vs f64 must stay within 4x the f32 oracle's own error
+    vs f64 (or 1e-3 of the tensor's gradient scale).  The running statistics follow
+    nn.BatchNorm2d's momentum-0.1 update."""
+    arch, sd, diffusion, wav = enc_setup
+    model = tr.TrainableModel(arch, sd, "cuda", train_encoder=True)
+    img = model.speech_encoder().frontend(wav.cuda())
+    z = model.encode(img=img)
+    g = th.Generator().manual_seed(19)
+    R = [th.randn(zi.shape, generator=g) for zi in z]
+    model.zero_grad()
+    sum((zi * r.cuda()).sum() for zi, r in zip(z, R)).backward()
+    names = [k for k in model.params if k.startswith("speech_encoder.")]
+
+    def oracle(dtype):
+        sdr = {k: v.detach().to(dtype).clone() if v.is_floating_point() else v for k, v in sd.items()}
+        for k in names:
+            sdr[k].requires_grad_(True)
+        zr = ref_denoiser.speech_encoder_from_image(sdr, img.cpu().to(dtype), train=True)
+        sum((zi * r.to(dtype)).sum() for zi, r in zip(zr, R)).backward()
+        return zr, {k: sdr[k].grad for k in names}
+
+    z64, g64 = oracle(th.float64)
+    z32, g32 = oracle(th.float32)
+    for a, b, c in zip(z, z32, z64):
+        e_ours = (a.detach().cpu().double() - c).abs().max().item()
+        e_ref = (b.detach().double() - c).abs().max().item()
+        assert e_ours <= max(4 * e_ref, 1e-5 * c.abs().max().item()), (e_ours, e_ref)
+    worst = []
+    for k in names:
+        s_ = g64[k].abs().max().item()
+        e_ours = (model.params[k].grad.cpu().double() - g64[k]).abs().max().item() / s_
+        e_ref = (g32[k].double() - g64[k]).abs().max().item() / s_
+        worst.append((e_ours / max(4 * e_ref, 1e-3), e_ours, e_ref, k))
+    worst.sort(reverse=True)
+    print("\nencoder gradients (ratio to bound, ours vs f64, f32 oracle vs f64):", worst[:5])
+    assert worst[0][0] <= 1.0, worst[:5]
+    # running statistics of the first BN: 0.9 init + 0.1 batch stats of relu(conv1(img))
+    r = "speech_encoder.wav_encoder.feat_extractor."
+    a = F.relu(F.conv2d(img.cpu()[:, None], sd[r + "conv1.weight"].float(), sd[r + "conv1.bias"].float(), padding=1))
+    rm = 0.9 * sd[r + "bn1.running_mean"] + 0.1 * a.mean(dim=(0, 2, 3))
+    rv = 0.9 * sd[r + "bn1.running_var"] + 0.1 * a.var(dim=(0, 2, 3), unbiased=True)
+    close(model.buffers[r + "bn1.running_mean"], rm, 1e-4)
+    close(model.buffers[r + "bn1.running_var"], rv, 1e-4)
+    assert int(model.buffers[r + "bn1.num_batches_tracked"]) == int(sd[r + "bn1.num_batches_tracked"]) + 1
+
+
+def test_training_step_with_encoder_matches_oracle_loss(tr, enc_setup):
+    """One full training step with the encoder trained: the loss (train-mode encoder + decoder) and
+    the decoder's gradients against the oracle from the same front-end image."""
     arch, sd, diffusion, wav = enc_setup
     model = tr.TrainableModel(arch, sd, "cuda", train_encoder=True)
     n = wav.shape[0]
@@ -352,30 +401,16 @@ def test_encoder_training_gradients_match_oracle(tr, enc_setup):
     out = tr.training_losses(diffusion, model, x0.cuda(), t.cuda(), {"wav": wav.cuda()}, noise=noise.cuda())
     loss = out["mse"].mean()
     loss.backward()
-    names = list(model.params)
-    assert any(k.startswith("speech_encoder.") for k in names)
+    img = model.speech_encoder().frontend(wav.cuda()).cpu()
     sd_ref = {k: v.detach().float().clone() for k, v in sd.items()}
-    for k in names:
+    dec = [k for k in model.params if not k.startswith("speech_encoder.")]
+    for k in dec:
         sd_ref[k].requires_grad_(True)
-    z_ref = ref_denoiser.speech_encoder(sd_ref, wav, train=True)
+    z_ref = ref_denoiser.speech_encoder_from_image(sd_ref, img, train=True)
     want = _oracle_loss(arch, sd_ref, diffusion, x0, t, noise, z_ref)
     want.backward()
     assert abs(loss.item() - want.item()) <= 1e-4 * want.item(), (loss.item(), want.item())
-    floor = 1e-4 * max(sd_ref[k].grad.abs().max().item() for k in names)
-    worst = []
-    for k in names:
-        gg, gr = model.params[k].grad.cpu(), sd_ref[k].grad
-        s = max(gr.abs().max().item(), floor)
-        worst.append(((gg - gr).abs().max().item() / s, k))
-    worst.sort(reverse=True)
-    print("\nworst gradient errors with the encoder trained:", worst[:6])
-    assert worst[0][0] <= 5e-3, worst[:6]
-    # running statistics of the first BN: 0.9 init + 0.1 batch stats of relu(conv1(img))
-    img = model.speech_encoder().frontend(wav.cuda()).cpu()
-    r = "speech_encoder.wav_encoder.feat_extractor."
-    a = F.relu(F.conv2d(img[:, None], sd[r + "conv1.weight"].float(), sd[r + "conv1.bias"].float(), padding=1))
-    rm = 0.9 * sd[r + "bn1.running_mean"] + 0.1 * a.mean(dim=(0, 2, 3))
-    rv = 0.9 * sd[r + "bn1.running_var"] + 0.1 * a.var(dim=(0, 2, 3), unbiased=True)
-    close(model.buffers[r + "bn1.running_mean"], rm, 1e-4)
-    close(model.buffers[r + "bn1.running_var"], rv, 1e-4)
-    assert int(model.buffers[r + "bn1.num_batches_tracked"]) == int(sd[r + "bn1.num_batches_tracked"]) + 1
+    floor = 1e-4 * max(sd_ref[k].grad.abs().max().item() for k in dec)
+    worst = max((model.params[k].grad.cpu() - sd_ref[k].grad).abs().max().item()
+                / max(sd_ref[k].grad.abs().max().item(), floor) for k in dec)
+    assert worst <= 2e-3, worst
