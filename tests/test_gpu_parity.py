@@ -14,6 +14,8 @@ from tests.conftest import oracle_cfg
 pytestmark = pytest.mark.gpu
 
 D_POSE, L, WAV = 123, 40, 32000
+ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_PAIR_WT, ROUTE_PHASE_LAUNCHES = 0, 1, 2, 3   # include/ggd.h GGD_ROUTE_*
+INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES = 0, 2              # include/ggd.h GGD_INFO_*
 
 
 def rel_rms(a, b):
@@ -91,15 +93,34 @@ def test_sample_injected_noise_f32(pkg, beat_cfg, setup, alg):
         assert err <= 1e-3, (k, err)
 
 
-def test_graph_equals_eager(pkg, beat_cfg, setup):
-    _, sd, _ = setup
-    model, diffusion = make_model(pkg, beat_cfg, sd, "bf16")
-    wav, x, _ = inputs(4, seed=9)
-    a = diffusion.p_sample_loop(model, (4, D_POSE, L), {"wav": wav.cuda()}, noise=x.cuda(), seed=11, n_steps=8,
-                                use_graph=True)["sample"]
-    b = diffusion.p_sample_loop(model, (4, D_POSE, L), {"wav": wav.cuda()}, noise=x.cuda(), seed=11, n_steps=8,
-                                use_graph=False)["sample"]
-    assert th.equal(a, b)
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_graph_step_matches_oracle(pkg, beat_cfg, setup, dtype):
+    """The per-step hipGraph (north_star: "the per-step graph captured with hipGraph"): the
+    per-phase route replayed as one captured graph per denoise step equals its eager launches bit
+    for bit and the oracle within the dtype's bound, on injected noise."""
+    _, sd, om = setup
+    model, diffusion = make_model(pkg, beat_cfg, sd, dtype)
+    n, steps = 4, 6
+    wav, x, _ = inputs(n, seed=9)
+    zs = th.randn(steps, n, D_POSE, L, generator=th.Generator().manual_seed(10))
+    ctx, _ = model.prepare(wav.cuda(), L)
+    run = lambda g: diffusion.p_sample_loop(model, (n, D_POSE, L), {"wav": wav.cuda()}, noise=x.cuda(),
+                                            step_noise=zs.cuda(), n_steps=steps, use_graph=g)["sample"].cpu()
+    try:
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_PER_CLIP, 1) == 0          # no per-clip loops
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_PHASE_LAUNCHES, 1) == 0    # per-phase launches
+        graph, eager = run(True), run(False)
+    finally:
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_PHASE_LAUNCHES, 0)
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_PER_CLIP, 0)
+    assert th.equal(graph, eager)
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    want = ref_diffusion.sample_loop(sch, om, (n, D_POSE, L), {"wav": wav}, ref_diffusion.InjectedNoise(x, zs),
+                                     "ddpm", x_T=x, n_steps=steps)["sample"]
+    if dtype == "f32":
+        assert (graph - want).abs().max().item() <= 1e-3
+    else:
+        assert rel_rms(graph, want) <= 5e-2
 
 
 def test_counter_noise_matches_oracle_stream(pkg, beat_cfg, setup):
@@ -384,8 +405,6 @@ def test_inpaint_model_generate_sample_f32(pkg, setup_inp):
 # automatically when the clip-group loop (mk_kernel) would need >= 3 chunks (the C5 shape,
 # 128 clips per GPU); both must agree with the oracle and with each other.
 # ------------------------------------------------------------------------------------------
-ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_PAIR_WT = 0, 1, 2            # include/ggd.h GGD_ROUTE_*
-INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES = 0, 2              # include/ggd.h GGD_INFO_*
 
 
 def _info(ctx, what):
