@@ -688,18 +688,23 @@ __global__ void head_flat_kernel(int N, int H, int W, int C, const float* __rest
 
 inline unsigned blocks_for(int64_t n, int per = TT) { return (unsigned)((n + per - 1) / per); }
 
-// grow-only device workspace for split-K slices and column-sum partials (one training process
-// per GPU drives one stream, so a single buffer suffices; it is never freed while loaded)
-float* g_ws = nullptr;
-size_t g_ws_bytes = 0;
+// grow-only workspace per device for split-K slices and reduction partials.  The training ops
+// of one device are issued on one stream (training.py uses torch's current stream), so the
+// consumers of a buffer run before the next op overwrites it; growing it frees the old one with
+// hipFree, which waits for the device.  Not thread-safe: one host thread drives a device.
+constexpr int WS_DEVICES = 64;
+float* g_ws[WS_DEVICES] = {};
+size_t g_ws_bytes[WS_DEVICES] = {};
 float* workspace(size_t bytes) {
-  if (bytes <= g_ws_bytes) return g_ws;
-  if (g_ws) (void)hipFree(g_ws);
-  g_ws = nullptr;
-  g_ws_bytes = 0;
-  if (hipMalloc((void**)&g_ws, bytes) != hipSuccess) return nullptr;
-  g_ws_bytes = bytes;
-  return g_ws;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= WS_DEVICES) return nullptr;
+  if (bytes <= g_ws_bytes[dev]) return g_ws[dev];
+  if (g_ws[dev]) (void)hipFree(g_ws[dev]);
+  g_ws[dev] = nullptr;
+  g_ws_bytes[dev] = 0;
+  if (hipMalloc((void**)&g_ws[dev], bytes) != hipSuccess) return nullptr;
+  g_ws_bytes[dev] = bytes;
+  return g_ws[dev];
 }
 
 // row slices of the per-channel reductions: at most 256 (the final stage loops over them), each
