@@ -181,7 +181,9 @@ enum {
   GGD_ROUTE_PAIR = 1,                /* per-clip loops: 0 auto, 1 never, 2 always two workgroups per clip */
   GGD_ROUTE_PAIR_WRITE_THROUGH = 2,  /* 1: clip-pair hand-offs written through on any placement */
   GGD_ROUTE_PHASE_LAUNCHES = 3,      /* 1: per-phase launches instead of the clip-group loop (ggd_mega.hip) */
-  GGD_ROUTE_PLACEMENT = 4            /* clip-group loop: 0 XCD-local, 1 part p on XCD p, 2 group per XCD */
+  GGD_ROUTE_PLACEMENT = 4,           /* clip-group loop: 0 XCD-local, 1 part p on XCD p, 2 group per XCD */
+  GGD_ROUTE_GEMM_LAUNCHES = 5        /* generic one-way route: 1 = one launch per GEMM instead of the
+                                        row-block chains (ggd_chain.hip) */
 };
 int ggd_set_route(ggd_ctx* ctx, int32_t knob, int32_t value);
 enum {
@@ -189,7 +191,8 @@ enum {
   GGD_INFO_LOOP_CAPACITY = 1,        /* clips per launch of the clip-group loop (0: unavailable) */
   GGD_INFO_PAIR_LAUNCHES = 2,        /* last ggd_sample: clip-pair launches (0: another route) */
   GGD_INFO_XL_LAUNCHES = 3,          /* last ggd_sample: XCD-local clip-group launches */
-  GGD_INFO_WT_RERUNS = 4             /* last ggd_sample: clip-group launches re-run write-through */
+  GGD_INFO_WT_RERUNS = 4,            /* last ggd_sample: clip-group launches re-run write-through */
+  GGD_INFO_CHAIN_AVAILABLE = 5       /* 1 when the generic one-way route runs as row-block chains */
 };
 int ggd_route_info(ggd_ctx* ctx, int32_t what, double* out);
 

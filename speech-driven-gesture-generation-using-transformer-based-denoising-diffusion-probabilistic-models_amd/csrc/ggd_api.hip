@@ -27,6 +27,7 @@ struct Lin {            // packed Linear: T [npad][kpad] (or e4m3 bytes + scale)
   void* w = nullptr;
   float* b = nullptr;
   float* scale = nullptr;  // GGD_FP8W per-step Linears: per-output-channel dequantization scale
+  void* wf = nullptr;      // row-block chain route: fragment-packed copy of w (ggd_chain.hip)
   int n = 0, k = 0, npad = 0, kpad = 0;
 };
 
@@ -103,6 +104,10 @@ struct ggd_ctx {
   int pe_len = 0;
   float* kv_step = nullptr;  // [layers][T_orig][2d]
   float* zero_row = nullptr; // 1 KiB of zeros: the attention conv's padding rows
+
+  // row-block chains (ggd_chain.hip): the one-way generic route's GEMMs, 4 launches per layer
+  bool chain = false;        // fragment-packed weights built (one-way, not fused, bf16 / fp8, d 256, FFN 1024)
+  int gemm_launches = 0;     // GGD_ROUTE_GEMM_LAUNCHES: 1 = one launch per GEMM instead
 
   // two-way decoder (generic kernels, joint layout [n][J = L + 1 + Ts][d])
   bool twoway = false;
@@ -676,10 +681,140 @@ int launch_decoder_twoway(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
   return GGD_OK;
 }
 
+ChainLin chain_lin(const Lin& L) {
+  ChainLin r{};
+  r.w = L.wf;
+  r.b = L.b;
+  r.scale = L.scale;
+  r.npad = L.npad;
+  r.kpad = L.kpad;
+  return r;
+}
+
+AttnArgs self_attn_args(ggd_ctx* c, const Layer& Ly) {
+  const ggd_desc& D = c->desc;
+  const int d = D.d_model, dk = d / D.heads;
+  AttnArgs at{};
+  at.zero = c->zero_row;
+  at.cross = 0;
+  at.q = c->qkv;
+  at.ldq = 3 * d;
+  at.k = (const char*)c->qkv + c->tsize * d;
+  at.v = (const char*)c->qkv + c->tsize * 2 * d;
+  at.ldkv = 3 * d;
+  at.cw_q = Ly.sa_q.w; at.cb_q = Ly.sa_q.b;
+  at.cw_k = Ly.sa_k.w; at.cb_k = Ly.sa_k.b;
+  at.cw_v = Ly.sa_v.w; at.cb_v = Ly.sa_v.b;
+  at.out = c->att;
+  at.ldo = d;
+  at.Lq = D.seq_len;
+  at.Lk = D.seq_len;
+  at.dk = dk;
+  at.heads = D.heads;
+  at.d = d;
+  at.scale = 1.0f / std::sqrt((float)dk);
+  return at;
+}
+
+void cross_attn_args(ggd_ctx* c, const Layer& Ly, int li, const int* t_clip, AttnArgs& at) {
+  const ggd_desc& D = c->desc;
+  const int d = D.d_model;
+  at.cross = 1;
+  at.q = c->q;
+  at.ldq = d;
+  at.kv_mem = c->kv_mem + (size_t)li * D.max_batch * D.speech_len * 2 * d;
+  at.kv_step = c->kv_step + (size_t)li * D.diffusion_steps * 2 * d;
+  at.t_clip = t_clip;
+  at.steps = c->d_steps;
+  at.step_counter = c->d_counter;
+  at.cw_q = Ly.ca_q.w; at.cb_q = Ly.ca_q.b;
+  at.cw_k = Ly.ca_k.w; at.cb_k = Ly.ca_k.b;
+  at.cw_v = Ly.ca_v.w; at.cb_v = Ly.ca_v.b;
+  at.Lk = 1 + D.speech_len;
+}
+
+// The one-way decoder as row-block chains (ggd_chain.hip): emb_x + PE, then per layer
+// [self-attention, chain R(o_sa) + P(LN2, q_ca), cross-attention, chain R(o_ca) + F + P(next
+// layer's LN1 + QKV, or out_layers)].  Same arithmetic as the per-GEMM route, bit for bit.
+int launch_decoder_chain(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
+  const ggd_desc& D = c->desc;
+  const int L = D.seq_len, d = D.d_model, M = n * L, w8 = D.dtype == GGD_FP8W;
+  hipStream_t s = c->stream;
+  GemmArgs g = gemm_args(c->emb_x, M, c->x, D.d_pose, c->h, d);
+  g.a_add = c->inp_on ? c->inp_delta : nullptr;
+  g.pe = c->pe;
+  g.pe_period = L;
+  g.pe_offset = 0;
+  g.step_counter = sampling ? c->d_counter : nullptr;
+  GEMM(c, PRO_F32, EPI_PE, g, s);
+  auto chain = [&](const ChainArgs& ca) -> int {
+    HIP_TRY(c, launch_chain(w8, ca, s));
+    return GGD_OK;
+  };
+  auto qkv_proj = [&](ChainArgs& ca, const Layer& Ly) {  // P: LN1 + the self-attention QKV
+    ca.p_g = Ly.ln1_g;
+    ca.p_b = Ly.ln1_b;
+    ca.p = chain_lin(Ly.qkv);
+    ca.out = c->qkv;
+    ca.ldo = 3 * d;
+  };
+  int r;
+  ChainArgs c0{};
+  c0.M = M;
+  c0.h = c->h;
+  qkv_proj(c0, c->layers[0]);
+  if ((r = chain(c0))) return r;
+  for (int li = 0; li < D.n_layers; ++li) {
+    const Layer& Ly = c->layers[li];
+    AttnArgs at = self_attn_args(c, Ly);
+    if (c->profiling && sampling && (r = prof_mark(c, s))) return r;
+    HIP_TRY(c, launch_attention(D.dtype, at, n, s));
+    if (c->profiling && sampling && (r = prof_mark(c, s))) return r;
+    ChainArgs ca{};
+    ca.M = M;
+    ca.h = c->h;
+    ca.a_in = (const bf16_t*)c->att;
+    ca.r = chain_lin(Ly.o_sa);
+    ca.p_g = Ly.ln2_g;
+    ca.p_b = Ly.ln2_b;
+    ca.p = chain_lin(Ly.q_ca);
+    ca.out = c->q;
+    ca.ldo = d;
+    if ((r = chain(ca))) return r;
+    cross_attn_args(c, Ly, li, t_clip, at);
+    if (c->profiling && sampling && (r = prof_mark(c, s))) return r;
+    HIP_TRY(c, launch_attention(D.dtype, at, n, s));
+    if (c->profiling && sampling && (r = prof_mark(c, s))) return r;
+    ChainArgs cb{};
+    cb.M = M;
+    cb.h = c->h;
+    cb.a_in = (const bf16_t*)c->att;
+    cb.r = chain_lin(Ly.o_ca);
+    cb.f_g = Ly.ln3_g;
+    cb.f_b = Ly.ln3_b;
+    cb.f1 = chain_lin(Ly.ff1);
+    cb.f2 = chain_lin(Ly.ff2);
+    if (li + 1 < D.n_layers) {
+      qkv_proj(cb, c->layers[li + 1]);
+    } else {  // out_layers: LayerNorm + Linear(d -> d_pose) (nn.py:211-214,228)
+      cb.p_g = c->out_ln_g;
+      cb.p_b = c->out_ln_b;
+      cb.p = chain_lin(c->out_lin);
+      cb.out = c->eps;
+      cb.ldo = c->cpad;
+      cb.out_f32 = 1;
+      cb.n_valid = c->out_lin.n;
+    }
+    if ((r = chain(cb))) return r;
+  }
+  return GGD_OK;
+}
+
 int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
   const ggd_desc& D = c->desc;
   if (c->twoway) return launch_decoder_twoway(c, n, sampling, t_clip);
   if (c->fused) return launch_fused_layers(c, n, sampling, t_clip);
+  if (c->chain && !c->gemm_launches) return launch_decoder_chain(c, n, sampling, t_clip);
   const int L = D.seq_len, d = D.d_model, M = n * L, dk = d / D.heads;
   hipStream_t s = c->stream;
 
@@ -1112,6 +1247,24 @@ int ggd_finalize_weights(ggd_ctx* c) {
     HIP_TRY(c, dalloc(c, &c->kvc, c->tsize * (size_t)D.n_layers * D.max_batch * D.heads * KVC_ELEMS));
     HIP_TRY(c, dalloc(c, &c->ffp, sizeof(float) * (size_t)D.max_batch * 8 * D.seq_len * D.d_model));
   }
+  // row-block chains for the one-way generic route (ggd_chain.hip)
+  c->chain = !c->fused && D.dtype != GGD_F32 && d == 256 && c->out_lin.kpad == 256;
+  for (int l = 0; c->chain && l < D.n_layers; ++l) {
+    const Layer& Ly = c->layers[l];
+    c->chain = Ly.qkv.npad == 3 * d && Ly.o_sa.npad == d && Ly.q_ca.npad == d && Ly.o_ca.npad == d &&
+               Ly.ff1.npad == 4 * d && Ly.ff1.kpad == d && Ly.ff2.npad == d && Ly.ff2.kpad == 4 * d;
+  }
+  if (c->chain) {
+    auto pack = [&](Lin& L) -> int {
+      const int w8 = L.scale != nullptr;
+      HIP_TRY(c, dalloc(c, &L.wf, chain_pack_bytes(w8, L.npad, L.kpad)));
+      HIP_TRY(c, launch_chain_pack(w8, L.w, L.wf, L.npad, L.kpad, c->stream));
+      return GGD_OK;
+    };
+    for (Layer& Ly : c->layers)
+      for (Lin* L : {&Ly.qkv, &Ly.o_sa, &Ly.q_ca, &Ly.o_ca, &Ly.ff1, &Ly.ff2}) TRY(pack(*L));
+    TRY(pack(c->out_lin));
+  }
   TRY(build_step_tables(c));
   c->persist = c->fused && persist_supported(D.dtype, D.d_model, D.heads, D.seq_len, D.speech_len, D.d_pose);
   if (c->persist) {
@@ -1345,6 +1498,9 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
       if (value < 0 || value > 2) break;
       c->mega_place = value;
       return GGD_OK;
+    case GGD_ROUTE_GEMM_LAUNCHES:   // 1: one launch per GEMM instead of the row-block chains
+      c->gemm_launches = value != 0;
+      return GGD_OK;
     default:
       break;
   }
@@ -1359,6 +1515,7 @@ int ggd_route_info(ggd_ctx* c, int32_t what, double* out) {
     case GGD_INFO_PAIR_LAUNCHES: *out = c->pair_launches; return GGD_OK;
     case GGD_INFO_XL_LAUNCHES: *out = c->mega_xl_launches; return GGD_OK;
     case GGD_INFO_WT_RERUNS: *out = c->mega_fallbacks; return GGD_OK;
+    case GGD_INFO_CHAIN_AVAILABLE: *out = c->chain ? 1.0 : 0.0; return GGD_OK;
     default: return fail(c, GGD_ERR_ARG, "unknown route info");
   }
 }
@@ -1871,9 +2028,9 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   }
   // pointer / shape key: a captured graph is reused only for identical arguments
   char keybuf[512];
-  std::snprintf(keybuf, sizeof keybuf, "%d|%d|%p|%p|%p|%p|%d", a->alg, a->n, (const void*)a->noise,
+  std::snprintf(keybuf, sizeof keybuf, "%d|%d|%p|%p|%p|%p|%d|%d", a->alg, a->n, (const void*)a->noise,
                 (const void*)a->inpaint_poses, (const void*)a->inpaint_masks, (const void*)a->trans,
-                (int)c->profiling);
+                (int)c->profiling, c->gemm_launches);
   const std::string key(keybuf);
   // fused path profiling: KB stamps its own launch span per (step, layer) on the device clock,
   // so the graph replays unchanged; the generic path brackets its launches with events (eager)

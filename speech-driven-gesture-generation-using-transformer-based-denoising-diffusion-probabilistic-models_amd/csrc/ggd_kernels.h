@@ -210,7 +210,30 @@ constexpr int MEGA_STAMP_STEPS = 2;
 constexpr int MEGA_MAX_CHUNKS = 16;  // status words: one per launch of up to mega_capacity() clips
 constexpr int MEGA_CTL_WORDS = 256 + 32 * 16 + 32 * 32;  // tickets/arrival, group counters, group flag lines
 
+// Row-block chains of the one-way decoder (ggd_chain.hip): one launch runs, on 32-row blocks of
+// the residual stream, R (h += A W_r^T + b), F (h += FFN(LN_f(h))) and P (out = LN_p(h) W_p^T + b)
+// as enabled (w non-null).  Weights are fragment-packed copies made by launch_chain_pack.
+struct ChainLin {
+  const void* w;          // fragment-packed (bf16, or e4m3 bytes when scale is set)
+  const float* b;         // [npad]
+  const float* scale;     // fp8: per-output-channel dequantization scale [npad]
+  int npad, kpad;
+};
+struct ChainArgs {
+  int M;                  // rows (clips x frames)
+  float* h;               // residual stream f32 [M][256], updated in place by R / F
+  const bf16_t* a_in;     // R operand: bf16 rows [M][256] (the attention output)
+  ChainLin r;
+  const float *f_g, *f_b; ChainLin f1, f2;   // F: LayerNorm, [1024][256], [256][1024]
+  const float *p_g, *p_b; ChainLin p;        // P: LayerNorm, [npad][256]
+  void* out; int ldo;     // P output rows: bf16, or f32 when out_f32 (columns >= n_valid skipped)
+  int out_f32, n_valid;
+};
+
 // launchers (return hipError_t of the launch)
+hipError_t launch_chain(int w8, const ChainArgs& a, hipStream_t s);
+hipError_t launch_chain_pack(int w8, const void* src, void* dst, int npad, int kpad, hipStream_t s);
+size_t chain_pack_bytes(int w8, int npad, int kpad);
 hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s);  // 0 KA, 1 KB, 2 KC, 3 KD
 hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s);
 // step-invariant convolved cross-attention K | V^T images of one layer (ggd_set_memory; fused paths)

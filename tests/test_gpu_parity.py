@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 
 D_POSE, L, WAV = 123, 40, 32000
 ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_PAIR_WT, ROUTE_PHASE_LAUNCHES = 0, 1, 2, 3   # include/ggd.h GGD_ROUTE_*
-INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES = 0, 2              # include/ggd.h GGD_INFO_*
+ROUTE_GEMM_LAUNCHES = 5
+INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES, INFO_CHAIN_AVAILABLE = 0, 2, 5     # include/ggd.h GGD_INFO_*
 
 
 def rel_rms(a, b):
@@ -526,3 +527,37 @@ def test_clip_pair_batches_ddim_bf16(pkg, beat_cfg, setup, n):
         _route(ctx, 2)
     assert bool(th.isfinite(pair).all())
     assert rel_rms(pair, psk) <= 1e-2
+
+
+# ------------------------------------------------------------------------------------------
+# Row-block chains (ggd_chain.hip): the generic one-way route's GEMMs as 4 launches per layer.
+# Same MFMA chains, LayerNorm arithmetic and epilogues as one launch per GEMM -> equal bit for
+# bit; and the oracle bound of the dtype.  fp8 at L = 160 (C4) and at L = 40 with 3 clips
+# (120 rows: a ragged last row block); bf16 at L = 160 (the fused kernels stop at L = 64).
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype,Lc,wav_len,n", [("fp8", 160, 128000, 2), ("fp8", 40, WAV, 3),
+                                                ("bf16", 160, 128000, 2)])
+def test_chain_route_equals_gemm_launches(pkg, beat_cfg, setup, setup_fp8, dtype, Lc, wav_len, n):
+    _, sd, om = setup
+    model, diffusion = make_model(pkg, beat_cfg, sd, dtype)
+    wav, x, t = inputs(n, seed=71, wav_len=wav_len, L_=Lc)
+    ctx, _ = model.prepare(wav.cuda(), Lc)
+    assert _info(ctx, INFO_CHAIN_AVAILABLE) == 1.0
+    zs = th.randn(3, n, D_POSE, Lc, generator=th.Generator().manual_seed(72))
+
+    def run():
+        eps = model(x.cuda(), t.cuda(), wav=wav.cuda()).cpu()
+        out = diffusion.p_sample_loop(model, (n, D_POSE, Lc), {"wav": wav.cuda()}, noise=x.cuda(),
+                                      step_noise=zs.cuda(), n_steps=3)["sample"].cpu()
+        return eps, out
+
+    try:
+        chain = run()
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_GEMM_LAUNCHES, 1) == 0
+        gemm = run()
+    finally:
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_GEMM_LAUNCHES, 0)
+    assert th.equal(chain[0], gemm[0])
+    assert th.equal(chain[1], gemm[1])
+    ref = (setup_fp8 if dtype == "fp8" else om)(x, t, wav=wav)
+    assert rel_rms(chain[0], ref) <= 1e-2
