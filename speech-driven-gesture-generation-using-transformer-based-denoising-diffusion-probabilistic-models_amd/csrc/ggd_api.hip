@@ -1248,7 +1248,9 @@ int ggd_finalize_weights(ggd_ctx* c) {
     HIP_TRY(c, dalloc(c, &c->ffp, sizeof(float) * (size_t)D.max_batch * 8 * D.seq_len * D.d_model));
   }
   // row-block chains for the one-way generic route (ggd_chain.hip)
-  c->chain = !c->fused && D.dtype != GGD_F32 && d == 256 && c->out_lin.kpad == 256;
+  const int on = c->out_lin.npad;
+  c->chain = !c->fused && D.dtype != GGD_F32 && d == 256 && c->out_lin.kpad == 256 &&
+             chain_p_supported(on) && chain_p_supported(3 * d) && chain_p_supported(d);
   for (int l = 0; c->chain && l < D.n_layers; ++l) {
     const Layer& Ly = c->layers[l];
     c->chain = Ly.qkv.npad == 3 * d && Ly.o_sa.npad == d && Ly.q_ca.npad == d && Ly.o_ca.npad == d &&

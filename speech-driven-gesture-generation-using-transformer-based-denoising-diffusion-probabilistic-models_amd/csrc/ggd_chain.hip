@@ -13,8 +13,8 @@
 //
 // Weights are read as MFMA B fragments straight from a fragment-packed copy (chain_pack_kernel)
 // into registers -- one coalesced 1 KiB load per wave per (16 columns, 64 k), no LDS staging,
-// no barrier per tile -- double-buffered so the next tile group's loads fly under this group's
-// MFMAs.  fp8 weights (GGD_FP8W) are widened with v_cvt_scalef32_pk_bf16_fp8 (scale 1: exact).
+// no barrier per tile -- with two more tile groups' loads in flight under each group's MFMAs;
+// 8 waves (two per SIMD) so one wave's widening and waits overlap the other's MFMAs.  fp8 weights (GGD_FP8W) are widened with v_cvt_scalef32_pk_bf16_fp8 (scale 1: exact).
 //
 // Bit-exact with the per-GEMM route: every output element is the same MFMA chain
 // (v_mfma_f32_16x16x32_bf16, k steps of 32 in order, lane k offsets 8 (lane >> 4)), the
@@ -31,7 +31,18 @@ constexpr int CH_FF = 1024;         // feed-forward hidden width
 constexpr int HS_STR = CH_D + 16;   // f32 residual rows: the LN lanes (4 rows x 4) hit distinct banks
 constexpr int XS_STR = CH_D + 8;    // bf16 A rows (16-byte row pad, as gemm_kernel)
 constexpr int HH_STR = CH_FF + 8;   // bf16 hidden rows
-constexpr size_t CH_LDS = sizeof(float) * CH_MT * HS_STR + sizeof(bf16_t) * CH_MT * (XS_STR + HH_STR);
+constexpr int CH_PMAX = 1024;       // P stage: widest projection
+constexpr int CH_DEPTH = 3;         // weight tile groups in flight per wave
+constexpr int CH_WAVES = 8;         // two waves per SIMD: one's fp8 widening and loads overlap the other's MFMAs
+constexpr int CH_NT = 64 * CH_WAVES;
+// per-column epilogue parameters and LayerNorm vectors, staged once per workgroup (LDS reads do
+// not queue behind the weight prefetch the way global loads would: vmcnt retires in order)
+constexpr int PRM_R = 0, PRM_F1 = PRM_R + 2 * CH_D, PRM_F2 = PRM_F1 + 2 * CH_FF, PRM_P = PRM_F2 + 2 * CH_D,
+              PRM_LN = PRM_P + 2 * CH_PMAX, PRM_FLOATS = PRM_LN + 4 * CH_D;
+constexpr size_t CH_LDS = sizeof(float) * (CH_MT * HS_STR + PRM_FLOATS) + sizeof(bf16_t) * CH_MT * (XS_STR + HH_STR);
+
+// workgroup barrier for LDS hand-offs only: global loads stay in flight across it
+__device__ __forceinline__ void ch_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 
@@ -52,20 +63,27 @@ __device__ __forceinline__ bf16x8 fp8x8_bf16(unsigned w0, unsigned w1) {
 //   ((nt * units_per_tile + u) * 64 + lane) * 16 bytes, lane = (g << 4) | r16:
 //   bf16: 8 values W[nt 16 + r16][32 u + 8 g + e]
 //   fp8:  bytes 0-7 W[nt 16 + r16][64 u + 8 g + e], bytes 8-15 W[..][64 u + 32 + 8 g + e]
-template <bool W8, int TG>
-__device__ __forceinline__ void ch_load(BBuf<W8, TG>& B, const unsigned char* wf, int upt, int nt0, int c, int lane) {
+// Loads of one iteration: TG tiles x the chunk's U units.  wb: this wave's first tile of the
+// stage (wave-uniform, so the constant offsets fold into the scalar base).
+template <bool W8, int TGB>
+__device__ __forceinline__ void ch_load(BBuf<W8, TGB>& B, const unsigned char* wb, unsigned lane16, int t0, int c,
+                                        int upt, int tg) {
   constexpr int U = Units<W8>::U;
 #pragma unroll
-  for (int j = 0; j < TG; ++j)
+  for (int j = 0; j < TGB; ++j)
+    if (j < tg)
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      B.v[j][u] = *(const uint4*)(wf + ((size_t)((nt0 + j) * upt + c * U + u) * 64 + lane) * 16);
+      for (int u = 0; u < U; ++u)
+        B.v[j][u] = *(const uint4*)(wb + (size_t)(((t0 + j) * upt + c * U + u) * 1024) + lane16);
+  // keep the loads where they are issued: the scheduler would otherwise sink them next to
+  // their first use (lower register pressure) and the prefetch distance would collapse
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // acc[i][j] += A[16 i + .][256 c + .] . W[16 (nt0 + j) + .][256 c + .]^T over the chunk's 8 k steps
-template <bool W8, int TG>
-__device__ __forceinline__ void ch_mma(const BBuf<W8, TG>& B, const bf16_t* As, int sa, int c, int lane,
-                                       f32x4 (&acc)[2][TG]) {
+template <bool W8, int TGB>
+__device__ __forceinline__ void ch_mma(const BBuf<W8, TGB>& B, const bf16_t* As, int sa, int c, int lane,
+                                       f32x4 (&acc)[2][TGB], int tg) {
   const int r16 = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -73,7 +91,8 @@ __device__ __forceinline__ void ch_mma(const BBuf<W8, TG>& B, const bf16_t* As, 
     const bf16x8 a0 = *(const bf16x8*)(As + r16 * sa + k);
     const bf16x8 a1 = *(const bf16x8*)(As + (16 + r16) * sa + k);
 #pragma unroll
-    for (int j = 0; j < TG; ++j) {
+    for (int j = 0; j < TGB; ++j) {
+      if (j >= tg) continue;
       bf16x8 bw;
       if constexpr (W8) {
         const uint4 u = B.v[j][q >> 1];
@@ -87,49 +106,9 @@ __device__ __forceinline__ void ch_mma(const BBuf<W8, TG>& B, const bf16_t* As, 
   }
 }
 
-// One GEMM of the chain: out[32][npad] = As[32][kpad] . W^T.  Wave w owns tile groups
-// (gi * 4 + w) * TG .. + TG - 1 (gi < ng); iterations (group, 256-k chunk) are double-buffered.
-// epi(acc, nt0) runs after a group's last chunk.
-template <bool W8, int TG, class Epi>
-__device__ __forceinline__ void ch_gemm(const bf16_t* As, int sa, const ChainLin& L, int wave, int lane, Epi&& epi) {
-  const unsigned char* wf = (const unsigned char*)L.w;
-  const int nch = L.kpad / 256, upt = nch * Units<W8>::U;
-  const int ng = L.npad / (64 * TG), I = ng * nch;
-  auto nt_of = [&](int it) { return ((it / nch) * 4 + wave) * TG; };
-  BBuf<W8, TG> b0, b1;
-  f32x4 acc[2][TG];
-  auto step = [&](const BBuf<W8, TG>& B, int it) {
-    const int c = it % nch;
-    if (c == 0) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < TG; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    ch_mma<W8, TG>(B, As, sa, c, lane, acc);
-    if (c == nch - 1) epi(acc, nt_of(it));
-  };
-  // loads are unconditional (clamped to the last iteration) so the wait counts stay static
-  ch_load<W8, TG>(b0, wf, upt, nt_of(0), 0, lane);
-  for (int it = 0; it < I; it += 2) {
-    const int i1 = min(it + 1, I - 1), i2 = min(it + 2, I - 1);
-    ch_load<W8, TG>(b1, wf, upt, nt_of(i1), i1 % nch, lane);
-    step(b0, it);
-    ch_load<W8, TG>(b0, wf, upt, nt_of(i2), i2 % nch, lane);
-    if (it + 1 < I) step(b1, it + 1);
-  }
-}
-
-template <bool W8, class Epi>
-__device__ __forceinline__ void ch_gemm_any(const bf16_t* As, int sa, const ChainLin& L, int wave, int lane, Epi&& epi) {
-  constexpr int TGMAX = W8 ? 4 : 2;  // 64 B-operand VGPRs per buffer
-  if (L.npad % (64 * TGMAX) == 0) ch_gemm<W8, TGMAX>(As, sa, L, wave, lane, epi);
-  else if (L.npad % 128 == 0) ch_gemm<W8, 2>(As, sa, L, wave, lane, epi);
-  else ch_gemm<W8, 1>(As, sa, L, wave, lane, epi);
-}
-
 // LayerNorm of the 32 LDS residual rows -> bf16 A rows, in gemm_kernel's PRO_LN arithmetic:
 // 4 lanes per row, lane j holds float4 columns (j + 4 i) 4, two-pass statistics, xor 1 / 2.
+// gm, bt: LDS copies of gamma / beta.
 __device__ __forceinline__ void ch_layernorm(const float* hs, const float* gm, const float* bt, bf16_t* xs) {
   const int tid = threadIdx.x;
   if (tid >= CH_MT * 4) return;  // waves 0, 1 (whole waves: the shuffles stay uniform)
@@ -166,130 +145,226 @@ __device__ __forceinline__ void ch_layernorm(const float* hs, const float* gm, c
   }
 }
 
-// acc + bias (and the fp8 per-channel scale) of element (i, j, r): gemm_kernel's expression
+// acc + bias (and the fp8 per-channel scale) of column n: gemm_kernel's expression; prm = the
+// stage's LDS parameters [bias[npad] | scale[npad]]
 template <bool W8>
-__device__ __forceinline__ float ch_val(const ChainLin& L, float acc, int n) {
-  const float bn = L.b[n];
-  const float sn = W8 ? L.scale[n] : 1.0f;
+__device__ __forceinline__ float ch_val(const float* prm, int npad, float acc, int n) {
+  const float bn = prm[n];
+  const float sn = W8 ? prm[npad + n] : 1.0f;
   return W8 ? acc * sn + bn : acc + bn;
 }
 
-template <bool W8>
-__global__ void __launch_bounds__(NTHREADS) chain_kernel(ChainArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* hs = (float*)smem;
-  bf16_t* xs = (bf16_t*)(smem + sizeof(float) * CH_MT * HS_STR);
-  bf16_t* hh = xs + CH_MT * XS_STR;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int m0 = blockIdx.x * CH_MT, rows = min(CH_MT, a.M - m0);
-  const int g4 = 4 * (lane >> 4), c16 = lane & 15;
-  const bool upd = a.r.w || a.f1.w;  // the residual rows change: written back at the end
+// The chain's iterations, fixed at compile time: stage, index within the stage, tile-group width,
+// groups per wave and 256-k chunks.  R 256 columns, F1 1024, F2 256 (K 1024), P PN columns.
+enum { ST_R = 0, ST_F1 = 1, ST_F2 = 2, ST_P = 3 };
+struct ChIt { int stage, l, tg, nch; };
 
-  // stage the residual rows (rows past M read as zero) and the R operand
-#pragma unroll
-  for (int i = 0; i < CH_MT * CH_D / 4 / NTHREADS; ++i) {
-    const int e = tid + i * NTHREADS, r = e / (CH_D / 4), c4 = e % (CH_D / 4);
-    const float4 v = r < rows ? *(const float4*)(a.h + (size_t)(m0 + r) * CH_D + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    *(float4*)(hs + r * HS_STR + 4 * c4) = v;
+template <bool W8, bool HR, bool HF, int PN>
+struct ChPlan {
+  static constexpr int TGB = W8 ? 2 : 1;               // 8 16-byte units per wave per iteration
+  static constexpr int TGP = PN == 128 ? 1 : TGB;      // 128 columns: one tile per wave
+  static constexpr int IR = HR ? 2 / TGB : 0;
+  static constexpr int IF1 = HF ? 8 / TGB : 0;
+  static constexpr int IF2 = HF ? 4 * (2 / TGB) : 0;
+  static constexpr int IP = PN ? PN / (128 * TGP) : 0;
+  static constexpr int TOTAL = IR + IF1 + IF2 + IP;
+  static __host__ __device__ constexpr ChIt at(int it) {
+    return it < IR ? ChIt{ST_R, it, TGB, 1}
+         : it < IR + IF1 ? ChIt{ST_F1, it - IR, TGB, 1}
+         : it < IR + IF1 + IF2 ? ChIt{ST_F2, it - IR - IF1, TGB, 4}
+         : ChIt{ST_P, it - IR - IF1 - IF2, TGP, 1};
   }
-  if (a.r.w) {
+};
+
+// PRM offsets of the per-column parameters of a stage, and its width
+__host__ __device__ constexpr int prm_of(int stage) {
+  return stage == ST_R ? PRM_R : stage == ST_F1 ? PRM_F1 : stage == ST_F2 ? PRM_F2 : PRM_P;
+}
+
+// Everything one workgroup's iterations share (registers and LDS pointers).
+template <bool W8, int TGB>
+struct ChCtx {
+  const ChainArgs& a;
+  float* hs;
+  bf16_t* xs;
+  bf16_t* hh;
+  float* prm;
+  int wave, lane, rows, m0, g4, c16;
+  unsigned lane16;
+  BBuf<W8, TGB> b[CH_DEPTH];
+  f32x4 acc[2][TGB];
+};
+
+template <bool W8, bool HR, bool HF, int PN, class X>
+__device__ __forceinline__ void ch_writeback(X& x) {  // residual rows back to HBM
+  const int tid = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < CH_MT * CH_D / 8 / NTHREADS; ++i) {
-      const int e = tid + i * NTHREADS, r = e / (CH_D / 8), cv = e % (CH_D / 8);
-      const uint4 v = r < rows ? *(const uint4*)(a.a_in + (size_t)(m0 + r) * CH_D + 8 * cv) : make_uint4(0, 0, 0, 0);
-      *(uint4*)(xs + r * XS_STR + 8 * cv) = v;
+  for (int i = 0; i < CH_MT * CH_D / 4 / CH_NT; ++i) {
+    const int e = tid + i * CH_NT, r = e / (CH_D / 4), c4 = e % (CH_D / 4);
+    if (r < x.rows)
+      *(float4*)(x.a.h + (size_t)(x.m0 + r) * CH_D + 4 * c4) = *(const float4*)(x.hs + r * HS_STR + 4 * c4);
+  }
+}
+
+// weight loads of iteration IT into buffer IT % CH_DEPTH
+template <bool W8, bool HR, bool HF, int PN, int IT, class X>
+__device__ __forceinline__ void ch_issue(X& x) {
+  using P = ChPlan<W8, HR, HF, PN>;
+  constexpr ChIt d = P::at(IT);
+  constexpr int upt = d.nch * Units<W8>::U;
+  const void* w = d.stage == ST_R ? x.a.r.w : d.stage == ST_F1 ? x.a.f1.w : d.stage == ST_F2 ? x.a.f2.w : x.a.p.w;
+  const unsigned char* wb = (const unsigned char*)w + (size_t)x.wave * d.tg * upt * 1024;
+  ch_load<W8, P::TGB>(x.b[IT % CH_DEPTH], wb, x.lane16, (d.l / d.nch) * CH_WAVES * d.tg, d.l % d.nch, upt, d.tg);
+}
+
+// iteration IT: prefetch IT + CH_DEPTH - 1, the stage hand-off if IT opens a stage, the MFMAs,
+// the epilogue if IT closes a tile group; then iteration IT + 1
+template <bool W8, bool HR, bool HF, int PN, int IT, class X>
+__device__ __forceinline__ void ch_iter(X& x) {
+  using P = ChPlan<W8, HR, HF, PN>;
+  constexpr int TGB = P::TGB, D1 = CH_DEPTH - 1;
+  constexpr ChIt d = P::at(IT);
+  if constexpr (IT + D1 < P::TOTAL) ch_issue<W8, HR, HF, PN, IT + D1>(x);
+  if constexpr (d.l == 0 && d.stage == ST_F1) {   // LDS hand-offs; prefetched weights stay in flight
+    if constexpr (HR) ch_bar();
+    ch_layernorm(x.hs, x.prm + PRM_LN, x.prm + PRM_LN + CH_D, x.xs);
+    ch_bar();
+  } else if constexpr (d.l == 0 && d.stage == ST_F2) {
+    ch_bar();
+  } else if constexpr (d.l == 0 && d.stage == ST_P) {
+    if constexpr (HR || HF) {
+      ch_bar();
+      ch_writeback<W8, HR, HF, PN>(x);
     }
+    ch_layernorm(x.hs, x.prm + PRM_LN + 2 * CH_D, x.prm + PRM_LN + 3 * CH_D, x.xs);
+    ch_bar();
   }
-  __syncthreads();
-
-  // R: h += A W_r^T + b_r  (EPI_RESID)
-  if (a.r.w) {
-    ch_gemm_any<W8>(xs, XS_STR, a.r, wave, lane, [&](auto& acc, int nt0) {
-      constexpr int TG = sizeof(acc[0]) / sizeof(acc[0][0]);
+  constexpr int c = d.l % d.nch;
+  const int nt0 = ((d.l / d.nch) * CH_WAVES + x.wave) * d.tg;
+  if constexpr (c == 0) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < TG; ++j) {
-          const int n = (nt0 + j) * 16 + c16;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float* p = hs + (i * 16 + g4 + r) * HS_STR + n;
-            *p = *p + ch_val<W8>(a.r, acc[i][j][r], n);
-          }
-        }
-    });
-    __syncthreads();
+      for (int j = 0; j < TGB; ++j) x.acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-
-  // F: h += relu2(LN_f(h) W_1^T + b_1) W_2^T + b_2
-  if (a.f1.w) {
-    ch_layernorm(hs, a.f_g, a.f_b, xs);
-    __syncthreads();
-    ch_gemm_any<W8>(xs, XS_STR, a.f1, wave, lane, [&](auto& acc, int nt0) {
-      constexpr int TG = sizeof(acc[0]) / sizeof(acc[0][0]);
+  if constexpr (d.stage == ST_F2)
+    ch_mma<W8, TGB>(x.b[IT % CH_DEPTH], x.hh, HH_STR, c, x.lane, x.acc, d.tg);
+  else
+    ch_mma<W8, TGB>(x.b[IT % CH_DEPTH], x.xs, XS_STR, c, x.lane, x.acc, d.tg);
+  if constexpr (c == d.nch - 1) {
+    // epilogues (C/D map of the 16x16 MFMA: column lane & 15, row 4 (lane >> 4) + r)
+    constexpr int np = d.stage == ST_F1 ? CH_FF : d.stage == ST_P ? PN : CH_D;
+    const float* pp = x.prm + prm_of(d.stage);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < TG; ++j) {
-          const int n = (nt0 + j) * 16 + c16;
+      for (int j = 0; j < d.tg; ++j) {
+        const int n = (nt0 + j) * 16 + x.c16;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float v = fmaxf(ch_val<W8>(a.f1, acc[i][j][r], n), 0.f);
-            hh[(i * 16 + g4 + r) * HH_STR + n] = f2bf(v * v);
-          }
-        }
-    });
-    __syncthreads();
-    ch_gemm_any<W8>(hh, HH_STR, a.f2, wave, lane, [&](auto& acc, int nt0) {
-      constexpr int TG = sizeof(acc[0]) / sizeof(acc[0][0]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < TG; ++j) {
-          const int n = (nt0 + j) * 16 + c16;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float* p = hs + (i * 16 + g4 + r) * HS_STR + n;
-            *p = *p + ch_val<W8>(a.f2, acc[i][j][r], n);
-          }
-        }
-    });
-    __syncthreads();
-  }
-
-  // residual rows back to HBM (the P stage below only reads them)
-  if (upd) {
-#pragma unroll
-    for (int i = 0; i < CH_MT * CH_D / 4 / NTHREADS; ++i) {
-      const int e = tid + i * NTHREADS, r = e / (CH_D / 4), c4 = e % (CH_D / 4);
-      if (r < rows) *(float4*)(a.h + (size_t)(m0 + r) * CH_D + 4 * c4) = *(const float4*)(hs + r * HS_STR + 4 * c4);
-    }
-  }
-
-  // P: out = LN_p(h) W_p^T + b_p  (EPI_T bf16, or EPI_F32 for out_layers)
-  if (a.p.w) {
-    ch_layernorm(hs, a.p_g, a.p_b, xs);
-    __syncthreads();
-    ch_gemm_any<W8>(xs, XS_STR, a.p, wave, lane, [&](auto& acc, int nt0) {
-      constexpr int TG = sizeof(acc[0]) / sizeof(acc[0][0]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < TG; ++j) {
-          const int n = (nt0 + j) * 16 + c16;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = i * 16 + g4 + r;
-            if (row >= rows) continue;
-            const float v = ch_val<W8>(a.p, acc[i][j][r], n);
-            if (a.out_f32) {
-              if (n < a.n_valid) ((float*)a.out)[(size_t)(m0 + row) * a.ldo + n] = v;
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + x.g4 + r;
+          const float v = ch_val<W8>(pp, np, x.acc[i][j][r], n);
+          if constexpr (d.stage == ST_R || d.stage == ST_F2) {   // EPI_RESID
+            float* p = x.hs + row * HS_STR + n;
+            *p = *p + v;
+          } else if constexpr (d.stage == ST_F1) {               // EPI_RELU2
+            const float y = fmaxf(v, 0.f);
+            x.hh[row * HH_STR + n] = f2bf(y * y);
+          } else if (row < x.rows) {                             // EPI_T / EPI_F32
+            if (x.a.out_f32) {
+              if (n < x.a.n_valid) ((float*)x.a.out)[(size_t)(x.m0 + row) * x.a.ldo + n] = v;
             } else {
-              ((bf16_t*)a.out)[(size_t)(m0 + row) * a.ldo + n] = f2bf(v);
+              ((bf16_t*)x.a.out)[(size_t)(x.m0 + row) * x.a.ldo + n] = f2bf(v);
             }
           }
         }
-    });
+      }
+  }
+  if constexpr (IT + 1 < P::TOTAL) ch_iter<W8, HR, HF, PN, IT + 1>(x);
+}
+
+template <bool W8, bool HR, bool HF, int PN>
+__global__ void __launch_bounds__(CH_NT) chain_kernel(ChainArgs a) {
+  using P = ChPlan<W8, HR, HF, PN>;
+  constexpr int D1 = CH_DEPTH - 1;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  ChCtx<W8, P::TGB> x{a};
+  x.hs = (float*)smem;
+  x.xs = (bf16_t*)(smem + sizeof(float) * CH_MT * HS_STR);
+  x.hh = x.xs + CH_MT * XS_STR;
+  x.prm = (float*)(x.hh + CH_MT * HH_STR);
+  x.wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  x.lane = lane;
+  x.m0 = blockIdx.x * CH_MT;
+  x.rows = min(CH_MT, a.M - x.m0);
+  x.g4 = 4 * (lane >> 4);
+  x.c16 = lane & 15;
+  x.lane16 = (unsigned)lane * 16u;
+  const int rows = x.rows, m0 = x.m0;
+
+  // the first iterations' weights fly while the rows and parameters are staged
+  ch_issue<W8, HR, HF, PN, 0>(x);
+  if constexpr (D1 > 1 && P::TOTAL > 1) ch_issue<W8, HR, HF, PN, 1>(x);
+  static_assert(CH_DEPTH == 3, "prologue issues CH_DEPTH - 1 iterations");
+
+  {  // staging: every global load issued before the first LDS write (one round trip)
+    constexpr int NSEG = 12;
+    const float* src[NSEG] = {a.r.b, a.r.scale, a.f1.b, a.f1.scale, a.f2.b, a.f2.scale, a.p.b, a.p.scale,
+                              a.f_g, a.f_b, a.p_g, a.p_b};
+    constexpr int dst[NSEG] = {PRM_R, PRM_R + CH_D, PRM_F1, PRM_F1 + CH_FF, PRM_F2, PRM_F2 + CH_D, PRM_P, PRM_P + PN,
+                               PRM_LN, PRM_LN + CH_D, PRM_LN + 2 * CH_D, PRM_LN + 3 * CH_D};
+    constexpr int len[NSEG] = {CH_D, CH_D, CH_FF, CH_FF, CH_D, CH_D, PN, PN, CH_D, CH_D, CH_D, CH_D};
+    constexpr bool on[NSEG] = {HR, HR, HF, HF, HF, HF, PN > 0, PN > 0, HF, HF, PN > 0, PN > 0};
+    constexpr bool scale[NSEG] = {false, true, false, true, false, true, false, true, false, false, false, false};
+    float v[NSEG][2];
+#pragma unroll
+    for (int sgi = 0; sgi < NSEG; ++sgi)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int e = tid + k * CH_NT;
+        v[sgi][k] = 1.0f;
+        if (on[sgi] && e < len[sgi] && (W8 || !scale[sgi])) v[sgi][k] = src[sgi][e];
+      }
+    float4 hv[CH_MT * CH_D / 4 / CH_NT];
+#pragma unroll
+    for (int i = 0; i < CH_MT * CH_D / 4 / CH_NT; ++i) {
+      const int e = tid + i * CH_NT, r = e / (CH_D / 4), c4 = e % (CH_D / 4);
+      hv[i] = r < rows ? *(const float4*)(a.h + (size_t)(m0 + r) * CH_D + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    uint4 av[CH_MT * CH_D / 8 / CH_NT];
+    if constexpr (HR) {
+#pragma unroll
+      for (int i = 0; i < CH_MT * CH_D / 8 / CH_NT; ++i) {
+        const int e = tid + i * CH_NT, r = e / (CH_D / 8), cv = e % (CH_D / 8);
+        av[i] = r < rows ? *(const uint4*)(a.a_in + (size_t)(m0 + r) * CH_D + 8 * cv) : make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int sgi = 0; sgi < NSEG; ++sgi)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int e = tid + k * CH_NT;
+        if (on[sgi] && e < len[sgi]) x.prm[dst[sgi] + e] = v[sgi][k];
+      }
+#pragma unroll
+    for (int i = 0; i < CH_MT * CH_D / 4 / CH_NT; ++i) {
+      const int e = tid + i * CH_NT, r = e / (CH_D / 4), c4 = e % (CH_D / 4);
+      *(float4*)(x.hs + r * HS_STR + 4 * c4) = hv[i];
+    }
+    if constexpr (HR) {
+#pragma unroll
+      for (int i = 0; i < CH_MT * CH_D / 8 / CH_NT; ++i) {
+        const int e = tid + i * CH_NT, r = e / (CH_D / 8), cv = e % (CH_D / 8);
+        *(uint4*)(x.xs + r * XS_STR + 8 * cv) = av[i];
+      }
+    }
+  }
+  ch_bar();
+  ch_iter<W8, HR, HF, PN, 0>(x);
+  if constexpr (!PN) {
+    ch_bar();
+    ch_writeback<W8, HR, HF, PN>(x);
   }
 }
 
@@ -335,27 +410,58 @@ hipError_t launch_chain_pack(int w8, const void* src, void* dst, int npad, int k
   return hipGetLastError();
 }
 
+namespace {
+
+template <bool W8, bool HR, bool HF, int PN>
+hipError_t chain_go(const ChainArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)chain_kernel<W8, HR, HF, PN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)CH_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((chain_kernel<W8, HR, HF, PN>), dim3((a.M + CH_MT - 1) / CH_MT), dim3(CH_NT), CH_LDS, s, a);
+  return hipGetLastError();
+}
+
+template <bool W8, bool HR, bool HF>
+hipError_t chain_pn(const ChainArgs& a, hipStream_t s) {
+  switch (a.p.w ? a.p.npad : 0) {
+    case 0:
+      if constexpr (HR) return chain_go<W8, HR, HF, 0>(a, s);
+      break;
+    case 128: return chain_go<W8, HR, HF, 128>(a, s);
+    case 256: return chain_go<W8, HR, HF, 256>(a, s);
+    case 768: return chain_go<W8, HR, HF, 768>(a, s);
+    default: break;
+  }
+  return hipErrorInvalidValue;
+}
+
+template <bool W8>
+hipError_t chain_stages(const ChainArgs& a, hipStream_t s) {
+  if (a.r.w && a.f1.w) return chain_pn<W8, true, true>(a, s);
+  if (a.r.w) return chain_pn<W8, true, false>(a, s);
+  if (a.f1.w) return hipErrorInvalidValue;  // F without R: not a decoder-layer shape
+  return chain_pn<W8, false, false>(a, s);
+}
+
+}  // namespace
+
+bool chain_p_supported(int npad) { return npad == 128 || npad == 256 || npad == 768; }
+
 hipError_t launch_chain(int w8, const ChainArgs& a, hipStream_t s) {
-  // shapes the kernel assumes: d_model 256, FFN hidden 1024, P columns a multiple of 64
+  // shapes the kernel assumes: d_model 256, FFN hidden 1024, P 128 / 256 / 768 columns
   if (a.M <= 0 || !a.h) return hipErrorInvalidValue;
   if (a.r.w && (!a.a_in || !lin_ok(a.r, CH_D, CH_D))) return hipErrorInvalidValue;
   if (a.f1.w && (!a.f_g || !a.f_b || !lin_ok(a.f1, CH_FF, CH_D) || !lin_ok(a.f2, CH_D, CH_FF)))
     return hipErrorInvalidValue;
-  if (a.p.w && (!a.p_g || !a.p_b || !a.out || a.p.kpad != CH_D || a.p.npad <= 0 || a.p.npad % 64 ||
-                a.ldo < a.p.npad))
+  if (a.p.w && (!a.p_g || !a.p_b || !a.p.b || !a.out || a.p.kpad != CH_D || a.ldo < a.p.npad ||
+                !chain_p_supported(a.p.npad)))
     return hipErrorInvalidValue;
   if (w8 && ((a.r.w && !a.r.scale) || (a.f1.w && (!a.f1.scale || !a.f2.scale)) || (a.p.w && !a.p.scale)))
     return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)chain_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CH_LDS);
-    (void)hipFuncSetAttribute((const void*)chain_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CH_LDS);
-    attr = true;
-  }
-  const dim3 grid((a.M + CH_MT - 1) / CH_MT);
-  if (w8) hipLaunchKernelGGL(chain_kernel<true>, grid, dim3(NTHREADS), CH_LDS, s, a);
-  else hipLaunchKernelGGL(chain_kernel<false>, grid, dim3(NTHREADS), CH_LDS, s, a);
-  return hipGetLastError();
+  return w8 ? chain_stages<true>(a, s) : chain_stages<false>(a, s);
 }
 
 }  // namespace ggd

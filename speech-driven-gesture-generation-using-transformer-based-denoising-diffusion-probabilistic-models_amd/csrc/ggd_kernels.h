@@ -234,6 +234,7 @@ struct ChainArgs {
 hipError_t launch_chain(int w8, const ChainArgs& a, hipStream_t s);
 hipError_t launch_chain_pack(int w8, const void* src, void* dst, int npad, int kpad, hipStream_t s);
 size_t chain_pack_bytes(int w8, int npad, int kpad);
+bool chain_p_supported(int npad);   // P stage widths with a kernel instance
 hipError_t launch_fused(int which, int dtype, const FusedArgs& a, int n, hipStream_t s);  // 0 KA, 1 KB, 2 KC, 3 KD
 hipError_t launch_final(int dtype, const FinalArgs& a, hipStream_t s);
 // step-invariant convolved cross-attention K | V^T images of one layer (ggd_set_memory; fused paths)
