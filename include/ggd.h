@@ -182,8 +182,10 @@ enum {
   GGD_ROUTE_PAIR_WRITE_THROUGH = 2,  /* 1: clip-pair hand-offs written through on any placement */
   GGD_ROUTE_PHASE_LAUNCHES = 3,      /* 1: per-phase launches instead of the clip-group loop (ggd_mega.hip) */
   GGD_ROUTE_PLACEMENT = 4,           /* clip-group loop: 0 XCD-local, 1 part p on XCD p, 2 group per XCD */
-  GGD_ROUTE_GEMM_LAUNCHES = 5        /* generic one-way route: 1 = one launch per GEMM instead of the
+  GGD_ROUTE_GEMM_LAUNCHES = 5,       /* generic one-way route: 1 = one launch per GEMM instead of the
                                         row-block chains (ggd_chain.hip) */
+  GGD_ROUTE_ATTN_QSPLIT = 6          /* 1: clips of >= 96 frames on the query-split attention kernel
+                                        instead of the whole-clip kernel (ggd_attn.hip) */
 };
 int ggd_set_route(ggd_ctx* ctx, int32_t knob, int32_t value);
 enum {

@@ -108,6 +108,7 @@ struct ggd_ctx {
   // row-block chains (ggd_chain.hip): the one-way generic route's GEMMs, 4 launches per layer
   bool chain = false;        // fragment-packed weights built (one-way, not fused, bf16 / fp8, d 256, FFN 1024)
   int gemm_launches = 0;     // GGD_ROUTE_GEMM_LAUNCHES: 1 = one launch per GEMM instead
+  int attn_qsplit = 0;       // GGD_ROUTE_ATTN_QSPLIT: 1 = long clips on the query-split attention
 
   // two-way decoder (generic kernels, joint layout [n][J = L + 1 + Ts][d])
   bool twoway = false;
@@ -626,6 +627,8 @@ int launch_decoder_twoway(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     GEMM(c, PRO_T, EPI_T, q, s);
     AttnArgs at{};
     at.zero = c->zero_row;
+    at.no_clip = c->attn_qsplit;
+  at.no_clip = c->attn_qsplit;
     at.cross = 0;
     at.q = c->qkvj;
     at.ldq = 3 * d;
@@ -696,6 +699,7 @@ AttnArgs self_attn_args(ggd_ctx* c, const Layer& Ly) {
   const int d = D.d_model, dk = d / D.heads;
   AttnArgs at{};
   at.zero = c->zero_row;
+  at.no_clip = c->attn_qsplit;
   at.cross = 0;
   at.q = c->qkv;
   at.ldq = 3 * d;
@@ -836,6 +840,8 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
 
     AttnArgs at{};
     at.zero = c->zero_row;
+    at.no_clip = c->attn_qsplit;
+  at.no_clip = c->attn_qsplit;
     at.cross = 0;
     at.q = c->qkv;
     at.ldq = 3 * d;
@@ -1503,6 +1509,9 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
     case GGD_ROUTE_GEMM_LAUNCHES:   // 1: one launch per GEMM instead of the row-block chains
       c->gemm_launches = value != 0;
       return GGD_OK;
+    case GGD_ROUTE_ATTN_QSPLIT:     // 1: long clips on the query-split attention kernel
+      c->attn_qsplit = value != 0;
+      return GGD_OK;
     default:
       break;
   }
@@ -1645,6 +1654,8 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     if (n > D.max_batch) rc = fail(c, GGD_ERR_ARG, "n > max_batch");
     AttnArgs at{};
     at.zero = c->zero_row;
+    at.no_clip = c->attn_qsplit;
+  at.no_clip = c->attn_qsplit;
     const Layer& Ly = c->layers[0];
     at.cross = p[0];
     at.q = c->qkv; at.ldq = 3 * d;
@@ -2032,7 +2043,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   char keybuf[512];
   std::snprintf(keybuf, sizeof keybuf, "%d|%d|%p|%p|%p|%p|%d|%d", a->alg, a->n, (const void*)a->noise,
                 (const void*)a->inpaint_poses, (const void*)a->inpaint_masks, (const void*)a->trans,
-                (int)c->profiling, c->gemm_launches);
+                (int)c->profiling, c->gemm_launches * 2 + c->attn_qsplit);
   const std::string key(keybuf);
   // fused path profiling: KB stamps its own launch span per (step, layer) on the device clock,
   // so the graph replays unchanged; the generic path brackets its launches with events (eager)

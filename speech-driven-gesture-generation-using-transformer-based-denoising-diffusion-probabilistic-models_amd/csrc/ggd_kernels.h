@@ -90,6 +90,7 @@ struct AttnArgs {
   int seq_stride, seq_off;  // self mode: clip b's rows start at b * seq_stride + seq_off (0: b * Lq)
   int no_qsplit;            // diagnostics: 1 = one workgroup per (head, clip) (attn_kernel)
   const float* zero;        // >= 256 zero bytes in global memory (the conv's padding rows)
+  int no_clip;              // 1: long clips on the query-split kernel instead of attn_clip_kernel
 };
 
 // Fused diffusion update on the internal layout (one denoise step's epilogue).
@@ -253,6 +254,9 @@ int mega_capacity(int dtype, int L);   // clips one launch can hold (all workgro
 hipError_t launch_mb(int mode, void* buf, size_t buf_bytes, int arg, int blocks, hipStream_t s);  // ggd_diag.hip
 hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s);
+// whole-clip attention (ggd_attn.hip): bf16, d_k 32, 96 <= Lq <= 192, self (no row map) or memory
+bool attention_clip_supported(int dtype, const AttnArgs& a);
+hipError_t launch_attention_clip(const AttnArgs& a, int n, hipStream_t s);
 hipError_t launch_update(const UpdArgs& a, hipStream_t s);
 hipError_t launch_inpaint_input(float* out, const float* pose, const float* mask, int M, int C, hipStream_t s);
 hipError_t launch_posterior(const PostArgs& a, hipStream_t s);

@@ -740,6 +740,7 @@ size_t attention_lds_bytes(int dtype, const AttnArgs& a) {
 
 hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s) {
   if (a.Lq > ATT_LMAX || a.Lk > ATT_LMAX || (a.dk != 32 && a.dk != 64)) return hipErrorInvalidValue;
+  if (attention_clip_supported(dtype, a)) return launch_attention_clip(a, n, s);  // long clips, bf16
   if (a.seq_stride && (a.cross || a.Lq != a.Lk)) return hipErrorInvalidValue;
   const size_t lds = attention_lds_bytes(dtype, a);
   static bool attr_set = false;

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 D_POSE, L, WAV = 123, 40, 32000
 ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_PAIR_WT, ROUTE_PHASE_LAUNCHES = 0, 1, 2, 3   # include/ggd.h GGD_ROUTE_*
-ROUTE_GEMM_LAUNCHES = 5
+ROUTE_GEMM_LAUNCHES, ROUTE_ATTN_QSPLIT = 5, 6
 INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES, INFO_CHAIN_AVAILABLE = 0, 2, 5     # include/ggd.h GGD_INFO_*
 
 
@@ -561,3 +561,26 @@ def test_chain_route_equals_gemm_launches(pkg, beat_cfg, setup, setup_fp8, dtype
     assert th.equal(chain[1], gemm[1])
     ref = (setup_fp8 if dtype == "fp8" else om)(x, t, wav=wav)
     assert rel_rms(chain[0], ref) <= 1e-2
+
+
+# ------------------------------------------------------------------------------------------
+# Whole-clip attention (ggd_attn.hip, clips of >= 96 frames, bf16 activations): one workgroup per
+# (head, clip), softmax on exp2.  Against the query-split kernel (libm expf) and the oracle; L = 100
+# leaves a partial last query tile and pads keys 100 -> 128 (self) and 79 -> 96 (memory).
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype,Lc,wav_len,n", [("fp8", 160, 128000, 2), ("bf16", 100, 80000, 3)])
+def test_clip_attention_matches_query_split(pkg, beat_cfg, setup, setup_fp8, dtype, Lc, wav_len, n):
+    _, sd, om = setup
+    model, _ = make_model(pkg, beat_cfg, sd, dtype)
+    wav, x, t = inputs(n, seed=81, wav_len=wav_len, L_=Lc)
+    ctx, _ = model.prepare(wav.cuda(), Lc)
+    try:
+        clip = model(x.cuda(), t.cuda(), wav=wav.cuda()).cpu()
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_ATTN_QSPLIT, 1) == 0
+        qsplit = model(x.cuda(), t.cuda(), wav=wav.cuda()).cpu()
+    finally:
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_ATTN_QSPLIT, 0)
+    assert not th.equal(clip, qsplit)          # the routes differ (exp2 vs expf): both really ran
+    assert rel_rms(clip, qsplit) <= 2e-3
+    ref = (setup_fp8 if dtype == "fp8" else om)(x, t, wav=wav)
+    assert rel_rms(clip, ref) <= 1e-2
