@@ -184,8 +184,10 @@ enum {
   GGD_ROUTE_PLACEMENT = 4,           /* clip-group loop: 0 XCD-local, 1 part p on XCD p, 2 group per XCD */
   GGD_ROUTE_GEMM_LAUNCHES = 5,       /* generic one-way route: 1 = one launch per GEMM instead of the
                                         row-block chains (ggd_chain.hip) */
-  GGD_ROUTE_ATTN_QSPLIT = 6          /* 1: clips of >= 96 frames on the query-split attention kernel
+  GGD_ROUTE_ATTN_QSPLIT = 6,         /* 1: clips of >= 96 frames on the query-split attention kernel
                                         instead of the whole-clip kernel (ggd_attn.hip) */
+  GGD_ROUTE_LONG_LOOP = 7            /* 1: never the long-clip persistent loop (ggd_long.hip): every
+                                        step on launches (chains + whole-clip attention) */
 };
 int ggd_set_route(ggd_ctx* ctx, int32_t knob, int32_t value);
 enum {
@@ -194,7 +196,8 @@ enum {
   GGD_INFO_PAIR_LAUNCHES = 2,        /* last ggd_sample: clip-pair launches (0: another route) */
   GGD_INFO_XL_LAUNCHES = 3,          /* last ggd_sample: XCD-local clip-group launches */
   GGD_INFO_WT_RERUNS = 4,            /* last ggd_sample: clip-group launches re-run write-through */
-  GGD_INFO_CHAIN_AVAILABLE = 5       /* 1 when the generic one-way route runs as row-block chains */
+  GGD_INFO_CHAIN_AVAILABLE = 5,      /* 1 when the generic one-way route runs as row-block chains */
+  GGD_INFO_LONG_LAUNCHES = 6         /* last ggd_sample: long-clip loop launches (0: another route) */
 };
 int ggd_route_info(ggd_ctx* ctx, int32_t what, double* out);
 

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-chain}
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread \
-  -k "chain or fp8 or long_clip or clip_attention" > gpurun_out/${TAG}_pytest.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest.log; exit 1; }
+  -k "chain or fp8 or long_clip or clip_attention or long_loop" > gpurun_out/${TAG}_pytest.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest.log; exit 1; }
 grep -E "passed|failed" gpurun_out/${TAG}_pytest.log
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- \
   python3 scripts/chain_probe.py ${PROBE_ARGS} > gpurun_out/${TAG}_probe.log 2>&1 || { tail -20 gpurun_out/${TAG}_probe.log; exit 1; }

@@ -109,6 +109,14 @@ struct ggd_ctx {
   bool chain = false;        // fragment-packed weights built (one-way, not fused, bf16 / fp8, d 256, FFN 1024)
   int gemm_launches = 0;     // GGD_ROUTE_GEMM_LAUNCHES: 1 = one launch per GEMM instead
   int attn_qsplit = 0;       // GGD_ROUTE_ATTN_QSPLIT: 1 = long clips on the query-split attention
+  // long-clip persistent loop (ggd_long.hip): every step of clips of >= 96 frames in one launch
+  bool long_ok = false;      // the shape and dtype have a long-loop instance (needs the chain weights)
+  int long_off = 0;          // GGD_ROUTE_LONG_LOOP: 1 = never
+  LongLayer* long_layers = nullptr;
+  ChainStage* long_stages = nullptr;
+  unsigned* long_ctl = nullptr;
+  int* long_status = nullptr;
+  int long_launches = 0, long_fallbacks = 0;  // last ggd_sample
 
   // two-way decoder (generic kernels, joint layout [n][J = L + 1 + Ts][d])
   bool twoway = false;
@@ -1272,6 +1280,9 @@ int ggd_finalize_weights(ggd_ctx* c) {
     for (Layer& Ly : c->layers)
       for (Lin* L : {&Ly.qkv, &Ly.o_sa, &Ly.q_ca, &Ly.o_ca, &Ly.ff1, &Ly.ff2}) TRY(pack(*L));
     TRY(pack(c->out_lin));
+    c->long_ok = D.model_type != GGD_MODEL_INPAINT && c->emb_x.npad == d && c->emb_x.kpad == d &&
+                 long_loop_supported(D.dtype, d, D.heads, D.seq_len, D.speech_len, C, c->out_lin.npad);
+    if (c->long_ok) TRY(pack(c->emb_x));
   }
   TRY(build_step_tables(c));
   c->persist = c->fused && persist_supported(D.dtype, D.d_model, D.heads, D.seq_len, D.speech_len, D.d_pose);
@@ -1512,6 +1523,9 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
     case GGD_ROUTE_ATTN_QSPLIT:     // 1: long clips on the query-split attention kernel
       c->attn_qsplit = value != 0;
       return GGD_OK;
+    case GGD_ROUTE_LONG_LOOP:       // 1: never the long-clip persistent loop
+      c->long_off = value != 0;
+      return GGD_OK;
     default:
       break;
   }
@@ -1527,6 +1541,7 @@ int ggd_route_info(ggd_ctx* c, int32_t what, double* out) {
     case GGD_INFO_XL_LAUNCHES: *out = c->mega_xl_launches; return GGD_OK;
     case GGD_INFO_WT_RERUNS: *out = c->mega_fallbacks; return GGD_OK;
     case GGD_INFO_CHAIN_AVAILABLE: *out = c->chain ? 1.0 : 0.0; return GGD_OK;
+    case GGD_INFO_LONG_LAUNCHES: *out = c->long_launches; return GGD_OK;
     default: return fail(c, GGD_ERR_ARG, "unknown route info");
   }
 }
@@ -1809,6 +1824,146 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
 
 namespace {
 
+// Tables of the long-clip loop (ggd_long.hip): per layer its chain-route weights, conv taps and
+// memory K|V; the chain stages [loop start: emb_x, QKV] + per layer [A: o_sa, q_ca | B: o_ca,
+// ff1, ff2, next QKV or out_layers, emb_x, layer 0's QKV].
+int long_tables(ggd_ctx* c) {
+  const ggd_desc& D = c->desc;
+  const int NL = D.n_layers, d = D.d_model;
+  if (c->long_layers) return GGD_OK;
+  std::vector<LongLayer> ly(NL);
+  std::vector<ChainStage> st(2 + LONG_STAGES_PER_LAYER * NL, ChainStage{});
+  auto stage = [&](int i, const Lin& w, const float* g, const float* b, void* out, int ldo) {
+    st[i].w = chain_lin(w);
+    st[i].ln_g = g;
+    st[i].ln_b = b;
+    st[i].out = out;
+    st[i].ldo = ldo;
+  };
+  stage(0, c->emb_x, nullptr, nullptr, nullptr, 0);
+  stage(1, c->layers[0].qkv, c->layers[0].ln1_g, c->layers[0].ln1_b, c->qkv, 3 * d);
+  for (int li = 0; li < NL; ++li) {
+    const Layer& Y = c->layers[li];
+    LongLayer& L = ly[li];
+    L.qkv = chain_lin(Y.qkv); L.o_sa = chain_lin(Y.o_sa); L.q_ca = chain_lin(Y.q_ca);
+    L.o_ca = chain_lin(Y.o_ca); L.ff1 = chain_lin(Y.ff1); L.ff2 = chain_lin(Y.ff2);
+    L.ln1_g = Y.ln1_g; L.ln1_b = Y.ln1_b; L.ln2_g = Y.ln2_g; L.ln2_b = Y.ln2_b; L.ln3_g = Y.ln3_g; L.ln3_b = Y.ln3_b;
+    L.sa_qw = Y.sa_q.w; L.sa_qb = Y.sa_q.b; L.sa_kw = Y.sa_k.w; L.sa_kb = Y.sa_k.b; L.sa_vw = Y.sa_v.w; L.sa_vb = Y.sa_v.b;
+    L.ca_qw = Y.ca_q.w; L.ca_qb = Y.ca_q.b; L.ca_kw = Y.ca_k.w; L.ca_kb = Y.ca_k.b; L.ca_vw = Y.ca_v.w; L.ca_vb = Y.ca_v.b;
+    L.kv_mem = c->kv_mem + (size_t)li * D.max_batch * D.speech_len * 2 * d;
+    L.kv_step = c->kv_step + (size_t)li * D.diffusion_steps * 2 * d;
+    const int b0 = 2 + LONG_STAGES_PER_LAYER * li;
+    stage(b0 + 0, Y.o_sa, nullptr, nullptr, nullptr, 0);
+    stage(b0 + 1, Y.q_ca, Y.ln2_g, Y.ln2_b, c->q, d);
+    stage(b0 + 2, Y.o_ca, nullptr, nullptr, nullptr, 0);
+    stage(b0 + 3, Y.ff1, Y.ln3_g, Y.ln3_b, nullptr, 0);
+    stage(b0 + 4, Y.ff2, nullptr, nullptr, nullptr, 0);
+    if (li + 1 < NL) {
+      stage(b0 + 5, c->layers[li + 1].qkv, c->layers[li + 1].ln1_g, c->layers[li + 1].ln1_b, c->qkv, 3 * d);
+    } else {
+      stage(b0 + 5, c->out_lin, c->out_ln_g, c->out_ln_b, nullptr, 0);
+      stage(b0 + 6, c->emb_x, nullptr, nullptr, nullptr, 0);
+      stage(b0 + 7, c->layers[0].qkv, c->layers[0].ln1_g, c->layers[0].ln1_b, c->qkv, 3 * d);
+    }
+  }
+  HIP_TRY(c, dalloc(c, &c->long_layers, sizeof(LongLayer) * NL));
+  HIP_TRY(c, dalloc(c, &c->long_stages, sizeof(ChainStage) * st.size()));
+  HIP_TRY(c, dalloc(c, &c->long_ctl, sizeof(unsigned) * LONG_CTL_WORDS));
+  HIP_TRY(c, dalloc(c, &c->long_status, sizeof(int) * MEGA_MAX_CHUNKS));
+  HIP_TRY(c, hipMemcpy(c->long_layers, ly.data(), sizeof(LongLayer) * NL, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->long_stages, st.data(), sizeof(ChainStage) * st.size(), hipMemcpyHostToDevice));
+  return GGD_OK;
+}
+
+// The first `nsteps` iterations of a long-clip batch in the persistent loop (ggd_long.hip), one
+// launch per `long_loop_capacity()` clips.  The first step's emb_x + PE and LN1 + QKV run as
+// launches in front (every later step's run inside the loop).  Returns 1 when the loop could not
+// be placed (status 3: nothing ran; the caller takes the launch route), after a host sync.
+int run_long(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
+  const ggd_desc& D = c->desc;
+  const int L = D.seq_len, d = D.d_model, M = a.n * L;
+  hipStream_t s = c->stream;
+  int r = long_tables(c);
+  if (r) return r;
+  const int cap = long_loop_capacity(), chunks = (a.n + cap - 1) / cap;
+  if (chunks > MEGA_MAX_CHUNKS) return fail(c, GGD_ERR_ARG, "batch too large for the long-clip loop");
+  GemmArgs g = gemm_args(c->emb_x, M, c->x, D.d_pose, c->h, d);
+  g.pe = c->pe;
+  g.pe_period = L;
+  g.pe_offset = 0;
+  GEMM(c, PRO_F32, EPI_PE, g, s);
+  ChainArgs c0{};
+  c0.M = M;
+  c0.h = c->h;
+  c0.p_g = c->layers[0].ln1_g;
+  c0.p_b = c->layers[0].ln1_b;
+  c0.p = chain_lin(c->layers[0].qkv);
+  c0.out = c->qkv;
+  c0.ldo = 3 * d;
+  HIP_TRY(c, launch_chain(D.dtype == GGD_FP8W, c0, s));
+  HIP_TRY(c, hipMemsetAsync(c->long_status, 0, sizeof(int) * MEGA_MAX_CHUNKS, s));
+  if (c->profiling) {
+    c->prof.next = 0;
+    if ((r = prof_mark(c, s))) return r;
+  }
+  for (int c0i = 0, ci = 0; c0i < a.n; c0i += cap, ++ci) {
+    LongArgs la{};
+    la.layers = c->long_layers;
+    la.stages = c->long_stages;
+    la.n_layers = D.n_layers;
+    la.n = a.n;
+    la.L = L;
+    la.Ts = D.speech_len;
+    la.C = D.d_pose;
+    la.alg = a.alg;
+    la.k0 = 0;
+    la.n_steps = nsteps;
+    la.clip0 = c0i;
+    la.emb = chain_lin(c->emb_x);
+    la.out = chain_lin(c->out_lin);
+    la.out_g = c->out_ln_g;
+    la.out_b = c->out_ln_b;
+    la.pe = c->pe;
+    la.x = c->x;
+    la.h = c->h;
+    la.qkv = c->qkv;
+    la.att = c->att;
+    la.q = c->q;
+    la.steps = c->d_steps;
+    la.noise = a.noise;
+    la.scale = 1.0f / std::sqrt((float)(d / D.heads));
+    la.ctl = c->long_ctl;
+    la.status = c->long_status + ci;
+    HIP_TRY(c, launch_long_loop(D.dtype == GGD_FP8W, la, std::min(cap, a.n - c0i), s));
+  }
+  if (c->profiling && (r = prof_mark(c, s))) return r;
+  int st[MEGA_MAX_CHUNKS];
+  HIP_TRY(c, hipMemcpyAsync(st, c->long_status, sizeof(int) * MEGA_MAX_CHUNKS, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  int worst = 0;
+  for (int ci = 0; ci < chunks; ++ci) worst = std::max(worst, st[ci]);
+  c->long_launches = chunks;
+  if (worst == 3) {  // not placeable: nothing ran in the chunks that report 3; all chunks re-run on launches
+    for (int ci = 0; ci < chunks; ++ci)
+      if (st[ci] != 3) return fail(c, GGD_ERR_HIP, "long-clip loop: placement differed between chunks");
+    c->long_launches = 0;
+    ++c->long_fallbacks;
+    return 1;
+  }
+  if (worst)
+    return fail(c, GGD_ERR_HIP, worst == 2 ? "long-clip loop: workgroups were not all resident"
+                                           : "long-clip loop: a clip-group barrier timed out");
+  if (c->profiling) {
+    float ms = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->prof.ev[0], c->prof.ev[1]));
+    c->prof_avg_us = ms * 1000.0 / chunks;
+    c->prof_launches = chunks;
+    c->prof_kind = 5;
+    c->span_pending = 0;
+  }
+  return GGD_OK;
+}
+
 // The first `nsteps` iterations as ONE persistent launch (ggd_mega.hip); blocks until it has
 // finished to report a barrier timeout (outputs are then invalid).
 int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
@@ -2038,6 +2193,22 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
     HIP_TRY(c, hipEventRecord(c->ev_out, s));
     HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
     return GGD_OK;
+  }
+  c->long_launches = 0;
+  if (c->long_ok && !c->long_off && !c->gemm_launches && !c->attn_qsplit && !a->inpaint_masks && graph_steps > 0) {
+    int r = run_long(c, *a, graph_steps);
+    if (r < 0) return r;
+    if (r == 0) {
+      if (a->extras) {  // the last iteration with its extras on the launch route
+        HIP_TRY(c, launch_set_int(c->d_counter, graph_steps - 1, s));
+        r = launch_step(c, *a, a->extras, -1);
+        if (r) return r;
+      }
+      HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));
+      HIP_TRY(c, hipEventRecord(c->ev_out, s));
+      HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
+      return GGD_OK;
+    }
   }
   // pointer / shape key: a captured graph is reused only for identical arguments
   char keybuf[512];

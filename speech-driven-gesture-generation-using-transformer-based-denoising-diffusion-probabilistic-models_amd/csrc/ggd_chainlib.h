@@ -1,0 +1,141 @@
+// ggd_chainlib.h -- building blocks of the row-block chains (ggd_chain.hip) and the long-clip
+// persistent loop (ggd_long.hip): fragment-packed weight loads, the bf16 MFMA chain of one 256-k
+// chunk, the PRO_LN-exact LayerNorm of 32 LDS rows and the epilogue parameter expression.
+#pragma once
+#include "ggd_common.h"
+
+namespace ggd {
+namespace chainlib {
+
+constexpr int CH_MT = 32;           // residual rows per workgroup
+constexpr int CH_D = 256;           // d_model
+constexpr int CH_FF = 1024;         // feed-forward hidden width
+constexpr int HS_STR = CH_D + 16;   // f32 residual rows: the LN lanes (4 rows x 4) hit distinct banks
+constexpr int XS_STR = CH_D + 8;    // bf16 A rows (16-byte row pad, as gemm_kernel)
+constexpr int HH_STR = CH_FF + 8;   // bf16 hidden rows
+constexpr int CH_PMAX = 1024;       // P stage: widest projection
+constexpr int CH_DEPTH = 3;         // weight tile groups in flight per wave
+constexpr int CH_WAVES = 8;         // two waves per SIMD: one's fp8 widening and loads overlap the other's MFMAs
+constexpr int CH_NT = 64 * CH_WAVES;
+// per-column epilogue parameters and LayerNorm vectors, staged once per workgroup (LDS reads do
+// not queue behind the weight prefetch the way global loads would: vmcnt retires in order)
+constexpr int PRM_R = 0, PRM_F1 = PRM_R + 2 * CH_D, PRM_F2 = PRM_F1 + 2 * CH_FF, PRM_P = PRM_F2 + 2 * CH_D,
+              PRM_LN = PRM_P + 2 * CH_PMAX, PRM_FLOATS = PRM_LN + 4 * CH_D;
+constexpr size_t CH_LDS = sizeof(float) * (CH_MT * HS_STR + PRM_FLOATS) + sizeof(bf16_t) * CH_MT * (XS_STR + HH_STR);
+
+// workgroup barrier for LDS hand-offs only: global loads stay in flight across it
+__device__ __forceinline__ void ch_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+
+// 16-byte units per (16-column tile, 256-k chunk): fp8 packs two k steps per unit
+template <bool W8> struct Units { static constexpr int U = W8 ? 4 : 8; };
+template <bool W8, int TG> struct BBuf { uint4 v[TG][Units<W8>::U]; };
+
+// 8 e4m3 bytes (two dwords, k ascending) -> the bf16x8 B operand
+__device__ __forceinline__ bf16x8 fp8x8_bf16(unsigned w0, unsigned w1) {
+  const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)w0, 1.0f, false);
+  const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)w0, 1.0f, true);
+  const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)w1, 1.0f, false);
+  const bf16x2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)w1, 1.0f, true);
+  return bf16x8{a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+}
+
+// Fragment-packed weights: unit u of tile nt (16 output rows of W) at
+//   ((nt * units_per_tile + u) * 64 + lane) * 16 bytes, lane = (g << 4) | r16:
+//   bf16: 8 values W[nt 16 + r16][32 u + 8 g + e]
+//   fp8:  bytes 0-7 W[nt 16 + r16][64 u + 8 g + e], bytes 8-15 W[..][64 u + 32 + 8 g + e]
+// Loads of one iteration: TG tiles x the chunk's U units.  wb: this wave's first tile of the
+// stage (wave-uniform, so the constant offsets fold into the scalar base).
+template <bool W8, int TGB>
+__device__ __forceinline__ void ch_load(BBuf<W8, TGB>& B, const unsigned char* wb, unsigned lane16, int t0, int c,
+                                        int upt, int tg) {
+  constexpr int U = Units<W8>::U;
+#pragma unroll
+  for (int j = 0; j < TGB; ++j)
+    if (j < tg)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        B.v[j][u] = *(const uint4*)(wb + (size_t)(((t0 + j) * upt + c * U + u) * 1024) + lane16);
+  // keep the loads where they are issued: the scheduler would otherwise sink them next to
+  // their first use (lower register pressure) and the prefetch distance would collapse
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// acc[i][j] += A[16 i + .][256 c + .] . W[16 (nt0 + j) + .][256 c + .]^T over the chunk's 8 k steps
+template <bool W8, int TGB>
+__device__ __forceinline__ void ch_mma(const BBuf<W8, TGB>& B, const bf16_t* As, int sa, int c, int lane,
+                                       f32x4 (&acc)[2][TGB], int tg) {
+  const int r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int k = (c * 8 + q) * 32 + g * 8;
+    const bf16x8 a0 = *(const bf16x8*)(As + r16 * sa + k);
+    const bf16x8 a1 = *(const bf16x8*)(As + (16 + r16) * sa + k);
+#pragma unroll
+    for (int j = 0; j < TGB; ++j) {
+      if (j >= tg) continue;
+      bf16x8 bw;
+      if constexpr (W8) {
+        const uint4 u = B.v[j][q >> 1];
+        bw = (q & 1) ? fp8x8_bf16(u.z, u.w) : fp8x8_bf16(u.x, u.y);
+      } else {
+        bw = __builtin_bit_cast(bf16x8, B.v[j][q]);
+      }
+      acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bw, acc[0][j], 0, 0, 0);
+      acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bw, acc[1][j], 0, 0, 0);
+    }
+  }
+}
+
+// LayerNorm of the 32 LDS residual rows -> bf16 A rows, in gemm_kernel's PRO_LN arithmetic:
+// 4 lanes per row, lane j holds float4 columns (j + 4 i) 4, two-pass statistics, xor 1 / 2.
+// gm, bt: LDS copies of gamma / beta.
+// tid: the thread index (a caller inside a persistent loop passes an opaque one)
+__device__ __forceinline__ void ch_layernorm(const float* hs, const float* gm, const float* bt, bf16_t* xs,
+                                             int tid = threadIdx.x) {
+  if (tid >= CH_MT * 4) return;  // waves 0, 1 (whole waves: the shuffles stay uniform)
+  const int r = tid >> 2, j = tid & 3;
+  float4 v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = *(const float4*)(hs + r * HS_STR + (j + 4 * i) * 4);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  const float mu = s / (float)CH_D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float d0 = v[i].x - mu, d1 = v[i].y - mu, d2 = v[i].z - mu, d3 = v[i].w - mu;
+    q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+  }
+  q += __shfl_xor(q, 1);
+  q += __shfl_xor(q, 2);
+  const float rs = 1.0f / sqrtf(q / (float)CH_D + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int k = (j + 4 * i) * 4;
+    const float4 g = *(const float4*)(gm + k);
+    const float4 b = *(const float4*)(bt + k);
+    const float4 x = v[i];
+    bf16_t* dst = xs + r * XS_STR + k;
+    dst[0] = f2bf((x.x - mu) * rs * g.x + b.x);
+    dst[1] = f2bf((x.y - mu) * rs * g.y + b.y);
+    dst[2] = f2bf((x.z - mu) * rs * g.z + b.z);
+    dst[3] = f2bf((x.w - mu) * rs * g.w + b.w);
+  }
+}
+
+// acc + bias (and the fp8 per-channel scale) of column n: gemm_kernel's expression; prm = the
+// stage's LDS parameters [bias[npad] | scale[npad]]
+template <bool W8>
+__device__ __forceinline__ float ch_val(const float* prm, int npad, float acc, int n) {
+  const float bn = prm[n];
+  const float sn = W8 ? prm[npad + n] : 1.0f;
+  return W8 ? acc * sn + bn : acc + bn;
+}
+
+}  // namespace chainlib
+}  // namespace ggd

@@ -231,7 +231,46 @@ struct ChainArgs {
   int out_f32, n_valid;
 };
 
+// Long-clip persistent loop (ggd_long.hip): 8 workgroups per clip run every step; per layer the
+// chain-route weights (fragment-packed ChainLin) and the attention conv taps / memory K|V.
+struct LongLayer {
+  ChainLin qkv, o_sa, q_ca, o_ca, ff1, ff2;
+  const float *ln1_g, *ln1_b, *ln2_g, *ln2_b, *ln3_g, *ln3_b;
+  const float *sa_qw, *sa_qb, *sa_kw, *sa_kb, *sa_vw, *sa_vb;
+  const float *ca_qw, *ca_qb, *ca_kw, *ca_kb, *ca_vw, *ca_vb;
+  const float *kv_mem, *kv_step;   // this layer's memory K|V rows [N * Ts][2d], step-token rows [T_orig][2d]
+};
+// one GEMM stage of a long-loop chain phase: weights, the LayerNorm in front, hand-off output rows
+struct ChainStage {
+  ChainLin w;
+  const float *ln_g, *ln_b;
+  void* out;
+  int ldo;
+};
+constexpr int LONG_STAGES_PER_LAYER = 8;   // chain A: 2 stages, chain B: 4 (+ emb, QKV at the last layer)
+struct LongArgs {
+  const LongLayer* layers;   // device [n_layers]
+  const ChainStage* stages;  // device [2 + 8 n_layers]: loop start (emb_x, QKV), then per layer A, B
+  int n_layers;
+  int n, L, Ts, C, alg;      // n: clips of the whole sampling call (noise indexing)
+  int k0, n_steps, clip0;    // iterations k0 .. k0 + n_steps - 1 of clips clip0 .. clip0 + G - 1
+  ChainLin emb, out;         // emb_x (K = C padded to 256), out_layers.1 (N = C padded to 128)
+  const float *out_g, *out_b, *pe;
+  float* x;                  // state (N, L, C): x_T in, the sample out
+  const float* h;            // h = emb_x(x_T) + PE of the first iteration (layer 0's QKV rows in qkv)
+  void *qkv, *att, *q;       // hand-off rows (bf16)
+  const StepRec* steps;
+  const float* noise;        // (T', N, C, L) injected noise, or null: the counter stream
+  float scale;
+  unsigned* ctl;             // LONG_CTL_WORDS, zeroed by launch_long_loop
+  int* status;               // 0 ok, 1 barrier timeout, 2 not resident, 3 not placeable (nothing ran)
+};
+constexpr int LONG_CTL_WORDS = 256 + 32 * 32;
+
 // launchers (return hipError_t of the launch)
+bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C, int out_npad);
+int long_loop_capacity();   // clips per launch
+hipError_t launch_long_loop(int w8, const LongArgs& a, int G, hipStream_t s);
 hipError_t launch_chain(int w8, const ChainArgs& a, hipStream_t s);
 hipError_t launch_chain_pack(int w8, const void* src, void* dst, int npad, int kpad, hipStream_t s);
 size_t chain_pack_bytes(int w8, int npad, int kpad);

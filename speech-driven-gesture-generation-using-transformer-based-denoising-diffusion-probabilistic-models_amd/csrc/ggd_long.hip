@@ -1,0 +1,599 @@
+// ggd_long.hip -- the long-clip reverse loop as ONE persistent launch (gfx950; bf16 activations,
+// bf16 or fp8 weights): the route of BASELINE configs[3] (32 clips x 160 frames, DDPM 1000).
+//
+// The launch route (ggd_chain.hip + ggd_attn.hip) runs a denoise step as 19 kernels; at 32 clips
+// a kernel boundary costs a few microseconds of fill / drain and cold loads, a third of the step.
+// Here 8 workgroups per clip run every step of the loop inside one launch and meet at barriers
+// of their clip group only (clips are independent): per layer
+//   self-attention   part p = head p                      (qkv rows -> att rows)
+//   chain A          parts p < L / 32: row block p         R(o_sa) + P(LN2, q_ca)      -> q rows
+//   cross-attention  part p = head p                      (q rows, speech memory -> att rows)
+//   chain B          row blocks                            R(o_ca) + F + P(next LN1, qkv)
+// and at the last layer chain B ends the step: P(out_layers) into LDS, the posterior update of
+// the block's frames (counter or injected noise), then the next step's emb_x + PE and LN1 + QKV.
+// A row block's residual rows stay resident in LDS for the whole loop (no h traffic at all).
+//
+// The chain and attention bodies are those of the launch route (ggd_chainlib.h; same MFMA chains
+// and epilogue expressions, so the two routes agree bit for bit -- tests/test_gpu_parity.py),
+// with the hand-off rows read past the CU's L1 (sc1) since other workgroups wrote them.
+// Placement and barriers follow ggd_mega.hip: a clip group lives on one XCD (XCC-id tickets,
+// grid padded to whole XCDs; a launch that cannot be placed leaves before any work with status 3
+// and the host runs the launch route), hand-off stores stay in that XCD's L2, every wait is
+// bounded (status 1).
+#include "ggd_chainlib.h"
+#include "ggd_fusedlib.h"
+
+namespace ggd {
+namespace {
+
+using namespace chainlib;
+
+constexpr int LK_SPIN_LIMIT = 1 << 21;
+constexpr int LK_ARRIVE = 128, LK_FLAGS = 256;  // ctl: tickets [x * 16], arrivals, group flag lines [g * 32]
+
+__device__ __forceinline__ unsigned lk_add(unsigned* p, unsigned v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned lk_load(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// thread 0: (group << 3 | part), -2 (idle surplus), -1 (status set).  Group g lives on XCD g % 8.
+__device__ int lk_role(unsigned* ctl, int* status, int nwg, int G) {
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 7;
+  const int t = (int)lk_add(ctl + xcc * 16, 1u);
+  __hip_atomic_fetch_add(ctl + LK_ARRIVE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  for (int spin = 0; __hip_atomic_load(ctl + LK_ARRIVE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg;
+       ++spin) {
+    if (spin > LK_SPIN_LIMIT) {
+      atomicMax(status, 2);
+      return -1;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  auto slots = [&](int x) { return x < G ? 8 * ((G - 1 - x) / 8 + 1) : 0; };
+  for (int x = 0; x < 8; ++x)  // every workgroup reads the same final counts: one launch-wide verdict
+    if ((int)lk_load(ctl + x * 16) < slots(x)) {
+      atomicMax(status, 3);
+      return -1;
+    }
+  if (t >= slots((int)xcc)) return -2;
+  return (((int)xcc + 8 * (t >> 3)) << 3) | (t & 7);
+}
+
+// barrier of the clip group's 8 workgroups (one L2): each publishes its epoch in its word of the
+// group's flag line after its stores have drained; wave 0 polls the 8 words with sc1 loads
+__device__ __forceinline__ bool lk_sync(unsigned* flags, int part, unsigned epoch, int* status, int* s_ok) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
+    __builtin_amdgcn_raw_buffer_store_b32(epoch, r, part * 4, 0, 0);
+  }
+  if (threadIdx.x < 64) {
+    const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
+    const int off = (threadIdx.x & 7) * 4;
+    int ok = 1;
+    for (int spin = 0;; ++spin) {
+      const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
+      if (__ballot(v < epoch) == 0) break;
+      if ((spin & 255) == 255 &&
+          (spin > LK_SPIN_LIMIT || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        if (threadIdx.x == 0) atomicMax(status, 1);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (threadIdx.x == 0) *s_ok = ok;
+  }
+  bar_lds();
+  return *s_ok != 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// LDS: [hs: the row block's residual rows, resident] [scratch: chain xs | hh | prm, or attention]
+// ------------------------------------------------------------------------------------------
+constexpr size_t LK_HS = sizeof(float) * CH_MT * HS_STR;
+constexpr int EPS_STR = 132;  // f32 eps rows of the out_layers projection (in the hh region)
+
+// ------------------------------------------------------------------------------------------
+// chain phases: a compile-time list of GEMM stages
+// ------------------------------------------------------------------------------------------
+enum { SK_E = 0, SK_R, SK_F1, SK_F2, SK_P, SK_PO, SK_P2 };
+struct Stg { int kind, ncols, nch; };
+enum { K_INIT = 0, K_A, K_B, K_BL, K_BLL };
+
+template <int KIND> struct LkPlan;
+template <> struct LkPlan<K_INIT> {
+  static constexpr int NS = 2;
+  static constexpr Stg s[NS] = {{SK_E, 256, 1}, {SK_P2, 768, 1}};
+};
+template <> struct LkPlan<K_A> {
+  static constexpr int NS = 2;
+  static constexpr Stg s[NS] = {{SK_R, 256, 1}, {SK_P, 256, 1}};
+};
+template <> struct LkPlan<K_B> {
+  static constexpr int NS = 4;
+  static constexpr Stg s[NS] = {{SK_R, 256, 1}, {SK_F1, 1024, 1}, {SK_F2, 256, 4}, {SK_P, 768, 1}};
+};
+template <> struct LkPlan<K_BL> {
+  static constexpr int NS = 6;
+  static constexpr Stg s[NS] = {{SK_R, 256, 1}, {SK_F1, 1024, 1}, {SK_F2, 256, 4}, {SK_PO, 128, 1},
+                                {SK_E, 256, 1},  {SK_P2, 768, 1}};
+};
+template <> struct LkPlan<K_BLL> {
+  static constexpr int NS = 4;
+  static constexpr Stg s[NS] = {{SK_R, 256, 1}, {SK_F1, 1024, 1}, {SK_F2, 256, 4}, {SK_PO, 128, 1}};
+};
+
+template <bool W8, int KIND>
+struct LkGeo {
+  using PL = LkPlan<KIND>;
+  static constexpr int TGB = W8 ? 2 : 1;
+  static constexpr int tg(int i) { return PL::s[i].ncols == 128 ? 1 : TGB; }
+  static constexpr int iters(int i) { return PL::s[i].ncols / (16 * CH_WAVES * tg(i)) * PL::s[i].nch; }
+  static constexpr int first(int i) { return i == 0 ? 0 : first(i - 1) + iters(i - 1); }
+  static constexpr int TOTAL = first(PL::NS - 1) + iters(PL::NS - 1);
+  static constexpr int stage_of(int it, int i = 0) { return it < first(i) + iters(i) ? i : stage_of(it, i + 1); }
+  static constexpr int prm(int i) { return i == 0 ? 0 : prm(i - 1) + 2 * PL::s[i - 1].ncols; }  // bias | scale
+  static constexpr int PRM_LN0 = prm(PL::NS - 1) + 2 * PL::s[PL::NS - 1].ncols;
+  static constexpr int ln(int i) { return PRM_LN0 + 2 * CH_D * i; }                            // gamma | beta
+  static constexpr int PRM_TOTAL = PRM_LN0 + 2 * CH_D * PL::NS;
+  static constexpr size_t LDS = LK_HS + sizeof(bf16_t) * CH_MT * (XS_STR + HH_STR) + sizeof(float) * PRM_TOTAL;
+};
+
+// stage arguments and layers live in constant memory: field reads are scalar loads
+typedef const __attribute__((address_space(4))) ChainStage* cst_t;
+typedef const __attribute__((address_space(4))) LongArgs cla_T;  // the kernel's argument block, in place
+typedef const __attribute__((address_space(4))) LongLayer* cll_t;
+
+template <bool W8, int TGB>
+struct LkCtx {
+  cla_T& a;
+  cst_t sa;
+  float* hs;
+  bf16_t* xs;
+  bf16_t* hh;
+  float* prm;
+  int wave, lane, g4, c16, b, part, it;  // it: the loop iteration (update, noise)
+  unsigned lane16;
+  BBuf<W8, TGB> bb[CH_DEPTH];
+  f32x4 acc[2][TGB];
+};
+
+template <bool W8, int KIND, int IT, class X>
+__device__ __forceinline__ void lk_issue(X& x) {
+  using GE = LkGeo<W8, KIND>;
+  constexpr int si = GE::stage_of(IT), l = IT - GE::first(si), tg = GE::tg(si), nch = LkPlan<KIND>::s[si].nch;
+  constexpr int upt = nch * Units<W8>::U;
+  const unsigned char* wb = (const unsigned char*)x.sa[si].w.w + (size_t)x.wave * tg * upt * 1024;
+  ch_load<W8, GE::TGB>(x.bb[IT % CH_DEPTH], wb, x.lane16, (l / nch) * CH_WAVES * tg, l % nch, upt, tg);
+}
+
+// x rows of the block (coherent: this workgroup wrote them in an earlier step) -> bf16 A rows,
+// columns >= C zero (the emb_x GEMM's PRO_F32 staging)
+template <class X>
+__device__ __forceinline__ void lk_x_to_xs(X& x, const float* xv, int n) {
+  const int C = x.a.C;
+  for (int e = ltid(); e < CH_MT * CH_D; e += CH_NT) {
+    const int r = e / CH_D, c = e % CH_D;
+    x.xs[r * XS_STR + c] = c < C ? f2bf(xv[r * C + c]) : (bf16_t)0;
+  }
+}
+
+// the posterior update of the block's frames (update_kernel's arithmetic), eps from LDS; the new
+// x rows go to HBM and, when `to_xs`, into the A rows of the next emb_x GEMM
+template <class X>
+__device__ __forceinline__ void lk_update(X& x, bool to_xs) {
+  cla_T& a = x.a;
+  const int C = a.C, L = a.L, l0 = x.part * CH_MT;
+  const StepRec r = a.steps[x.it];
+  const float* eps = (const float*)x.hh;
+  float* xg = a.x + ((size_t)x.b * L + l0) * C;
+  for (int e = ltid(); e < CH_MT * CH_D; e += CH_NT) {
+    const int rr = e / CH_D, c = e % CH_D, l = l0 + rr;
+    if (c < C) {
+      const float xo = ld_f32<CP_COH>(xg, (uint32_t)(rr * C + c));
+      const float ev = eps[rr * EPS_STR + c];
+      const size_t ncl = ((size_t)x.b * C + c) * L + l;
+      float z;
+      if (a.noise)
+        z = a.noise[(size_t)x.it * a.n * C * L + ncl];
+      else
+        z = philox_normal(((uint64_t)r.seed_hi << 32) | r.seed_lo, r.clip_offset + (uint32_t)x.b, (uint32_t)r.i, TAG_STEP,
+                          (uint32_t)(c * L + l));
+      const UpdOut o = upd_math(r, a.alg, xo, ev, false, 0.f, false, 0.f, 0.f, 0.f, z);
+      xg[rr * C + c] = o.xn;
+      if (to_xs) x.xs[rr * XS_STR + c] = f2bf(o.xn);
+    } else if (to_xs) {
+      x.xs[rr * XS_STR + c] = 0;
+    }
+  }
+}
+
+template <bool W8, int KIND, int IT, class X>
+__device__ __forceinline__ void lk_iter(X& x) {
+  using GE = LkGeo<W8, KIND>;
+  using PL = LkPlan<KIND>;
+  constexpr int TGB = GE::TGB, D1 = CH_DEPTH - 1;
+  constexpr int si = GE::stage_of(IT), l = IT - GE::first(si), tg = GE::tg(si), nch = PL::s[si].nch;
+  constexpr int kind = PL::s[si].kind;
+  if constexpr (IT + D1 < GE::TOTAL) lk_issue<W8, KIND, IT + D1>(x);
+  if constexpr (l == 0 && si > 0) {  // stage hand-offs (LDS); the prefetched weights stay in flight
+    ch_bar();
+    if constexpr (kind == SK_F1 || kind == SK_P || kind == SK_PO || kind == SK_P2) {
+      ch_layernorm(x.hs, x.prm + GE::ln(si), x.prm + GE::ln(si) + CH_D, x.xs, ltid());
+      ch_bar();
+    } else if constexpr (kind == SK_E) {  // after out_layers: the update, its x rows feed emb_x
+      lk_update(x, true);
+      ch_bar();
+    }
+  }
+  constexpr int c = l % nch;
+  const int nt0 = ((l / nch) * CH_WAVES + x.wave) * tg;
+  if constexpr (c == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TGB; ++j) x.acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if constexpr (kind == SK_F2)
+    ch_mma<W8, TGB>(x.bb[IT % CH_DEPTH], x.hh, HH_STR, c, x.lane, x.acc, tg);
+  else
+    ch_mma<W8, TGB>(x.bb[IT % CH_DEPTH], x.xs, XS_STR, c, x.lane, x.acc, tg);
+  if constexpr (c == nch - 1) {
+    constexpr int np = PL::s[si].ncols;
+    const float* pp = x.prm + GE::prm(si);
+    const int L = x.a.L, l0 = x.part * CH_MT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < tg; ++j) {
+        const int n = (nt0 + j) * 16 + x.c16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + x.g4 + r;
+          const float v = ch_val<W8>(pp, np, x.acc[i][j][r], n);
+          if constexpr (kind == SK_R || kind == SK_F2) {          // EPI_RESID
+            float* p = x.hs + row * HS_STR + n;
+            *p = *p + v;
+          } else if constexpr (kind == SK_F1) {                   // EPI_RELU2
+            const float y = fmaxf(v, 0.f);
+            x.hh[row * HH_STR + n] = f2bf(y * y);
+          } else if constexpr (kind == SK_E) {                    // EPI_PE: h = emb_x(x) + PE[frame]
+            x.hs[row * HS_STR + n] = v + x.a.pe[(size_t)((l0 + row) % L) * CH_D + n];
+          } else if constexpr (kind == SK_PO) {                   // eps rows -> LDS (the update reads them)
+            ((float*)x.hh)[row * EPS_STR + n] = v;
+          } else {                                                 // EPI_T: hand-off rows
+            ((bf16_t*)x.sa[si].out)[((size_t)x.b * L + l0 + row) * x.sa[si].ldo + n] = f2bf(v);
+          }
+        }
+      }
+  }
+  if constexpr (IT + 1 < GE::TOTAL) lk_iter<W8, KIND, IT + 1>(x);
+}
+
+// one chain phase of row block `part` of clip b
+template <bool W8, int KIND>
+__device__ __forceinline__ void lk_chain(cla_T& a, cst_t sa, int b, int part, int it,
+                                                   unsigned char* smem) {
+  using GE = LkGeo<W8, KIND>;
+  using PL = LkPlan<KIND>;
+  const int tid = ltid(), lane = tid & 63;  // opaque: nothing thread-derived is hoisted across phases
+  LkCtx<W8, GE::TGB> x{a, sa};
+  x.hs = (float*)smem;
+  x.xs = (bf16_t*)(smem + LK_HS);
+  x.hh = x.xs + CH_MT * XS_STR;
+  x.prm = (float*)(x.hh + CH_MT * HH_STR);
+  x.wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  x.lane = lane;
+  x.g4 = 4 * (lane >> 4);
+  x.c16 = lane & 15;
+  x.lane16 = (unsigned)lane * 16u;
+  x.b = b;
+  x.part = part;
+  x.it = it;
+  lk_issue<W8, KIND, 0>(x);
+  if constexpr (GE::TOTAL > 1) lk_issue<W8, KIND, 1>(x);
+  // parameters (bias | scale per stage, LayerNorm vectors), the first stage's A rows
+#pragma unroll
+  for (int si = 0; si < PL::NS; ++si) {
+    const float* wb = sa[si].w.b;
+    const float* ws = sa[si].w.scale;
+    const int np = PL::s[si].ncols;
+    for (int e = tid; e < np; e += CH_NT) {
+      x.prm[GE::prm(si) + e] = wb[e];
+      x.prm[GE::prm(si) + np + e] = W8 ? ws[e] : 1.0f;
+    }
+    if (sa[si].ln_g && tid < CH_D) {
+      x.prm[GE::ln(si) + tid] = sa[si].ln_g[tid];
+      x.prm[GE::ln(si) + CH_D + tid] = sa[si].ln_b[tid];
+    }
+  }
+  constexpr int k0 = PL::s[0].kind;
+  if constexpr (k0 == SK_R) {  // attention output rows of the block (written by the head parts)
+    const bf16_t* src = (const bf16_t*)a.att + ((size_t)b * a.L + part * CH_MT) * CH_D;
+#pragma unroll
+    for (int i = 0; i < CH_MT * CH_D / 8 / CH_NT; ++i) {
+      const int e = tid + i * CH_NT, r = e / (CH_D / 8), cv = e % (CH_D / 8);
+      *(uint4*)(x.xs + r * XS_STR + 8 * cv) = ld_16B<CP_XL>(src, (uint32_t)((r * CH_D + 8 * cv) * 2));
+    }
+  } else {  // SK_E at the loop start: x_T rows
+    lk_x_to_xs(x, a.x + ((size_t)b * a.L + part * CH_MT) * a.C, 0);
+  }
+  ch_bar();
+  lk_iter<W8, KIND, 0>(x);
+  if constexpr (KIND == K_BLL) {  // the last step: update only
+    ch_bar();
+    lk_update(x, false);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// attention phase: head `head` of clip b over all its frames (ggd_attn.hip with 8 waves; the
+// Q / K / V rows another workgroup wrote are read past L1)
+// ------------------------------------------------------------------------------------------
+constexpr int LA_VPR = 4;                    // 16-byte channel vectors per 32-channel row
+constexpr int LA_NS = CH_NT / LA_VPR;        // 128 row strips
+constexpr int LA_SLMAX = (ATT_LMAX + LA_NS - 1) / LA_NS;
+constexpr int LA_SQ = 40;
+
+struct LaSrc {
+  const void* base;
+  size_t row0;
+  int ld, col, len;
+  const float* step_row;  // memory mode: f32 rows (constant inputs: plain loads)
+  __device__ __forceinline__ void load(int j, int cv, float (&o)[8]) const {
+    if (j < 0 || j >= len) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = 0.f;
+      return;
+    }
+    if (step_row) {
+      const float* p = j == 0 ? step_row + cv * 8 : (const float*)base + (row0 + j - 1) * (size_t)ld + col + cv * 8;
+      const float4 u = *(const float4*)p, v = *(const float4*)(p + 4);
+      o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w;
+      o[4] = v.x; o[5] = v.y; o[6] = v.z; o[7] = v.w;
+    } else {
+      const uint4 u = ld_16B<CP_XL>(base, (uint32_t)(((row0 + j) * (size_t)ld + col + cv * 8) * 2));
+      const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        o[2 * q] = __uint_as_float(w[q] << 16);
+        o[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+      }
+    }
+  }
+};
+
+struct LaStrip {
+  float x[LA_SLMAX + 2][8];
+  int sl, rows;
+  __device__ __forceinline__ void load(const LaSrc& src, int rows_) {
+    rows = rows_;
+    sl = (rows + LA_NS - 1) / LA_NS;
+    const int t = ltid(), cv = t % LA_VPR, sid = t / LA_VPR;
+#pragma unroll
+    for (int s = 0; s < LA_SLMAX + 2; ++s)
+      if (s < sl + 2) src.load(sid * sl - 1 + s, cv, x[s]);
+  }
+  template <bool TRANS>
+  __device__ __forceinline__ void conv(bf16_t* dst, int S, const float* wl) const {
+    const int t = ltid(), cv = t % LA_VPR, sid = t / LA_VPR;
+#pragma unroll
+    for (int s = 0; s < LA_SLMAX; ++s) {
+      const int r = sid * sl + s;
+      if (s >= sl || r >= rows) continue;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = cv * 8 + e;
+        const float v = wl[96 + c] + wl[c] * x[s][e] + wl[32 + c] * x[s + 1][e] + wl[64 + c] * x[s + 2][e];
+        if (TRANS)
+          dst[c * S + r] = f2bf(v);
+        else
+          dst[r * S + c] = f2bf(v);
+      }
+    }
+  }
+};
+
+template <bool CROSS>
+__device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, int t_orig,
+                                                  unsigned char* scratch) {
+  const __attribute__((address_space(4))) LongLayer& Ly = *lyp;
+  const int Lq = a.L, Lk = CROSS ? 1 + a.Ts : a.L, tid = ltid(), lane = tid & 63, wave = tid >> 6;
+  const int Lkp = (Lk + 31) / 32 * 32, SV = Lkp + 8, SP = Lkp + 8, Lqp = (Lq + 15) / 16 * 16;
+  bf16_t* Qm = (bf16_t*)scratch;
+  bf16_t* Km = Qm + Lqp * LA_SQ;
+  bf16_t* Vt = Km + Lkp * LA_SQ;
+  bf16_t* Pall = Vt + 32 * SV;
+  float* wl = (float*)(Pall + CH_WAVES * 16 * SP);
+  const size_t row0 = (size_t)b * Lq;
+  LaSrc sq, sk, sv;
+  if constexpr (CROSS) {
+    const float* r0 = Ly.kv_step + (size_t)t_orig * 2 * CH_D;
+    const size_t mrow0 = (size_t)b * (Lk - 1);
+    sq = LaSrc{a.q, row0, CH_D, head * 32, Lq, nullptr};
+    sk = LaSrc{Ly.kv_mem, mrow0, 2 * CH_D, head * 32, Lk, r0 + head * 32};
+    sv = LaSrc{Ly.kv_mem, mrow0, 2 * CH_D, CH_D + head * 32, Lk, r0 + CH_D + head * 32};
+  } else {
+    sq = LaSrc{a.qkv, row0, 3 * CH_D, head * 32, Lq, nullptr};
+    sk = LaSrc{a.qkv, row0, 3 * CH_D, CH_D + head * 32, Lk, nullptr};
+    sv = LaSrc{a.qkv, row0, 3 * CH_D, 2 * CH_D + head * 32, Lk, nullptr};
+  }
+  LaStrip xq, xk, xv;
+  xq.load(sq, Lq);
+  xk.load(sk, Lk);
+  xv.load(sv, Lk);
+  for (int i = tid; i < 12 * 32; i += CH_NT) {
+    const int m = i / 128, k = (i / 32) % 4, c = i % 32;
+    const float* w = CROSS ? (m == 0 ? Ly.ca_qw : m == 1 ? Ly.ca_kw : Ly.ca_vw) : (m == 0 ? Ly.sa_qw : m == 1 ? Ly.sa_kw : Ly.sa_vw);
+    const float* bb = CROSS ? (m == 0 ? Ly.ca_qb : m == 1 ? Ly.ca_kb : Ly.ca_vb) : (m == 0 ? Ly.sa_qb : m == 1 ? Ly.sa_kb : Ly.sa_vb);
+    wl[i] = k < 3 ? w[c * 3 + k] : bb[c];
+  }
+  for (int i = tid; i < (Lkp - Lk) * 32; i += CH_NT) {
+    const int r = Lk + i / 32, c = i % 32;
+    Km[r * LA_SQ + c] = 0;
+    Vt[c * SV + r] = 0;
+  }
+  bar_lds();
+  xq.conv<false>(Qm, LA_SQ, wl);
+  xk.conv<false>(Km, LA_SQ, wl + 128);
+  xv.conv<true>(Vt, SV, wl + 256);
+  bar_lds();
+  const int c16 = lane & 15, g4 = lane >> 4, LKT = Lkp / 16;
+  bf16_t* P = Pall + wave * 16 * SP;
+  bf16_t* out = (bf16_t*)a.att + row0 * CH_D + (size_t)head * 32;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  for (int rt = wave; rt * 16 < Lq; rt += CH_WAVES) {
+    f32x4 s[ATT_KT];
+#pragma unroll
+    for (int t = 0; t < ATT_KT; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t < LKT) att_mma<bf16_t>(s[t], Qm, rt * 16, LA_SQ, Km, t * 16, LA_SQ, 32, lane);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < ATT_KT; ++t) {
+        const bool ok = t < LKT && t * 16 + c16 < Lk;
+        const float v = ok ? s[t][r] * sl2 : -INFINITY;
+        s[t][r] = v;
+        mx = fmaxf(mx, v);
+      }
+      mx = group_max<16>(mx);
+      float sum = 0.f;
+#pragma unroll
+      for (int t = 0; t < ATT_KT; ++t) {
+        const bool ok = t < LKT && t * 16 + c16 < Lk;
+        const float p = ok ? __builtin_amdgcn_exp2f(s[t][r] - mx) : 0.f;
+        s[t][r] = p;
+        sum += p;
+      }
+      sum = group_sum<16>(sum);
+      const float inv = 1.0f / sum;
+#pragma unroll
+      for (int t = 0; t < ATT_KT; ++t)
+        if (t < LKT) P[(4 * g4 + r) * SP + t * 16 + c16] = f2bf(s[t][r] * inv);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+      att_mma<bf16_t>(o, P, 0, SP, Vt, ct * 16, SV, Lkp, lane);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = rt * 16 + 4 * g4 + r;
+        if (i < Lq) out[(size_t)i * CH_D + ct * 16 + c16] = f2bf(o[r]);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+size_t lk_attn_lds(int L, int Lk) {
+  const int Lkp = (Lk + 31) / 32 * 32, Lqp = (L + 15) / 16 * 16;
+  return 2 * ((size_t)Lqp * LA_SQ + (size_t)Lkp * LA_SQ + 32 * (size_t)(Lkp + 8) + CH_WAVES * 16 * (size_t)(Lkp + 8)) +
+         sizeof(float) * 12 * 32;
+}
+
+// ------------------------------------------------------------------------------------------
+// the persistent loop
+// ------------------------------------------------------------------------------------------
+template <bool W8>
+__global__ void __launch_bounds__(CH_NT) lk_kernel(LongArgs args, int G) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int s_role, s_ok;
+  cla_T& a = *(const __attribute__((address_space(4))) LongArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  if (threadIdx.x == 0) s_role = lk_role(a.ctl, a.status, gridDim.x, G);
+  __syncthreads();
+  const int role = s_role;
+  if (role < 0) return;
+  const int grp = role >> 3, part = role & 7, b = a.clip0 + grp, NB = a.L / CH_MT, NL = a.n_layers;
+  unsigned* flags = a.ctl + LK_FLAGS + grp * 32;
+  unsigned epoch = 0;
+  const cll_t lay = (cll_t)a.layers;
+  const cst_t st = (cst_t)a.stages;
+  const bool rows = part < NB;
+  if (rows) {  // the block's residual rows (h = emb_x(x_T) + PE; its LN1 + QKV rows are in qkv)
+    float* hs = (float*)smem;
+    const float* hg = a.h + ((size_t)b * a.L + part * CH_MT) * CH_D;
+    for (int e = ltid(); e < CH_MT * CH_D / 4; e += CH_NT) {
+      const int r = e / (CH_D / 4), c4 = e % (CH_D / 4);
+      *(float4*)(hs + r * HS_STR + 4 * c4) = *(const float4*)(hg + r * CH_D + 4 * c4);
+    }
+  }
+  __syncthreads();
+  for (int k = 0; k < a.n_steps; ++k) {
+    const int it = a.k0 + k;
+    const int t_orig = a.steps[it].t_orig;
+    for (int li = 0; li < NL; ++li) {
+      const cst_t sl = st + 2 + LONG_STAGES_PER_LAYER * li;
+      lk_attn<false>(a, lay + li, b, part, t_orig, smem + LK_HS);
+      if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
+      if (rows) lk_chain<W8, K_A>(a, sl, b, part, it, smem);         // R(o_sa) + P(LN2, q_ca)
+      if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
+      lk_attn<true>(a, lay + li, b, part, t_orig, smem + LK_HS);
+      if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
+      if (rows) {
+        if (li + 1 < NL)
+          lk_chain<W8, K_B>(a, sl + 2, b, part, it, smem);             // R(o_ca) + F + P(next LN1, QKV)
+        else if (k + 1 < a.n_steps)
+          lk_chain<W8, K_BL>(a, sl + 2, b, part, it, smem);            // ... + out_layers, update, emb_x, LN1 + QKV
+        else
+          lk_chain<W8, K_BLL>(a, sl + 2, b, part, it, smem);           // ... + out_layers, update
+      }
+      if (k + 1 < a.n_steps || li + 1 < NL)
+        if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
+    }
+  }
+}
+
+template <bool W8>
+size_t lk_lds(int L, int Lk) {
+  size_t m = LkGeo<W8, K_BL>::LDS;
+  m = std::max(m, LkGeo<W8, K_B>::LDS);
+  return std::max(m, LK_HS + lk_attn_lds(L, Lk));
+}
+
+}  // namespace
+
+bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C, int out_npad) {
+  const size_t lds = std::max(lk_lds<true>(L, 1 + Ts), lk_lds<false>(L, 1 + Ts));
+  return dtype != 0 && d_model == CH_D && heads == 8 && L % CH_MT == 0 && L / CH_MT <= 8 && L >= 96 &&
+         L <= ATT_LMAX && 1 + Ts <= ATT_LMAX && C <= 128 && out_npad == 128 && lds <= 160 * 1024 - 256;
+}
+
+int long_loop_capacity() {
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipGetLastError();
+  return std::min(32, cus / 8);
+}
+
+hipError_t launch_long_loop(int w8, const LongArgs& a, int G, hipStream_t s) {
+  if (G < 1 || G > long_loop_capacity() || 64 * ((G + 7) / 8) > 8 * long_loop_capacity()) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(a.ctl, 0, sizeof(unsigned) * LONG_CTL_WORDS, s);
+  if (e != hipSuccess) return e;
+  const size_t lds = w8 ? lk_lds<true>(a.L, 1 + a.Ts) : lk_lds<false>(a.L, 1 + a.Ts);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)lk_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+    (void)hipFuncSetAttribute((const void*)lk_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+    (void)hipGetLastError();
+    attr = true;
+  }
+  const int nwg = 64 * ((G + 7) / 8);
+  if (w8) hipLaunchKernelGGL(lk_kernel<true>, dim3(nwg), dim3(CH_NT), lds, s, a, G);
+  else hipLaunchKernelGGL(lk_kernel<false>, dim3(nwg), dim3(CH_NT), lds, s, a, G);
+  return hipGetLastError();
+}
+
+}  // namespace ggd

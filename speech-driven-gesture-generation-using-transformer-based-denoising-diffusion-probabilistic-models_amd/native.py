@@ -17,10 +17,10 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 PRODUCT_LIB = os.path.join(PKG_DIR, "libggd.so")
 DIAG_LIB = os.path.join(PKG_DIR, "libggd_diag.so")
 LIB_PATH = DIAG_LIB if os.environ.get("GGD_DIAG") == "1" else PRODUCT_LIB
-SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_encoder.hip", "ggd_train.hip", "ggd_chain.hip", "ggd_attn.hip",
+SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_encoder.hip", "ggd_train.hip", "ggd_chain.hip", "ggd_attn.hip", "ggd_long.hip",
            "ggd_api.hip"]
 DIAG_SOURCES = ["ggd_diag.hip"]   # + ggd_api.hip again with -DGGD_DIAG
-HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_fusedlib.h", "ggd_phases.h", os.path.join("..", "..", "include", "ggd.h"),
+HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_chainlib.h", "ggd_fusedlib.h", "ggd_phases.h", os.path.join("..", "..", "include", "ggd.h"),
            os.path.join("..", "..", "include", "ggd_train.h")]
 
 GGD_OK, GGD_IGNORED = 0, 1

@@ -15,8 +15,8 @@ pytestmark = pytest.mark.gpu
 
 D_POSE, L, WAV = 123, 40, 32000
 ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_PAIR_WT, ROUTE_PHASE_LAUNCHES = 0, 1, 2, 3   # include/ggd.h GGD_ROUTE_*
-ROUTE_GEMM_LAUNCHES, ROUTE_ATTN_QSPLIT = 5, 6
-INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES, INFO_CHAIN_AVAILABLE = 0, 2, 5     # include/ggd.h GGD_INFO_*
+ROUTE_GEMM_LAUNCHES, ROUTE_ATTN_QSPLIT, ROUTE_LONG_LOOP = 5, 6, 7
+INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES, INFO_CHAIN_AVAILABLE, INFO_LONG_LAUNCHES = 0, 2, 5, 6  # GGD_INFO_*
 
 
 def rel_rms(a, b):
@@ -584,3 +584,48 @@ def test_clip_attention_matches_query_split(pkg, beat_cfg, setup, setup_fp8, dty
     assert rel_rms(clip, qsplit) <= 2e-3
     ref = (setup_fp8 if dtype == "fp8" else om)(x, t, wav=wav)
     assert rel_rms(clip, ref) <= 1e-2
+
+
+# ------------------------------------------------------------------------------------------
+# Long-clip persistent loop (ggd_long.hip): every step of the batch in one launch of 8
+# workgroups per clip.  Same chain arithmetic, attention and update as the launch route, so the
+# two routes agree bit for bit: DDPM on injected noise (fp8, 2 clips), DDIM on the counter stream
+# over 33 clips (two launches: 32 + 1 clips), bf16 weights; and the oracle bound.
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype,n,alg,injected", [("fp8", 2, "ddpm", True), ("fp8", 33, "ddim", False),
+                                                  ("bf16", 3, "ddpm", False)])
+def test_long_loop_equals_launch_route(pkg, beat_cfg, setup, setup_fp8, dtype, n, alg, injected):
+    _, sd, om = setup
+    model, diffusion = make_model(pkg, beat_cfg, sd, dtype)
+    if alg == "ddim":
+        diffusion = pkg.create_diffusion(dict(beat_cfg.Model.Diffusion.to_dict(), timestep_respacing="ddim50"), False)
+    Lc, steps = 160, 4
+    wav, x, _ = inputs(n, seed=91, wav_len=128000, L_=Lc)
+    zs = th.randn(steps, n, D_POSE, Lc, generator=th.Generator().manual_seed(92)) if injected else None
+    ctx, _ = model.prepare(wav.cuda(), Lc)
+    loop = diffusion.p_sample_loop if alg == "ddpm" else diffusion.ddim_sample_loop
+
+    def run():
+        kw = dict(noise=x.cuda(), n_steps=steps)
+        if injected:
+            kw["step_noise"] = zs.cuda()
+        else:
+            kw["seed"] = 93
+        return loop(model, (n, D_POSE, Lc), model_kwargs={"wav": wav.cuda()}, **kw)
+
+    try:
+        out_l = run()
+        launches = int(_info(ctx, INFO_LONG_LAUNCHES))
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_LONG_LOOP, 1) == 0
+        out_r = run()
+        assert int(_info(ctx, INFO_LONG_LAUNCHES)) == 0
+    finally:
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_LONG_LOOP, 0)
+    assert launches == (n + 31) // 32
+    for k in ("sample", "eps"):
+        assert th.equal(out_l[k].cpu(), out_r[k].cpu()), k
+    if injected:
+        sch = ref_diffusion.make_schedule("linear", 1000, "")
+        want = ref_diffusion.sample_loop(sch, setup_fp8, (n, D_POSE, Lc), {"wav": wav},
+                                         ref_diffusion.InjectedNoise(x, zs), "ddpm", x_T=x, n_steps=steps)
+        assert rel_rms(out_l["sample"].cpu(), want["sample"]) <= 5e-2
