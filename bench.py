@@ -94,7 +94,7 @@ WORKLOADS = {
 # this same command (scripts/pmc_all.sh -> scripts/pmc.sh + pmc_summary.py: 2 x FETCH_SIZE +
 # WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), one summary per workload; PMC cannot
 # run inside the timed region, so the figure is the profile's, keyed by kernel symbol and workload
-PMC_SUMMARY = {"c2": "r02a", "c4": "r02a", "c5": "r02d"}   # profile tag per workload (its dominant kernel's code)
+PMC_SUMMARY = {"c2": "r02a", "c4": "r02k", "c5": "r02d"}   # profile tag per workload (its dominant kernel's code)
 
 
 def pmc_traffic(kernel_prefix, workload):
@@ -107,7 +107,8 @@ def pmc_traffic(kernel_prefix, workload):
     if d.get("_workload") != workload:
         return None
     for k, e in d.items():
-        if k.startswith("void ggd::" + kernel_prefix) and "hbm_read_bytes" in e and "hbm_write_bytes" in e:
+        name = k.replace("(anonymous namespace)::", "")
+        if name.startswith("void ggd::" + kernel_prefix) and "hbm_read_bytes" in e and "hbm_write_bytes" in e:
             return {"bytes_per_launch": e["hbm_read_bytes"] + e["hbm_write_bytes"],
                     "read": e["hbm_read_bytes"], "write": e["hbm_write_bytes"],
                     "source": os.path.relpath(path, ROOT)}
@@ -406,6 +407,11 @@ def main():
             kernel = (f"psk_kernel<{args.dtype}, pair> (two workgroups per clip, all {T} denoise steps in one launch"
                       " per <= 128 clips)")
             timing = "hipEvent pair around the loop's launches in the last timed pass"
+        elif prof_kind == 5:  # long-clip loop: one launch (per 32 clips) runs all T steps of the batch
+            flop = clip_step * B * T / prof_n
+            kernel = (f"lk_kernel<{args.dtype}> (long-clip persistent loop: 8 workgroups per clip, all {T} denoise"
+                      " steps, 16 clip-group barriers each)")
+            timing = "hipEvent pair around the loop's launches in the last timed pass"
         elif prof_kind == 2:  # generic path: the attention launches (self and cross, the top rocprof row)
             flop = (attn_flop(B, L, L, d) + attn_flop(B, L, Tm, d)) / 2
             kernel = (f"attn_q_kernel<{args.dtype}> (self- and cross-attention with the 3-tap convs, one workgroup per"
@@ -417,7 +423,7 @@ def main():
             timing = "device realtime-clock span of every KB launch of the last timed pass"
         ach = flop / (avg_us * 1e-6) / 1e12
         tr = pmc_traffic({1: "mk_kernel", 2: "attn_q_kernel", 3: "psk_kernel<3, false>",
-                          4: "psk_kernel<3, true>"}.get(
+                          4: "psk_kernel<3, true>", 5: "lk_kernel"}.get(
             prof_kind, "kb_kernel"),
                          args.workload)
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
