@@ -221,7 +221,8 @@ int ggd_route_info(ggd_ctx* ctx, int32_t what, double* out);
  * ggd_sample through the per-phase launches instead of the persistent loop (ggd_mega.hip), {0}
  * back (returns the loop's clip capacity in *avg_us); what = 10 / 11: clip-group loop barrier / phase
  * stamps; what = 12 / 14: as GGD_ROUTE_PLACEMENT / GGD_ROUTE_PAIR (p[1]: write-through);
- * what = 13 / 15: as ggd_route_info. */
+ * what = 13 / 15: as ggd_route_info; what = 16: long-clip loop barrier stamps ({1} arm, {2} read:
+ * avg_us[j] = us from the loop start to barrier j of clip group 0, {0} off). */
 #ifdef GGD_DIAG
 int ggd_diag(ggd_ctx* ctx, int32_t what, const int32_t* p, int32_t np, int32_t iters, double* avg_us);
 #endif

@@ -117,6 +117,7 @@ struct ggd_ctx {
   unsigned* long_ctl = nullptr;
   int* long_status = nullptr;
   int long_launches = 0, long_fallbacks = 0;  // last ggd_sample
+  unsigned long long* long_stamps = nullptr;  // ggd_diag what = 16
 
   // two-way decoder (generic kernels, joint layout [n][J = L + 1 + Ts][d])
   bool twoway = false;
@@ -1565,6 +1566,20 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     if (p[0] == 0) c->mega_stamps = nullptr;  // stays owned by the ctx allocation list
     return GGD_OK;
   }
+  if (what == 16 && np >= 1) {  // long-clip loop barrier stamps: {1} arm, {2} read, {0} off
+    if (p[0] == 1) {
+      if (!c->long_stamps) HIP_TRY(c, dalloc(c, &c->long_stamps, LONG_STAMPS * sizeof(unsigned long long)));
+      HIP_TRY(c, hipMemset(c->long_stamps, 0, LONG_STAMPS * sizeof(unsigned long long)));
+    }
+    if (p[0] == 2 && c->long_stamps) {  // avg_us[j] = us from the loop start to barrier j (-1: not stamped)
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      std::vector<unsigned long long> h(LONG_STAMPS);
+      HIP_TRY(c, hipMemcpy(h.data(), c->long_stamps, LONG_STAMPS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      for (int j = 0; j < LONG_STAMPS; ++j) avg_us[j] = h[j] && h[0] ? (double)(h[j] - h[0]) / c->wall_mhz : -1.0;
+    }
+    if (p[0] == 0) c->long_stamps = nullptr;
+    return GGD_OK;
+  }
   if (what == 11 && np >= 1) {  // persistent-loop phase stamps of layer 1 + KE: {1} arm, {2} read, {0} off
     if (p[0] == 1) {
       if (!c->mega_phase_stamps) HIP_TRY(c, dalloc(c, &c->mega_phase_stamps, 80 * sizeof(unsigned long long)));
@@ -1934,6 +1949,7 @@ int run_long(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
     la.scale = 1.0f / std::sqrt((float)(d / D.heads));
     la.ctl = c->long_ctl;
     la.status = c->long_status + ci;
+    la.stamps = ci == 0 ? c->long_stamps : nullptr;
     HIP_TRY(c, launch_long_loop(D.dtype == GGD_FP8W, la, std::min(cap, a.n - c0i), s));
   }
   if (c->profiling && (r = prof_mark(c, s))) return r;

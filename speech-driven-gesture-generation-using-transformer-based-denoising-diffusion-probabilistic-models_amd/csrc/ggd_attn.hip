@@ -52,24 +52,24 @@ struct AcSrc {
   size_t row0;
   int ld, col, len;
   const float* step_row;
+  // the load is always issued (on a clamped row) and the value selected after, so the loads of a
+  // strip are in flight together (a load under a divergent branch is waited for before the join)
   __device__ __forceinline__ void load(int j, int cv, float (&o)[8]) const {
-    if (j < 0 || j >= len) {
+    const bool in = j >= 0 && j < len;
+    const int jj = in ? j : 0;
+    if (step_row) {  // uniform
+      const float* p = jj == 0 ? step_row + cv * 8 : (const float*)base + (row0 + jj - 1) * (size_t)ld + col + cv * 8;
+      const float4 u = *(const float4*)p, v = *(const float4*)(p + 4);
+      const float t[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = 0.f;
-      return;
-    }
-    if (step_row) {
-      const float* p = j == 0 ? step_row + cv * 8 : (const float*)base + (row0 + j - 1) * (size_t)ld + col + cv * 8;
-      const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
-      o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
-      o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+      for (int e = 0; e < 8; ++e) o[e] = in ? t[e] : 0.f;
     } else {
-      const uint4 u = *(const uint4*)((const bf16_t*)base + (row0 + j) * (size_t)ld + col + cv * 8);
+      const uint4 u = *(const uint4*)((const bf16_t*)base + (row0 + jj) * (size_t)ld + col + cv * 8);
       const unsigned w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        o[2 * q] = __uint_as_float(w[q] << 16);
-        o[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+        o[2 * q] = in ? __uint_as_float(w[q] << 16) : 0.f;
+        o[2 * q + 1] = in ? __uint_as_float(w[q] & 0xffff0000u) : 0.f;
       }
     }
   }

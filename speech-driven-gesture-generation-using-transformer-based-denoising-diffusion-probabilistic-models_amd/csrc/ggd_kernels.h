@@ -264,8 +264,11 @@ struct LongArgs {
   float scale;
   unsigned* ctl;             // LONG_CTL_WORDS, zeroed by launch_long_loop
   int* status;               // 0 ok, 1 barrier timeout, 2 not resident, 3 not placeable (nothing ran)
+  unsigned long long* stamps;  // diagnostics: clip group 0 part 0 stamps the realtime clock at the loop
+                               // start [0] and after each of the first LONG_STAMPS - 1 barriers
 };
 constexpr int LONG_CTL_WORDS = 256 + 32 * 32;
+constexpr int LONG_STAMPS = 64;
 
 // launchers (return hipError_t of the launch)
 bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C, int out_npad);

@@ -341,29 +341,33 @@ constexpr int LA_NS = CH_NT / LA_VPR;        // 128 row strips
 constexpr int LA_SLMAX = (ATT_LMAX + LA_NS - 1) / LA_NS;
 constexpr int LA_SQ = 40;
 
+// conv input rows.  Rows outside [0, len) are the conv's zero padding; the load itself is always
+// issued (on a clamped row) and the value selected after, so every load of a strip is in flight at
+// once (a load under a divergent branch makes the compiler wait for it before the branch joins).
+// MEM = false: bf16 hand-off rows base[(row0 + j) ld + col], read past L1.  MEM = true: memory mode,
+// f32 rows: j = 0 the step-token row, j >= 1 base[(row0 + j - 1) ld + col] (constant inputs).
+template <bool MEM>
 struct LaSrc {
   const void* base;
   size_t row0;
   int ld, col, len;
-  const float* step_row;  // memory mode: f32 rows (constant inputs: plain loads)
+  const float* step_row;
   __device__ __forceinline__ void load(int j, int cv, float (&o)[8]) const {
-    if (j < 0 || j >= len) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = 0.f;
-      return;
-    }
-    if (step_row) {
-      const float* p = j == 0 ? step_row + cv * 8 : (const float*)base + (row0 + j - 1) * (size_t)ld + col + cv * 8;
+    const bool in = j >= 0 && j < len;
+    const int jj = in ? j : 0;
+    if constexpr (MEM) {
+      const float* p = jj == 0 ? step_row + cv * 8 : (const float*)base + (row0 + jj - 1) * (size_t)ld + col + cv * 8;
       const float4 u = *(const float4*)p, v = *(const float4*)(p + 4);
-      o[0] = u.x; o[1] = u.y; o[2] = u.z; o[3] = u.w;
-      o[4] = v.x; o[5] = v.y; o[6] = v.z; o[7] = v.w;
+      const float t[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = in ? t[e] : 0.f;
     } else {
-      const uint4 u = ld_16B<CP_XL>(base, (uint32_t)(((row0 + j) * (size_t)ld + col + cv * 8) * 2));
+      const uint4 u = ld_16B<CP_XL>(base, (uint32_t)(((row0 + jj) * (size_t)ld + col + cv * 8) * 2));
       const unsigned w[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        o[2 * q] = __uint_as_float(w[q] << 16);
-        o[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+        o[2 * q] = in ? __uint_as_float(w[q] << 16) : 0.f;
+        o[2 * q + 1] = in ? __uint_as_float(w[q] & 0xffff0000u) : 0.f;
       }
     }
   }
@@ -372,7 +376,8 @@ struct LaSrc {
 struct LaStrip {
   float x[LA_SLMAX + 2][8];
   int sl, rows;
-  __device__ __forceinline__ void load(const LaSrc& src, int rows_) {
+  template <class S>
+  __device__ __forceinline__ void load(const S& src, int rows_) {
     rows = rows_;
     sl = (rows + LA_NS - 1) / LA_NS;
     const int t = ltid(), cv = t % LA_VPR, sid = t / LA_VPR;
@@ -400,9 +405,74 @@ struct LaStrip {
   }
 };
 
+// the query tiles of one wave, LKT (16-key tiles, Lk padded to 32) fixed at compile time: every
+// LDS fragment of a matrix product is read before its MFMAs (no per-tile branch between them)
+template <int LKT>
+__device__ __forceinline__ void lk_attn_tiles(const bf16_t* Qm, const bf16_t* Km, const bf16_t* Vt, bf16_t* P, int SV,
+                                              int SP, int Lq, int Lk, float sl2, bf16_t* out, int wave, int lane) {
+  const int c16 = lane & 15, g4 = lane >> 4;
+  for (int rt = wave; rt * 16 < Lq; rt += CH_WAVES) {
+    const bf16x8 qa = *(const bf16x8*)(Qm + (rt * 16 + c16) * LA_SQ + g4 * 8);
+    bf16x8 kb[LKT];
+#pragma unroll
+    for (int t = 0; t < LKT; ++t) kb[t] = *(const bf16x8*)(Km + (t * 16 + c16) * LA_SQ + g4 * 8);
+    f32x4 s[LKT];
+#pragma unroll
+    for (int t = 0; t < LKT; ++t)
+      s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kb[t], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < LKT; ++t) {
+        const float v = t * 16 + c16 < Lk ? s[t][r] * sl2 : -INFINITY;
+        s[t][r] = v;
+        mx = fmaxf(mx, v);
+      }
+      mx = group_max<16>(mx);
+      float sum = 0.f;
+#pragma unroll
+      for (int t = 0; t < LKT; ++t) {
+        const float p = t * 16 + c16 < Lk ? __builtin_amdgcn_exp2f(s[t][r] - mx) : 0.f;
+        s[t][r] = p;
+        sum += p;
+      }
+      sum = group_sum<16>(sum);
+      const float inv = 1.0f / sum;
+#pragma unroll
+      for (int t = 0; t < LKT; ++t) P[(4 * g4 + r) * SP + t * 16 + c16] = f2bf(s[t][r] * inv);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    constexpr int KS = LKT / 2;  // 32-key steps of P V
+    bf16x8 pa[KS], vb[2][KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      pa[k] = *(const bf16x8*)(P + c16 * SP + k * 32 + g4 * 8);
+      vb[0][k] = *(const bf16x8*)(Vt + c16 * SV + k * 32 + g4 * 8);
+      vb[1][k] = *(const bf16x8*)(Vt + (16 + c16) * SV + k * 32 + g4 * 8);
+    }
+    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[k], vb[ct][k], o[ct], 0, 0, 0);
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = rt * 16 + 4 * g4 + r;
+        if (i < Lq) out[(size_t)i * CH_D + ct * 16 + c16] = f2bf(o[ct][r]);
+      }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 template <bool CROSS>
 __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, int t_orig,
-                                                  unsigned char* scratch) {
+                                                  unsigned char* scratch, unsigned long long* sub = nullptr) {
+  // sub (diagnostics): realtime stamps after staging, after the convs, after the query tiles
   const __attribute__((address_space(4))) LongLayer& Ly = *lyp;
   const int Lq = a.L, Lk = CROSS ? 1 + a.Ts : a.L, tid = ltid(), lane = tid & 63, wave = tid >> 6;
   const int Lkp = (Lk + 31) / 32 * 32, SV = Lkp + 8, SP = Lkp + 8, Lqp = (Lq + 15) / 16 * 16;
@@ -412,22 +482,18 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
   bf16_t* Pall = Vt + 32 * SV;
   float* wl = (float*)(Pall + CH_WAVES * 16 * SP);
   const size_t row0 = (size_t)b * Lq;
-  LaSrc sq, sk, sv;
+  LaStrip xq, xk, xv;
   if constexpr (CROSS) {
     const float* r0 = Ly.kv_step + (size_t)t_orig * 2 * CH_D;
     const size_t mrow0 = (size_t)b * (Lk - 1);
-    sq = LaSrc{a.q, row0, CH_D, head * 32, Lq, nullptr};
-    sk = LaSrc{Ly.kv_mem, mrow0, 2 * CH_D, head * 32, Lk, r0 + head * 32};
-    sv = LaSrc{Ly.kv_mem, mrow0, 2 * CH_D, CH_D + head * 32, Lk, r0 + CH_D + head * 32};
+    xq.load(LaSrc<false>{a.q, row0, CH_D, head * 32, Lq, nullptr}, Lq);
+    xk.load(LaSrc<true>{Ly.kv_mem, mrow0, 2 * CH_D, head * 32, Lk, r0 + head * 32}, Lk);
+    xv.load(LaSrc<true>{Ly.kv_mem, mrow0, 2 * CH_D, CH_D + head * 32, Lk, r0 + CH_D + head * 32}, Lk);
   } else {
-    sq = LaSrc{a.qkv, row0, 3 * CH_D, head * 32, Lq, nullptr};
-    sk = LaSrc{a.qkv, row0, 3 * CH_D, CH_D + head * 32, Lk, nullptr};
-    sv = LaSrc{a.qkv, row0, 3 * CH_D, 2 * CH_D + head * 32, Lk, nullptr};
+    xq.load(LaSrc<false>{a.qkv, row0, 3 * CH_D, head * 32, Lq, nullptr}, Lq);
+    xk.load(LaSrc<false>{a.qkv, row0, 3 * CH_D, CH_D + head * 32, Lk, nullptr}, Lk);
+    xv.load(LaSrc<false>{a.qkv, row0, 3 * CH_D, 2 * CH_D + head * 32, Lk, nullptr}, Lk);
   }
-  LaStrip xq, xk, xv;
-  xq.load(sq, Lq);
-  xk.load(sk, Lk);
-  xv.load(sv, Lk);
   for (int i = tid; i < 12 * 32; i += CH_NT) {
     const int m = i / 128, k = (i / 32) % 4, c = i % 32;
     const float* w = CROSS ? (m == 0 ? Ly.ca_qw : m == 1 ? Ly.ca_kw : Ly.ca_vw) : (m == 0 ? Ly.sa_qw : m == 1 ? Ly.sa_kw : Ly.sa_vw);
@@ -440,61 +506,22 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
     Vt[c * SV + r] = 0;
   }
   bar_lds();
+  if (sub && tid == 0) sub[0] = __builtin_amdgcn_s_memrealtime();
   xq.conv<false>(Qm, LA_SQ, wl);
   xk.conv<false>(Km, LA_SQ, wl + 128);
   xv.conv<true>(Vt, SV, wl + 256);
   bar_lds();
-  const int c16 = lane & 15, g4 = lane >> 4, LKT = Lkp / 16;
+  if (sub && tid == 0) sub[1] = __builtin_amdgcn_s_memrealtime();
   bf16_t* P = Pall + wave * 16 * SP;
   bf16_t* out = (bf16_t*)a.att + row0 * CH_D + (size_t)head * 32;
-  const float sl2 = a.scale * 1.4426950408889634f;
-  for (int rt = wave; rt * 16 < Lq; rt += CH_WAVES) {
-    f32x4 s[ATT_KT];
-#pragma unroll
-    for (int t = 0; t < ATT_KT; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (t < LKT) att_mma<bf16_t>(s[t], Qm, rt * 16, LA_SQ, Km, t * 16, LA_SQ, 32, lane);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < ATT_KT; ++t) {
-        const bool ok = t < LKT && t * 16 + c16 < Lk;
-        const float v = ok ? s[t][r] * sl2 : -INFINITY;
-        s[t][r] = v;
-        mx = fmaxf(mx, v);
-      }
-      mx = group_max<16>(mx);
-      float sum = 0.f;
-#pragma unroll
-      for (int t = 0; t < ATT_KT; ++t) {
-        const bool ok = t < LKT && t * 16 + c16 < Lk;
-        const float p = ok ? __builtin_amdgcn_exp2f(s[t][r] - mx) : 0.f;
-        s[t][r] = p;
-        sum += p;
-      }
-      sum = group_sum<16>(sum);
-      const float inv = 1.0f / sum;
-#pragma unroll
-      for (int t = 0; t < ATT_KT; ++t)
-        if (t < LKT) P[(4 * g4 + r) * SP + t * 16 + c16] = f2bf(s[t][r] * inv);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct) {
-      f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
-      att_mma<bf16_t>(o, P, 0, SP, Vt, ct * 16, SV, Lkp, lane);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = rt * 16 + 4 * g4 + r;
-        if (i < Lq) out[(size_t)i * CH_D + ct * 16 + c16] = f2bf(o[r]);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+  const float sl2 = a.scale * 1.4426950408889634f;  // softmax on exp2: e^(s - m) = 2^((s - m) log2 e)
+  switch (Lkp / 16) {  // long_loop_supported: 96 <= Lk_pad <= 192
+    case 6: lk_attn_tiles<6>(Qm, Km, Vt, P, SV, SP, Lq, Lk, sl2, out, wave, lane); break;
+    case 8: lk_attn_tiles<8>(Qm, Km, Vt, P, SV, SP, Lq, Lk, sl2, out, wave, lane); break;
+    case 10: lk_attn_tiles<10>(Qm, Km, Vt, P, SV, SP, Lq, Lk, sl2, out, wave, lane); break;
+    default: lk_attn_tiles<12>(Qm, Km, Vt, P, SV, SP, Lq, Lk, sl2, out, wave, lane); break;
   }
+  if (sub && tid == 0) sub[2] = __builtin_amdgcn_s_memrealtime();  // wave 0's tiles done
 }
 
 size_t lk_attn_lds(int L, int Lk) {
@@ -518,6 +545,11 @@ __global__ void __launch_bounds__(CH_NT) lk_kernel(LongArgs args, int G) {
   const int grp = role >> 3, part = role & 7, b = a.clip0 + grp, NB = a.L / CH_MT, NL = a.n_layers;
   unsigned* flags = a.ctl + LK_FLAGS + grp * 32;
   unsigned epoch = 0;
+  unsigned long long* stamps = role == 0 ? a.stamps : nullptr;
+  if (stamps && threadIdx.x == 0) stamps[0] = __builtin_amdgcn_s_memrealtime();
+  auto stamp = [&]() {
+    if (stamps && threadIdx.x == 0 && epoch < LONG_STAMPS) stamps[epoch] = __builtin_amdgcn_s_memrealtime();
+  };
   const cll_t lay = (cll_t)a.layers;
   const cst_t st = (cst_t)a.stages;
   const bool rows = part < NB;
@@ -535,12 +567,15 @@ __global__ void __launch_bounds__(CH_NT) lk_kernel(LongArgs args, int G) {
     const int t_orig = a.steps[it].t_orig;
     for (int li = 0; li < NL; ++li) {
       const cst_t sl = st + 2 + LONG_STAGES_PER_LAYER * li;
-      lk_attn<false>(a, lay + li, b, part, t_orig, smem + LK_HS);
+      lk_attn<false>(a, lay + li, b, part, t_orig, smem + LK_HS, stamps && k == 1 && li == 0 ? stamps + 56 : nullptr);
       if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
+      stamp();
       if (rows) lk_chain<W8, K_A>(a, sl, b, part, it, smem);         // R(o_sa) + P(LN2, q_ca)
       if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
-      lk_attn<true>(a, lay + li, b, part, t_orig, smem + LK_HS);
+      stamp();
+      lk_attn<true>(a, lay + li, b, part, t_orig, smem + LK_HS, stamps && k == 1 && li == 0 ? stamps + 60 : nullptr);
       if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
+      stamp();
       if (rows) {
         if (li + 1 < NL)
           lk_chain<W8, K_B>(a, sl + 2, b, part, it, smem);             // R(o_ca) + F + P(next LN1, QKV)
@@ -551,6 +586,7 @@ __global__ void __launch_bounds__(CH_NT) lk_kernel(LongArgs args, int G) {
       }
       if (k + 1 < a.n_steps || li + 1 < NL)
         if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
+      stamp();
     }
   }
 }
@@ -566,8 +602,9 @@ size_t lk_lds(int L, int Lk) {
 
 bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C, int out_npad) {
   const size_t lds = std::max(lk_lds<true>(L, 1 + Ts), lk_lds<false>(L, 1 + Ts));
+  const int lkp = (1 + Ts + 31) / 32 * 32;  // memory keys, padded (whole-clip tiles: 96 .. 192)
   return dtype != 0 && d_model == CH_D && heads == 8 && L % CH_MT == 0 && L / CH_MT <= 8 && L >= 96 &&
-         L <= ATT_LMAX && 1 + Ts <= ATT_LMAX && C <= 128 && out_npad == 128 && lds <= 160 * 1024 - 256;
+         L <= ATT_LMAX && lkp >= 96 && lkp <= ATT_LMAX && C <= 128 && out_npad == 128 && lds <= 160 * 1024 - 256;
 }
 
 int long_loop_capacity() {
