@@ -113,6 +113,7 @@ struct ggd_ctx {
   bool long_ok = false;      // the shape and dtype have a long-loop instance (needs the chain weights)
   int long_off = 0;          // GGD_ROUTE_LONG_LOOP: 1 = never
   LongLayer* long_layers = nullptr;
+  bf16_t* long_kvc = nullptr;  // [layers][max_batch] convolved memory K / V^T (ggd_set_memory)
   ChainStage* long_stages = nullptr;
   unsigned* long_ctl = nullptr;
   int* long_status = nullptr;
@@ -1283,7 +1284,10 @@ int ggd_finalize_weights(ggd_ctx* c) {
     TRY(pack(c->out_lin));
     c->long_ok = D.model_type != GGD_MODEL_INPAINT && c->emb_x.npad == d && c->emb_x.kpad == d &&
                  long_loop_supported(D.dtype, d, D.heads, D.seq_len, D.speech_len, C, c->out_lin.npad);
-    if (c->long_ok) TRY(pack(c->emb_x));
+    if (c->long_ok) {
+      TRY(pack(c->emb_x));
+      HIP_TRY(c, dalloc(c, &c->long_kvc, D.n_layers * long_kv_cache_bytes(D.max_batch, D.speech_len, D.heads)));
+    }
   }
   TRY(build_step_tables(c));
   c->persist = c->fused && persist_supported(D.dtype, D.d_model, D.heads, D.seq_len, D.speech_len, D.d_pose);
@@ -1366,6 +1370,14 @@ int ggd_set_memory(ggd_ctx* c, const float* tok, int32_t n, int32_t ts, int32_t 
       const Layer& Ly = c->layers[l];
       HIP_TRY(c, launch_ca_kv_conv(D.dtype == GGD_F32 ? 0 : 1, c->kv_mem + (size_t)l * D.max_batch * D.speech_len * 2 * d,
                                    Ly.ca_k.w, Ly.ca_k.b, Ly.ca_v.w, Ly.ca_v.b, n, ts, (char*)c->kvc + per_layer * l, s));
+    }
+  }
+  if (c->long_ok) {  // the long loop's convolved memory keys (2 ..) per layer
+    for (int l = 0; l < D.n_layers; ++l) {
+      const Layer& Ly = c->layers[l];
+      HIP_TRY(c, launch_long_kv_cache(c->kv_mem + (size_t)l * D.max_batch * D.speech_len * 2 * d, Ly.ca_k.w, Ly.ca_k.b,
+                                      Ly.ca_v.w, Ly.ca_v.b, n, D.speech_len,  D.heads,
+                                      (bf16_t*)((char*)c->long_kvc + l * long_kv_cache_bytes(D.max_batch, D.speech_len, D.heads)), s));
     }
   }
   HIP_TRY(c, hipEventRecord(c->ev_out, s));
@@ -1867,6 +1879,7 @@ int long_tables(ggd_ctx* c) {
     L.ca_qw = Y.ca_q.w; L.ca_qb = Y.ca_q.b; L.ca_kw = Y.ca_k.w; L.ca_kb = Y.ca_k.b; L.ca_vw = Y.ca_v.w; L.ca_vb = Y.ca_v.b;
     L.kv_mem = c->kv_mem + (size_t)li * D.max_batch * D.speech_len * 2 * d;
     L.kv_step = c->kv_step + (size_t)li * D.diffusion_steps * 2 * d;
+    L.kvc = (const bf16_t*)((const char*)c->long_kvc + li * long_kv_cache_bytes(D.max_batch, D.speech_len, D.heads));
     const int b0 = 2 + LONG_STAGES_PER_LAYER * li;
     stage(b0 + 0, Y.o_sa, nullptr, nullptr, nullptr, 0);
     stage(b0 + 1, Y.q_ca, Y.ln2_g, Y.ln2_b, c->q, d);

@@ -10,7 +10,7 @@ namespace chainlib {
 constexpr int CH_MT = 32;           // residual rows per workgroup
 constexpr int CH_D = 256;           // d_model
 constexpr int CH_FF = 1024;         // feed-forward hidden width
-constexpr int HS_STR = CH_D + 16;   // f32 residual rows: the LN lanes (4 rows x 4) hit distinct banks
+constexpr int HS_STR = CH_D + 4;    // f32 residual rows: the MFMA epilogue (rows 4g + r, 16 columns) hits 64 distinct banks
 constexpr int XS_STR = CH_D + 8;    // bf16 A rows (16-byte row pad, as gemm_kernel)
 constexpr int HH_STR = CH_FF + 8;   // bf16 hidden rows
 constexpr int CH_PMAX = 1024;       // P stage: widest projection

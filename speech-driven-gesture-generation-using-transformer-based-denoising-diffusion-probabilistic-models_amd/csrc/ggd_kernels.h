@@ -239,6 +239,7 @@ struct LongLayer {
   const float *sa_qw, *sa_qb, *sa_kw, *sa_kb, *sa_vw, *sa_vb;
   const float *ca_qw, *ca_qb, *ca_kw, *ca_kb, *ca_vw, *ca_vb;
   const float *kv_mem, *kv_step;   // this layer's memory K|V rows [N * Ts][2d], step-token rows [T_orig][2d]
+  const bf16_t* kvc;               // convolved memory keys 2.. as [N][heads][K [Lk_pad][32] | V^T [32][Lk_pad]]
 };
 // one GEMM stage of a long-loop chain phase: weights, the LayerNorm in front, hand-off output rows
 struct ChainStage {
@@ -274,6 +275,10 @@ constexpr int LONG_STAMPS = 64;
 bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C, int out_npad);
 int long_loop_capacity();   // clips per launch
 hipError_t launch_long_loop(int w8, const LongArgs& a, int G, hipStream_t s);
+// step-invariant convolved memory K / V^T of one layer for the long loop (keys 0, 1 and >= 1 + Ts zero)
+hipError_t launch_long_kv_cache(const float* kv_mem, const float* kw, const float* kb, const float* vw, const float* vb,
+                                int n, int Ts, int heads, bf16_t* out, hipStream_t s);
+size_t long_kv_cache_bytes(int n, int Ts, int heads);
 hipError_t launch_chain(int w8, const ChainArgs& a, hipStream_t s);
 hipError_t launch_chain_pack(int w8, const void* src, void* dst, int npad, int kpad, hipStream_t s);
 size_t chain_pack_bytes(int w8, int npad, int kpad);

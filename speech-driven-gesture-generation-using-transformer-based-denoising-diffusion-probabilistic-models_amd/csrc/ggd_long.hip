@@ -484,11 +484,41 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
   const size_t row0 = (size_t)b * Lq;
   LaStrip xq, xk, xv;
   if constexpr (CROSS) {
-    const float* r0 = Ly.kv_step + (size_t)t_orig * 2 * CH_D;
-    const size_t mrow0 = (size_t)b * (Lk - 1);
+    // keys >= 2 from the step-invariant convolved cache (ggd_set_memory); keys 0 and 1 depend on the
+    // step token (memory row 0) and are convolved here, in the cache kernel's expression
     xq.load(LaSrc<false>{a.q, row0, CH_D, head * 32, Lq, nullptr}, Lq);
-    xk.load(LaSrc<true>{Ly.kv_mem, mrow0, 2 * CH_D, head * 32, Lk, r0 + head * 32}, Lk);
-    xv.load(LaSrc<true>{Ly.kv_mem, mrow0, 2 * CH_D, CH_D + head * 32, Lk, r0 + CH_D + head * 32}, Lk);
+    const bf16_t* kc = Ly.kvc + ((size_t)b * CH_WAVES + head) * 2 * Lkp * 32;
+    const bf16_t* vc = kc + Lkp * 32;
+    const int kpr = Lkp / 8;  // 16-byte units per V^T row
+    for (int u = tid; u < (Lkp - 2) * 4; u += CH_NT) {  // K rows 2 .. Lk_pad - 1
+      const int r = 2 + u / 4, cv = u % 4;
+      *(uint4*)(Km + r * LA_SQ + cv * 8) = *(const uint4*)(kc + r * 32 + cv * 8);
+    }
+    const float* r0 = Ly.kv_step + (size_t)t_orig * 2 * CH_D;
+    const float* m0 = Ly.kv_mem + (size_t)b * (Lk - 1) * 2 * CH_D;
+    for (int u = tid; u < 32 * kpr; u += CH_NT) {  // V^T rows; keys 0, 1 patched in
+      const int c = u / kpr, kb = u % kpr;
+      uint4 v = *(const uint4*)(vc + c * Lkp + kb * 8);
+      if (kb == 0) {
+        const int col = CH_D + head * 32 + c;
+        const float x0 = r0[col], x1 = m0[col], x2 = Lk > 2 ? m0[2 * CH_D + col] : 0.f;
+        const float* w = Ly.ca_vw;
+        const float bb = Ly.ca_vb[c];
+        const float k0 = bb + w[c * 3] * 0.f + w[c * 3 + 1] * x0 + w[c * 3 + 2] * x1;
+        const float k1 = bb + w[c * 3] * x0 + w[c * 3 + 1] * x1 + w[c * 3 + 2] * x2;
+        v.x = (unsigned)f2bf(k0) | ((unsigned)f2bf(k1) << 16);
+      }
+      *(uint4*)(Vt + c * SV + kb * 8) = v;
+    }
+    if (tid < 64) {  // K keys 0, 1
+      const int r = tid / 32, c = tid % 32, col = head * 32 + c;
+      const float x0 = r0[col], x1 = m0[col], x2 = Lk > 2 ? m0[2 * CH_D + col] : 0.f;
+      const float* w = Ly.ca_kw;
+      const float bb = Ly.ca_kb[c];
+      const float v = r == 0 ? bb + w[c * 3] * 0.f + w[c * 3 + 1] * x0 + w[c * 3 + 2] * x1
+                             : bb + w[c * 3] * x0 + w[c * 3 + 1] * x1 + w[c * 3 + 2] * x2;
+      Km[r * LA_SQ + c] = f2bf(v);
+    }
   } else {
     xq.load(LaSrc<false>{a.qkv, row0, 3 * CH_D, head * 32, Lq, nullptr}, Lq);
     xk.load(LaSrc<false>{a.qkv, row0, 3 * CH_D, CH_D + head * 32, Lk, nullptr}, Lk);
@@ -500,16 +530,20 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
     const float* bb = CROSS ? (m == 0 ? Ly.ca_qb : m == 1 ? Ly.ca_kb : Ly.ca_vb) : (m == 0 ? Ly.sa_qb : m == 1 ? Ly.sa_kb : Ly.sa_vb);
     wl[i] = k < 3 ? w[c * 3 + k] : bb[c];
   }
-  for (int i = tid; i < (Lkp - Lk) * 32; i += CH_NT) {
-    const int r = Lk + i / 32, c = i % 32;
-    Km[r * LA_SQ + c] = 0;
-    Vt[c * SV + r] = 0;
+  if constexpr (!CROSS) {
+    for (int i = tid; i < (Lkp - Lk) * 32; i += CH_NT) {
+      const int r = Lk + i / 32, c = i % 32;
+      Km[r * LA_SQ + c] = 0;
+      Vt[c * SV + r] = 0;
+    }
   }
   bar_lds();
   if (sub && tid == 0) sub[0] = __builtin_amdgcn_s_memrealtime();
   xq.conv<false>(Qm, LA_SQ, wl);
-  xk.conv<false>(Km, LA_SQ, wl + 128);
-  xv.conv<true>(Vt, SV, wl + 256);
+  if constexpr (!CROSS) {
+    xk.conv<false>(Km, LA_SQ, wl + 128);
+    xv.conv<true>(Vt, SV, wl + 256);
+  }
   bar_lds();
   if (sub && tid == 0) sub[1] = __builtin_amdgcn_s_memrealtime();
   bf16_t* P = Pall + wave * 16 * SP;
@@ -522,6 +556,32 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
     default: lk_attn_tiles<12>(Qm, Km, Vt, P, SV, SP, Lq, Lk, sl2, out, wave, lane); break;
   }
   if (sub && tid == 0) sub[2] = __builtin_amdgcn_s_memrealtime();  // wave 0's tiles done
+}
+
+// convolved memory keys 2 .. Lk - 1 of one layer (the expression of LaStrip::conv); one workgroup
+// per (head, clip): K [Lk_pad][32] then V^T [32][Lk_pad], bf16, other keys zero
+__global__ void lk_kv_cache_kernel(const float* __restrict__ kv_mem, const float* __restrict__ kw,
+                                   const float* __restrict__ kb, const float* __restrict__ vw,
+                                   const float* __restrict__ vb, int Ts, int Lkp, bf16_t* __restrict__ out) {
+  const int h = blockIdx.x, b = blockIdx.y, heads = gridDim.x, Lk = 1 + Ts;
+  bf16_t* kc = out + ((size_t)b * heads + h) * 2 * Lkp * 32;
+  bf16_t* vc = kc + Lkp * 32;
+  const float* m0 = kv_mem + (size_t)b * Ts * 2 * CH_D;
+  for (int e = threadIdx.x; e < 2 * Lkp * 32; e += blockDim.x) {
+    const bool isv = e >= Lkp * 32;
+    const int i = isv ? e - Lkp * 32 : e;
+    const int j = isv ? i % Lkp : i / 32, c = isv ? i / Lkp : i % 32;  // key, channel
+    float v = 0.f;
+    if (j >= 2 && j < Lk) {
+      const int col = (isv ? CH_D : 0) + h * 32 + c;
+      const float* w = isv ? vw : kw;
+      const float bb = isv ? vb[c] : kb[c];
+      const float x0 = m0[(size_t)(j - 2) * 2 * CH_D + col], x1 = m0[(size_t)(j - 1) * 2 * CH_D + col];
+      const float x2 = j + 1 < Lk ? m0[(size_t)j * 2 * CH_D + col] : 0.f;
+      v = bb + w[c * 3] * x0 + w[c * 3 + 1] * x1 + w[c * 3 + 2] * x2;
+    }
+    (isv ? vc : kc)[i] = j >= 2 && j < Lk ? f2bf(v) : (bf16_t)0;
+  }
 }
 
 size_t lk_attn_lds(int L, int Lk) {
@@ -605,6 +665,19 @@ bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C
   const int lkp = (1 + Ts + 31) / 32 * 32;  // memory keys, padded (whole-clip tiles: 96 .. 192)
   return dtype != 0 && d_model == CH_D && heads == 8 && L % CH_MT == 0 && L / CH_MT <= 8 && L >= 96 &&
          L <= ATT_LMAX && lkp >= 96 && lkp <= ATT_LMAX && C <= 128 && out_npad == 128 && lds <= 160 * 1024 - 256;
+}
+
+size_t long_kv_cache_bytes(int n, int Ts, int heads) {
+  const int Lkp = (1 + Ts + 31) / 32 * 32;
+  return (size_t)n * heads * 2 * Lkp * 32 * sizeof(bf16_t);
+}
+
+hipError_t launch_long_kv_cache(const float* kv_mem, const float* kw, const float* kb, const float* vw, const float* vb,
+                                int n, int Ts, int heads, bf16_t* out, hipStream_t s) {
+  if (n <= 0 || heads != CH_WAVES) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lk_kv_cache_kernel, dim3(heads, n), dim3(256), 0, s, kv_mem, kw, kb, vw, vb, Ts,
+                     (1 + Ts + 31) / 32 * 32, out);
+  return hipGetLastError();
 }
 
 int long_loop_capacity() {
