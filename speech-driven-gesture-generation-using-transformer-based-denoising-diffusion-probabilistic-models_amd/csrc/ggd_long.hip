@@ -188,30 +188,37 @@ __device__ __forceinline__ void lk_x_to_xs(X& x, const float* xv, int n) {
 // x rows go to HBM and, when `to_xs`, into the A rows of the next emb_x GEMM
 template <class X>
 __device__ __forceinline__ void lk_update(X& x, bool to_xs) {
+  // one work item = channel c x 4 consecutive frames: one Philox call gives their 4 normals
+  // (counter quad (c L + l) / 4, update_kernel's element -> quad map; L and l0 are multiples of 32)
   cla_T& a = x.a;
   const int C = a.C, L = a.L, l0 = x.part * CH_MT;
   const StepRec r = a.steps[x.it];
   const float* eps = (const float*)x.hh;
   float* xg = a.x + ((size_t)x.b * L + l0) * C;
-  for (int e = ltid(); e < CH_MT * CH_D; e += CH_NT) {
-    const int rr = e / CH_D, c = e % CH_D, l = l0 + rr;
-    if (c < C) {
+  const uint64_t seed = ((uint64_t)r.seed_hi << 32) | r.seed_lo;
+  for (int w = ltid(); w < C * (CH_MT / 4); w += CH_NT) {
+    const int c = w / (CH_MT / 4), q4 = (w % (CH_MT / 4)) * 4, l = l0 + q4;
+    float z[4];
+    if (a.noise) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) z[i] = a.noise[(size_t)x.it * a.n * C * L + ((size_t)x.b * C + c) * L + l + i];
+    } else {
+      philox_normal4(seed, r.clip_offset + (uint32_t)x.b, (uint32_t)r.i, TAG_STEP, (uint32_t)(c * L + l) >> 2, z);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = q4 + i;
       const float xo = ld_f32<CP_COH>(xg, (uint32_t)(rr * C + c));
-      const float ev = eps[rr * EPS_STR + c];
-      const size_t ncl = ((size_t)x.b * C + c) * L + l;
-      float z;
-      if (a.noise)
-        z = a.noise[(size_t)x.it * a.n * C * L + ncl];
-      else
-        z = philox_normal(((uint64_t)r.seed_hi << 32) | r.seed_lo, r.clip_offset + (uint32_t)x.b, (uint32_t)r.i, TAG_STEP,
-                          (uint32_t)(c * L + l));
-      const UpdOut o = upd_math(r, a.alg, xo, ev, false, 0.f, false, 0.f, 0.f, 0.f, z);
+      const UpdOut o = upd_math(r, a.alg, xo, eps[rr * EPS_STR + c], false, 0.f, false, 0.f, 0.f, 0.f, z[i]);
       xg[rr * C + c] = o.xn;
       if (to_xs) x.xs[rr * XS_STR + c] = f2bf(o.xn);
-    } else if (to_xs) {
-      x.xs[rr * XS_STR + c] = 0;
     }
   }
+  if (to_xs)  // emb_x's K padding: columns C .. 255 of the A rows are zero
+    for (int e = ltid(); e < CH_MT * (CH_D - C); e += CH_NT) {
+      const int rr = e / (CH_D - C), c = C + e % (CH_D - C);
+      x.xs[rr * XS_STR + c] = 0;
+    }
 }
 
 template <bool W8, int KIND, int IT, class X>
@@ -336,74 +343,63 @@ __device__ __forceinline__ void lk_chain(cla_T& a, cst_t sa, int b, int part, in
 // attention phase: head `head` of clip b over all its frames (ggd_attn.hip with 8 waves; the
 // Q / K / V rows another workgroup wrote are read past L1)
 // ------------------------------------------------------------------------------------------
-constexpr int LA_VPR = 4;                    // 16-byte channel vectors per 32-channel row
-constexpr int LA_NS = CH_NT / LA_VPR;        // 128 row strips
-constexpr int LA_SLMAX = (ATT_LMAX + LA_NS - 1) / LA_NS;
-constexpr int LA_SQ = 40;
+constexpr int LA_SQ = 40;                    // Q / K operand row stride (bf16, 16-byte pad)
 
-// conv input rows.  Rows outside [0, len) are the conv's zero padding; the load itself is always
-// issued (on a clamped row) and the value selected after, so every load of a strip is in flight at
-// once (a load under a divergent branch makes the compiler wait for it before the branch joins).
-// MEM = false: bf16 hand-off rows base[(row0 + j) ld + col], read past L1.  MEM = true: memory mode,
-// f32 rows: j = 0 the step-token row, j >= 1 base[(row0 + j - 1) ld + col] (constant inputs).
-template <bool MEM>
-struct LaSrc {
-  const void* base;
-  size_t row0;
-  int ld, col, len;
-  const float* step_row;
-  __device__ __forceinline__ void load(int j, int cv, float (&o)[8]) const {
-    const bool in = j >= 0 && j < len;
-    const int jj = in ? j : 0;
-    if constexpr (MEM) {
-      const float* p = jj == 0 ? step_row + cv * 8 : (const float*)base + (row0 + jj - 1) * (size_t)ld + col + cv * 8;
-      const float4 u = *(const float4*)p, v = *(const float4*)(p + 4);
-      const float t[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+// Raw conv inputs: NM bf16 hand-off images of `rows` rows x 32 channels into LDS [NM][rows + 2][32]
+// (rows 0 and rows + 1 are the conv's zero padding), each 16-byte unit loaded once (no halo
+// re-reads), every load issued before the first LDS write.  src[m] = base + col[m] (row stride ld).
+constexpr int LA_RAW_UNITS = (3 * ATT_LMAX * 4 + CH_NT - 1) / CH_NT;  // units per thread (max)
+template <int NM>
+__device__ __forceinline__ void la_stage_raw(const void* base, size_t row0, int ld, const int (&col)[3], int rows,
+                                             bf16_t* raw) {
+  const int tid = ltid(), per = rows * 4, total = NM * per;
+  uint4 v[LA_RAW_UNITS];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = in ? t[e] : 0.f;
-    } else {
-      const uint4 u = ld_16B<CP_XL>(base, (uint32_t)(((row0 + jj) * (size_t)ld + col + cv * 8) * 2));
-      const unsigned w[4] = {u.x, u.y, u.z, u.w};
+  for (int i = 0; i < LA_RAW_UNITS; ++i) {
+    const int u = min(tid + i * CH_NT, total - 1), m = u / per, r = (u % per) / 4, cv = u % 4;
+    v[i] = ld_16B<CP_XL>(base, (uint32_t)(((row0 + r) * (size_t)ld + col[m] + cv * 8) * 2));
+  }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        o[2 * q] = in ? __uint_as_float(w[q] << 16) : 0.f;
-        o[2 * q + 1] = in ? __uint_as_float(w[q] & 0xffff0000u) : 0.f;
+  for (int i = 0; i < LA_RAW_UNITS; ++i) {
+    const int u = tid + i * CH_NT;
+    if (u >= total) continue;
+    const int m = u / per, r = (u % per) / 4, cv = u % 4;
+    *(uint4*)(raw + ((size_t)m * (rows + 2) + r + 1) * 32 + cv * 8) = v[i];
+  }
+  for (int u = tid; u < NM * 2 * 4; u += CH_NT) {  // halo rows
+    const int m = u / 8, h = (u / 4) % 2, cv = u % 4;
+    *(uint4*)(raw + ((size_t)m * (rows + 2) + h * (rows + 1)) * 32 + cv * 8) = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// conv of raw image m into its operand image: out[i] = b + w0 in[i-1] + w1 in[i] + w2 in[i+1]
+// (LaStrip::conv's expression); TRANS writes V^T.  wl = [w0|w1|w2|b][32] of this matrix.
+template <bool TRANS>
+__device__ __forceinline__ void la_conv_raw(const bf16_t* raw, int rows, const float* wl, bf16_t* dst, int S) {
+  for (int u = ltid(); u < rows * 4; u += CH_NT) {
+    const int i = u / 4, cv = u % 4;
+    float x[3][8];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint4 q = *(const uint4*)(raw + (size_t)(i + k) * 32 + cv * 8);
+      const unsigned w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        x[k][2 * e] = __uint_as_float(w[e] << 16);
+        x[k][2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
       }
     }
-  }
-};
-
-struct LaStrip {
-  float x[LA_SLMAX + 2][8];
-  int sl, rows;
-  template <class S>
-  __device__ __forceinline__ void load(const S& src, int rows_) {
-    rows = rows_;
-    sl = (rows + LA_NS - 1) / LA_NS;
-    const int t = ltid(), cv = t % LA_VPR, sid = t / LA_VPR;
 #pragma unroll
-    for (int s = 0; s < LA_SLMAX + 2; ++s)
-      if (s < sl + 2) src.load(sid * sl - 1 + s, cv, x[s]);
-  }
-  template <bool TRANS>
-  __device__ __forceinline__ void conv(bf16_t* dst, int S, const float* wl) const {
-    const int t = ltid(), cv = t % LA_VPR, sid = t / LA_VPR;
-#pragma unroll
-    for (int s = 0; s < LA_SLMAX; ++s) {
-      const int r = sid * sl + s;
-      if (s >= sl || r >= rows) continue;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = cv * 8 + e;
-        const float v = wl[96 + c] + wl[c] * x[s][e] + wl[32 + c] * x[s + 1][e] + wl[64 + c] * x[s + 2][e];
-        if (TRANS)
-          dst[c * S + r] = f2bf(v);
-        else
-          dst[r * S + c] = f2bf(v);
-      }
+    for (int e = 0; e < 8; ++e) {
+      const int c = cv * 8 + e;
+      const float v = wl[96 + c] + wl[c] * x[0][e] + wl[32 + c] * x[1][e] + wl[64 + c] * x[2][e];
+      if (TRANS)
+        dst[c * S + i] = f2bf(v);
+      else
+        dst[i * S + c] = f2bf(v);
     }
   }
-};
+}
 
 // the query tiles of one wave, LKT (16-key tiles, Lk padded to 32) fixed at compile time: every
 // LDS fragment of a matrix product is read before its MFMAs (no per-tile branch between them)
@@ -481,12 +477,13 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
   bf16_t* Vt = Km + Lkp * LA_SQ;
   bf16_t* Pall = Vt + 32 * SV;
   float* wl = (float*)(Pall + CH_WAVES * 16 * SP);
+  bf16_t* raw = (bf16_t*)(wl + 12 * 32);
   const size_t row0 = (size_t)b * Lq;
-  LaStrip xq, xk, xv;
   if constexpr (CROSS) {
     // keys >= 2 from the step-invariant convolved cache (ggd_set_memory); keys 0 and 1 depend on the
     // step token (memory row 0) and are convolved here, in the cache kernel's expression
-    xq.load(LaSrc<false>{a.q, row0, CH_D, head * 32, Lq, nullptr}, Lq);
+    const int colq[3] = {head * 32, 0, 0};
+    la_stage_raw<1>(a.q, row0, CH_D, colq, Lq, raw);
     const bf16_t* kc = Ly.kvc + ((size_t)b * CH_WAVES + head) * 2 * Lkp * 32;
     const bf16_t* vc = kc + Lkp * 32;
     const int kpr = Lkp / 8;  // 16-byte units per V^T row
@@ -520,9 +517,8 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
       Km[r * LA_SQ + c] = f2bf(v);
     }
   } else {
-    xq.load(LaSrc<false>{a.qkv, row0, 3 * CH_D, head * 32, Lq, nullptr}, Lq);
-    xk.load(LaSrc<false>{a.qkv, row0, 3 * CH_D, CH_D + head * 32, Lk, nullptr}, Lk);
-    xv.load(LaSrc<false>{a.qkv, row0, 3 * CH_D, 2 * CH_D + head * 32, Lk, nullptr}, Lk);
+    const int cols[3] = {head * 32, CH_D + head * 32, 2 * CH_D + head * 32};
+    la_stage_raw<3>(a.qkv, row0, 3 * CH_D, cols, Lq, raw);  // self: Lk = Lq
   }
   for (int i = tid; i < 12 * 32; i += CH_NT) {
     const int m = i / 128, k = (i / 32) % 4, c = i % 32;
@@ -539,10 +535,10 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
   }
   bar_lds();
   if (sub && tid == 0) sub[0] = __builtin_amdgcn_s_memrealtime();
-  xq.conv<false>(Qm, LA_SQ, wl);
+  la_conv_raw<false>(raw, Lq, wl, Qm, LA_SQ);
   if constexpr (!CROSS) {
-    xk.conv<false>(Km, LA_SQ, wl + 128);
-    xv.conv<true>(Vt, SV, wl + 256);
+    la_conv_raw<false>(raw + (size_t)(Lq + 2) * 32, Lk, wl + 128, Km, LA_SQ);
+    la_conv_raw<true>(raw + (size_t)2 * (Lq + 2) * 32, Lk, wl + 256, Vt, SV);
   }
   bar_lds();
   if (sub && tid == 0) sub[1] = __builtin_amdgcn_s_memrealtime();
@@ -587,7 +583,7 @@ __global__ void lk_kv_cache_kernel(const float* __restrict__ kv_mem, const float
 size_t lk_attn_lds(int L, int Lk) {
   const int Lkp = (Lk + 31) / 32 * 32, Lqp = (L + 15) / 16 * 16;
   return 2 * ((size_t)Lqp * LA_SQ + (size_t)Lkp * LA_SQ + 32 * (size_t)(Lkp + 8) + CH_WAVES * 16 * (size_t)(Lkp + 8)) +
-         sizeof(float) * 12 * 32;
+         sizeof(float) * 12 * 32 + 2 * (size_t)3 * (L + 2) * 32;  // + the raw conv inputs
 }
 
 // ------------------------------------------------------------------------------------------
