@@ -143,8 +143,52 @@ struct LkGeo {
   static constexpr int PRM_LN0 = prm(PL::NS - 1) + 2 * PL::s[PL::NS - 1].ncols;
   static constexpr int ln(int i) { return PRM_LN0 + 2 * CH_D * i; }                            // gamma | beta
   static constexpr int PRM_TOTAL = PRM_LN0 + 2 * CH_D * PL::NS;
-  static constexpr size_t LDS = LK_HS + sizeof(bf16_t) * CH_MT * (XS_STR + HH_STR) + sizeof(float) * PRM_TOTAL;
+  static constexpr size_t LDS = LK_HS + sizeof(bf16_t) * CH_MT * (XS_STR + HH_STR) + sizeof(float) * (PRM_TOTAL + 2 * CH_MT);
 };
+
+// ch_layernorm with the statistics on two waves (gemm_kernel's PRO_LN lanes and order) and the
+// normalisation on all eight: the same values, a quarter of the per-thread element work.
+// st: LDS [32][mu, rs]
+__device__ __forceinline__ void lk_layernorm(const float* hs, const float* gm, const float* bt, bf16_t* xs, float* st) {
+  const int tid = ltid();
+  if (tid < CH_MT * 4) {
+    const int r = tid >> 2, j = tid & 3;
+    float4 v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = *(const float4*)(hs + r * HS_STR + (j + 4 * i) * 4);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    const float mu = s / (float)CH_D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float d0 = v[i].x - mu, d1 = v[i].y - mu, d2 = v[i].z - mu, d3 = v[i].w - mu;
+      q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    }
+    q += __shfl_xor(q, 1);
+    q += __shfl_xor(q, 2);
+    if (j == 0) {
+      st[2 * r] = mu;
+      st[2 * r + 1] = 1.0f / sqrtf(q / (float)CH_D + 1e-5f);
+    }
+  }
+  ch_bar();
+  for (int e = tid; e < CH_MT * CH_D / 4; e += CH_NT) {
+    const int r = e / (CH_D / 4), k = (e % (CH_D / 4)) * 4;
+    const float mu = st[2 * r], rs = st[2 * r + 1];
+    const float4 x = *(const float4*)(hs + r * HS_STR + k);
+    const float4 g = *(const float4*)(gm + k);
+    const float4 b = *(const float4*)(bt + k);
+    bf16_t* dst = xs + r * XS_STR + k;
+    dst[0] = f2bf((x.x - mu) * rs * g.x + b.x);
+    dst[1] = f2bf((x.y - mu) * rs * g.y + b.y);
+    dst[2] = f2bf((x.z - mu) * rs * g.z + b.z);
+    dst[3] = f2bf((x.w - mu) * rs * g.w + b.w);
+  }
+}
 
 // stage arguments and layers live in constant memory: field reads are scalar loads
 typedef const __attribute__((address_space(4))) ChainStage* cst_t;
@@ -233,7 +277,7 @@ __device__ __forceinline__ void lk_iter(X& x) {
   if constexpr (l == 0 && si > 0) {  // stage hand-offs (LDS); the prefetched weights stay in flight
     ch_bar();
     if constexpr (kind == SK_F1 || kind == SK_P || kind == SK_PO || kind == SK_P2) {
-      ch_layernorm(x.hs, x.prm + GE::ln(si), x.prm + GE::ln(si) + CH_D, x.xs, ltid());
+      lk_layernorm(x.hs, x.prm + GE::ln(si), x.prm + GE::ln(si) + CH_D, x.xs, x.prm + GE::PRM_TOTAL);
       ch_bar();
     } else if constexpr (kind == SK_E) {  // after out_layers: the update, its x rows feed emb_x
       lk_update(x, true);
