@@ -105,13 +105,9 @@ constexpr int EPS_STR = 132;  // f32 eps rows of the out_layers projection (in t
 // ------------------------------------------------------------------------------------------
 enum { SK_E = 0, SK_R, SK_F1, SK_F2, SK_P, SK_PO, SK_P2 };
 struct Stg { int kind, ncols, nch; };
-enum { K_INIT = 0, K_A, K_B, K_BL, K_BLL };
+enum { K_A = 0, K_B, K_BL, K_BLL };  // chain A, chain B, chain B ending a step, ending the loop
 
 template <int KIND> struct LkPlan;
-template <> struct LkPlan<K_INIT> {
-  static constexpr int NS = 2;
-  static constexpr Stg s[NS] = {{SK_E, 256, 1}, {SK_P2, 768, 1}};
-};
 template <> struct LkPlan<K_A> {
   static constexpr int NS = 2;
   static constexpr Stg s[NS] = {{SK_R, 256, 1}, {SK_P, 256, 1}};
@@ -218,19 +214,6 @@ __device__ __forceinline__ void lk_issue(X& x) {
   ch_load<W8, GE::TGB>(x.bb[IT % LK_DEPTH], wb, x.lane16, (l / nch) * CH_WAVES * tg, l % nch, upt, tg);
 }
 
-// x rows of the block (coherent: this workgroup wrote them in an earlier step) -> bf16 A rows,
-// columns >= C zero (the emb_x GEMM's PRO_F32 staging)
-template <class X>
-__device__ __forceinline__ void lk_x_to_xs(X& x, const float* xv, int n) {
-  const int C = x.a.C;
-  for (int e = ltid(); e < CH_MT * CH_D; e += CH_NT) {
-    const int r = e / CH_D, c = e % CH_D;
-    x.xs[r * XS_STR + c] = c < C ? f2bf(xv[r * C + c]) : (bf16_t)0;
-  }
-}
-
-// the posterior update of the block's frames (update_kernel's arithmetic), eps from LDS; the new
-// x rows go to HBM and, when `to_xs`, into the A rows of the next emb_x GEMM
 template <class X>
 __device__ __forceinline__ void lk_update(X& x, bool to_xs) {
   // one work item = channel c x 4 consecutive frames: one Philox call gives their 4 normals
@@ -367,16 +350,14 @@ __device__ __forceinline__ void lk_chain(cla_T& a, cst_t sa, int b, int part, in
       x.prm[GE::ln(si) + CH_D + tid] = sa[si].ln_b[tid];
     }
   }
-  constexpr int k0 = PL::s[0].kind;
-  if constexpr (k0 == SK_R) {  // attention output rows of the block (written by the head parts)
+  static_assert(PL::s[0].kind == SK_R, "every chain phase opens with the attention output projection");
+  {  // attention output rows of the block (written by the head parts)
     const bf16_t* src = (const bf16_t*)a.att + ((size_t)b * a.L + part * CH_MT) * CH_D;
 #pragma unroll
     for (int i = 0; i < CH_MT * CH_D / 8 / CH_NT; ++i) {
       const int e = tid + i * CH_NT, r = e / (CH_D / 8), cv = e % (CH_D / 8);
       *(uint4*)(x.xs + r * XS_STR + 8 * cv) = ld_16B<CP_XL>(src, (uint32_t)((r * CH_D + 8 * cv) * 2));
     }
-  } else {  // SK_E at the loop start: x_T rows
-    lk_x_to_xs(x, a.x + ((size_t)b * a.L + part * CH_MT) * a.C, 0);
   }
   ch_bar();
   lk_iter<W8, KIND, 0>(x);
