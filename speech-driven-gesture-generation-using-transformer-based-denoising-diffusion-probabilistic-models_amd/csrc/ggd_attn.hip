@@ -110,6 +110,70 @@ struct AcStrip {
   }
 };
 
+// one wave's 16-query tiles with LKT 16-key tiles (Lk padded to 32) fixed at compile time: every
+// LDS fragment of a matrix product is read before its MFMAs
+template <int LKT>
+__device__ __forceinline__ void ac_tiles(const bf16_t* Qm, const bf16_t* Km, const bf16_t* Vt, bf16_t* P, int SV, int SP,
+                                         int Lq, int Lk, float sl2, bf16_t* out, int ldo, int wave, int lane) {
+  const int c16 = lane & 15, g4 = lane >> 4;
+  for (int rt = wave; rt * 16 < Lq; rt += AC_NW) {
+    const bf16x8 qa = *(const bf16x8*)(Qm + (rt * 16 + c16) * AC_SQ + g4 * 8);
+    bf16x8 kb[LKT];
+#pragma unroll
+    for (int t = 0; t < LKT; ++t) kb[t] = *(const bf16x8*)(Km + (t * 16 + c16) * AC_SQ + g4 * 8);
+    f32x4 s[LKT];
+#pragma unroll
+    for (int t = 0; t < LKT; ++t)
+      s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kb[t], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < LKT; ++t) {
+        const float v = t * 16 + c16 < Lk ? s[t][r] * sl2 : -INFINITY;
+        s[t][r] = v;
+        mx = fmaxf(mx, v);
+      }
+      mx = group_max<16>(mx);
+      float sum = 0.f;
+#pragma unroll
+      for (int t = 0; t < LKT; ++t) {
+        const float p = t * 16 + c16 < Lk ? __builtin_amdgcn_exp2f(s[t][r] - mx) : 0.f;
+        s[t][r] = p;
+        sum += p;
+      }
+      sum = group_sum<16>(sum);
+      const float inv = 1.0f / sum;
+#pragma unroll
+      for (int t = 0; t < LKT; ++t) P[(4 * g4 + r) * SP + t * 16 + c16] = f2bf(s[t][r] * inv);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    constexpr int KS = LKT / 2;  // 32-key steps of P V
+    bf16x8 pa[KS], vb[2][KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      pa[k] = *(const bf16x8*)(P + c16 * SP + k * 32 + g4 * 8);
+      vb[0][k] = *(const bf16x8*)(Vt + c16 * SV + k * 32 + g4 * 8);
+      vb[1][k] = *(const bf16x8*)(Vt + (16 + c16) * SV + k * 32 + g4 * 8);
+    }
+    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[k], vb[ct][k], o[ct], 0, 0, 0);
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = rt * 16 + 4 * g4 + r;
+        if (i < Lq) out[(size_t)i * ldo + ct * 16 + c16] = f2bf(o[ct][r]);
+      }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 __global__ void __launch_bounds__(AC_NT) attn_clip_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int h = blockIdx.x, b = blockIdx.y, Lq = a.Lq, Lk = a.Lk;
@@ -154,57 +218,17 @@ __global__ void __launch_bounds__(AC_NT) attn_clip_kernel(AttnArgs a) {
   xv.conv<true>(Vt, G.SV, wl + 8 * AC_DK);
   __syncthreads();
 
-  // per wave: 16-query tiles rt = wave, wave + NW, ...
-  const int c16 = lane & 15, g4 = lane >> 4, LKT = G.Lkp / 16;
+  // per wave: 16-query tiles rt = wave, wave + NW, ...; the key-tile count is a template constant
   bf16_t* P = (bf16_t*)(smem + G.off_p) + wave * 16 * G.SP;
   bf16_t* out = (bf16_t*)a.out + row0 * a.ldo + (size_t)h * AC_DK;
   const float sl2 = a.scale * 1.4426950408889634f;  // softmax on exp2: e^(s - m) = 2^((s - m) log2 e)
-  for (int rt = wave; rt * 16 < Lq; rt += AC_NW) {
-    f32x4 s[ATT_KT];
-#pragma unroll
-    for (int t = 0; t < ATT_KT; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (t < LKT) att_mma<bf16_t>(s[t], Qm, rt * 16, AC_SQ, Km, t * 16, AC_SQ, AC_DK, lane);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < ATT_KT; ++t) {
-        const bool ok = t < LKT && t * 16 + c16 < Lk;
-        const float v = ok ? s[t][r] * sl2 : -INFINITY;
-        s[t][r] = v;
-        mx = fmaxf(mx, v);
-      }
-      mx = group_max<16>(mx);
-      float sum = 0.f;
-#pragma unroll
-      for (int t = 0; t < ATT_KT; ++t) {
-        const bool ok = t < LKT && t * 16 + c16 < Lk;
-        const float p = ok ? __builtin_amdgcn_exp2f(s[t][r] - mx) : 0.f;
-        s[t][r] = p;
-        sum += p;
-      }
-      sum = group_sum<16>(sum);
-      const float inv = 1.0f / sum;
-#pragma unroll
-      for (int t = 0; t < ATT_KT; ++t)
-        if (t < LKT) P[(4 * g4 + r) * G.SP + t * 16 + c16] = f2bf(s[t][r] * inv);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int ct = 0; ct < AC_DK / 16; ++ct) {
-      f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
-      att_mma<bf16_t>(o, P, 0, G.SP, Vt, ct * 16, G.SV, G.Lkp, lane);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = rt * 16 + 4 * g4 + r;
-        if (i < Lq) out[(size_t)i * a.ldo + ct * 16 + c16] = f2bf(o[r]);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+  switch (G.Lkp / 16) {  // attention_clip_supported: 1 <= Lk <= 192
+    case 2: ac_tiles<2>(Qm, Km, Vt, P, G.SV, G.SP, Lq, Lk, sl2, out, a.ldo, wave, lane); break;
+    case 4: ac_tiles<4>(Qm, Km, Vt, P, G.SV, G.SP, Lq, Lk, sl2, out, a.ldo, wave, lane); break;
+    case 6: ac_tiles<6>(Qm, Km, Vt, P, G.SV, G.SP, Lq, Lk, sl2, out, a.ldo, wave, lane); break;
+    case 8: ac_tiles<8>(Qm, Km, Vt, P, G.SV, G.SP, Lq, Lk, sl2, out, a.ldo, wave, lane); break;
+    case 10: ac_tiles<10>(Qm, Km, Vt, P, G.SV, G.SP, Lq, Lk, sl2, out, a.ldo, wave, lane); break;
+    default: ac_tiles<12>(Qm, Km, Vt, P, G.SV, G.SP, Lq, Lk, sl2, out, a.ldo, wave, lane); break;
   }
 }
 
