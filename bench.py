@@ -3,8 +3,12 @@
 One "step" = one full sampling pass over one batch of synthetic BEAT-shaped clips: the HIP
 speech encoder (once per clip) + all T' denoise steps + the all-gather of the final poses.
 Workloads (BASELINE.json configs; beat-ours, 123 pose channels, random-init weights):
+  c1: configs/tedexp-ours.json (two-way CrossAttention decoder, d 512, 10 layers, 126 pose
+     channels), ONE clip of L = 34 frames, 36,266-sample wav, respacing "50" DDPM, f32 (the
+     reference computes in fp32) -- the CPU oracle's full 50-step loop is timed end to end beside it;
   c2 (default, the metric's config): 32 clips/GPU, L = 40, 32,000-sample wavs, DDPM T = 1000,
-     bf16 -- one launch of the clip-group persistent loop mk_kernel per pass;
+     bf16 -- one launch of the clip-group persistent loop mk_kernel per pass; plus an f32
+     sub-record (one pass of the same workload in f32, the parity precision);
   c4: 32 clips/GPU, L = 160, DDPM 1000, fp8-e4m3 step weights -- generic per-phase kernels;
   c5: 128 clips/GPU, L = 40, DDIM-50 -- one launch of the clip-pair loop (psk_kernel, two
      workgroups per clip) per pass; the encoder runs inline (WORKLOADS[...]["overlap"]).
@@ -55,11 +59,29 @@ def encoder_flop(wav_len):
 def clip_step_flops(L, Tm, d, C, layers):
     """Algorithmic FLOPs of one decoder forward for one clip with the step-invariant memory
     K/V cached (314.3 MFLOP at L=40, Tm=32): GEMMs 2*M*K*N, attention
-    4*Lq*Lk*d, depthwise conv 6 FLOP per output (Q/K/V self, Q cross)."""
+    4*Lq*Lk*d, depthwise conv 6 FLOP per output (Q/K/V self, Q cross); plus the per-step
+    memory work the cache cannot remove: the step MLP, emb_mem of the step token and, per layer,
+    the cross-attention K / V of memory rows 0-1 (the step token and its 3-tap conv reach).
+    313.9 MFLOP at L = 40 (SURVEY's 314.3 within 0.2 %), 1,389.1 at L = 160."""
     gemm = 2 * L * (C * d + layers * (3 * d * d + d * d + d * d + d * d + 2 * 4 * d * d) + d * C)
     attn = layers * 4 * L * (L + Tm) * d
     conv = layers * 6 * L * d * 4
-    return gemm + attn + conv
+    step = 2 * 2 * d * d + 2 * d * d + layers * 2 * (2 * 2 * d * d)
+    return gemm + attn + conv + step
+
+
+def twoway_clip_step_flops(L, Tm, d, C, layers):
+    """The two-way CrossAttention decoder (nn.py:381-447; C1): per layer self-attention on x (L
+    rows) and on the memory (Tm rows), joint cross-attention over J = L + Tm rows, FFN on x and
+    (all but the last layer) on the memory; emb_x, emb_mem, out projection, step MLP.  GEMMs +
+    attention = SURVEY.md 8d's 11,839.6 MFLOP at L = 34, Tm = 104, d = 512; + the 3-tap convs."""
+    J = L + Tm
+    g = sum(8 * L * d * d + 8 * Tm * d * d + 8 * J * d * d + 16 * L * d * d + (16 * Tm * d * d if i < layers - 1 else 0)
+            for i in range(layers))
+    g += 2 * L * C * d + 2 * Tm * d * d + 2 * L * d * C + 4 * d * d
+    attn = layers * 4 * d * (L * L + Tm * Tm + J * J)
+    conv = layers * 6 * 3 * d * (L + Tm + J)
+    return g + attn + conv
 
 
 def kb_flop(n, L, Lk, d):
@@ -77,8 +99,11 @@ def attn_flop(n, L, Lk, d):
 
 # BASELINE.json configs as bench workloads (per GPU); C3 is C2 on 8 GPUs (--gpus 8)
 WORKLOADS = {
+    "c1": dict(batch_per_gpu=1, alg="ddpm", respacing="50", seq_mult=1, dtype="f32",
+               config=os.path.join(ROOT, "configs", "tedexp-ours.json"),
+               label="tedexp-ours C1 (two-way decoder)", overlap=False),
     "c2": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=1,
-               label="beat-ours C2", overlap=False),
+               label="beat-ours C2", overlap=False, f32_subrecord=True),
     "c4": dict(batch_per_gpu=32, alg="ddpm", respacing="", seq_mult=4, dtype="fp8",
                label="beat-ours C4 long clip (seq_len x4)", overlap=False),
     "c5": dict(batch_per_gpu=128, alg="ddim", respacing="ddim50", seq_mult=1,
@@ -97,6 +122,22 @@ WORKLOADS = {
 PMC_SUMMARY = {"c2": "r02a", "c4": "r02n", "c5": "r02d"}   # profile tag per workload (its dominant kernel's code)
 
 
+def csrc_hash():
+    """sha256 over the HIP sources the kernels are built from (csrc/*.hip, *.h, include/*.h):
+    a PMC summary records it (scripts/pmc_summary.py) and is used only while it still matches."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    pkg_csrc = glob.glob(os.path.join(ROOT, "*_amd", "csrc"))
+    files = sorted(glob.glob(os.path.join(pkg_csrc[0], "*.h*")) if pkg_csrc else []) + \
+        sorted(glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(kernel_prefix, workload):
     path = os.path.join(ROOT, "profiles", f"{PMC_SUMMARY.get(workload, 'r02a')}_pmc_{workload}_summary.json")
     try:
@@ -106,6 +147,9 @@ def pmc_traffic(kernel_prefix, workload):
         return None
     if d.get("_workload") != workload:
         return None
+    if d.get("_csrc") != csrc_hash():   # the kernels changed since the counters were taken: no traffic figure
+        return {"stale": True, "source": os.path.relpath(path, ROOT), "summary_csrc": d.get("_csrc"),
+                "current_csrc": csrc_hash()}
     for k, e in d.items():
         name = k.replace("(anonymous namespace)::", "")
         if name.startswith("void ggd::" + kernel_prefix) and "hbm_read_bytes" in e and "hbm_write_bytes" in e:
@@ -120,9 +164,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--config", default=os.path.join(ROOT, "configs", "beat-ours.json"))
+    p.add_argument("--config", default=None, help="config JSON (default: the workload's)")
     p.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
-                   help="BASELINE.json config: c2 (default, the metric's config), c4 long clip, c5 DDIM-50")
+                   help="BASELINE.json config: c2 (default, the metric's config), c1 tedexp, c4 long clip, c5 DDIM-50")
+    p.add_argument("--no-f32-subrecord", action="store_true", help="c2: skip the one-pass f32 sub-record")
     p.add_argument("--batch-per-gpu", type=int, default=None)
     p.add_argument("--dtype", default=None, choices=["bf16", "f32", "fp8"],
                    help="fp8: bf16 activations + e4m3 per-step decoder weights (default for c4)")
@@ -146,6 +191,8 @@ def parse():
         if getattr(a, k) is None:
             setattr(a, k, w[k])
     a.seq_mult = w["seq_mult"]
+    if a.config is None:
+        a.config = w.get("config", os.path.join(ROOT, "configs", "beat-ours.json"))
     if a.dtype is None:
         a.dtype = w.get("dtype", "bf16")
     if a.cpu_steps is None:
@@ -184,9 +231,10 @@ def log(*a):
 T_START = time.perf_counter()
 
 
-def cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, n_steps, alg, n_samples=3):
+def cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, n_steps, alg, n_samples=3, respacing=""):
     """Oracle on the host cores: faithful per-step encoder; ``n_samples`` timed samples of
-    ``n_steps`` denoise steps each, extrapolated x T; the median is the value."""
+    ``n_steps`` denoise steps each, extrapolated x T; the median is the value.  n_steps >= T: the
+    whole loop end to end (C1), no extrapolation."""
     from oracle import ref_denoiser, ref_diffusion
     affinity = sorted(os.sched_getaffinity(0))
     cores = len(affinity)
@@ -198,7 +246,9 @@ def cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, n_steps, alg, n_samples=3
     om = ref_denoiser.OracleModel(sd, ocfg, cache_speech=False)
     g = th.Generator().manual_seed(1)
     wav = th.randn(B, wav_len, generator=g) * 0.1
-    sch = ref_diffusion.make_schedule("linear", 1000, "ddim%d" % T if alg == "ddim" and T < 1000 else "")
+    sch = ref_diffusion.make_schedule("linear", 1000, respacing)
+    assert sch.num_timesteps == T
+    n_steps = min(n_steps, T)
     noise = ref_diffusion.TorchNoise(2)
     ref_diffusion.sample_loop(sch, om, (B, arch["d_pose"], L), {"wav": wav}, noise, alg, n_steps=1)
     log("cpu baseline warm-up step done")
@@ -226,10 +276,40 @@ def cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, n_steps, alg, n_samples=3
         "spread": round((max(fps) - min(fps)) / statistics.median(fps), 4),
         "sample": (f"median of {n_samples} samples, each {n_steps} {alg.upper()} denoise steps of B={B} clips "
                    f"(per-step speech encoder, fp32 oracle) after 1 warm-up step; ms/step "
-                   f"{', '.join('%.0f' % (p * 1e3) for p in per)}; extrapolated x{T} steps; "
+                   f"{', '.join('%.0f' % (p * 1e3) for p in per)}; "
+                   + (f"the whole {T}-step loop end to end (no extrapolation); " if n_steps == T else
+                      f"extrapolated x{T} steps; ") +
                    f"{th.get_num_threads()} torch threads, process affinity CPUs {aff} ({len(affinity)}); "
                    f"CPU: {model_name}"),
     }
+
+
+def f32_subrecord(pkg, cfg, sd, d_pose, L, B, wav, loop_name, diffusion, dev, T, clip_step):
+    """One pass of the same workload with the f32 decoder (the parity precision; the reference
+    computes in fp32), after one warm-up pass: frames/s and its loop's fraction of the f32 MFMA peak."""
+    import ctypes
+    model, _, _, _, _ = pkg.create_model(d_pose, cfg.Model, dtype="f32", device=dev)
+    model.load_state_dict(sd)
+    loop = diffusion.p_sample_loop if loop_name == "ddpm" else diffusion.ddim_sample_loop
+    run = lambda: loop(model, (B, d_pose, L), model_kwargs={"wav": wav}, seed=7, extras=False)["sample"]
+    run()
+    th.cuda.synchronize(dev)
+    ctx = next(iter(model._ctx.values()))
+    ctx.lib.ggd_set_profiling(ctx.h, 1)
+    t0 = time.perf_counter()
+    out = run()
+    th.cuda.synchronize(dev)
+    model.sync()
+    el = time.perf_counter() - t0
+    ctx.lib.ggd_set_profiling(ctx.h, 0)
+    avg, cnt = ctypes.c_double(), ctypes.c_int64()
+    ctx.lib.ggd_kernel_time(ctx.h, 0, ctypes.byref(avg), ctypes.byref(cnt))
+    assert bool(th.isfinite(out).all())
+    ach = clip_step * B * T / max(1, cnt.value) / (avg.value * 1e-6) / 1e12 if avg.value > 0 else None
+    model._release()
+    return {"value": round(B * L / el, 2), "unit": "frames/s", "ms_per_step": round(el * 1e3, 3), "steps": 1,
+            "warmup": 1, "dtype": "f32", "kernel_avg_launch_us": round(avg.value, 3), "launches": cnt.value,
+            "roofline_frac_f32": round(ach / F32_PEAK_TFLOPS, 6) if ach else None, "peak_tflops": F32_PEAK_TFLOPS}
 
 
 def rehearse(args, rank, world):
@@ -287,6 +367,8 @@ def rehearse(args, rank, world):
 
 def main():
     args = parse()
+    if args.workload == "c1" and args.gpus > 1:
+        raise SystemExit("c1 is one clip (B = 1): single GPU only")
     if args.gpus > 1 and "RANK" not in os.environ:
         # one rank per GPU: spawn them before anything touches the GPU, exit with their code
         raise SystemExit(self_launch(sys.argv[1:], args.gpus))
@@ -308,14 +390,19 @@ def main():
     pkg = ge.load_package()
     sharding = __import__(ge.PKG_NAME + ".sharding", fromlist=["x"])
     cfg = pkg.load_config(args.config)
-    d_pose = int(cfg.Data.get("d_pose", 123)) if "Data" in cfg else 123
-    L = int(cfg.Data.pose_window_len) * args.seq_mult
-    wav_len = int(cfg.Data.wav_sr * L / cfg.Data.pose_fps)
+    if "pose_window_len" in cfg.Data:   # beat-ours
+        d_pose = int(cfg.Data.get("d_pose", 123))
+        L = int(cfg.Data.pose_window_len) * args.seq_mult
+        wav_len = int(cfg.Data.wav_sr * L / cfg.Data.pose_fps)
+    else:                               # tedexp (legacy schema): n_poses at 15 fps, 16 kHz audio (generator.py:115)
+        d_pose = int(cfg.Data.pose_dim)
+        L = int(cfg.Data.n_poses)
+        wav_len = int(16000 * L / cfg.Data.pose_resampling_fps)
     model, diffusion, _, _, _ = pkg.create_model(d_pose, cfg.Model, dtype=args.dtype, device=dev)
     if args.respacing:
         diffusion = pkg.create_diffusion(dict(cfg.Model.Diffusion, timestep_respacing=args.respacing), False)
     arch = model.arch
-    sd = pkg.init_state_dict(arch, seed=0)
+    sd = pkg.init_state_dict(arch, seed=0, bounded=args.workload == "c1")
     model.load_state_dict(sd)
     B = args.batch_per_gpu
     n_total = B * world
@@ -365,6 +452,7 @@ def main():
         if profiled:
             lib.ggd_set_profiling(ctx.h, 0)
     th.cuda.synchronize(dev)
+    model.sync()   # every pass's persistent-loop status words (checked after the non-blocking calls)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -387,12 +475,19 @@ def main():
     value = frames / elapsed
     d = arch["d_model"]
     Tm = 1 + int(ctx.desc.speech_len)
-    clip_step = clip_step_flops(L, Tm, d, d_pose, arch["n_layers"])
+    twoway = arch["decoder"] == "cross_attention"
+    clip_step = (twoway_clip_step_flops if twoway else clip_step_flops)(L, Tm, d, d_pose, arch["n_layers"])
     # fp8 weights are dequantized into bf16 MFMA tiles (non-scaled fp8 MFMA runs at the bf16 rate,
     # MI355X_MICROARCH.md): priced against the bf16 peak
     peak = F32_PEAK_TFLOPS if args.dtype == "f32" else BF16_PEAK_TFLOPS
     roof = None
-    if prof and prof_n:
+    if twoway:   # C1 runs on the generic kernels, no single dominant kernel: the whole pass is priced
+        ach = clip_step * B * T / (elapsed / args.steps) / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 6), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 8), "traffic": None,
+                "kernel": "whole pass (two-way decoder on the generic per-op kernels, B = 1: launch-bound)",
+                "timing": "wall clock of the timed passes", "flop_per_launch": clip_step * B * T, "launches": args.steps}
+    elif prof and prof_n:
         avg_us = sum(prof_us) / prof_n
         if prof_kind == 1:   # the persistent loop: one launch runs all T denoise steps of the batch
             flop = clip_step * B * T / prof_n   # one launch per chunk of <= 32 clips
@@ -427,7 +522,8 @@ def main():
             prof_kind, "kb_kernel"),
                          args.workload)
         roof = {"bound": "mfma", "achieved": round(ach, 3), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 6), "traffic": tr and tr["bytes_per_launch"], "traffic_detail": tr, "kernel": kernel, "timing": timing,
+                "frac": round(ach / peak, 6), "traffic": tr.get("bytes_per_launch") if tr else None,
+                "traffic_detail": tr, "kernel": kernel, "timing": timing,
                 "flop_per_launch": flop, "avg_launch_us": round(avg_us, 3), "launches": prof_n}
     frame_flop = (T * clip_step + encoder_flop(wav_len)) / L
     res = {
@@ -456,9 +552,14 @@ def main():
                       "achieved_tflops_per_gpu": round(value * frame_flop / world / 1e12, 3),
                       "frac_of_peak": round(value * frame_flop / world / 1e12 / peak, 5)},
     }
+    if rank == 0 and WORKLOADS[args.workload].get("f32_subrecord") and args.dtype == "bf16" and \
+            not args.no_f32_subrecord:
+        res["f32_subrecord"] = f32_subrecord(pkg, cfg, sd, d_pose, L, B, wavs[-1][start:stop], loop_name=args.alg,
+                                             diffusion=diffusion, dev=dev, T=T, clip_step=clip_step)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T, args.cpu_steps, args.alg,
-                                           args.cpu_samples)
+        res["cpu_baseline"] = cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T,
+                                           T if args.workload == "c1" else args.cpu_steps, args.alg,
+                                           1 if args.workload == "c1" else args.cpu_samples, args.respacing)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist is not None:

@@ -150,6 +150,11 @@ typedef struct ggd_sample_args {
                              eps, pred_x_start, raw_x_start (gaussian_diffusion.py:278-285) */
   int32_t n_steps;        /* run only the first n_steps iterations (<=0: all T') */
   int32_t use_graph;      /* 1: replay a captured hipGraph per step */
+  int32_t sync;           /* 0 (default): return once the work is issued; a persistent loop's status
+                             words are checked by a later call (ggd_sample, ggd_sync), and a failure is
+                             returned by that call.  1: block until the loop has finished, check it,
+                             and re-run a loop whose workgroups were never co-resident on a route
+                             that needs no co-residency (per-phase launches / one workgroup per clip) */
 } ggd_sample_args;
 
 /* Full reverse loop, i = T'-1 ... 0, one fused model+update per step.
@@ -157,6 +162,11 @@ typedef struct ggd_sample_args {
  * (gaussian_diffusion.py:331-529) as driven by Generator.generate_sample
  * (generator.py:283-294). */
 int ggd_sample(ggd_ctx* ctx, const ggd_sample_args* args, void* stream);
+
+/* Wait for the ctx stream and every deferred status check of earlier non-blocking ggd_sample
+ * calls; returns the error of a failed one (GGD_ERR_HIP) or GGD_OK -- the point at which the
+ * reference's asynchronous CUDA errors would surface (reading the result). */
+int ggd_sync(ggd_ctx* ctx);
 
 /* Timing of the dominant kernel over the last profiled ggd_sample: average microseconds of one
  * launch of `which` (0 = the dominant kernel: fused path kb_kernel, timed by its own per-workgroup

@@ -85,6 +85,9 @@ int ggd_tr_adamw(int64_t n, float* p, const float* g, float* m, float* v, float 
                  float weight_decay, int64_t step, float grad_scale, void* stream);
 /* x *= s (clip_grad_norm_ applied in place). */
 int ggd_tr_scale(int64_t n, float* x, float s, void* stream);
+/* x = clamp(x s, -clip_value, clip_value): clip_grad_norm_'s coefficient followed by
+ * clip_grad_value_ (models/trainer.py:233-236), in place. */
+int ggd_tr_scale_clamp(int64_t n, float* x, float s, float clip_value, void* stream);
 
 /* ---- speech-encoder training (HA2G SE-ResNet34, ha2g/model/ResNetSE34V2.py:118-188,
  * ResNetBlocks.py:7-96) on NHWC activations: rows = pixels (n, h, w), channels innermost ---- */

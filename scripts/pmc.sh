@@ -16,4 +16,4 @@ for CTRS in "$@"; do
   echo "pass $i ($CTRS) rc=$rc"
   [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_$i.log; exit $rc; }
 done
-python3 scripts/pmc_summary.py gpurun_out ${TAG} > gpurun_out/${TAG}_summary.json && cat gpurun_out/${TAG}_summary.json
+python3 scripts/pmc_summary.py gpurun_out ${TAG} ${WORKLOAD} > gpurun_out/${TAG}_summary.json && cat gpurun_out/${TAG}_summary.json

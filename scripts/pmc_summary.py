@@ -12,7 +12,7 @@ import sys
 from collections import defaultdict
 
 
-def main(root, tag):
+def main(root, tag, workload=None):
     per = defaultdict(lambda: defaultdict(list))
     dur = defaultdict(list)
     for f in sorted(glob.glob(os.path.join(root, f"{tag}_*", "**", "*counter_collection.csv"), recursive=True)):
@@ -37,8 +37,15 @@ def main(root, tag):
         if dur.get(k):
             e["avg_duration_ns"] = sum(dur[k]) / len(dur[k])
         out[k] = e
+    if workload:
+        out["_workload"] = workload
+    # the kernels' source hash at collection time: bench.py uses the summary's traffic only while
+    # csrc/ still hashes to this (a stale summary is reported as such, never silently reused)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    import bench
+    out["_csrc"] = bench.csrc_hash()
     print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)

@@ -13,13 +13,13 @@ from .config import JsonConfig, adapt_legacy, load_config
 from .diffusion import (GaussianDiffusion, GaussianSpacedDiffusion, InpaintDenoise, get_named_beta_schedule,
                         space_timesteps)
 from .generator import Generator
-from .model import Speech2GestureModel
+from .model import Speech2GestureModel, sync_all
 from .model_creation import create_diffusion, create_model
 from .weights import arch_from_config, count_parameters, init_state_dict, parameter_shapes
 
 __all__ = [
     "JsonConfig", "adapt_legacy", "load_config", "GaussianDiffusion", "GaussianSpacedDiffusion",
     "InpaintDenoise", "get_named_beta_schedule", "space_timesteps", "Generator", "Speech2GestureModel",
-    "create_diffusion", "create_model", "arch_from_config", "count_parameters", "init_state_dict",
+    "create_diffusion", "create_model", "sync_all", "arch_from_config", "count_parameters", "init_state_dict",
     "parameter_shapes",
 ]

@@ -179,6 +179,25 @@ struct ggd_ctx {
   int mega_status_host = 0;
   int mega_xl_launches = 0, mega_fallbacks = 0;  // last ggd_sample: XCD-local launches, write-through re-runs
   double wall_mhz = 100.0;             // realtime counter rate (hipDeviceAttributeWallClockRate)
+
+  // Deferred status checks of the persistent loops: a ggd_sample that does not ask for `sync`
+  // returns once its launches are issued; the loop's status words are copied to pinned host memory
+  // behind it and an event marks their arrival.  Later calls (and ggd_sync) read them; a failure
+  // becomes a sticky error returned by the next call.
+  struct Pending {
+    hipEvent_t ev = nullptr;
+    int* host = nullptr;     // pinned: [2 * MEGA_MAX_CHUNKS] status words
+    int kind = 0;            // 1 clip-group loop (XCD-local words, then the gated write-through re-runs), 4 clip pairs
+    int chunks = 0;
+    bool xl = false;
+  };
+  std::vector<Pending> pend;           // ring
+  size_t pend_head = 0, pend_count = 0;
+  int sticky = 0;                      // 0, or the ggd_status of a failed earlier loop
+  std::string sticky_msg;
+  bool mega_none_ran = false;          // settled clip-group check: every chunk reported 2 (nothing ran)
+  bool prof_lazy = false;              // profiled loop: elapsed time read by ggd_kernel_time
+  int prof_lazy_div = 1;
 };
 
 namespace {
@@ -197,6 +216,94 @@ int fail(ggd_ctx* c, int code, const std::string& msg) {
     if (_e != hipSuccess)                                                                   \
       return fail(ctx, GGD_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));     \
   } while (0)
+
+constexpr size_t PEND_RING = 8;
+
+// Read the status words of a finished deferred check (see ggd_ctx::Pending).
+void settle(ggd_ctx* c, const ggd_ctx::Pending& p) {
+  if (p.kind == 1) {
+    int worst = 0, unrun = 0;
+    c->mega_xl_launches = 0;
+    c->mega_fallbacks = 0;
+    for (int ci = 0; ci < p.chunks; ++ci) {
+      int st = p.host[ci];
+      if (p.xl && st == 3) {  // the gated write-through launch ran instead
+        ++c->mega_fallbacks;
+        st = p.host[MEGA_MAX_CHUNKS + ci];
+      } else if (p.xl) {
+        ++c->mega_xl_launches;
+      }
+      worst = std::max(worst, st);
+      unrun += st == 2 ? 1 : 0;
+    }
+    c->mega_none_ran = unrun == p.chunks;
+    c->mega_status_host = worst;
+    if (worst && !c->sticky) {
+      c->sticky = GGD_ERR_HIP;
+      c->sticky_msg = worst == 2 ? "persistent loop (earlier ggd_sample): workgroups were not all resident"
+                                 : "persistent loop (earlier ggd_sample): a clip-group barrier timed out";
+    }
+  } else if (p.kind == 4) {
+    if (p.host[0] && !c->sticky) {
+      c->sticky = GGD_ERR_HIP;
+      c->sticky_msg = p.host[0] == 2 ? "clip-pair loop (earlier ggd_sample): workgroups were not all resident"
+                                     : "clip-pair loop (earlier ggd_sample): a pair barrier timed out";
+    }
+  }
+}
+
+// Settle every deferred check whose copy has landed (wait = true: all of them, blocking).
+int poll_pending(ggd_ctx* c, bool wait) {
+  while (c->pend_count) {
+    ggd_ctx::Pending& p = c->pend[c->pend_head];
+    if (wait) {
+      HIP_TRY(c, hipEventSynchronize(p.ev));
+    } else {
+      const hipError_t q = hipEventQuery(p.ev);
+      if (q == hipErrorNotReady) break;
+      if (q != hipSuccess) return fail(c, GGD_ERR_HIP, std::string("status event: ") + hipGetErrorString(q));
+    }
+    settle(c, p);
+    c->pend_head = (c->pend_head + 1) % PEND_RING;
+    --c->pend_count;
+  }
+  return GGD_OK;
+}
+
+// Queue a deferred check of `nwords` device status words (stream-ordered behind the loop).
+int defer_check(ggd_ctx* c, const int* dev_words, int nwords, int kind, int chunks, bool xl, hipStream_t s) {
+  if (c->pend.empty()) {
+    c->pend.resize(PEND_RING);
+    for (auto& p : c->pend) {
+      HIP_TRY(c, hipEventCreateWithFlags(&p.ev, hipEventDisableTiming));
+      HIP_TRY(c, hipHostMalloc((void**)&p.host, sizeof(int) * 2 * MEGA_MAX_CHUNKS, hipHostMallocDefault));
+    }
+  }
+  if (c->pend_count == PEND_RING) {  // ring full: the oldest check must settle first
+    ggd_ctx::Pending& o = c->pend[c->pend_head];
+    HIP_TRY(c, hipEventSynchronize(o.ev));
+    settle(c, o);
+    c->pend_head = (c->pend_head + 1) % PEND_RING;
+    --c->pend_count;
+  }
+  ggd_ctx::Pending& p = c->pend[(c->pend_head + c->pend_count) % PEND_RING];
+  p.kind = kind;
+  p.chunks = chunks;
+  p.xl = xl;
+  HIP_TRY(c, hipMemcpyAsync(p.host, dev_words, sizeof(int) * nwords, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipEventRecord(p.ev, s));
+  ++c->pend_count;
+  return GGD_OK;
+}
+
+// The sticky error of an earlier deferred check, reported once.
+int take_sticky(ggd_ctx* c) {
+  if (!c->sticky) return GGD_OK;
+  const int r = fail(c, c->sticky, c->sticky_msg);
+  c->sticky = 0;
+  c->sticky_msg.clear();
+  return r;
+}
 
 // Device memory of a context: sub-allocated (256-B aligned) from a few 64 MiB arenas, so the
 // weights, tables and workspaces that every step streams sit in a handful of large, physically
@@ -511,6 +618,7 @@ FinalArgs final_args(ggd_ctx* c, int n) {
   f.x = c->x;
   f.steps = c->d_steps;
   f.step_counter = c->d_counter;
+  f.extras_k = -1;
   return f;
 }
 
@@ -1125,6 +1233,11 @@ int ggd_destroy(ggd_ctx* c) {
   if (!c) return GGD_OK;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  for (auto& p : c->pend) {
+    if (p.ev) hipEventDestroy(p.ev);
+    if (p.host) hipHostFree(p.host);
+  }
+  c->pend.clear();
   if (c->gexec) hipGraphExecDestroy(c->gexec);
   if (c->graph) hipGraphDestroy(c->graph);
   for (void* p : c->allocs) hipFree(p);
@@ -1478,6 +1591,14 @@ int ggd_profile_kind(ggd_ctx* c) { return c ? c->prof_kind : GGD_ERR_ARG; }
 
 int ggd_kernel_time(ggd_ctx* c, int32_t which, double* avg_us, int64_t* launches) {
   if (!c || !avg_us || !launches || which != 0) return fail(c, GGD_ERR_ARG, "bad argument");
+  if (c->prof_lazy) {  // a non-blocking loop's event pair: read once both have completed
+    c->prof_lazy = false;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipEventSynchronize(c->prof.ev[1]));
+    float ms = 0;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->prof.ev[0], c->prof.ev[1]));
+    c->prof_avg_us = ms * 1000.0 / std::max(1, c->prof_lazy_div);
+  }
   if (c->span_pending) {  // launch span = latest workgroup end - earliest workgroup start
     const size_t n = c->span_pending, wg = c->span_wg;
     c->span_pending = 0;
@@ -1547,6 +1668,11 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
 
 int ggd_route_info(ggd_ctx* c, int32_t what, double* out) {
   if (!c || !out) return GGD_ERR_ARG;
+  if (what == GGD_INFO_XL_LAUNCHES || what == GGD_INFO_WT_RERUNS) {  // counters of a deferred check
+    HIP_TRY(c, hipSetDevice(c->device));
+    int r = poll_pending(c, true);
+    if (r) return r;
+  }
   switch (what) {
     case GGD_INFO_PER_CLIP_AVAILABLE: *out = c->persist ? 1.0 : 0.0; return GGD_OK;
     case GGD_INFO_LOOP_CAPACITY: *out = c->fused ? (double)mega_capacity(c->desc.dtype, c->desc.seq_len) : 0.0; return GGD_OK;
@@ -1959,6 +2085,7 @@ int run_long(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
     la.q = c->q;
     la.steps = c->d_steps;
     la.noise = a.noise;
+    la.extras = a.extras;           // written by the loop's own last iteration
     la.scale = 1.0f / std::sqrt((float)(d / D.heads));
     la.ctl = c->long_ctl;
     la.status = c->long_status + ci;
@@ -1993,9 +2120,13 @@ int run_long(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
   return GGD_OK;
 }
 
-// The first `nsteps` iterations as ONE persistent launch (ggd_mega.hip); blocks until it has
-// finished to report a barrier timeout (outputs are then invalid).
-int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
+// The first `nsteps` iterations as ONE persistent launch (ggd_mega.hip) per chunk of clips.
+// The XCD-local variant runs first; a chunk it cannot place (status 3: nothing ran) is re-run on the
+// write-through variant by a second launch that the device gates on that status word, so the host
+// never waits.  sync = false: returns once issued, the status words are checked later
+// (defer_check); sync = true: blocks, and returns 1 when the loop could not run at all (status 2:
+// its workgroups were never all resident, nothing ran) so that the caller takes the launch route.
+int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
   const ggd_desc& D = c->desc;
   const int NL = D.n_layers;
   hipStream_t s = c->stream;
@@ -2003,7 +2134,7 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
     HIP_TRY(c, dalloc(c, &c->mega_fa, sizeof(FusedArgs) * 4 * NL));
     HIP_TRY(c, dalloc(c, &c->mega_fe, sizeof(FinalArgs)));
     HIP_TRY(c, dalloc(c, &c->mega_ctl, sizeof(unsigned) * MEGA_CTL_WORDS));
-    HIP_TRY(c, dalloc(c, &c->mega_status, sizeof(int) * MEGA_MAX_CHUNKS));
+    HIP_TRY(c, dalloc(c, &c->mega_status, sizeof(int) * 2 * MEGA_MAX_CHUNKS));
   }
   c->mega_fa_host.assign(4 * NL, FusedArgs{});
   for (int li = 0; li < NL; ++li) {
@@ -2028,6 +2159,8 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
   fe.trans = a.trans;
   fe.do_out = 1;
   fe.do_update = 1;
+  fe.extras = a.extras;             // written by the loop's own last iteration
+  fe.extras_k = nsteps - 1;
   fe.stamps = c->mega_phase_stamps ? c->mega_phase_stamps + 64 : nullptr;
   HIP_TRY(c, hipMemcpyAsync(c->mega_fa, c->mega_fa_host.data(), sizeof(FusedArgs) * 4 * NL, hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipMemcpyAsync(c->mega_fe, &fe, sizeof(FinalArgs), hipMemcpyHostToDevice, s));
@@ -2035,9 +2168,7 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
   const int cap = mega_capacity(D.dtype, D.seq_len);
   const int chunks = (a.n + cap - 1) / cap;
   if (chunks > MEGA_MAX_CHUNKS) return fail(c, GGD_ERR_ARG, "batch too large for the persistent loop");
-  HIP_TRY(c, hipMemsetAsync(c->mega_status, 0, sizeof(int) * MEGA_MAX_CHUNKS, s));
-  // XCD-local variant first (every clip group on one XCD); a chunk it cannot place (status 3,
-  // nothing ran) is launched again on the write-through path
+  HIP_TRY(c, hipMemsetAsync(c->mega_status, 0, sizeof(int) * 2 * MEGA_MAX_CHUNKS, s));
   const bool xl = c->mega_place == 0;
   if (c->profiling) {
     c->prof.next = 0;
@@ -2046,44 +2177,34 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
   }
   for (int c0 = 0, ci = 0; c0 < a.n; c0 += cap, ++ci) {
     MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + ci,
-               c0 == 0 ? c->mega_stamps : nullptr, c0, c->mega_place == 1 ? 1 : 0};
+               c0 == 0 ? c->mega_stamps : nullptr, c0, c->mega_place == 1 ? 1 : 0, nullptr};
     HIP_TRY(c, launch_mega(D.dtype, D.seq_len, m, std::min(cap, a.n - c0), xl, s));
+    if (xl) {  // the write-through re-run of this chunk, live only if the launch above reported 3
+      MegaArgs g{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + MEGA_MAX_CHUNKS + ci,
+                 nullptr, c0, 0, c->mega_status + ci};
+      HIP_TRY(c, launch_mega(D.dtype, D.seq_len, g, std::min(cap, a.n - c0), false, s));
+    }
   }
-  if (c->profiling) {
+  if (c->profiling) {  // the loop's launches are the one timed span (read by ggd_kernel_time)
     int r = prof_mark(c, s);
     if (r) return r;
-  }
-  int st[MEGA_MAX_CHUNKS];
-  HIP_TRY(c, hipMemcpyAsync(st, c->mega_status, sizeof(int) * MEGA_MAX_CHUNKS, hipMemcpyDeviceToHost, s));
-  HIP_TRY(c, hipStreamSynchronize(s));
-  c->mega_xl_launches = 0;
-  c->mega_fallbacks = 0;
-  for (int c0 = 0, ci = 0; c0 < a.n; c0 += cap, ++ci) {
-    if (st[ci] != 3) {
-      c->mega_xl_launches += xl ? 1 : 0;
-      continue;
-    }
-    ++c->mega_fallbacks;
-    MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + ci, nullptr, c0, 0};
-    HIP_TRY(c, hipMemsetAsync(c->mega_status + ci, 0, sizeof(int), s));
-    HIP_TRY(c, launch_mega(D.dtype, D.seq_len, m, std::min(cap, a.n - c0), false, s));
-    HIP_TRY(c, hipMemcpyAsync(st + ci, c->mega_status + ci, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-  }
-  c->mega_status_host = 0;
-  for (int ci = 0; ci < chunks; ++ci) c->mega_status_host = std::max(c->mega_status_host, st[ci]);
-  if (c->mega_status_host)
-    return fail(c, GGD_ERR_HIP, c->mega_status_host == 2 ? "persistent loop: workgroups were not all resident"
-                                                          : "persistent loop: a clip-group barrier timed out");
-  if (c->profiling) {  // the whole loop is the one timed launch
-    float ms = 0;
-    HIP_TRY(c, hipEventElapsedTime(&ms, c->prof.ev[0], c->prof.ev[1]));
-    c->prof_avg_us = ms * 1000.0 / chunks;
+    c->prof_lazy = true;
+    c->prof_lazy_div = chunks;
     c->prof_launches = chunks;
     c->prof_kind = 1;
     c->span_pending = 0;
   }
-  return GGD_OK;
+  int r = defer_check(c, c->mega_status, 2 * MEGA_MAX_CHUNKS, 1, chunks, xl, s);
+  if (r) return r;
+  if (!sync) return GGD_OK;
+  if ((r = poll_pending(c, true))) return r;
+  if (c->sticky && c->mega_none_ran) {  // nothing ran (status 2 everywhere): the caller takes the launch route
+    c->sticky = 0;
+    c->sticky_msg.clear();
+    ++c->mega_fallbacks;
+    return 1;
+  }
+  return take_sticky(c);
 }
 
 }  // namespace
@@ -2100,10 +2221,16 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
     return fail(c, GGD_ERR_ARG, "inpaint poses and masks must be given together");
   if (a->inpaint_masks && !a->trans) return fail(c, GGD_ERR_ARG, "inpaint requires the trans ramp");
   HIP_TRY(c, hipSetDevice(c->device));
+  {  // an earlier non-blocking loop that failed is reported here, once
+    int r = poll_pending(c, false);
+    if (r) return r;
+    if ((r = take_sticky(c))) return r;
+  }
   const ggd_desc& D = c->desc;
   const int T = (int)c->betas.size();
   int nsteps = a->n_steps > 0 && a->n_steps < T ? a->n_steps : T;
   hipStream_t s = c->stream;
+  const bool sync = a->sync != 0;
 
   std::vector<StepRec> recs;
   make_records(c, a->alg, a->eta, recs, a->seed, a->clip_offset);
@@ -2183,24 +2310,32 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
     } else {
       HIP_TRY(c, launch_persist(p, s));
     }
-    if (pair) {
-      int st = 0;
-      HIP_TRY(c, hipMemcpyAsync(&st, c->pair_status, sizeof(int), hipMemcpyDeviceToHost, s));
-      HIP_TRY(c, hipStreamSynchronize(s));
-      if (st)
-        return fail(c, GGD_ERR_HIP, st == 2 ? "clip-pair loop: workgroups were not all resident"
-                                            : "clip-pair loop: a pair barrier timed out");
-    }
-    if (c->profiling) {
+    if (c->profiling) {  // the loop's launches are the one timed span (read by ggd_kernel_time)
       int r = prof_mark(c, s);
       if (r) return r;
-      HIP_TRY(c, hipStreamSynchronize(s));
-      float ms = 0;
-      HIP_TRY(c, hipEventElapsedTime(&ms, c->prof.ev[0], c->prof.ev[1]));
-      c->prof_avg_us = ms * 1000.0;
+      c->prof_lazy = true;
+      c->prof_lazy_div = 1;
       c->prof_launches = 1;
       c->prof_kind = pair ? 4 : 3;
       c->span_pending = 0;
+    }
+    if (pair) {  // status words checked later (or now, with sync; then status 2 -- nothing ran -- re-runs
+                 // on the one-workgroup-per-clip loop, which needs no co-residency)
+      int r = defer_check(c, c->pair_status, 1, 4, 1, false, s);
+      if (r) return r;
+      if (sync) {
+        if ((r = poll_pending(c, true))) return r;
+        if (c->sticky) {
+          int st = 0;
+          HIP_TRY(c, hipMemcpy(&st, c->pair_status, sizeof(int), hipMemcpyDeviceToHost));
+          if (st != 2) return take_sticky(c);
+          c->sticky = 0;
+          c->sticky_msg.clear();
+          HIP_TRY(c, launch_init_state(c->x, a->x_T, a->seed, a->clip_offset, a->n, D.d_pose, D.seq_len, s));
+          HIP_TRY(c, launch_persist(p, s));
+          c->pair_launches = 0;
+        }
+      }
     }
     HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));
     HIP_TRY(c, hipEventRecord(c->ev_out, s));
@@ -2209,36 +2344,30 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   }
   HIP_TRY(c, launch_set_int(c->d_counter, -1, s));
 
-  const int graph_steps = a->extras ? nsteps - 1 : nsteps;
-  if (c->fused && !c->no_mega && graph_steps > 0 && mega_capacity(D.dtype, D.seq_len) > 0) {
-    int r = run_mega(c, *a, graph_steps);
-    if (r) return r;
-    if (a->extras) {  // the last iteration with its extras through the per-phase kernels
-      HIP_TRY(c, launch_set_int(c->d_counter, graph_steps - 1, s));
-      r = launch_step(c, *a, a->extras, -1);
-      if (r) return r;
-    }
-    HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));
-    HIP_TRY(c, hipEventRecord(c->ev_out, s));
-    HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
-    return GGD_OK;
-  }
-  c->long_launches = 0;
-  if (c->long_ok && !c->long_off && !c->gemm_launches && !c->attn_qsplit && !a->inpaint_masks && graph_steps > 0) {
-    int r = run_long(c, *a, graph_steps);
+  // the persistent loops run every iteration, the last one writing the extras itself
+  if (c->fused && !c->no_mega && nsteps > 0 && mega_capacity(D.dtype, D.seq_len) > 0) {
+    int r = run_mega(c, *a, nsteps, sync);
     if (r < 0) return r;
     if (r == 0) {
-      if (a->extras) {  // the last iteration with its extras on the launch route
-        HIP_TRY(c, launch_set_int(c->d_counter, graph_steps - 1, s));
-        r = launch_step(c, *a, a->extras, -1);
-        if (r) return r;
-      }
+      HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));
+      HIP_TRY(c, hipEventRecord(c->ev_out, s));
+      HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
+      return GGD_OK;
+    }
+    // r == 1 (sync only): the loop's workgroups were never all resident -> the per-phase launches
+  }
+  c->long_launches = 0;
+  if (c->long_ok && !c->long_off && !c->gemm_launches && !c->attn_qsplit && !a->inpaint_masks && nsteps > 0) {
+    int r = run_long(c, *a, nsteps);
+    if (r < 0) return r;
+    if (r == 0) {
       HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));
       HIP_TRY(c, hipEventRecord(c->ev_out, s));
       HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
       return GGD_OK;
     }
   }
+  const int graph_steps = a->extras ? nsteps - 1 : nsteps;
   // pointer / shape key: a captured graph is reused only for identical arguments
   char keybuf[512];
   std::snprintf(keybuf, sizeof keybuf, "%d|%d|%p|%p|%p|%p|%d|%d", a->alg, a->n, (const void*)a->noise,
@@ -2318,6 +2447,15 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   HIP_TRY(c, hipEventRecord(c->ev_out, s));
   HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
   return GGD_OK;
+}
+
+int ggd_sync(ggd_ctx* c) {
+  if (!c) return GGD_ERR_ARG;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  int r = poll_pending(c, true);
+  if (r) return r;
+  return take_sticky(c);
 }
 
 }  // extern "C"

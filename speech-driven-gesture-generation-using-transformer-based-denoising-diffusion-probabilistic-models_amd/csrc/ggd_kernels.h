@@ -160,6 +160,7 @@ struct FinalArgs {
   const float* noise; uint64_t seed; int64_t clip_offset;
   const float *inp_pose, *inp_mask, *trans;
   float* extras;
+  int extras_k;            // extras are written at iteration extras_k only (< 0: at every iteration)
   int do_out, do_update;
   unsigned long long* stamps;  // diagnostics
 };
@@ -206,6 +207,9 @@ struct MegaArgs {
                                // of the first MEGA_STAMP_STEPS iterations ([phase][2]: done, passed)
   int clip0;             // first clip of this launch (batches above the capacity run as chunks)
   int placement;         // 0: a clip's 8 workgroups share one XCD; 1: workgroup part p of every clip on XCD p
+  const int* gate;       // non-null: the launch runs only if *gate == 3 (the XCD-local launch of the same
+                         // chunk could not place its clip groups) -- the write-through re-run, decided on
+                         // the device so the host never waits for the first launch's status
 };
 constexpr int MEGA_STAMP_STEPS = 2;
 constexpr int MEGA_MAX_CHUNKS = 16;  // status words: one per launch of up to mega_capacity() clips
@@ -262,6 +266,7 @@ struct LongArgs {
   void *qkv, *att, *q;       // hand-off rows (bf16)
   const StepRec* steps;
   const float* noise;        // (T', N, C, L) injected noise, or null: the counter stream
+  float* extras;             // (6, N, C, L) of iteration k0 + n_steps - 1, or null
   float scale;
   unsigned* ctl;             // LONG_CTL_WORDS, zeroed by launch_long_loop
   int* status;               // 0 ok, 1 barrier timeout, 2 not resident, 3 not placeable (nothing ran)

@@ -237,8 +237,18 @@ __device__ __forceinline__ void lk_update(X& x, bool to_xs) {
     for (int i = 0; i < 4; ++i) {
       const int rr = q4 + i;
       const float xo = ld_f32<CP_COH>(xg, (uint32_t)(rr * C + c));
-      const UpdOut o = upd_math(r, a.alg, xo, eps[rr * EPS_STR + c], false, 0.f, false, 0.f, 0.f, 0.f, z[i]);
+      const float ev = eps[rr * EPS_STR + c];
+      const UpdOut o = upd_math(r, a.alg, xo, ev, false, 0.f, false, 0.f, 0.f, 0.f, z[i]);
       xg[rr * C + c] = o.xn;
+      if (a.extras && x.it == a.k0 + a.n_steps - 1) {  // the last iteration's p_sample dict entries
+        const size_t plane = (size_t)a.n * C * L, ncl = ((size_t)x.b * C + c) * L + l + i;
+        a.extras[0 * plane + ncl] = o.mean;
+        a.extras[1 * plane + ncl] = r.var;
+        a.extras[2 * plane + ncl] = r.logvar;
+        a.extras[3 * plane + ncl] = ev;
+        a.extras[4 * plane + ncl] = o.x0;
+        a.extras[5 * plane + ncl] = o.raw;
+      }
       if (to_xs) x.xs[rr * XS_STR + c] = f2bf(o.xn);
     }
   }

@@ -170,6 +170,7 @@ template <typename T, int RT, int CPV>
 __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_role, s_ok;
+  if (m.gate && ggd::G(m.gate)[0] != 3) return;  // gated re-run: the XCD-local launch placed (or failed otherwise)
   if (threadIdx.x == 0) s_role = CPV == CP_XL ? mk_role_xl(m, gridDim.x, G) : mk_role(m, gridDim.x);
   __syncthreads();
   const int role = s_role;

@@ -529,7 +529,7 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
         const float ev = E[l * SE + (cc - c0)];
         const UpdOut o = upd_math(rec, a.alg, xq[u], ev, false, 0.f, inp, mq[u], pq[u], tq[u], zq[u]);
         xo.template put<float>((uint32_t)((row0 + l) * C + cc), o.xn);
-        if (a.extras) {
+        if (a.extras && (a.extras_k < 0 || k == a.extras_k)) {
           const size_t ncl = (size_t)b * LC + e;
           a.extras[0 * plane + ncl] = o.mean;
           a.extras[1 * plane + ncl] = rec.var;

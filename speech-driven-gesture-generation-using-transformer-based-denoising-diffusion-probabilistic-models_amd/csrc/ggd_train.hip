@@ -498,6 +498,12 @@ __global__ void scale_kernel(int64_t n, float* x, float s) {
   if (i < n) x[i] *= s;
 }
 
+// clip_grad_norm_'s coefficient, then clip_grad_value_'s clamp (trainer.py:233-236), in place
+__global__ void scale_clamp_kernel(int64_t n, float* x, float s, float lim) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = fminf(fmaxf(x[i] * s, -lim), lim);
+}
+
 // ------------------------------------------------------------------------------------------
 // speech-encoder training ops, NHWC activations (rows = pixels (n, h, w), channels innermost)
 // ------------------------------------------------------------------------------------------
@@ -885,6 +891,13 @@ int ggd_tr_scale(int64_t n, float* x, float s, void* stream) {
   if (n < 0 || !x) return -1;
   if (n == 0) return 0;
   hipLaunchKernelGGL(scale_kernel, dim3(blocks_for(n)), dim3(TT), 0, (hipStream_t)stream, n, x, s);
+  return rc(hipGetLastError());
+}
+
+int ggd_tr_scale_clamp(int64_t n, float* x, float s, float clip_value, void* stream) {
+  if (n < 0 || !x || !(clip_value >= 0.f)) return -1;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(scale_clamp_kernel, dim3(blocks_for(n)), dim3(TT), 0, (hipStream_t)stream, n, x, s, clip_value);
   return rc(hipGetLastError());
 }
 

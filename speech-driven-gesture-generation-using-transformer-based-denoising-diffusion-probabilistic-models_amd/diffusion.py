@@ -148,7 +148,11 @@ class GaussianSpacedDiffusion(GaussianDiffusion):
         return self._loop(native.DDIM, float(eta), model, shape, model_kwargs, noise, denoise_fn, device, **kw)
 
     def _loop(self, alg, eta, model, shape, model_kwargs, noise, denoise_fn, device, step_noise=None,
-              seed=None, clip_offset=0, n_steps=None, use_graph=False, extras=True, prefetch_wav=None):
+              seed=None, clip_offset=0, n_steps=None, use_graph=False, extras=True, prefetch_wav=None, sync=False):
+        """sync=False (default): returns once the loop is issued on the device, like any PyTorch GPU
+        op; a persistent loop's status words are checked by the next call or model.sync() / .sync_all().
+        sync=True blocks, checks, and re-runs a loop that could not be co-resident on a route that
+        needs no co-residency."""
         assert isinstance(shape, (tuple, list)) and len(shape) == 3, "shape must be (N, C, L)"
         model_kwargs = dict(model_kwargs or {})
         wav = model_kwargs.pop("wav", None)
@@ -192,7 +196,7 @@ class GaussianSpacedDiffusion(GaussianDiffusion):
         a = native.SampleArgs(alg=alg, eta=eta, n=N, x_T=ptr(x_T), noise=ptr(zs), seed=seed,
                               clip_offset=int(clip_offset), inpaint_poses=ptr(inp_p), inpaint_masks=ptr(inp_m),
                               trans=ptr(trans), out=ptr(out), extras=ptr(ext), n_steps=steps,
-                              use_graph=1 if use_graph else 0)
+                              use_graph=1 if use_graph else 0, sync=1 if sync else 0)
         native.check(ctx.h, ctx.lib.ggd_sample(ctx.h, ctypes.byref(a),
                                                ctypes.c_void_p(th.cuda.current_stream(dev).cuda_stream)), "sample")
         res = {"sample": out}

@@ -11,6 +11,7 @@ runs as hand-written gfx950 kernels through ``ggd_denoise``.  There is no CPU
 or eager-PyTorch fallback for the decoder.
 """
 import ctypes
+import weakref
 
 import numpy as np
 import torch as th
@@ -21,6 +22,16 @@ from .weights import arch_from_config, parameter_shapes
 
 # "fp8": bf16 activations, OCP e4m3 per-step decoder weights with per-channel scales (GGD_FP8W)
 _DTYPES = {"bf16": native.BF16, "f32": native.F32, "fp32": native.F32, "fp8": native.FP8W}
+
+
+_LIVE = weakref.WeakSet()   # every open context (sync_all)
+
+
+def sync_all():
+    """ggd_sync on every open context: waits for their streams and raises the error of any
+    persistent loop that failed after a non-blocking ggd_sample returned."""
+    for c in list(_LIVE):
+        c.sync()
 
 
 class _Ctx:
@@ -47,6 +58,12 @@ class _Ctx:
         native.check(self.h, lib.ggd_finalize_weights(self.h), "finalize weights")
         self.schedule_key = None
         self.memory_key = None
+        _LIVE.add(self)
+
+    def sync(self):
+        """Wait for the context's work; raise if an earlier non-blocking loop failed (ggd_sync)."""
+        if self.h:
+            native.check(self.h, self.lib.ggd_sync(self.h), "sync")
 
     def set_schedule(self, betas, timestep_map):
         key = (np.asarray(betas, np.float64).tobytes(), tuple(int(t) for t in timestep_map))
@@ -114,6 +131,11 @@ class Speech2GestureModel:
 
     def state_dict(self):
         return dict(self._sd) if self._sd is not None else {}
+
+    def sync(self):
+        """Wait for this model's contexts; raise if a non-blocking sampling loop failed (ggd_sync)."""
+        for c in list(self._ctx.values()):
+            c.sync()
 
     def load_state_dict(self, sd, strict=True):
         """Accepts the reference's model_state_dict (models/model.py module tree key names)."""

@@ -33,13 +33,14 @@ DDPM, DDIM = 0, 1
 EXPORTS = [
     "ggd_create", "ggd_destroy", "ggd_last_error", "ggd_load_weight", "ggd_finalize_weights",
     "ggd_set_schedule", "ggd_set_memory", "ggd_set_inpaint", "ggd_denoise", "ggd_posterior_step", "ggd_sample",
+    "ggd_sync",
     "ggd_set_profiling", "ggd_kernel_time", "ggd_profile_kind", "ggd_set_route", "ggd_route_info", "ggd_version",
     "ggd_enc_create", "ggd_enc_destroy", "ggd_enc_last_error", "ggd_enc_load_weight", "ggd_enc_finalize",
     "ggd_enc_lengths", "ggd_enc_run",
     # training path (include/ggd_train.h)
     "ggd_tr_gemm", "ggd_tr_colsum", "ggd_tr_layernorm_fwd", "ggd_tr_layernorm_bwd", "ggd_tr_seqconv_fwd",
     "ggd_tr_seqconv_bwd", "ggd_tr_attention_fwd", "ggd_tr_attention_bwd", "ggd_tr_elementwise", "ggd_tr_q_sample",
-    "ggd_tr_mse", "ggd_tr_sumsq", "ggd_tr_sumsq_blocks", "ggd_tr_adamw", "ggd_tr_scale",
+    "ggd_tr_mse", "ggd_tr_sumsq", "ggd_tr_sumsq_blocks", "ggd_tr_adamw", "ggd_tr_scale", "ggd_tr_scale_clamp",
     "ggd_tr_im2col", "ggd_tr_col2im", "ggd_tr_batchnorm_fwd", "ggd_tr_batchnorm_bwd", "ggd_tr_image_channel_sum",
     "ggd_tr_channel_scale", "ggd_tr_pixel_shuffle", "ggd_tr_head_flatten", "ggd_enc_frontend",
 ]
@@ -58,6 +59,7 @@ class SampleArgs(ctypes.Structure):
         ("clip_offset", ctypes.c_int64), ("inpaint_poses", ctypes.c_void_p),
         ("inpaint_masks", ctypes.c_void_p), ("trans", ctypes.c_void_p), ("out", ctypes.c_void_p),
         ("extras", ctypes.c_void_p), ("n_steps", ctypes.c_int32), ("use_graph", ctypes.c_int32),
+        ("sync", ctypes.c_int32),
     ]
 
 
@@ -135,6 +137,7 @@ def load():
         "ggd_denoise": (ctypes.c_int, [CTX, VP, VP, VP, I32, VP]),
         "ggd_posterior_step": (ctypes.c_int, [CTX, I32, F, I32, VP, VP, VP, VP, VP, VP, I32, VP]),
         "ggd_sample": (ctypes.c_int, [CTX, P(SampleArgs), VP]),
+        "ggd_sync": (ctypes.c_int, [CTX]),
         "ggd_set_profiling": (ctypes.c_int, [CTX, I32]),
         "ggd_kernel_time": (ctypes.c_int, [CTX, I32, P(ctypes.c_double), P(I64)]),
         "ggd_profile_kind": (ctypes.c_int, [CTX]),
@@ -164,6 +167,7 @@ def load():
         "ggd_tr_sumsq_blocks": (ctypes.c_int, []),
         "ggd_tr_adamw": (ctypes.c_int, [I64, VP, VP, VP, VP, F, F, F, F, F, I64, F, VP]),
         "ggd_tr_scale": (ctypes.c_int, [I64, VP, F, VP]),
+        "ggd_tr_scale_clamp": (ctypes.c_int, [I64, VP, F, F, VP]),
         "ggd_tr_im2col": (ctypes.c_int, [I32, I32, I32, I32, I32, I32, I32, I32, VP, VP, VP]),
         "ggd_tr_col2im": (ctypes.c_int, [I32, I32, I32, I32, I32, I32, I32, I32, VP, VP, VP]),
         "ggd_tr_batchnorm_fwd": (ctypes.c_int, [I32, I32, VP, VP, VP, F, VP, VP, VP, VP, VP]),

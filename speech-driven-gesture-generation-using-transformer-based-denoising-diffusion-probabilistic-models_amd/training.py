@@ -6,7 +6,9 @@ Mirrors the reference's training step (models/trainer.py:131-248):
   Trainer._train_step: zero_grad, backward, compute_grad_norm (trainer.py:341-349), optional
       clip_grad_norm_ / clip_grad_value_, optimizer.step (AdamW, model_creation.py:176-178),
       lr_scheduler.step (lr_scheduler.py: ConstantLR / NoamLR "noamxf" / NoamDecayLR "noam")
-  DDP (trainer.py:83, utils/pytorch_ddp.py:18): gradients averaged over ranks by an all-reduce.
+  DDP (trainer.py:83, utils/pytorch_ddp.py:18): rank 0's parameters and buffers broadcast once at
+      construction (broadcast_parameters), its BatchNorm buffers again before every forward
+      (broadcast_buffers=True, DDP's default), gradients averaged over ranks by an all-reduce.
 
 Every arithmetic op of the decoder's forward and backward is a hand-written HIP kernel behind
 include/ggd_train.h (csrc/ggd_train.hip), wrapped here in torch.autograd.Function objects: torch
@@ -16,9 +18,11 @@ second flat buffer (each parameter's .grad a view; autograd accumulates into it 
 the all-reduce is one RCCL call per bucket and AdamW is one HIP launch over the whole model.
 
 Scope: the s2g_v2 model with the one-way decoder (the beat-ours configuration): step encoder,
-blend layer, decoder.  The HA2G speech encoder runs frozen (eval mode, the HIP inference
-encoder) and its parameters are not updated -- the reference also trains it, with BatchNorm in
-train mode; that backward is not built.
+blend layer, decoder and -- by default (train_encoder=True, as the reference) -- the HA2G speech
+encoder, whose SE-ResNet trains with BatchNorm in train mode (batch statistics, running-stat
+updates).  train_encoder=False freezes the encoder: it then runs as the HIP inference encoder
+(eval mode) and its weights pass through state_dict() unchanged.  TrainableModel.eval() switches
+the trained encoder to its running statistics (the reference's model.eval(), trainer.py:252).
 """
 import ctypes
 import math
@@ -463,39 +467,83 @@ class TrainableModel:
             p.grad = self.flat_grad[off:off + n].view(shape)
             self.params[k] = p
             off += n
-        self.load_state_dict(sd)
         self._pe = {}
-        self._enc_sd = {k: v for k, v in sd.items() if k.startswith("speech_encoder.")}
+        self._enc_sd = {k: v.detach().cpu().clone() for k, v in sd.items() if k.startswith("speech_encoder.")}
         self._encoder = None
+        self.training = True
         # BatchNorm running statistics of the trained encoder (buffers, updated in train mode)
         self.buffers = {k: v.detach().to(self.device).clone() for k, v in sd.items()
                         if k.startswith("speech_encoder.") and k.endswith(_ENC_BUFFERS[:3])} if self.train_encoder else {}
+        self.load_state_dict(sd)
+
+    # -- mode (nn.Module.train / eval) ---------------------------------------------------------
+    def train(self, mode=True):
+        """Train mode: the trained encoder's BatchNorms use batch statistics and update their
+        running statistics.  Eval mode (model.eval(), trainer.py:252): the encoder runs with the
+        running statistics and updates nothing."""
+        self.training = bool(mode)
+        self._encoder = None      # an eval-mode encoder is rebuilt from the current weights
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def _encoder_state(self):
+        """The speech encoder's entries of state_dict(): trained parameters and running statistics
+        when the encoder trains, the frozen weights otherwise; the front-end constants always."""
+        sd = {}
+        for k, v in self._enc_sd.items():
+            if k in self.params:
+                v = self.params[k].detach()
+            elif k in self.buffers:
+                v = self.buffers[k]
+            sd[k] = v
+        return sd
 
     def speech_encoder(self):
-        """The frozen HA2G encoder (HIP, f32, eval mode) on this model's encoder weights."""
+        """The HA2G encoder as the HIP inference encoder (f32, eval mode: BatchNorm on running
+        statistics) on this model's CURRENT encoder weights."""
         if self._encoder is None:
             from .encoder import SpeechEncoder
-            self._encoder = SpeechEncoder(self._enc_sd, self.device, dtype="f32", d_model=self.arch["d_model"])
+            self._encoder = SpeechEncoder(self._encoder_state(), self.device, dtype="f32", d_model=self.arch["d_model"])
         return self._encoder
 
     # -- state ---------------------------------------------------------------------------------
     def load_state_dict(self, sd, strict=False):
-        missing = [k for k in self.params if k not in sd]
+        """Reference state_dict keys; with strict, every key of state_dict() must be present."""
+        want = self.state_dict_keys()
+        missing = [k for k in want if k not in sd]
         if strict and missing:
             raise RuntimeError(f"missing keys {missing[:5]}")
         with th.no_grad():
             for k, p in self.params.items():
                 if k in sd:
                     p.copy_(sd[k].to(p.device, th.float32).reshape(p.shape))
-            for k, b in getattr(self, "buffers", {}).items():
+            for k, b in self.buffers.items():
                 if k in sd:
                     b.copy_(sd[k].to(b.device, b.dtype).reshape(b.shape))
+            for k in self._enc_sd:
+                if k in sd and k not in self.params and k not in self.buffers:
+                    self._enc_sd[k] = sd[k].detach().cpu().clone()
+        self._encoder = None
         return missing
 
+    def state_dict_keys(self):
+        return [k for k in parameter_shapes(self.arch) if k in self.params or k in self._enc_sd]
+
     def state_dict(self):
-        sd = {k: p.detach().clone() for k, p in self.params.items()}
-        sd.update({k: v.clone() for k, v in self.buffers.items()})
-        return sd
+        """The reference module tree's full state_dict (model.module.state_dict(), trainer.py:202),
+        in its key order: parameters, BatchNorm buffers and the front-end constants
+        (wav2spec.*: pre-emphasis filter, Hann window, mel filterbank); the frozen encoder's
+        weights when train_encoder is False.  Loads into create_model(...)[0] with strict=True."""
+        enc = self._encoder_state()
+        out = {}
+        for k in parameter_shapes(self.arch):
+            if k in self.params:
+                out[k] = self.params[k].detach().clone()
+            elif k in enc:
+                out[k] = enc[k].clone()
+        return out
 
     def named_parameters(self):
         return iter(self.params.items())
@@ -528,6 +576,10 @@ class TrainableModel:
 
     # -- the HA2G encoder in train mode (ResNetSE34V2.py:118-188), NHWC ---------------------------
     def _bn(self, name, x):
+        if not self.training:
+            raise RuntimeError("encode() builds the train-mode graph; in eval mode the model encodes with "
+                               "speech_encoder() (running statistics)")
+        self._encoder = None     # the weights / statistics the cached eval encoder holds are changing
         stats = []
         y = _BatchNorm2d.apply(x, self.params[name + ".weight"], self.params[name + ".bias"], stats)
         mean, var_u = stats[0]
@@ -582,9 +634,10 @@ class TrainableModel:
     def __call__(self, x_t, t, z=None, wav=None):
         """x_t (N, C, L), t (N,) int64 original timesteps -> eps (N, C, L).  Speech: z = (z_low, z_mid,
         z_high) tokens (N, T_i, d) from the frozen encoder, or wav (N, T_wav) encoded here (through the
-        trained encoder when train_encoder, else the frozen HIP encoder)."""
+        trained encoder in train mode when train_encoder, else the HIP eval-mode encoder on the
+        current weights -- no gradient reaches the encoder in eval mode)."""
         if z is None:
-            z = self.encode(wav) if self.train_encoder else self.speech_encoder()(wav)
+            z = self.encode(wav) if (self.train_encoder and self.training) else self.speech_encoder()(wav)
         P, a = self.params, self.arch
         d = a["d_model"]
         N, C, L = x_t.shape
@@ -699,21 +752,64 @@ class AdamW:
                                 float(self.param_groups[0]["lr"]), self.betas[0], self.betas[1], self.eps,
                                 self.weight_decay, self.step_count, float(grad_scale), _s(f)), "adamw")
 
+    def _views(self, flat):
+        """(index, view of `flat`) per parameter, in the model's parameter order (the reference
+        module tree's model.parameters() order: its state_dict order without the buffers)."""
+        off = 0
+        for i, p in enumerate(self.model.params.values()):
+            n = p.numel()
+            yield i, flat[off:off + n].view(p.shape)
+            off += n
+
     def state_dict(self):
-        return {"step": self.step_count, "exp_avg": self.exp_avg.clone(), "exp_avg_sq": self.exp_avg_sq.clone(),
-                "param_groups": [dict(g) for g in self.param_groups]}
+        """torch.optim.AdamW's layout ({'state': {i: {step, exp_avg, exp_avg_sq}}, 'param_groups'}),
+        so the reference Trainer (trainer.py:203, 218) and this one read each other's checkpoints."""
+        state = {}
+        if self.step_count > 0:
+            sq = dict(self._views(self.exp_avg_sq))
+            for i, m in self._views(self.exp_avg):
+                state[i] = {"step": th.tensor(float(self.step_count)), "exp_avg": m.clone(), "exp_avg_sq": sq[i].clone()}
+        g = dict(self.param_groups[0])
+        g.update({"betas": tuple(self.betas), "eps": self.eps, "weight_decay": self.weight_decay, "amsgrad": False,
+                  "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+                  "params": list(range(len(self.model.params)))})
+        return {"state": state, "param_groups": [g]}
 
     def load_state_dict(self, st):
-        self.step_count = int(st["step"])
-        self.exp_avg.copy_(st["exp_avg"])
-        self.exp_avg_sq.copy_(st["exp_avg_sq"])
-        self.param_groups = [dict(g) for g in st["param_groups"]]
+        """torch.optim's layout (above), or this class's round-2 flat layout {step, exp_avg, exp_avg_sq}."""
+        if "state" in st:
+            n = len(self.model.params)
+            if len(st["param_groups"]) != 1 or len(st["param_groups"][0]["params"]) != n:
+                raise ValueError("optimizer state: expected one parameter group over %d parameters" % n)
+            order = st["param_groups"][0]["params"]
+            state = st["state"]
+            self.step_count = 0
+            with th.no_grad():
+                for i, (j, m) in zip(order, self._views(self.exp_avg)):
+                    s = state.get(i)
+                    if s is None:
+                        m.zero_()
+                        continue
+                    m.copy_(s["exp_avg"].reshape(m.shape))
+                    self.step_count = int(float(s["step"]))
+                for i, (j, v) in zip(order, self._views(self.exp_avg_sq)):
+                    s = state.get(i)
+                    v.copy_(s["exp_avg_sq"].reshape(v.shape)) if s is not None else v.zero_()
+        else:
+            self.step_count = int(st["step"])
+            self.exp_avg.copy_(st["exp_avg"])
+            self.exp_avg_sq.copy_(st["exp_avg_sq"])
+        g = st["param_groups"][0]
+        self.param_groups = [{"lr": float(g["lr"]), "initial_lr": float(g.get("initial_lr", g["lr"]))}]
 
 
 def parse_steps(s):
-    """model_creation.py parse_steps: '4k' -> 4000, '200k' -> 200000."""
+    """utils/string_parser.py parse_steps, as written: base * (number of 'k') * 1000, e.g. '4k' -> 4000,
+    '200k' -> 200000, '100kk' -> 200000 (the reference's code, not its docstring)."""
     s = str(s)
-    return int(float(s[:-1]) * 1000) if s.endswith("k") else int(s)
+    nk = s.count("k")
+    base = int(s.strip("k"))
+    return base if nk == 0 else base * nk * 1000
 
 
 class LRScheduler:
@@ -727,7 +823,6 @@ class LRScheduler:
             raise ValueError("Unsupport lr_scheduler type.")
         self.warmup = float(parse_steps(params["warmup_steps"])) if self.type != "const" else 0.0
         self.d_model = float(params["d_model"]) if self.type == "noamxf" else 0.0
-        self.minimum = (params or {}).get("minimum")
         self.base_lr = optimizer.param_groups[0]["initial_lr"]
         self.last_epoch = 0
         self._apply()
@@ -738,11 +833,9 @@ class LRScheduler:
         if self.type == "noamxf":
             cur = self.last_epoch + 1
             return self.base_lr * self.d_model ** -0.5 * min(cur ** -0.5, cur * self.warmup ** -1.5)
+        # NoamDecayLR as create_lr_scheduler builds it (model_creation.py:23): no `minimum` floor
         last = max(1, self.last_epoch)
-        lr = self.base_lr * self.warmup ** 0.5 * min(last ** -0.5, last * self.warmup ** -1.5)
-        if self.minimum is not None and last > self.warmup and lr < self.minimum:
-            lr = self.minimum
-        return lr
+        return self.base_lr * self.warmup ** 0.5 * min(last ** -0.5, last * self.warmup ** -1.5)
 
     def _apply(self):
         self.opt.param_groups[0]["lr"] = self.get_lr()
@@ -795,6 +888,42 @@ def allreduce_gradients(flat_grad, group=None):
     return flat_grad
 
 
+def _dist_world(group=None):
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return 1
+    return dist.get_world_size(group)
+
+
+def broadcast_parameters(model, src=0, group=None):
+    """DDP's construction-time synchronisation (DistributedDataParallel(model), trainer.py:83):
+    every rank takes rank `src`'s parameters and buffers.  The parameters are ONE flat buffer
+    (model.flat), so that is bucketed broadcasts of it, then one per buffer (BN statistics)."""
+    import torch.distributed as dist
+    if _dist_world(group) == 1:
+        return model
+    with th.no_grad():
+        for o in range(0, model.flat.numel(), BUCKET_ELEMS):
+            dist.broadcast(model.flat[o:o + BUCKET_ELEMS], src, group=group)
+        broadcast_buffers(model, src, group)
+    return model
+
+
+def broadcast_buffers(model, src=0, group=None):
+    """DDP's per-forward buffer broadcast (broadcast_buffers=True, its default): the BatchNorm
+    running statistics of rank `src` overwrite every other rank's before the forward."""
+    import torch.distributed as dist
+    if _dist_world(group) == 1:
+        return model
+    bufs = getattr(model, "buffers", {}) or {}
+    with th.no_grad():
+        for k in sorted(bufs):
+            dist.broadcast(bufs[k], src, group=group)
+    if bufs and hasattr(model, "_encoder"):
+        model._encoder = None
+    return model
+
+
 def grad_norm(model):
     """compute_grad_norm (trainer.py:341-349): the 2-norm of all gradients (HIP reduction)."""
     g = model.flat_grad
@@ -806,16 +935,16 @@ def grad_norm(model):
 
 
 class Trainer:
-    """The reference Trainer's step (trainer.py:131-248) on one rank; world > 1 averages the
-    gradients with allreduce_gradients (torch.distributed must be initialised by the caller,
-    backend 'nccl' = RCCL on ROCm)."""
+    """The reference Trainer's step (trainer.py:131-248) on one rank.  With world > 1 (the caller
+    initialises torch.distributed, backend 'nccl' = RCCL on ROCm) it behaves as the reference's
+    DDP wrapper (trainer.py:83): rank 0's parameters and buffers are broadcast at construction,
+    its BN buffers again before every forward, and gradients are averaged by allreduce_gradients."""
 
     def __init__(self, model, diffusion, speech_encoder, lr=1e-3, weight_decay=None, scheduler_params=None,
                  grad_norm_clip_value=None, grad_clip_value=None, loss_params=None, seed=0):
-        if grad_clip_value is not None:
-            raise ValueError("clip_grad_value_ is not built (beat-ours sets neither clip)")
         if loss_params:
             raise ValueError("extra losses (speed_loss, ...) are not built; beat-ours uses none")
+        broadcast_parameters(model)
         self.model = model
         self.diffusion = diffusion
         self.encoder = speech_encoder if speech_encoder is not None else (lambda wav: model.speech_encoder()(wav))
@@ -823,6 +952,7 @@ class Trainer:
         self.lr_scheduler = LRScheduler(self.optimizer, scheduler_params)
         self.schedule_sampler = UniformSampler(diffusion)
         self.grad_norm_clip_value = grad_norm_clip_value
+        self.grad_clip_value = grad_clip_value
         self.rng = np.random.RandomState(seed)
         self.train_step = 0
 
@@ -844,8 +974,11 @@ class Trainer:
         return {"loss": loss, "denoise": loss}
 
     def step(self, batch, noise=None, t=None):
-        """zero_grad -> loss -> backward -> all-reduce -> grad norm -> clip -> AdamW -> lr step."""
+        """zero_grad -> (buffer broadcast) -> loss -> backward -> all-reduce -> grad norm ->
+        clip_grad_norm_ -> clip_grad_value_ -> AdamW -> lr step."""
+        self.model.train()
         self.optimizer.zero_grad()
+        broadcast_buffers(self.model)
         terms = self._compute_loss(batch, noise=noise, t=t)
         terms["loss"].backward()
         allreduce_gradients(self.model.flat_grad)
@@ -853,6 +986,11 @@ class Trainer:
         scale = 1.0
         if self.grad_norm_clip_value is not None:   # clip_grad_norm_: coef = max_norm / (norm + 1e-6), <= 1
             scale = min(1.0, float(self.grad_norm_clip_value) / (gn + 1e-6))
+        if self.grad_clip_value is not None:        # clip_grad_value_ on the clipped gradients, in place
+            g = self.model.flat_grad
+            _ok(_lib().ggd_tr_scale_clamp(g.numel(), _p(g), float(scale), float(self.grad_clip_value), _s(g)),
+                "clip_grad_value_")
+            scale = 1.0
         self.optimizer.step(grad_scale=scale)
         self.lr_scheduler.step()
         self.train_step += 1

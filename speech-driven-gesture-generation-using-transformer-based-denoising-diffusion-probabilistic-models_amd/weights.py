@@ -168,12 +168,13 @@ def _mel_fb(n_freqs=513, n_mels=128, sr=16000):
     return th.clamp(th.min(down, up), min=0.0)
 
 
-def init_state_dict(arch, seed=0, perturb=False, bounded=False):
+def init_state_dict(arch, seed=0, perturb=False, bounded=False, speech=False):
     """Seeded synthetic state_dict.  ``perturb`` randomises LN affines and BN statistics
     (non-trivial values for parity tests; the benchmark uses the reference init).
 
     ``bounded`` gives the denoiser a pose skip path so that a 1000-step trajectory stays O(1)
-    (parity tests at full length; see bounded_skip)."""
+    (parity tests at full length; see bounded_skip).  ``speech`` (implies ``bounded``) makes the
+    output depend on the speech at O(0.1) (see speech_driven)."""
     g = th.Generator().manual_seed(seed)
     sd = {}
     for name, (shape, init) in parameter_shapes(arch).items():
@@ -215,8 +216,34 @@ def init_state_dict(arch, seed=0, perturb=False, bounded=False):
         if perturb and name.endswith("running_var"):
             t = 0.5 + th.rand(shape, generator=g)
         sd[name] = t.contiguous()
-    if bounded:
+    if speech:
+        bounded_skip(sd, arch, seed, emb_scale=3.0)
+        speech_driven(sd, arch)
+    elif bounded:
         bounded_skip(sd, arch, seed)
+    return sd
+
+
+def speech_driven(sd, arch, mem_gain=30.0, ca_out_gain=3.0, ca_qk_gain=4.0):
+    """Scale the memory embedding and the cross-attention so that the speech visibly drives the
+    output (parity tests that must see the cross-attention / encoder path).
+
+    With reference-init weights the memory tokens are dominated by the positional table (the
+    speech part of emb_mem's input is ~0.27 rms against PE's ~0.7) and attention over them is
+    near uniform, so two different wavs change eps by only ~0.2 % (oracle, seed 0) and a
+    1000-step trajectory by less: a parity test with those weights is blind to the speech path.
+    Here emb_mem x mem_gain makes the memory speech-dominated, cross-attention query / key
+    weights x ca_qk_gain make its attention content-dependent, and its output projections x
+    ca_out_gain give it weight in the residual stream.  Measured with the oracle (2 clips, two
+    N(0, 0.1^2) wavs): eps differs by 14.7 % rel-RMS between the wavs, the final x of a T = 1000
+    DDPM run by 16 % (rms(x) 3.0: still bounded with bounded_skip(emb_scale=3))."""
+    sd["pose_decoder.emb_mem.weight"] = (sd["pose_decoder.emb_mem.weight"] * mem_gain).contiguous()
+    for i in range(arch["n_layers"]):
+        p = f"pose_decoder.layers.{i}.cross_attn."
+        sd[p + "output.weight"] = (sd[p + "output.weight"] * ca_out_gain).contiguous()
+        for w in ("query", "key"):
+            k = p + w + ".0.linear.weight"
+            sd[k] = (sd[k] * ca_qk_gain).contiguous()
     return sd
 
 

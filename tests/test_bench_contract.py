@@ -33,15 +33,25 @@ def test_clip_step_flops_hand_count():
     gemm = 2 * L * (C * d + d * C + layers * 14 * d * d)
     attn = layers * 4 * L * (L + Tm) * d
     conv = layers * 4 * 6 * L * d
-    assert bench.clip_step_flops(L, Tm, d, C, layers) == gemm + attn + conv
-    assert abs(bench.clip_step_flops(L, Tm, d, C, layers) / 1e6 - 311.42) < 0.01
+    # the step token's per-step memory work: step MLP 2 x d^2, emb_mem row 0, per layer K and V of
+    # memory rows 0 and 1
+    step = 2 * 2 * d * d + 2 * d * d + layers * 2 * 2 * (2 * d * d)
+    assert bench.clip_step_flops(L, Tm, d, C, layers) == gemm + attn + conv + step
+    assert abs(bench.clip_step_flops(L, Tm, d, C, layers) / 1e6 - 314.3) / 314.3 < 2e-3
+    # C1's two-way decoder: GEMMs + attention = SURVEY.md 8d's 11,839.6 MFLOP
+    tw = bench.twoway_clip_step_flops(34, 104, 512, 126, 10)
+    conv2 = 10 * 6 * 3 * 512 * (34 + 104 + 138)
+    assert abs((tw - conv2) / 1e6 - 11839.6) < 0.1
 
 
 @pytest.mark.parametrize("workload,prefix", [("c2", "mk_kernel"), ("c5", "psk_kernel")])
 def test_pmc_traffic_reads_committed_summary(workload, prefix):
     tr = bench.pmc_traffic(prefix, workload)
-    assert tr is not None and tr["bytes_per_launch"] == tr["read"] + tr["write"] > 0
-    assert os.path.exists(os.path.join(ROOT, tr["source"]))
+    assert tr is not None and os.path.exists(os.path.join(ROOT, tr["source"]))
+    if tr.get("stale"):   # taken on other kernel sources: reported as stale, never as this code's traffic
+        assert "bytes_per_launch" not in tr and tr["summary_csrc"] != tr["current_csrc"] == bench.csrc_hash()
+    else:
+        assert tr["bytes_per_launch"] == tr["read"] + tr["write"] > 0
     assert bench.pmc_traffic(prefix, "nope") is None
 
 

@@ -127,11 +127,29 @@ def test_diagnostics_stay_out_of_the_product_library(pkg):
         assert hasattr(diag, s), s
 
 
-def test_abi_struct_layouts_match_header(pkg):
+def test_abi_struct_layouts_match_header(pkg, tmp_path):
+    """Every field offset and the size of the ctypes mirrors equal what a C compiler makes of
+    include/ggd.h (gcc on a generated probe)."""
+    import subprocess
     native = importlib.import_module(pkg.__name__ + ".native")
-    assert ctypes.sizeof(native.Desc) == 11 * 4
-    # ggd_sample_args: 3 x 4 B + pad, 2 ptrs, u64 seed, i64 offset, 4 ptrs, extras ptr, 2 x int32
-    assert ctypes.sizeof(native.SampleArgs) == 96
+    lines = []
+    for cname, py in (("ggd_desc", native.Desc), ("ggd_sample_args", native.SampleArgs)):
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    src = tmp_path / "probe.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "ggd.h"\nint main(void) {\n' +
+                   "\n".join(lines) + "\nreturn 0;\n}\n")
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        s, f, v = line.split()
+        got[(s, f)] = int(v)
+    for cname, py in (("ggd_desc", native.Desc), ("ggd_sample_args", native.SampleArgs)):
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
 
 
 def test_null_context_is_an_argument_error(pkg):

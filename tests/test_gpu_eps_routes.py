@@ -1,0 +1,169 @@
+"""eps / pred_x_start of every benched sampling route against the CPU oracle, at t spread over
+[0, 999], and a check that these comparisons see a 5 % change of ONE cross-attention weight.
+
+Each case runs ONE denoise step from an injected x_t at a chosen original timestep t (a spaced
+diffusion keeping only step t, respace.py:71-101), so the route's own last iteration writes the
+p_sample dict (gaussian_diffusion.py:278-285) -- eps and pred_x_start of exactly the injected input.
+Unlike a short trajectory's final sample (x_T and the shared noise dominate it near t = 999), eps
+has no such floor: the bf16 bound of SURVEY.md 8d, eps rel-RMS <= 1e-2, applies directly.
+
+Routes (include/ggd.h GGD_ROUTE_*): the clip-group persistent loop mk_kernel (C2 / C3, bf16 and
+f32), the one-workgroup-per-clip loop and the clip-pair loop psk_kernel (C5), the long-clip loop
+lk_kernel (C4, fp8 step weights and bf16).  Weights: reference init with perturbed LN / BN
+(perturb=True), as models/modules/transformer.py:88-118 and models/model.py:94-112 run them.
+"""
+import numpy as np
+import pytest
+import torch as th
+
+from oracle import ref_denoiser, ref_diffusion
+from tests.conftest import oracle_cfg
+
+pytestmark = pytest.mark.gpu
+
+D_POSE = 123
+T_SPREAD = (999, 731, 402, 118, 0)
+ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_LONG_LOOP = 0, 1, 7
+INFO_PAIR_LAUNCHES, INFO_LONG_LAUNCHES = 2, 6
+PERTURBED = "pose_decoder.layers.0.cross_attn.output.weight"
+
+
+def rel_rms(a, b):
+    return (((a - b) ** 2).mean().sqrt() / (b ** 2).mean().sqrt()).item()
+
+
+def _info(ctx, what):
+    import ctypes
+    out = ctypes.c_double()
+    assert ctx.lib.ggd_route_info(ctx.h, what, ctypes.cast(ctypes.byref(out), ctypes.c_void_p)) == 0
+    return out.value
+
+
+# route name -> (dtype, clips, L, wav samples, per-clip mode, pair mode, bound on eps / pred_x_start)
+ROUTES = {
+    "mk_bf16": ("bf16", 4, 40, 32000, 1, 0, 1e-2),
+    "mk_f32": ("f32", 3, 40, 32000, 1, 0, 1e-5),
+    "psk_bf16": ("bf16", 4, 40, 32000, 2, 1, 1e-2),
+    "pair_bf16": ("bf16", 4, 40, 32000, 2, 2, 1e-2),
+    "lk_fp8": ("fp8", 2, 160, 128000, 0, 0, 1e-2),
+    "lk_bf16": ("bf16", 2, 160, 128000, 0, 0, 1e-2),
+}
+
+
+@pytest.fixture(scope="module")
+def weights(pkg, beat_cfg):
+    arch = pkg.arch_from_config(beat_cfg.Model, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    return arch, sd
+
+
+def one_step(pkg, t):
+    betas = pkg.get_named_beta_schedule("linear", 1000)
+    return pkg.GaussianSpacedDiffusion(use_timesteps={t}, betas=betas, model_var_type="fixed_small")
+
+
+def run_route(pkg, beat_cfg, sd, route, ts, seed=5):
+    """eps and pred_x_start of one injected step at each t in ts on `route`; and the inputs."""
+    dtype, n, L, wav_len, per_clip, pair, _ = ROUTES[route]
+    model, _, _, _, _ = pkg.create_model(D_POSE, beat_cfg.Model, dtype=dtype, device="cuda:0")
+    model.load_state_dict(sd)
+    g = th.Generator().manual_seed(seed)
+    wav = th.randn(n, wav_len, generator=g) * 0.1
+    wav_d = wav.cuda()
+    ctx, _ = model.prepare(wav_d, L)
+    out = {}
+    try:
+        # per-clip loops: 2 = always (psk / pair), 1 = never (the clip-group loop); long clips: auto
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_PER_CLIP, {0: 0, 1: 1, 2: 2}[per_clip]) == 0
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_PAIR, pair) == 0
+        for t in ts:
+            x = th.randn(n, D_POSE, L, generator=g)
+            z = th.randn(1, n, D_POSE, L, generator=g)
+            res = one_step(pkg, t).p_sample_loop(model, (n, D_POSE, L), {"wav": wav_d}, noise=x.cuda(),
+                                                 step_noise=z.cuda(), sync=True)
+            out[t] = (x, res["eps"].cpu(), res["pred_x_start"].cpu(), res["sample"].cpu())
+            if route.startswith("pair"):
+                assert int(_info(ctx, INFO_PAIR_LAUNCHES)) == 1
+            if route.startswith("lk"):
+                assert int(_info(ctx, INFO_LONG_LAUNCHES)) == 1
+    finally:
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_PER_CLIP, 0)
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_PAIR, 0)
+    return wav, out
+
+
+def oracle_for(route, arch, sd):
+    from oracle import fp8
+    w = fp8.dequantized_state_dict(sd) if ROUTES[route][0] == "fp8" else sd
+    return ref_denoiser.OracleModel(w, oracle_cfg(arch), cache_speech=True)
+
+
+def reference_step(om, wav, x, t):
+    """eps = model(x, t) and pred_x_start = sqrt(1/abar_t) x - sqrt(1/abar_t - 1) eps
+    (gaussian_diffusion.py:287-292, tables in fp64 cast to f32 as _extract_into_tensor does)."""
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    eps = om(x, th.full((x.shape[0],), t, dtype=th.long), wav=wav)
+    a = np.float32(sch.sqrt_recip_alphas_cumprod[t])
+    b = np.float32(sch.sqrt_recipm1_alphas_cumprod[t])
+    return eps, a * x - b * eps
+
+
+@pytest.mark.parametrize("route", sorted(ROUTES))
+def test_route_eps_and_pred_x_start_match_oracle(pkg, beat_cfg, weights, route):
+    arch, sd = weights
+    bound = ROUTES[route][6]
+    wav, out = run_route(pkg, beat_cfg, sd, route, T_SPREAD)
+    om = oracle_for(route, arch, sd)
+    for t, (x, eps, x0, _) in out.items():
+        e_ref, x0_ref = reference_step(om, wav, x, t)
+        e_err, x_err = rel_rms(eps, e_ref), rel_rms(x0, x0_ref)
+        print(f"{route} t={t}: eps rel-RMS {e_err:.2e}, pred_x_start rel-RMS {x_err:.2e}")
+        assert e_err <= bound, (t, e_err)
+        assert x_err <= bound, (t, x_err)
+
+
+@pytest.mark.parametrize("route", sorted(ROUTES))
+def test_route_eps_check_sees_one_cross_attention_weight(pkg, beat_cfg, weights, route):
+    """The same comparison with the GPU model's layer-0 cross-attention output projection scaled
+    by 1.05 (GPU side only; the oracle keeps the original weights) must FAIL the bound -- the
+    test above can see an error of this size in the cross-attention path (the oracle moves by
+    1.7 % rel-RMS in eps under this change, seed-0 weights)."""
+    arch, sd = weights
+    if ROUTES[route][0] == "f32":
+        pytest.skip("f32's bound (1e-5) trivially sees it; the question is the bf16 / fp8 bound")
+    bad = dict(sd)
+    bad[PERTURBED] = sd[PERTURBED] * 1.05
+    wav, out = run_route(pkg, beat_cfg, bad, route, (402,))
+    om = oracle_for(route, arch, sd)
+    x, eps, _, _ = out[402]
+    e_ref, _ = reference_step(om, wav, x, 402)
+    err = rel_rms(eps, e_ref)
+    print(f"{route}: eps rel-RMS with the perturbed weight {err:.2e}")
+    assert err > ROUTES[route][6], err
+
+
+def test_speech_driven_weights_make_eps_depend_on_speech(pkg, beat_cfg):
+    """weights.speech_driven: two wavs move eps by O(0.1) (oracle), and the bf16 clip-group loop
+    reproduces that difference: rel-RMS of (eps_a - eps_b) GPU vs oracle <= 0.1."""
+    arch = pkg.arch_from_config(beat_cfg.Model, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True, speech=True)
+    om = ref_denoiser.OracleModel(sd, oracle_cfg(arch), cache_speech=True)
+    model, _, _, _, _ = pkg.create_model(D_POSE, beat_cfg.Model, dtype="bf16", device="cuda:0")
+    model.load_state_dict(sd)
+    g = th.Generator().manual_seed(12)
+    n, L = 4, 40
+    wa, wb = (th.randn(n, 32000, generator=g) * 0.1 for _ in range(2))
+    x = th.randn(n, D_POSE, L, generator=g)
+    z = th.randn(1, n, D_POSE, L, generator=g)
+    for t in (731, 118):
+        got, want = [], []
+        for w in (wa, wb):
+            res = one_step(pkg, t).p_sample_loop(model, (n, D_POSE, L), {"wav": w.cuda()}, noise=x.cuda(),
+                                                 step_noise=z.cuda(), sync=True)
+            got.append(res["eps"].cpu())
+            want.append(reference_step(om, w, x, t)[0])
+        speech = rel_rms(want[0], want[1])
+        d_err = rel_rms(got[0] - got[1], want[0] - want[1])
+        print(f"t={t}: speech moves eps by {speech:.3f}; GPU difference vs oracle rel-RMS {d_err:.3e}")
+        assert speech >= 0.05
+        assert d_err <= 0.1, d_err

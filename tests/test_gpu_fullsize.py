@@ -103,3 +103,55 @@ def test_c4_fp8_long_clip_ddpm1000(pkg, beat_cfg, bounded):
     om_q = ref_denoiser.OracleModel(fp8.dequantized_state_dict(sd), oracle_cfg(arch), cache_speech=True)
     curve = _run(pkg, beat_cfg, sd, om_q, "fp8", 32, 160, 128000, "ddpm", "", [0, 31], 8, (250, 1000))
     assert curve[-1][1] <= 5e-2, curve
+
+
+def test_c2_bf16_full_batch_sees_the_speech(pkg, beat_cfg):
+    """C2 at full size (32 clips, DDPM T = 1000, bf16) on weights.speech_driven weights, where the
+    speech moves the final poses by O(0.1): for two wav batches, (a) each run matches the oracle on
+    clips {0, 31} within BASELINE's 5e-2 (the cross-attention / encoder path now carries a share of
+    x several times that bound, so a broken speech path cannot pass), and (b) the GPU's difference
+    out(wav_a) - out(wav_b) matches the oracle's."""
+    arch = pkg.arch_from_config(beat_cfg.Model, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True, speech=True)
+    om = ref_denoiser.OracleModel(sd, oracle_cfg(arch), cache_speech=True)
+    model, diffusion = _model(pkg, beat_cfg, sd, "bf16")
+    n, L, seed, ids = 32, 40, 9, np.array([0, 31])
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    got, want = [], []
+    for ws in (101, 202):
+        wav = th.randn(n, 32000, generator=th.Generator().manual_seed(ws)) * 0.1
+        got.append(diffusion.p_sample_loop(model, (n, D_POSE, L), {"wav": wav.cuda()}, seed=seed,
+                                           extras=False, sync=True)["sample"].cpu()[ids])
+        om._cache = None
+        want.append(ref_diffusion.sample_loop(sch, om, (len(ids), D_POSE, L), {"wav": wav[ids]},
+                                              ref_diffusion.PhiloxNoise(seed, ids), "ddpm")["sample"])
+    speech = rel_rms(want[0], want[1])
+    errs = [rel_rms(g, w) for g, w in zip(got, want)]
+    d_err = rel_rms(got[0] - got[1], want[0] - want[1])
+    print(f"\nspeech moves x by {speech:.3f} rel-RMS (rms x {want[0].pow(2).mean().sqrt().item():.2f}); "
+          f"per-wav rel-RMS {errs}; difference rel-RMS {d_err:.3e}")
+    assert speech >= 0.1
+    assert max(errs) <= 5e-2, errs
+    assert d_err <= 0.25, d_err
+
+
+def test_c2_f32_full_batch_speech_difference(pkg, beat_cfg):
+    """The f32 clip-group loop on the same speech-driven weights: the speech difference itself
+    within 5e-2 rel-RMS of the oracle's (T = 1000, clips {0, 31})."""
+    arch = pkg.arch_from_config(beat_cfg.Model, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True, speech=True)
+    om = ref_denoiser.OracleModel(sd, oracle_cfg(arch), cache_speech=True)
+    model, diffusion = _model(pkg, beat_cfg, sd, "f32")
+    n, L, seed, ids = 32, 40, 9, np.array([0, 31])
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    got, want = [], []
+    for ws in (101, 202):
+        wav = th.randn(n, 32000, generator=th.Generator().manual_seed(ws)) * 0.1
+        got.append(diffusion.p_sample_loop(model, (n, D_POSE, L), {"wav": wav.cuda()}, seed=seed,
+                                           extras=False, sync=True)["sample"].cpu()[ids])
+        om._cache = None
+        want.append(ref_diffusion.sample_loop(sch, om, (len(ids), D_POSE, L), {"wav": wav[ids]},
+                                              ref_diffusion.PhiloxNoise(seed, ids), "ddpm")["sample"])
+    d_err = rel_rms(got[0] - got[1], want[0] - want[1])
+    print(f"\nf32 speech difference rel-RMS {d_err:.3e}")
+    assert d_err <= 5e-2, d_err

@@ -629,3 +629,24 @@ def test_long_loop_equals_launch_route(pkg, beat_cfg, setup, setup_fp8, dtype, n
         want = ref_diffusion.sample_loop(sch, setup_fp8, (n, D_POSE, Lc), {"wav": wav},
                                          ref_diffusion.InjectedNoise(x, zs), "ddpm", x_T=x, n_steps=steps)
         assert rel_rms(out_l["sample"].cpu(), want["sample"]) <= 5e-2
+
+
+def test_c1_tedexp_b1_full_50_step_loop_f32(pkg, tedexp_cfg, setup_c1):
+    """Config C1 as BASELINE.md states it: tedexp (two-way CrossAttention, d 512, 10 layers), B = 1,
+    timestep_respacing "50", ALL 50 DDPM steps on injected noise vs the oracle loop, f32 (nn.py:381-447)."""
+    _, sd, om, wav, x = setup_c1
+    model, diffusion = make_c1(pkg, tedexp_cfg, sd, "f32", respacing="50")
+    assert diffusion.num_timesteps == 50
+    w1, x1 = wav[:1], x[:1]
+    zs = th.randn(50, 1, 126, 34, generator=th.Generator().manual_seed(23))
+    out = diffusion.p_sample_loop(model, (1, 126, 34), model_kwargs={"wav": w1.cuda()}, noise=x1.cuda(),
+                                  step_noise=zs.cuda(), sync=True)
+    sch = ref_diffusion.make_schedule("linear", 1000, "50")
+    want = ref_diffusion.sample_loop(sch, om, (1, 126, 34), {"wav": w1}, ref_diffusion.InjectedNoise(x1, zs),
+                                     "ddpm", x_T=x1)
+    err = (out["sample"].cpu() - want["sample"]).abs().max().item()
+    e_err = (out["eps"].cpu() - want["eps"]).abs().max().item()
+    print(f"C1 50 steps: sample max|diff| {err:.3e} (max|x| {want['sample'].abs().max().item():.3f}), "
+          f"last eps max|diff| {e_err:.3e}")
+    assert err <= 1e-3, err
+    assert e_err <= 1e-3, e_err

@@ -50,3 +50,44 @@ def test_prefetch_out_of_order_and_inline_calls():
     model._release()
     assert th.equal(o1, gen.generate_sample(shape, w1, device="cuda:0", progress=False, seed=3))
     assert th.equal(o2, gen.generate_sample(shape, w2, device="cuda:0", progress=False, seed=3))
+
+
+@pytest.mark.gpu
+def test_prefetch_beside_persistent_loop_matches_oracle():
+    """The next batch's encoder on the side stream WHILE the clip-group persistent loop runs
+    (C2 shape, 32 clips: the loop needs every one of its 256 workgroups resident, the encoder's
+    kernels hold CUs meanwhile).  One non-blocking run: no status error (ggd_sync), the output
+    equals the run without the prefetch bit for bit, and eps / the sample match the oracle."""
+    import numpy as np
+    from oracle import ref_denoiser, ref_diffusion
+    from tests.conftest import oracle_cfg
+    pkg = ge.load_package()
+    cfg = pkg.load_config(os.path.join(ROOT, "configs", "beat-ours.json"))
+    model, diffusion, _, _, _ = pkg.create_model(123, cfg.Model, dtype="bf16", device="cuda:0")
+    sd = pkg.init_state_dict(model.arch, seed=0, perturb=True)
+    model.load_state_dict(sd)
+    n, L, steps = 32, 40, 6
+    g = th.Generator().manual_seed(13)
+    w1, w2 = (th.randn(n, 32000, generator=g) * 0.1 for _ in range(2))
+    x = th.randn(n, 123, L, generator=g)
+    zs = th.randn(steps, n, 123, L, generator=g)
+    w1d, w2d, xd, zd = w1.cuda(), w2.cuda(), x.cuda(), zs.cuda()
+    run = lambda pre: diffusion.p_sample_loop(model, (n, 123, L), {"wav": w1d}, noise=xd, step_noise=zd,
+                                              n_steps=steps, prefetch_wav=pre)
+    with_pre = run(w2d)
+    model.sync()                                   # raises if the loop reported a status error
+    assert len(model._pending) == 1                # w2's tokens wait for their sampling call
+    model._release()
+    plain = run(None)
+    model.sync()
+    for k in ("sample", "eps"):
+        assert th.equal(with_pre[k], plain[k]), k
+    ids = np.array([0, 17, 31])
+    om = ref_denoiser.OracleModel(sd, oracle_cfg(model.arch), cache_speech=True)
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    want = ref_diffusion.sample_loop(sch, om, (len(ids), 123, L), {"wav": w1[ids]},
+                                     ref_diffusion.InjectedNoise(x[ids], zs[:, ids]), "ddpm", x_T=x[ids],
+                                     n_steps=steps)
+    rr = lambda a, b: (((a - b) ** 2).mean().sqrt() / (b ** 2).mean().sqrt()).item()
+    assert rr(with_pre["eps"].cpu()[ids], want["eps"]) <= 1e-2
+    assert rr(with_pre["sample"].cpu()[ids], want["sample"]) <= 5e-2

@@ -414,3 +414,90 @@ def test_training_step_with_encoder_matches_oracle_loss(tr, enc_setup):
     worst = max((model.params[k].grad.cpu() - sd_ref[k].grad).abs().max().item()
                 / max(sd_ref[k].grad.abs().max().item(), floor) for k in dec)
     assert worst <= 2e-3, worst
+
+
+# ------------------------------------------------------------------------------------------
+# checkpoints written by training feed the sampler (main.py:113-115: strict load of
+# chkpt["model_state_dict"]); optimizer state in torch.optim.AdamW's layout (trainer.py:203, 218)
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("train_encoder", [False, True])
+def test_trained_checkpoint_loads_into_sampler(pkg, beat_cfg, tr, tmp_path, train_encoder):
+    import importlib
+    fm = importlib.import_module(pkg.__name__ + ".formats")
+    arch = pkg.arch_from_config(beat_cfg.Model, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    diffusion = pkg.create_diffusion(beat_cfg.Model.Diffusion.to_dict(), True)
+    model = tr.TrainableModel(arch, sd, "cuda", train_encoder=train_encoder)
+    trainer = tr.Trainer(model, diffusion, None, lr=1e-3, weight_decay=0.0)
+    g = th.Generator().manual_seed(31)
+    wav = th.randn(3, WAV, generator=g) * 0.1
+    trainer.step({"pose": th.randn(3, L, D_POSE, generator=g).cuda(), "wav": wav.cuda()})
+    path = tmp_path / "chkpt_gpu0_seed0.pt"
+    fm.save_checkpoint(str(path), trainer)
+    trained = {k: v.cpu() for k, v in model.state_dict().items()}
+    assert list(trained) == list(sd)                    # the reference module tree's full key set, in order
+    sampler, _, _, _, _ = pkg.create_model(D_POSE, beat_cfg.Model, dtype="f32", device="cuda:0")
+    fm.load_model_checkpoint(sampler, str(path), strict=True)
+    x = th.randn(3, D_POSE, L, generator=g)
+    t = th.tensor([999, 500, 0])
+    eps = sampler(x.cuda(), t.cuda(), wav=wav.cuda()).cpu()
+    want = ref_denoiser.OracleModel(trained, oracle_cfg(arch), cache_speech=True)(x, t, wav=wav)
+    assert (eps - want).abs().max().item() <= 1e-4
+    if train_encoder:   # the step moved the encoder's BN statistics; the sampler sees the moved ones
+        k = "speech_encoder.wav_encoder.feat_extractor.bn1.running_mean"
+        assert not th.equal(trained[k], sd[k]) and int(trained[k.replace("running_mean", "num_batches_tracked")]) == 1
+
+
+def test_eval_mode_uses_running_statistics(pkg, beat_cfg, tr):
+    """TrainableModel.eval() (model.eval(), trainer.py:252): the encoder normalises with the running
+    statistics and a forward leaves them unchanged; train() restores batch statistics."""
+    arch = pkg.arch_from_config(beat_cfg.Model, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    model = tr.TrainableModel(arch, sd, "cuda", train_encoder=True)
+    g = th.Generator().manual_seed(41)
+    wav = th.randn(2, WAV, generator=g) * 0.1
+    x = th.randn(2, D_POSE, L, generator=g)
+    t = th.tensor([10, 900])
+    before = {k: v.clone() for k, v in model.buffers.items()}
+    model.eval()
+    with th.no_grad():
+        e1 = model(x.cuda(), t.cuda(), wav=wav.cuda()).cpu()
+    assert all(th.equal(before[k], v) for k, v in model.buffers.items())
+    want = ref_denoiser.OracleModel(sd, oracle_cfg(arch), cache_speech=True)(x, t, wav=wav)
+    assert (e1 - want).abs().max().item() <= 1e-4            # eval-mode BN = the oracle's running stats
+    model.train()
+    with th.no_grad():
+        model(x.cuda(), t.cuda(), wav=wav.cuda())
+    k = "speech_encoder.wav_encoder.feat_extractor.bn1.running_mean"
+    assert not th.equal(before[k], model.buffers[k])
+
+
+def test_optimizer_state_is_torch_adamw_layout(pkg, beat_cfg, tr):
+    """Our AdamW's state_dict loads into torch.optim.AdamW over the reference parameter order and
+    both take the same next step; and a torch AdamW state loads back into ours."""
+    arch = pkg.arch_from_config(beat_cfg.Model, D_POSE)
+    sd = pkg.init_state_dict(arch, seed=0)
+    model = tr.TrainableModel(arch, sd, "cuda")
+    opt = tr.AdamW(model, lr=3e-3, weight_decay=0.01)
+    g = th.Generator().manual_seed(6)
+    for _ in range(2):
+        model.flat_grad.copy_(th.randn(model.flat.shape, generator=g) * 1e-2)
+        opt.step()
+    st = opt.state_dict()
+    params = [p.detach().cpu().clone().requires_grad_(True) for p in model.params.values()]
+    ref = th.optim.AdamW(params, lr=3e-3, weight_decay=0.01)
+    ref.load_state_dict(st)
+    grad = th.randn(model.flat.shape, generator=g) * 1e-2
+    off = 0
+    for p in params:
+        p.grad = grad[off:off + p.numel()].view(p.shape).clone()
+        off += p.numel()
+    ref.step()
+    model.flat_grad.copy_(grad)
+    opt.step()
+    close(model.flat, th.cat([p.detach().reshape(-1) for p in params]), 2e-6)
+    opt2 = tr.AdamW(tr.TrainableModel(arch, sd, "cuda"), lr=3e-3, weight_decay=0.01)
+    opt2.load_state_dict(ref.state_dict())
+    assert opt2.step_count == 3
+    close(opt2.exp_avg, opt.exp_avg, 1e-6)
+    close(opt2.exp_avg_sq, opt.exp_avg_sq, 1e-6)

@@ -110,3 +110,129 @@ def test_uniform_sampler_draws_every_step_with_unit_weights():
     t, w = tr.UniformSampler(D()).sample(4000, "cpu", np.random.RandomState(0))
     assert t.dtype == th.int64 and int(t.min()) == 0 and int(t.max()) == 49
     assert len(th.unique(t)) == 50 and th.equal(w, th.ones(4000))
+
+
+# ------------------------------------------------------------------------------------------
+# DDP semantics (trainer.py:83): construction-time broadcast of rank 0's parameters / buffers,
+# and the averaged gradient of per-rank half batches == the gradient of the union batch
+# ------------------------------------------------------------------------------------------
+class _FlatModel:
+    """What broadcast_parameters touches on a TrainableModel: the flat parameter buffer and the
+    BatchNorm buffers (CPU tensors here; the same calls move device tensors over RCCL)."""
+
+    def __init__(self, rank, n):
+        g = th.Generator().manual_seed(100 + rank)
+        self.flat = th.randn(n, generator=g)
+        self.buffers = {"a.running_mean": th.randn(7, generator=g), "a.num_batches_tracked": th.tensor(rank + 3)}
+
+
+def _bcast_worker(rank, world, port, n, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tr = _training()
+        tr.BUCKET_ELEMS = 300
+        m = _FlatModel(rank, n)
+        tr.broadcast_parameters(m)
+        q.put((rank, m.flat.numpy().copy(), {k: v.numpy().copy() for k, v in m.buffers.items()}))  # by value
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port) + args + (q,)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(res, key=lambda r: r[0])
+
+
+def test_broadcast_parameters_takes_rank0_state():
+    n = 1000
+    res = _spawn(_bcast_worker, 2, n)
+    want = _FlatModel(0, n)
+    assert not th.equal(_FlatModel(1, n).flat, want.flat)     # rank 1 started elsewhere
+    for rank, flat, bufs in res:
+        assert th.equal(th.from_numpy(flat), want.flat), rank
+        for k, v in want.buffers.items():
+            assert th.equal(th.from_numpy(bufs[k]), v), (rank, k)
+
+
+def _decoder_grad(clips):
+    """Flat gradient (training._trainable order, encoder frozen) of the mean per-clip diffusion MSE
+    over `clips` of a fixed synthetic batch, by torch autograd through the CPU oracle
+    (gaussian_diffusion.py:531-569 on oracle/ref_denoiser.denoise, speech tokens given)."""
+    import __graft_entry__ as ge
+    from oracle import ref_denoiser
+    from tests.conftest import oracle_cfg
+    pkg = ge.load_package()
+    tr = _training()
+    cfg = pkg.load_config(os.path.join(ROOT, "configs", "beat-ours.json"))
+    arch = pkg.arch_from_config(cfg.Model, 123)
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    names = [k for k, _ in tr._trainable(arch, False)]
+    for k in names:
+        sd[k] = sd[k].float().clone().requires_grad_(True)
+    g = th.Generator().manual_seed(11)
+    n, L = 4, 40
+    x0 = th.randn(n, 123, L, generator=g)
+    noise = th.randn(n, 123, L, generator=g)
+    t = th.tensor([999, 421, 77, 3])
+    z = tuple(th.randn(n, Ti, 256, generator=g) * 0.3 for Ti in (31, 30, 30))
+    diffusion = pkg.create_diffusion(cfg.Model.Diffusion.to_dict(), True)
+    idx = t.numpy()
+    ca = th.from_numpy(diffusion.sqrt_alphas_cumprod[idx]).float().reshape(-1, 1, 1)
+    cb = th.from_numpy(diffusion.sqrt_one_minus_alphas_cumprod[idx]).float().reshape(-1, 1, 1)
+    sel = th.tensor(clips)
+    x_t = (ca * x0 + cb * noise)[sel]
+    speech = ref_denoiser.speech_memory(sd, oracle_cfg(arch), tuple(a[sel] for a in z))
+    eps = ref_denoiser.denoise(sd, oracle_cfg(arch), x_t, t[sel], speech=speech)
+    loss = ((eps - noise[sel]) ** 2).mean(dim=(1, 2)).mean()
+    loss.backward()
+    return th.cat([sd[k].grad.reshape(-1) for k in names])
+
+
+def _grad_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    th.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = _decoder_grad([2 * rank, 2 * rank + 1])
+        out = _training().allreduce_gradients(g)
+        q.put((rank, out.numpy().copy()))   # by value: the worker exits before the parent reads
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_average_of_half_batches_equals_union_batch_gradient():
+    res = _spawn(_grad_worker, 2)
+    want = _decoder_grad([0, 1, 2, 3])
+    scale = want.abs().max().item()
+    for rank, got in res:
+        err = (th.from_numpy(got) - want).abs().max().item()
+        assert err <= 1e-5 * scale, (rank, err, scale)
+    assert (res[0][1] == res[1][1]).all()       # every rank holds the same averaged gradient
+
+
+def test_parse_steps_follows_string_parser_code():
+    tr = _training()
+    assert tr.parse_steps("100") == 100 and tr.parse_steps("500k") == 500000
+    assert tr.parse_steps("100kk") == 200000    # string_parser.py: base * count('k') * 1000
+
+
+def test_noam_decay_has_no_floor():
+    """create_lr_scheduler builds NoamDecayLR without `minimum` (model_creation.py:23)."""
+    tr = _training()
+    o = _Opt(1.0)
+    s = tr.LRScheduler(o, {"type": "noam", "warmup_steps": "10", "minimum": 0.5})
+    for _ in range(1000):
+        s.step()
+    assert o.param_groups[0]["lr"] == pytest.approx(10 ** 0.5 * 1000 ** -0.5)
