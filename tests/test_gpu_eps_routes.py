@@ -2,8 +2,11 @@
 [0, 999], and a check that these comparisons see a 5 % change of ONE cross-attention weight.
 
 Each case runs ONE denoise step from an injected x_t at a chosen original timestep t (a spaced
-diffusion keeping only step t, respace.py:71-101), so the route's own last iteration writes the
-p_sample dict (gaussian_diffusion.py:278-285) -- eps and pred_x_start of exactly the injected input.
+diffusion keeping steps {t // 2, t}, respace.py:71-101, stopped after its first iteration), so the
+route's own last iteration writes the p_sample dict (gaussian_diffusion.py:278-285) -- eps and
+pred_x_start of exactly the injected input.  t = 0 can only be a loop's LAST step: the spaced
+diffusion {0, 1} runs one step (whose sample is the input of the next) and then both steps; the
+second run's t = 0 extras are checked on the first run's sample, reproduced bit for bit.
 Unlike a short trajectory's final sample (x_T and the shared noise dominate it near t = 999), eps
 has no such floor: the bf16 bound of SURVEY.md 8d, eps rel-RMS <= 1e-2, applies directly.
 
@@ -57,9 +60,23 @@ def weights(pkg, beat_cfg):
     return arch, sd
 
 
-def one_step(pkg, t):
+def spaced(pkg, steps):
     betas = pkg.get_named_beta_schedule("linear", 1000)
-    return pkg.GaussianSpacedDiffusion(use_timesteps={t}, betas=betas, model_var_type="fixed_small")
+    return pkg.GaussianSpacedDiffusion(use_timesteps=set(steps), betas=betas, model_var_type="fixed_small")
+
+
+def step_at(pkg, model, n, L, wav_d, x, z, t):
+    """(input x, eps, pred_x_start) of the loop iteration at original timestep t."""
+    if t > 0:   # the first iteration of {t // 2, t} (GaussianDiffusion needs >= 2 kept steps)
+        res = spaced(pkg, (t // 2, t)).p_sample_loop(model, (n, D_POSE, L), {"wav": wav_d}, noise=x.cuda(),
+                                                      step_noise=z.cuda(), n_steps=1, sync=True)
+        return x, res["eps"].cpu(), res["pred_x_start"].cpu()
+    d = spaced(pkg, (0, 1))
+    zz = th.cat([z, z]).cuda()
+    x1 = d.p_sample_loop(model, (n, D_POSE, L), {"wav": wav_d}, noise=x.cuda(), step_noise=zz, n_steps=1,
+                         sync=True)["sample"].cpu()
+    res = d.p_sample_loop(model, (n, D_POSE, L), {"wav": wav_d}, noise=x.cuda(), step_noise=zz, sync=True)
+    return x1, res["eps"].cpu(), res["pred_x_start"].cpu()
 
 
 def run_route(pkg, beat_cfg, sd, route, ts, seed=5):
@@ -79,9 +96,7 @@ def run_route(pkg, beat_cfg, sd, route, ts, seed=5):
         for t in ts:
             x = th.randn(n, D_POSE, L, generator=g)
             z = th.randn(1, n, D_POSE, L, generator=g)
-            res = one_step(pkg, t).p_sample_loop(model, (n, D_POSE, L), {"wav": wav_d}, noise=x.cuda(),
-                                                 step_noise=z.cuda(), sync=True)
-            out[t] = (x, res["eps"].cpu(), res["pred_x_start"].cpu(), res["sample"].cpu())
+            out[t] = step_at(pkg, model, n, L, wav_d, x, z, t)
             if route.startswith("pair"):
                 assert int(_info(ctx, INFO_PAIR_LAUNCHES)) == 1
             if route.startswith("lk"):
@@ -114,11 +129,15 @@ def test_route_eps_and_pred_x_start_match_oracle(pkg, beat_cfg, weights, route):
     bound = ROUTES[route][6]
     wav, out = run_route(pkg, beat_cfg, sd, route, T_SPREAD)
     om = oracle_for(route, arch, sd)
-    for t, (x, eps, x0, _) in out.items():
+    for t, (x, eps, x0) in out.items():
         e_ref, x0_ref = reference_step(om, wav, x, t)
         e_err, x_err = rel_rms(eps, e_ref), rel_rms(x0, x0_ref)
-        print(f"{route} t={t}: eps rel-RMS {e_err:.2e}, pred_x_start rel-RMS {x_err:.2e}")
-        assert e_err <= bound, (t, e_err)
+        e_abs = (eps - e_ref).abs().max().item()
+        print(f"{route} t={t}: eps rel-RMS {e_err:.2e} (max|diff| {e_abs:.2e}), pred_x_start rel-RMS {x_err:.2e}")
+        if ROUTES[route][0] == "f32":   # f32 eps max-abs <= 1e-4
+            assert e_abs <= 1e-4, (t, e_abs)
+        else:
+            assert e_err <= bound, (t, e_err)
         assert x_err <= bound, (t, x_err)
 
 
@@ -135,7 +154,7 @@ def test_route_eps_check_sees_one_cross_attention_weight(pkg, beat_cfg, weights,
     bad[PERTURBED] = sd[PERTURBED] * 1.05
     wav, out = run_route(pkg, beat_cfg, bad, route, (402,))
     om = oracle_for(route, arch, sd)
-    x, eps, _, _ = out[402]
+    x, eps, _ = out[402]
     e_ref, _ = reference_step(om, wav, x, 402)
     err = rel_rms(eps, e_ref)
     print(f"{route}: eps rel-RMS with the perturbed weight {err:.2e}")
@@ -158,9 +177,8 @@ def test_speech_driven_weights_make_eps_depend_on_speech(pkg, beat_cfg):
     for t in (731, 118):
         got, want = [], []
         for w in (wa, wb):
-            res = one_step(pkg, t).p_sample_loop(model, (n, D_POSE, L), {"wav": w.cuda()}, noise=x.cuda(),
-                                                 step_noise=z.cuda(), sync=True)
-            got.append(res["eps"].cpu())
+            got.append(step_at(pkg, model, n, L, w.cuda(), x, z, t)[1])
+            om._cache = None
             want.append(reference_step(om, w, x, t)[0])
         speech = rel_rms(want[0], want[1])
         d_err = rel_rms(got[0] - got[1], want[0] - want[1])
