@@ -29,13 +29,16 @@ def diag(what, p, n_out=1):
 
 
 diffusion.p_sample_loop(model, (32, 123, 40), model_kwargs={"wav": wav}, seed=1, extras=False, n_steps=5)
-names = [f"L{li}{ph}" for li in range(4) for ph in "ABCD"] + ["E"]
+# bf16 loop: KA KB KC per layer (the FFN-down reduction runs inside the next phase) + KE
+PH = "ABCD" if os.environ.get("MEGA_KD", "1") == "1" else "ABC"
+names = [f"L{li}{ph}" for li in range(4) for ph in PH] + ["E"]
+NB = len(names)
 for rep in range(3):
     diag(10, [1])
     diffusion.p_sample_loop(model, (32, 123, 40), model_kwargs={"wav": wav}, seed=1, extras=False, n_steps=5)
     t = diag(10, [2], 2 * 17 * 2)
     for step in range(2):
-        base = step * 34
+        base = step * 2 * NB
         prev = t[base - 1] if step else 0.0
         cells = []
         tb = tw = 0.0

@@ -16,6 +16,10 @@
 //   heads    low conv2x2 / mid shuffle2+conv3x3 / high shuffle4+conv3x3, ReLU, BN, flatten (c*H + h),
 //            Linear -> 32, wav_proj Linear 32 -> d (ResNetSE34V2.py:157-188, speech_encoder.py:59-61)
 //
+// Activations between the kernels are bf16 in bf16 contexts (the convolutions round their inputs to
+// bf16 anyway: storing them so halves every activation byte moved -- conv inputs / outputs, the SE
+// squeeze, the SE apply, the shuffles) and f32 in f32 contexts.
+//
 // Convolutions are implicit GEMMs on MFMA: rows = output pixels (NHWC, channels innermost),
 // columns = output channels, K = taps x input channels in chunks of 32.  Every lane reads its
 // own operand fragment straight from global memory (8 consecutive channels of one pixel, 8
@@ -109,9 +113,10 @@ __global__ void __launch_bounds__(NMEL) enc_inorm_kernel(const float* __restrict
 }
 
 // conv1 (1 -> 32, 3x3, pad 1) + bias, ReLU, BN; one thread per (pixel, 8 output channels)
+template <typename TA>
 __global__ void enc_conv1_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                  const float* __restrict__ bias, const float* __restrict__ s,
-                                 const float* __restrict__ t, float* __restrict__ out, int n, int H, int W) {
+                                 const float* __restrict__ t, TA* __restrict__ out, int n, int H, int W) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x, total = (size_t)n * H * W * 4;
   if (idx >= total) return;
   const int cg = (int)(idx & 3);
@@ -134,23 +139,51 @@ __global__ void enc_conv1_kernel(const float* __restrict__ img, const float* __r
     for (int q = 0; q < 9; ++q) acc += w[c * 9 + q] * tap[q];
     o[j] = fmaxf(acc + bias[c], 0.f) * s[c] + t[c];
   }
-  float4* dst = (float4*)(out + p * 32 + cg * 8);
-  dst[0] = make_float4(o[0], o[1], o[2], o[3]);
-  dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+  if constexpr (sizeof(TA) == 2) {
+    uint4 u;
+    u.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+    u.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+    u.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+    u.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+    *(uint4*)(out + p * 32 + cg * 8) = u;
+  } else {
+    float4* dst = (float4*)(out + p * 32 + cg * 8);
+    dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
 // implicit-GEMM convolution
 // ------------------------------------------------------------------------------------------
 enum { CONV_BN = 0, CONV_RELU_BN = 1 };
+
+// activation element access (f32 or bf16 tensors)
+__device__ __forceinline__ void act_load8(const float* p, float (&v)[8]) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void act_load8(const bf16_t* p, float (&v)[8]) {
+  const uint4 u = *(const uint4*)p;
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ float act_ld(const float* p) { return *p; }
+__device__ __forceinline__ float act_ld(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ void act_st(float* p, float v) { *p = v; }
+__device__ __forceinline__ void act_st(bf16_t* p, float v) { *p = f2bf(v); }
 enum { LAYOUT_NHWC = 0, LAYOUT_NWCH = 1 };
 
 struct ConvArgs {
-  const float* in;          // f32 NHWC [N][H][W][Cin] (Cin a multiple of 32)
+  const void* in;           // NHWC [N][H][W][Cin] (Cin a multiple of 32), f32 or bf16 (in_bf16)
   const void* w;            // T [Cout_pad][KH * KW][Cin]
   const float *bias, *s, *t;  // [Cout_pad]: BN folded to y = x * s + t
-  float* out;
-  int N, H, W, Cin, Ho, Wo, Cout_pad, Cvalid, KH, KW, stride, pad, mode, layout;
+  void* out;                // f32 or bf16 (out_bf16)
+  int N, H, W, Cin, Ho, Wo, Cout_pad, Cvalid, KH, KW, stride, pad, mode, layout, in_bf16, out_bf16;
 };
 
 template <typename T> struct ConvB;
@@ -187,8 +220,10 @@ struct ConvStage {
   ConvB<T> b[NJ];
 };
 
-template <typename T, int NJ>
+template <typename T, int NJ, typename TI, typename TO>
 __global__ void __launch_bounds__(CONV_TPB) enc_conv_kernel(ConvArgs a) {
+  const TI* in = (const TI*)a.in;
+  TO* out = (TO*)a.out;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r16 = lane & 15, g = lane >> 4;
   const int HWo = a.Ho * a.Wo, P = a.N * HWo;
   const int p0 = blockIdx.x * 128 + wave * 32, n0 = blockIdx.y * (NJ * 16);
@@ -215,11 +250,11 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_kernel(ConvArgs a) {
       const int iy = iy0[i] + ky, ix = ix0[i] + kx;
       const bool ok = pv[i] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
       const int pix = base[i] + min(max(iy, 0), a.H - 1) * a.W + min(max(ix, 0), a.W - 1);
-      const float* src = a.in + (size_t)pix * a.Cin + c0 + g * 8;
-      const float4 u = *(const float4*)src, v = *(const float4*)(src + 4);
+      float u[8];
+      act_load8(in + (size_t)pix * a.Cin + c0 + g * 8, u);
       const float m = ok ? 1.f : 0.f;
-      st.a[i].v[0] = u.x * m; st.a[i].v[1] = u.y * m; st.a[i].v[2] = u.z * m; st.a[i].v[3] = u.w * m;
-      st.a[i].v[4] = v.x * m; st.a[i].v[5] = v.y * m; st.a[i].v[6] = v.z * m; st.a[i].v[7] = v.w * m;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) st.a[i].v[e] = u[e] * m;
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) st.b[j].load(wb + j * wj + (size_t)tap * a.Cin + c0);
@@ -255,10 +290,10 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_kernel(ConvArgs a) {
         float v = acc[i][j][r];
         v = a.mode == CONV_RELU_BN ? fmaxf(v + bi, 0.f) * sc + sh : (v + bi) * sc + sh;
         if (a.layout == LAYOUT_NHWC) {
-          a.out[(size_t)p * a.Cout_pad + co] = v;
+          act_st(out + (size_t)p * a.Cout_pad + co, v);
         } else if (co < a.Cvalid) {
           const int b = p / HWo, rem = p - b * HWo, oy = rem / a.Wo, ox = rem - oy * a.Wo;
-          a.out[(((size_t)b * a.Wo + ox) * a.Cvalid + co) * a.Ho + oy] = v;
+          act_st(out + (((size_t)b * a.Wo + ox) * a.Cvalid + co) * a.Ho + oy, v);
         }
       }
   }
@@ -269,24 +304,25 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_kernel(ConvArgs a) {
 // ------------------------------------------------------------------------------------------
 // SE squeeze, stage 1: grid (clips, S slices); each workgroup sums its slice of the clip's pixels
 // for every channel -> part[clip][slice][C] (fixed partition and order: deterministic)
-__global__ void __launch_bounds__(256) enc_se_sum_kernel(const float* __restrict__ v, int HW, int C,
+template <typename TA>
+__global__ void __launch_bounds__(256) enc_se_sum_kernel(const TA* __restrict__ v, int HW, int C,
                                                          float* __restrict__ part) {
   __shared__ float red[256];
   const int b = blockIdx.x, sl = blockIdx.y, S = gridDim.y, tid = threadIdx.x;
   const int stripes = 256 / C, c = tid % C, st = tid / C;
   const int p0 = (int)((long)HW * sl / S), p1 = (int)((long)HW * (sl + 1) / S);
-  const float* src = v + (size_t)b * HW * C;
+  const TA* src = v + (size_t)b * HW * C;
   // four independent partial sums keep four loads in flight per thread (fixed order per clip)
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (st < stripes) {
     int p = p0 + st;
     for (; p + 3 * stripes < p1; p += 4 * stripes) {
-      s0 += src[(size_t)p * C + c];
-      s1 += src[(size_t)(p + stripes) * C + c];
-      s2 += src[(size_t)(p + 2 * stripes) * C + c];
-      s3 += src[(size_t)(p + 3 * stripes) * C + c];
+      s0 += act_ld(src + (size_t)p * C + c);
+      s1 += act_ld(src + (size_t)(p + stripes) * C + c);
+      s2 += act_ld(src + (size_t)(p + 2 * stripes) * C + c);
+      s3 += act_ld(src + (size_t)(p + 3 * stripes) * C + c);
     }
-    for (; p < p1; p += stripes) s0 += src[(size_t)p * C + c];
+    for (; p < p1; p += stripes) s0 += act_ld(src + (size_t)p * C + c);
   }
   red[tid] = (s0 + s1) + (s2 + s3);
   __syncthreads();
@@ -324,27 +360,38 @@ __global__ void __launch_bounds__(256) enc_se_kernel(const float* __restrict__ p
   }
 }
 
-// out = relu(v * y[clip][c] + res), NHWC
-__global__ void enc_se_apply_kernel(const float* __restrict__ v, const float* __restrict__ y,
-                                    const float* __restrict__ res, float* __restrict__ out, int HW, int C,
-                                    size_t total4) {
+// out = relu(v * y[clip][c] + res), NHWC; 8 consecutive channels per thread
+template <typename TA>
+__global__ void enc_se_apply_kernel(const TA* __restrict__ v, const float* __restrict__ y,
+                                    const TA* __restrict__ res, TA* __restrict__ out, int HW, int C,
+                                    size_t total8) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= total4) return;
-  const size_t e = idx * 4;
+  if (idx >= total8) return;
+  const size_t e = idx * 8;
   const int c = (int)(e % C);
   const size_t b = e / ((size_t)HW * C);
-  const float4 a = ((const float4*)v)[idx], r = ((const float4*)res)[idx];
+  float a[8], r[8];
+  act_load8(v + e, a);
+  act_load8(res + e, r);
   const float* ys = y + b * C + c;
-  float4 o;
-  o.x = fmaxf(a.x * ys[0] + r.x, 0.f);
-  o.y = fmaxf(a.y * ys[1] + r.y, 0.f);
-  o.z = fmaxf(a.z * ys[2] + r.z, 0.f);
-  o.w = fmaxf(a.w * ys[3] + r.w, 0.f);
-  ((float4*)out)[idx] = o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = fmaxf(a[i] * ys[i] + r[i], 0.f);
+  if constexpr (sizeof(TA) == 2) {
+    uint4 u;
+    u.x = (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
+    u.y = (uint32_t)f2bf(a[2]) | ((uint32_t)f2bf(a[3]) << 16);
+    u.z = (uint32_t)f2bf(a[4]) | ((uint32_t)f2bf(a[5]) << 16);
+    u.w = (uint32_t)f2bf(a[6]) | ((uint32_t)f2bf(a[7]) << 16);
+    *(uint4*)(out + e) = u;
+  } else {
+    *(float4*)(out + e) = make_float4(a[0], a[1], a[2], a[3]);
+    *(float4*)(out + e + 4) = make_float4(a[4], a[5], a[6], a[7]);
+  }
 }
 
 // PixelShuffle(r): in NHWC [n][H][W][C r^2] -> out NHWC [n][H r][W r][Cp] (channels >= C zero)
-__global__ void enc_shuffle_kernel(const float* __restrict__ in, float* __restrict__ out, int n, int H, int W,
+template <typename TA>
+__global__ void enc_shuffle_kernel(const TA* __restrict__ in, TA* __restrict__ out, int n, int H, int W,
                                    int C, int r, int Cp) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int Ho = H * r, Wo = W * r;
@@ -355,9 +402,9 @@ __global__ void enc_shuffle_kernel(const float* __restrict__ in, float* __restri
   float v = 0.f;
   if (c < C) {
     const int h = yy / r, i = yy - h * r, w = x / r, j = x - w * r;
-    v = in[(((size_t)b * H + h) * W + w) * (C * r * r) + c * r * r + i * r + j];
+    v = act_ld(in + (((size_t)b * H + h) * W + w) * (C * r * r) + c * r * r + i * r + j);
   }
-  out[idx] = v;
+  act_st(out + idx, v);
 }
 
 // one workgroup per (clip, time) row: z = Wp (W1 a + b1) + bp, a = the row's (c, h) features
@@ -428,9 +475,13 @@ __host__ __device__ inline ConvLdsGeom conv_lds_geom(const ConvArgs& a, int TW, 
   return g;
 }
 
-template <int NJ, int PM>
+template <int NJ, int PM, typename TI, typename TO>
 __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int TW) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // an input piece is one 16-byte load: 4 f32 or 8 bf16 channels; QP pieces per 32-channel chunk
+  constexpr int CPP = 16 / (int)sizeof(TI), QP = 32 / CPP;
+  const TI* in = (const TI*)a.in;
+  TO* out = (TO*)a.out;
   const ConvLdsGeom G = conv_lds_geom(a, TW, NJ);
   bf16_t* patch = (bf16_t*)smem;
   bf16_t* wl = (bf16_t*)(smem + G.patch_bytes);
@@ -455,8 +506,8 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int 
   // the next chunk's patch and filter taps are fetched into registers while this chunk's MFMAs
   // run (PM / WMAX pieces per thread bound them; launch_conv checks the shape fits)
   constexpr int WMAX = (NJ * 16 * CL_TAPS_MAX * 4 + CONV_TPB - 1) / CONV_TPB;
-  const int np8 = npos * 8, nw = NJ * 16 * G.taps * 4;
-  f32x4 xr[PM];
+  const int np8 = npos * QP, nw = NJ * 16 * G.taps * 4;
+  uint4 xr[PM];
   bf16x8 wr[WMAX];  // native vectors (HIP's uint4 struct copies keep the array in scratch)
   uint32_t okm = 0;  // bit k: patch piece k lies inside the image (else it stages as zero)
   auto fetch = [&](int ck) __attribute__((always_inline)) {
@@ -466,11 +517,11 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int 
       const int v = tid + k * CONV_TPB;
       {
         const int vc = min(v, np8 - 1);
-        const int pos = vc >> 3, q4 = vc & 7, py = pos / G.PW, px = pos - py * G.PW;
+        const int pos = vc / QP, q4 = vc % QP, py = pos / G.PW, px = pos - py * G.PW;
         const int ih = ih0 + py, iw = iw0 + px;
         const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
         const int ihc = min(max(ih, 0), a.H - 1), iwc = min(max(iw, 0), a.W - 1);
-        xr[k] = *(const f32x4*)(a.in + (((size_t)b * a.H + ihc) * a.W + iwc) * a.Cin + ck * 32 + q4 * 4);
+        xr[k] = *(const uint4*)(in + (((size_t)b * a.H + ihc) * a.W + iwc) * a.Cin + ck * 32 + q4 * CPP);
         okm |= (ok && v < np8) ? (1u << k) : 0u;
       }
     }
@@ -486,11 +537,15 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int 
     for (int k = 0; k < PM; ++k) {
       const int v = tid + k * CONV_TPB;
       if (v < np8) {
-        const int pos = v >> 3, q4 = v & 7;
+        const int pos = v / QP, q4 = v % QP;
         const bool ok = (okm >> k) & 1u;
-        const uint32_t lo = (uint32_t)f2bf(xr[k].x) | ((uint32_t)f2bf(xr[k].y) << 16);
-        const uint32_t hi = (uint32_t)f2bf(xr[k].z) | ((uint32_t)f2bf(xr[k].w) << 16);
-        *(uint2*)(patch + pos * CL_CS + q4 * 4) = ok ? make_uint2(lo, hi) : make_uint2(0u, 0u);
+        if constexpr (sizeof(TI) == 2) {  // 8 bf16 channels as they are
+          *(uint4*)(patch + pos * CL_CS + q4 * 8) = ok ? xr[k] : make_uint4(0u, 0u, 0u, 0u);
+        } else {
+          const uint32_t lo = (uint32_t)f2bf(__uint_as_float(xr[k].x)) | ((uint32_t)f2bf(__uint_as_float(xr[k].y)) << 16);
+          const uint32_t hi = (uint32_t)f2bf(__uint_as_float(xr[k].z)) | ((uint32_t)f2bf(__uint_as_float(xr[k].w)) << 16);
+          *(uint2*)(patch + pos * CL_CS + q4 * 4) = ok ? make_uint2(lo, hi) : make_uint2(0u, 0u);
+        }
       }
     }
 #pragma unroll
@@ -537,50 +592,62 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int 
         float v = acc[i][j][r];
         v = a.mode == CONV_RELU_BN ? fmaxf(v + bi, 0.f) * sc + sh : (v + bi) * sc + sh;
         if (a.layout == LAYOUT_NHWC) {
-          a.out[(size_t)p * a.Cout_pad + co] = v;
+          act_st(out + (size_t)p * a.Cout_pad + co, v);
         } else if (co < a.Cvalid) {
-          a.out[(((size_t)b * a.Wo + ow) * a.Cvalid + co) * a.Ho + oh] = v;
+          act_st(out + (((size_t)b * a.Wo + ow) * a.Cvalid + co) * a.Ho + oh, v);
         }
       }
   }
+}
+
+template <typename TI, typename TO>
+hipError_t launch_conv_t(int dtype, const ConvArgs& a, hipStream_t s) {
+  const int P = a.N * a.Ho * a.Wo;
+  const int nj = a.Cout_pad % 64 == 0 ? 4 : 2;
+  const dim3 grid(blocks_for(P, 128), a.Cout_pad / (nj * 16));
+  if (dtype == GGD_BF16 && !conv_no_lds) {
+    const int TW = a.Wo >= 16 ? 16 : a.Wo >= 8 ? 8 : 4;
+    const ConvLdsGeom G = conv_lds_geom(a, TW, nj);
+    const size_t lds = G.patch_bytes + G.w_bytes;
+    const int qp = 32 / (16 / (int)sizeof(TI));  // input pieces per patch position
+    if (lds <= 96 * 1024 && G.PH * G.PW * qp <= CL_PMAX * CONV_TPB && G.taps <= CL_TAPS_MAX) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<4, CL_PMAX, TI, TO>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<2, CL_PMAX, TI, TO>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<4, CL_PMIN, TI, TO>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<2, CL_PMIN, TI, TO>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        attr = true;
+      }
+      const int blocks = a.N * ((a.Ho + G.TH - 1) / G.TH) * ((a.Wo + TW - 1) / TW);
+      const dim3 gl(blocks, a.Cout_pad / (nj * 16));
+      const bool small = G.PH * G.PW * qp <= CL_PMIN * CONV_TPB;
+      if (nj == 4 && small) hipLaunchKernelGGL((enc_conv_lds_kernel<4, CL_PMIN, TI, TO>), gl, dim3(CONV_TPB), lds, s, a, TW);
+      else if (nj == 4) hipLaunchKernelGGL((enc_conv_lds_kernel<4, CL_PMAX, TI, TO>), gl, dim3(CONV_TPB), lds, s, a, TW);
+      else if (small) hipLaunchKernelGGL((enc_conv_lds_kernel<2, CL_PMIN, TI, TO>), gl, dim3(CONV_TPB), lds, s, a, TW);
+      else hipLaunchKernelGGL((enc_conv_lds_kernel<2, CL_PMAX, TI, TO>), gl, dim3(CONV_TPB), lds, s, a, TW);
+      return hipGetLastError();
+    }
+  }
+  if (dtype == GGD_BF16) {
+    if (nj == 4) hipLaunchKernelGGL((enc_conv_kernel<bf16_t, 4, TI, TO>), grid, dim3(CONV_TPB), 0, s, a);
+    else hipLaunchKernelGGL((enc_conv_kernel<bf16_t, 2, TI, TO>), grid, dim3(CONV_TPB), 0, s, a);
+  } else {
+    if (nj == 4) hipLaunchKernelGGL((enc_conv_kernel<float, 4, TI, TO>), grid, dim3(CONV_TPB), 0, s, a);
+    else hipLaunchKernelGGL((enc_conv_kernel<float, 2, TI, TO>), grid, dim3(CONV_TPB), 0, s, a);
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_conv(int dtype, const ConvArgs& a, hipStream_t s) {
   const int P = a.N * a.Ho * a.Wo;
   const int nj = a.Cout_pad % 64 == 0 ? 4 : 2;
   if (a.Cin % 32 || a.Cout_pad % (nj * 16) || P <= 0) return hipErrorInvalidValue;
-  const dim3 grid(blocks_for(P, 128), a.Cout_pad / (nj * 16));
-  if (dtype == GGD_BF16 && !conv_no_lds) {
-    const int TW = a.Wo >= 16 ? 16 : a.Wo >= 8 ? 8 : 4;
-    const ConvLdsGeom G = conv_lds_geom(a, TW, nj);
-    const size_t lds = G.patch_bytes + G.w_bytes;
-    if (lds <= 96 * 1024 && G.PH * G.PW * 8 <= CL_PMAX * CONV_TPB && G.taps <= CL_TAPS_MAX) {
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<4, CL_PMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<2, CL_PMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<4, CL_PMIN>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<2, CL_PMIN>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        attr = true;
-      }
-      const int blocks = a.N * ((a.Ho + G.TH - 1) / G.TH) * ((a.Wo + TW - 1) / TW);
-      const dim3 gl(blocks, a.Cout_pad / (nj * 16));
-      const bool small = G.PH * G.PW * 8 <= CL_PMIN * CONV_TPB;
-      if (nj == 4 && small) hipLaunchKernelGGL((enc_conv_lds_kernel<4, CL_PMIN>), gl, dim3(CONV_TPB), lds, s, a, TW);
-      else if (nj == 4) hipLaunchKernelGGL((enc_conv_lds_kernel<4, CL_PMAX>), gl, dim3(CONV_TPB), lds, s, a, TW);
-      else if (small) hipLaunchKernelGGL((enc_conv_lds_kernel<2, CL_PMIN>), gl, dim3(CONV_TPB), lds, s, a, TW);
-      else hipLaunchKernelGGL((enc_conv_lds_kernel<2, CL_PMAX>), gl, dim3(CONV_TPB), lds, s, a, TW);
-      return hipGetLastError();
-    }
-  }
-  if (dtype == GGD_BF16) {
-    if (nj == 4) hipLaunchKernelGGL((enc_conv_kernel<bf16_t, 4>), grid, dim3(CONV_TPB), 0, s, a);
-    else hipLaunchKernelGGL((enc_conv_kernel<bf16_t, 2>), grid, dim3(CONV_TPB), 0, s, a);
-  } else {
-    if (nj == 4) hipLaunchKernelGGL((enc_conv_kernel<float, 4>), grid, dim3(CONV_TPB), 0, s, a);
-    else hipLaunchKernelGGL((enc_conv_kernel<float, 2>), grid, dim3(CONV_TPB), 0, s, a);
-  }
-  return hipGetLastError();
+  if (dtype != GGD_BF16 && (a.in_bf16 || a.out_bf16)) return hipErrorInvalidValue;  // f32 contexts stay f32
+  if (a.in_bf16 && a.out_bf16) return launch_conv_t<bf16_t, bf16_t>(dtype, a, s);
+  if (a.in_bf16) return launch_conv_t<bf16_t, float>(dtype, a, s);
+  if (a.out_bf16) return launch_conv_t<float, bf16_t>(dtype, a, s);
+  return launch_conv_t<float, float>(dtype, a, s);
 }
 
 struct EConv {            // one convolution + its folded BN epilogue
@@ -622,7 +689,9 @@ struct ggd_enc {
   float *proj_w = nullptr, *proj_b = nullptr;
   // workspaces (chunk clips)
   float *pw = nullptr, *mel = nullptr, *img = nullptr;
-  float *buf[4] = {}, *feat[3] = {}, *se_y = nullptr, *se_part = nullptr, *hbuf = nullptr, *sbuf = nullptr;
+  void *buf[4] = {}, *feat[3] = {}, *sbuf = nullptr;   // activations: bf16 in bf16 contexts, else f32
+  float *se_y = nullptr, *se_part = nullptr, *hbuf = nullptr;
+  size_t asz = 4;                                     // bytes per activation element
 };
 
 namespace {
@@ -812,10 +881,12 @@ int make_lin(ggd_enc* e, const std::string& name, int out, int in, float** w, fl
   return GGD_OK;
 }
 
-int run_conv(ggd_enc* e, const EConv& cv, const float* in, int n, int H, int W, float* out, int mode, int layout,
-             hipStream_t s) {
+int run_conv(ggd_enc* e, const EConv& cv, const void* in, int n, int H, int W, void* out, int mode, int layout,
+             hipStream_t s, bool out_act = true) {
   ConvArgs a{};
   a.in = in;
+  a.in_bf16 = e->asz == 2;
+  a.out_bf16 = out_act && e->asz == 2;   // the heads' outputs feed f32 Linear layers
   a.w = cv.w;
   a.bias = cv.bias;
   a.s = cv.s;
@@ -923,17 +994,18 @@ int ggd_enc_finalize(ggd_enc* e) {
   }
   // workspaces for one chunk of clips
   const size_t n = e->chunk, F = e->F;
+  e->asz = e->dtype == GGD_BF16 ? 2 : 4;
   ENC_TRY(e, ealloc(e, &e->pw, sizeof(float) * n * F * POW_LD));
   ENC_TRY(e, ealloc(e, &e->mel, sizeof(float) * n * F * NMEL));
   ENC_TRY(e, ealloc(e, &e->img, sizeof(float) * n * F * NMEL));
   size_t big = 0;
   for (int l = 1; l <= 4; ++l) big = std::max(big, (size_t)e->H[l] * e->W[l] * planes_l[l - 1]);
-  for (int i = 0; i < 4; ++i) ENC_TRY(e, ealloc(e, &e->buf[i], sizeof(float) * n * big));
+  for (int i = 0; i < 4; ++i) ENC_TRY(e, ealloc(e, &e->buf[i], e->asz * n * big));
   for (int i = 0; i < 3; ++i)
-    ENC_TRY(e, ealloc(e, &e->feat[i], sizeof(float) * n * e->H[i + 2] * e->W[i + 2] * planes_l[i + 1]));
+    ENC_TRY(e, ealloc(e, &e->feat[i], e->asz * n * e->H[i + 2] * e->W[i + 2] * planes_l[i + 1]));
   ENC_TRY(e, ealloc(e, &e->se_y, sizeof(float) * n * 256));
   ENC_TRY(e, ealloc(e, &e->se_part, sizeof(float) * n * SE_SLICES * 256));
-  ENC_TRY(e, ealloc(e, &e->sbuf, sizeof(float) * n * 32 *
+  ENC_TRY(e, ealloc(e, &e->sbuf, e->asz * n * 32 *
                                     std::max((size_t)e->H[3] * 2 * e->W[3] * 2, (size_t)e->H[4] * 4 * e->W[4] * 4)));
   size_t hb = 0;
   for (int i = 0; i < 3; ++i) hb = std::max(hb, (size_t)e->head[i].K * (size_t)(e->W[2] + e->W[4] * 4));
@@ -1004,41 +1076,55 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
     hipLaunchKernelGGL(enc_inorm_kernel, dim3(m), dim3(NMEL), 0, s, e->mel, e->img, F);
     ENC_TRY(e, hipGetLastError());
     const size_t n1 = (size_t)m * e->H[1] * e->W[1] * 4;
-    hipLaunchKernelGGL(enc_conv1_kernel, dim3(blocks_for(n1, 256)), dim3(256), 0, s, e->img, e->c1_w, e->c1_b,
-                       e->c1_s, e->c1_t, e->buf[0], m, e->H[1], e->W[1]);
+    const bool hb = e->asz == 2;
+    if (hb)
+      hipLaunchKernelGGL(enc_conv1_kernel<bf16_t>, dim3(blocks_for(n1, 256)), dim3(256), 0, s, e->img, e->c1_w, e->c1_b,
+                         e->c1_s, e->c1_t, (bf16_t*)e->buf[0], m, e->H[1], e->W[1]);
+    else
+      hipLaunchKernelGGL(enc_conv1_kernel<float>, dim3(blocks_for(n1, 256)), dim3(256), 0, s, e->img, e->c1_w, e->c1_b,
+                         e->c1_s, e->c1_t, (float*)e->buf[0], m, e->H[1], e->W[1]);
     ENC_TRY(e, hipGetLastError());
     // residual tower: x is the current input; u, v, r are the scratch buffers other than x
-    const float* x = e->buf[0];
+    const void* x = e->buf[0];
     int H = e->H[1], W = e->W[1], bidx = 0;
     const int nblk[4] = {3, 4, 6, 3};
     for (int l = 0; l < 4; ++l)
       for (int bi = 0; bi < nblk[l]; ++bi, ++bidx) {
         const EBlock& B = e->blocks[bidx];
-        float* sc[3];
+        void* sc[3];
         for (int i = 0, k = 0; i < 4 && k < 3; ++i)
           if (e->buf[i] != x) sc[k++] = e->buf[i];
-        float *u = sc[0], *v = sc[1], *r = sc[2];
+        void *u = sc[0], *v = sc[1], *r = sc[2];
         const int Ho = conv_out(H, 3, B.c1.stride, 1), Wo = conv_out(W, 3, B.c1.stride, 1);
         int rc = run_conv(e, B.c1, x, m, H, W, u, CONV_RELU_BN, LAYOUT_NHWC, s);
         if (!rc) rc = run_conv(e, B.c2, u, m, Ho, Wo, v, CONV_BN, LAYOUT_NHWC, s);
-        const float* res = x;
+        const void* res = x;
         if (!rc && B.has_ds) {
           rc = run_conv(e, B.ds, x, m, H, W, r, CONV_BN, LAYOUT_NHWC, s);
           res = r;
         }
         if (rc) return rc;
         const int S = std::max(1, std::min(SE_SLICES, Ho * Wo / 64));
-        hipLaunchKernelGGL(enc_se_sum_kernel, dim3(m, S), dim3(256), 0, s, v, Ho * Wo, B.planes, e->se_part);
+        if (hb)
+          hipLaunchKernelGGL(enc_se_sum_kernel<bf16_t>, dim3(m, S), dim3(256), 0, s, (const bf16_t*)v, Ho * Wo, B.planes,
+                             e->se_part);
+        else
+          hipLaunchKernelGGL(enc_se_sum_kernel<float>, dim3(m, S), dim3(256), 0, s, (const float*)v, Ho * Wo, B.planes,
+                             e->se_part);
         ENC_TRY(e, hipGetLastError());
         hipLaunchKernelGGL(enc_se_kernel, dim3(m), dim3(256), 0, s, e->se_part, S, Ho * Wo, B.planes, B.se_w0,
                            B.se_b0, B.se_w2, B.se_b2, e->se_y);
         ENC_TRY(e, hipGetLastError());
         // the block output goes to u (consumed by conv2 already), or to the saved feature map
         // of layers 2..4 that the heads read
-        float* o = (bi == nblk[l] - 1 && l >= 1) ? e->feat[l - 1] : u;
-        const size_t tot4 = (size_t)m * Ho * Wo * B.planes / 4;
-        hipLaunchKernelGGL(enc_se_apply_kernel, dim3(blocks_for(tot4, 256)), dim3(256), 0, s, v, e->se_y, res, o,
-                           Ho * Wo, B.planes, tot4);
+        void* o = (bi == nblk[l] - 1 && l >= 1) ? e->feat[l - 1] : u;
+        const size_t tot8 = (size_t)m * Ho * Wo * B.planes / 8;
+        if (hb)
+          hipLaunchKernelGGL(enc_se_apply_kernel<bf16_t>, dim3(blocks_for(tot8, 256)), dim3(256), 0, s, (const bf16_t*)v,
+                             e->se_y, (const bf16_t*)res, (bf16_t*)o, Ho * Wo, B.planes, tot8);
+        else
+          hipLaunchKernelGGL(enc_se_apply_kernel<float>, dim3(blocks_for(tot8, 256)), dim3(256), 0, s, (const float*)v,
+                             e->se_y, (const float*)res, (float*)o, Ho * Wo, B.planes, tot8);
         ENC_TRY(e, hipGetLastError());
         x = o;
         H = Ho;
@@ -1050,19 +1136,23 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
     const int tl[3] = {e->t_low, e->t_mid, e->t_high};
     for (int i = 0; i < 3; ++i) {
       const EHead& h = e->head[i];
-      const float* fin = e->feat[i];
+      const void* fin = e->feat[i];
       int Hh = e->H[i + 2], Wh = e->W[i + 2];
       if (h.shuffle > 1) {
         const int C = h.conv.cin, r = h.shuffle;
         const size_t tot = (size_t)m * Hh * r * Wh * r * h.conv.cin_pad;
-        hipLaunchKernelGGL(enc_shuffle_kernel, dim3(blocks_for(tot, 256)), dim3(256), 0, s, fin, e->sbuf, m, Hh, Wh,
-                           C, r, h.conv.cin_pad);
+        if (hb)
+          hipLaunchKernelGGL(enc_shuffle_kernel<bf16_t>, dim3(blocks_for(tot, 256)), dim3(256), 0, s, (const bf16_t*)fin,
+                             (bf16_t*)e->sbuf, m, Hh, Wh, C, r, h.conv.cin_pad);
+        else
+          hipLaunchKernelGGL(enc_shuffle_kernel<float>, dim3(blocks_for(tot, 256)), dim3(256), 0, s, (const float*)fin,
+                             (float*)e->sbuf, m, Hh, Wh, C, r, h.conv.cin_pad);
         ENC_TRY(e, hipGetLastError());
         fin = e->sbuf;
         Hh *= r;
         Wh *= r;
       }
-      int rc = run_conv(e, h.conv, fin, m, Hh, Wh, e->hbuf, CONV_RELU_BN, LAYOUT_NWCH, s);
+      int rc = run_conv(e, h.conv, fin, m, Hh, Wh, e->hbuf, CONV_RELU_BN, LAYOUT_NWCH, s, false);
       if (rc) return rc;
       const int Wo = conv_out(Wh, h.conv.kw, 1, 0);
       if (Wo != tl[i]) return efail(e, GGD_ERR_STATE, "head length mismatch");

@@ -63,6 +63,20 @@ class SampleArgs(ctypes.Structure):
     ]
 
 
+def _deps(path, seen=None):
+    """The file and every local header it includes, transitively (#include "...")."""
+    import re
+    seen = set() if seen is None else seen
+    path = os.path.normpath(path)
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    with open(path) as f:
+        for inc in re.findall(r'^\s*#include\s+"([^"]+)"', f.read(), re.M):
+            _deps(os.path.join(os.path.dirname(path), inc), seen)
+    return seen
+
+
 def _sources():
     return [os.path.join(CSRC, s) for s in SOURCES + DIAG_SOURCES] + [os.path.join(CSRC, h) for h in HEADERS]
 
@@ -86,14 +100,14 @@ def build(force=False, verbose=False):
     # register of psk_kernel (the per-thread pose state) around the one-pass LayerNorm.
     flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-fno-slp-vectorize", "-Wno-unused-value", "-Wno-unused-result"]
     os.makedirs(os.path.join(PKG_DIR, "build"), exist_ok=True)
-    hdr_t = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
     units = [(src, src.replace(".hip", ".o"), []) for src in SOURCES + DIAG_SOURCES]
     units.append(("ggd_api.hip", "ggd_api_diag.o", ["-DGGD_DIAG"]))
     procs = []
     for src, obj_name, extra in units:  # one hipcc per translation unit, in parallel
         obj = os.path.join(PKG_DIR, "build", obj_name)
-        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(hdr_t, os.path.getmtime(os.path.join(CSRC, src))):
-            continue  # object newer than its source and every header
+        dep_t = max(os.path.getmtime(f) for f in _deps(os.path.join(CSRC, src)))
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > dep_t:
+            continue  # object newer than its source and every header it includes
         cmd = ["hipcc"] + flags + extra + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))

@@ -51,6 +51,7 @@ def test_encoder_bf16_matches_oracle(pkg, sd):
     for a, b in zip(got, want):
         assert a.shape == b.shape
         r = rel_rms(a, b)
+        print(f"bf16 encoder tokens {tuple(a.shape)}: rel-RMS {r:.3e}")
         assert r <= 3e-2, r
 
 
