@@ -95,21 +95,28 @@ __global__ void __launch_bounds__(256) enc_stft_power_kernel(const float* __rest
 }
 
 // +1e-6, instance norm over frames per (clip, mel bin) -> image [n][128][F]; one workgroup per clip
-__global__ void __launch_bounds__(NMEL) enc_inorm_kernel(const float* __restrict__ mel, float* __restrict__ img,
-                                                         int F) {
-  const int b = blockIdx.x, m = threadIdx.x;
+__global__ void __launch_bounds__(4 * NMEL) enc_inorm_kernel(const float* __restrict__ mel, float* __restrict__ img,
+                                                             int F) {
+  // four frame groups per mel bin (frames gr, gr + 4, ...), added in group order
+  __shared__ float red[4][NMEL];
+  const int b = blockIdx.x, m = threadIdx.x % NMEL, gr = threadIdx.x / NMEL;
   const float* src = mel + (size_t)b * F * NMEL + m;
   float s = 0.f;
-  for (int f = 0; f < F; ++f) s += src[(size_t)f * NMEL] + 1e-6f;
-  const float mean = s / (float)F;
+  for (int f = gr; f < F; f += 4) s += src[(size_t)f * NMEL] + 1e-6f;
+  red[gr][m] = s;
+  __syncthreads();
+  const float mean = ((red[0][m] + red[1][m]) + (red[2][m] + red[3][m])) / (float)F;
+  __syncthreads();
   float v = 0.f;
-  for (int f = 0; f < F; ++f) {
+  for (int f = gr; f < F; f += 4) {
     const float d = (src[(size_t)f * NMEL] + 1e-6f) - mean;
     v += d * d;
   }
-  const float inv = 1.0f / sqrtf(v / (float)F + 1e-5f);
+  red[gr][m] = v;
+  __syncthreads();
+  const float inv = 1.0f / sqrtf(((red[0][m] + red[1][m]) + (red[2][m] + red[3][m])) / (float)F + 1e-5f);
   float* dst = img + ((size_t)b * NMEL + m) * F;
-  for (int f = 0; f < F; ++f) dst[f] = ((src[(size_t)f * NMEL] + 1e-6f) - mean) * inv;
+  for (int f = gr; f < F; f += 4) dst[f] = ((src[(size_t)f * NMEL] + 1e-6f) - mean) * inv;
 }
 
 // conv1 (1 -> 32, 3x3, pad 1) + bias, ReLU, BN; one thread per (pixel, 8 output channels)
@@ -117,6 +124,14 @@ template <typename TA>
 __global__ void enc_conv1_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                  const float* __restrict__ bias, const float* __restrict__ s,
                                  const float* __restrict__ t, TA* __restrict__ out, int n, int H, int W) {
+  __shared__ float ws[32 * 9], bs[32], ss[32], ts[32];
+  for (int i = threadIdx.x; i < 32 * 9; i += blockDim.x) ws[i] = w[i];
+  if (threadIdx.x < 32) {
+    bs[threadIdx.x] = bias[threadIdx.x];
+    ss[threadIdx.x] = s[threadIdx.x];
+    ts[threadIdx.x] = t[threadIdx.x];
+  }
+  __syncthreads();
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x, total = (size_t)n * H * W * 4;
   if (idx >= total) return;
   const int cg = (int)(idx & 3);
@@ -136,8 +151,8 @@ __global__ void enc_conv1_kernel(const float* __restrict__ img, const float* __r
     const int c = cg * 8 + j;
     float acc = 0.f;
 #pragma unroll
-    for (int q = 0; q < 9; ++q) acc += w[c * 9 + q] * tap[q];
-    o[j] = fmaxf(acc + bias[c], 0.f) * s[c] + t[c];
+    for (int q = 0; q < 9; ++q) acc += ws[c * 9 + q] * tap[q];
+    o[j] = fmaxf(acc + bs[c], 0.f) * ss[c] + ts[c];
   }
   if constexpr (sizeof(TA) == 2) {
     uint4 u;
@@ -184,6 +199,8 @@ struct ConvArgs {
   const float *bias, *s, *t;  // [Cout_pad]: BN folded to y = x * s + t
   void* out;                // f32 or bf16 (out_bf16)
   int N, H, W, Cin, Ho, Wo, Cout_pad, Cvalid, KH, KW, stride, pad, mode, layout, in_bf16, out_bf16;
+  float* se_part;           // LDS kernel, non-null: the SE squeeze's partial sums of the f32 outputs,
+                            // one row of Cout_pad per (image, output tile): [N][tiles][Cout_pad]
 };
 
 template <typename T> struct ConvB;
@@ -334,24 +351,40 @@ __global__ void __launch_bounds__(256) enc_se_sum_kernel(const TA* __restrict__ 
 }
 
 // stage 2, one workgroup per clip: y[c] = sigmoid(fc2(relu(fc0(mean_hw(v)))))  (ResNetBlocks.py:81-96)
+// from the squeeze's partial-sum rows (S per clip, added in a fixed order: deterministic).  A
+// separate launch: recomputing it in every workgroup of the channel scale below (measured, r03k)
+// put three dependent load rounds in front of every one of them and was slower than this launch.
 __global__ void __launch_bounds__(256) enc_se_kernel(const float* __restrict__ part, int S, int HW, int C,
                                                      const float* __restrict__ w0, const float* __restrict__ b0,
                                                      const float* __restrict__ w2, const float* __restrict__ b2,
                                                      float* __restrict__ y) {
-  __shared__ float mean[256], hid[32];
+  __shared__ float mean[256], hid[32], red[256];
   const int b = blockIdx.x, tid = threadIdx.x;
-  if (tid < C) {
-    float tot = 0.f;
-    for (int k = 0; k < S; ++k) tot += part[((size_t)b * S + k) * C + tid];
-    mean[tid] = tot / (float)HW;
+  {  // 256 / C stripes of the S rows, then the stripes in order
+    const int stripes = 256 / C, c = tid % C, st = tid / C;
+    float s0 = 0.f, s1 = 0.f;
+    int k = st;
+    for (; k + stripes < S; k += 2 * stripes) {
+      s0 += part[((size_t)b * S + k) * C + c];
+      s1 += part[((size_t)b * S + k + stripes) * C + c];
+    }
+    if (k < S) s0 += part[((size_t)b * S + k) * C + c];
+    red[tid] = s0 + s1;
+    __syncthreads();
+    if (tid < C) {
+      float tot = 0.f;
+      for (int j = 0; j < stripes; ++j) tot += red[j * C + tid];
+      mean[tid] = tot / (float)HW;
+    }
   }
   __syncthreads();
-  const int Ch = C / 8;
-  if (tid < Ch) {
-    float a = b0[tid];
-    for (int k = 0; k < C; ++k) a += w0[tid * C + k] * mean[k];
-    hid[tid] = fmaxf(a, 0.f);
-  }
+  // fc.0 (C -> C / 8 <= 32): eight lanes per hidden unit, each a strided eighth of the dot product
+  const int Ch = C / 8, u = tid >> 3, q = tid & 7;
+  float a0 = 0.f;
+  if (u < Ch)
+    for (int k = q; k < C; k += 8) a0 += w0[u * C + k] * mean[k];
+  a0 = group_sum<8>(a0);
+  if (u < Ch && q == 0) hid[u] = fmaxf(a0 + b0[u], 0.f);
   __syncthreads();
   if (tid < C) {
     float a = b2[tid];
@@ -389,53 +422,122 @@ __global__ void enc_se_apply_kernel(const TA* __restrict__ v, const float* __res
   }
 }
 
-// PixelShuffle(r): in NHWC [n][H][W][C r^2] -> out NHWC [n][H r][W r][Cp] (channels >= C zero)
+// PixelShuffle(r): in NHWC [n][H][W][C r^2] -> out NHWC [n][H r][W r][Cp] (channels >= C zero);
+// one thread per 8 consecutive output channels (one 16- / 32-byte store), Cp % 8 == 0
 template <typename TA>
 __global__ void enc_shuffle_kernel(const TA* __restrict__ in, TA* __restrict__ out, int n, int H, int W,
                                    int C, int r, int Cp) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int Ho = H * r, Wo = W * r;
-  if (idx >= (size_t)n * Ho * Wo * Cp) return;
-  const int c = (int)(idx % Cp);
-  const size_t p = idx / Cp;
+  const int Ho = H * r, Wo = W * r, C8 = Cp / 8;
+  if (idx >= (size_t)n * Ho * Wo * C8) return;
+  const int c0 = (int)(idx % C8) * 8;
+  const size_t p = idx / C8;
   const int x = (int)(p % Wo), yy = (int)((p / Wo) % Ho), b = (int)(p / ((size_t)Wo * Ho));
-  float v = 0.f;
-  if (c < C) {
-    const int h = yy / r, i = yy - h * r, w = x / r, j = x - w * r;
-    v = act_ld(in + (((size_t)b * H + h) * W + w) * (C * r * r) + c * r * r + i * r + j);
+  const int h = yy / r, i = yy - h * r, w = x / r, j = x - w * r;
+  const TA* src = in + (((size_t)b * H + h) * W + w) * (C * r * r) + i * r + j;
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = c0 + k < C ? act_ld(src + (c0 + k) * r * r) : 0.f;
+  TA* dst = out + p * Cp + c0;
+  if constexpr (sizeof(TA) == 2) {
+    uint4 o;
+    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+    o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+    *(uint4*)dst = o;
+  } else {
+    *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
   }
-  act_st(out + idx, v);
 }
 
-// one workgroup per (clip, time) row: z = Wp (W1 a + b1) + bp, a = the row's (c, h) features
-__global__ void __launch_bounds__(256) enc_head_fc_kernel(const float* __restrict__ feat, int K,
-                                                          const float* __restrict__ w1, const float* __restrict__ b1,
-                                                          const float* __restrict__ wp, const float* __restrict__ bp,
-                                                          float* __restrict__ z, int d) {
-  __shared__ float red[4][32], h1[32];
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const float* a = feat + (size_t)row * K;
-  float acc[32];
+// The heads' Linear pair z = Wp (W1 a + b1) + bp (speech_encoder.py: fc_low / fc_mid / fc_high, then
+// wav_proj_layer) for 16 (clip, time) rows per workgroup: a = the row's K = C x H conv features,
+// read from the NHWC f32 conv output [clip][h][w][Cp] in (h, c) order -- W1's columns are permuted
+// to that order at finalize (the reference flattens (c, h)).  W1 a on v_mfma_f32_16x16x4_f32 (f32 products, f32 accumulation): wave w
+// takes the 16-deep K steps w, w + 8, ...; lane (row r16, group g) feeds k = 16 s + 4 g + i of step s
+// to MFMA i (the same permutation for A and B); the 8 waves' partial sums are added in wave order.
+// The 32 -> d projection follows from LDS.  K % 16 == 0.
+constexpr int HFC_WAVES = 8, HFC_DEPTH = 4;  // K split over 8 waves; 4 K steps of loads in flight per wave
+__global__ void __launch_bounds__(64 * HFC_WAVES) enc_head_fc_kernel(const float* __restrict__ feat, int M, int K,
+                                                                     int Hh, int Wo, int Cp, int lc,
+                                                                     const float* __restrict__ w1,
+                                                                     const float* __restrict__ b1,
+                                                                     const float* __restrict__ wp,
+                                                                     const float* __restrict__ bp,
+                                                                     float* __restrict__ z, int d) {
+  __shared__ float red[HFC_WAVES][16][33], h1[16][33];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  const int row0 = blockIdx.x * 16;
+  const int row = min(row0 + r16, M - 1), rb = row / Wo, cm = (1 << lc) - 1;
+  // (h, c) of k = 16 st + 4 g: h = k >> lc, c = k & cm (4 consecutive channels: C % 4 == 0)
+  const float* a0 = feat + ((size_t)rb * Hh * Wo + (row - rb * Wo)) * Cp;
+  auto aptr = [&](int st) { const int k = st * 16 + 4 * g; return a0 + (size_t)(k >> lc) * Wo * Cp + (k & cm); };
+  const float* wa = w1 + (size_t)r16 * K + 4 * g;
+  const float* wb = w1 + (size_t)(16 + r16) * K + 4 * g;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const int steps = K / 16, nst = steps > wave ? (steps - wave + HFC_WAVES - 1) / HFC_WAVES : 0;
+  float4 xa[HFC_DEPTH], xw0[HFC_DEPTH], xw1[HFC_DEPTH];
+  auto load = [&](int p, int i) __attribute__((always_inline)) {
+    const int st = wave + i * HFC_WAVES;
+    xa[p] = *(const float4*)aptr(st);
+    xw0[p] = *(const float4*)(wa + st * 16);
+    xw1[p] = *(const float4*)(wb + st * 16);
+  };
 #pragma unroll
-  for (int j = 0; j < 32; ++j) acc[j] = 0.f;
-  for (int k = tid; k < K; k += 256) {
-    const float x = a[k];
+  for (int p = 0; p < HFC_DEPTH; ++p)
+    if (p < nst) load(p, p);
+  for (int i0 = 0; i0 < nst; i0 += HFC_DEPTH) {
 #pragma unroll
-    for (int j = 0; j < 32; ++j) acc[j] += w1[(size_t)j * K + k] * x;
+    for (int p = 0; p < HFC_DEPTH; ++p) {
+      const int i = i0 + p;
+      if (i < nst) {
+        const float4 ca = xa[p], c0 = xw0[p], c1 = xw1[p];
+        if (i + HFC_DEPTH < nst) load(p, i + HFC_DEPTH);  // refill the slot HFC_DEPTH steps ahead
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca.x, c0.x, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca.x, c1.x, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca.y, c0.y, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca.y, c1.y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca.z, c0.z, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca.z, c1.z, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca.w, c0.w, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ca.w, c1.w, acc1, 0, 0, 0);
+      }
+    }
   }
+  // C layout: row 4 g + i, column r16 (tile 0) / 16 + r16 (tile 1)
 #pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const float s = wave_sum(acc[j]);
-    if (lane == 0) red[wave][j] = s;
+  for (int i = 0; i < 4; ++i) {
+    red[wave][4 * g + i][r16] = acc0[i];
+    red[wave][4 * g + i][16 + r16] = acc1[i];
   }
   __syncthreads();
-  if (tid < 32) h1[tid] = ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])) + b1[tid];
-  __syncthreads();
-  for (int o = tid; o < d; o += 256) {
-    float s = bp[o];
+  for (int e = tid; e < 16 * 32; e += 64 * HFC_WAVES) {
+    const int r = e >> 5, j = e & 31;
+    float t = red[0][r][j];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) s += wp[o * 32 + j] * h1[j];
-    z[(size_t)row * d + o] = s;
+    for (int w = 1; w < HFC_WAVES; ++w) t += red[w][r][j];
+    h1[r][j] = t + b1[j];
+  }
+  __syncthreads();
+  for (int o = tid; o < d; o += 64 * HFC_WAVES) {
+    float wr[32];
+#pragma unroll
+    for (int j = 0; j < 32; j += 4) {
+      const float4 t = *(const float4*)(wp + (size_t)o * 32 + j);
+      wr[j] = t.x;
+      wr[j + 1] = t.y;
+      wr[j + 2] = t.z;
+      wr[j + 3] = t.w;
+    }
+    const float bo = bp[o];
+    for (int r = 0; r < 16 && row0 + r < M; ++r) {
+      float v = bo;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) v += wr[j] * h1[r][j];
+      z[(size_t)(row0 + r) * d + o] = v;
+    }
   }
 }
 
@@ -598,6 +700,260 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int 
         }
       }
   }
+  if (a.se_part) {
+    // SE squeeze of this tile (ResNetBlocks.py:81-96, the mean's first stage): per output channel the
+    // sum of the tile's valid f32 outputs, in a fixed order (lane rows, lane groups, waves) -> one
+    // [Cout_pad] row per (image, tile); enc_se_kernel adds the tiles of an image in tile order
+    __syncthreads();  // every wave is past the MMA loop: the patch / filter images are free
+    float* red = (float*)smem;  // [4 waves][NJ * 16]
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int co = n0 + j * 16 + r16;
+      const float bi = a.bias[co], sc = a.s[co], sh = a.t[co];
+      float cs = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = wave * 32 + i * 16 + 4 * g + r, ty = q / G.TW, tx = q - ty * G.TW;
+          float v = acc[i][j][r];
+          v = a.mode == CONV_RELU_BN ? fmaxf(v + bi, 0.f) * sc + sh : (v + bi) * sc + sh;
+          cs += (oh0 + ty < a.Ho && ow0 + tx < a.Wo) ? v : 0.f;
+        }
+      cs += __shfl_xor(cs, 16);
+      cs += __shfl_xor(cs, 32);
+      if (g == 0) red[wave * NJ * 16 + j * 16 + r16] = cs;
+    }
+    __syncthreads();
+    if (tid < NJ * 16)
+      a.se_part[((size_t)b * per + tix) * a.Cout_pad + n0 + tid] =
+          (red[tid] + red[NJ * 16 + tid]) + (red[2 * NJ * 16 + tid] + red[3 * NJ * 16 + tid]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// The residual tower's convolutions (NHWC bf16 in / out; 3x3 stride 1 and 2, the 1x1 stride-2
+// downsample), with the tile geometry fixed at compile time.  Same tiling as enc_conv_lds_kernel
+// (128 output pixels x NJ 16 output channels per 256-thread workgroup, per 32-channel chunk the
+// patch and the filter taps staged in LDS, the next chunk in registers), three differences:
+//   * the geometry is constexpr: every index split is a shift / multiply (the runtime version
+//     spent ~2x its MFMA time on integer division in the staging and the epilogue), and the
+//     per-piece source offsets are computed once, each chunk adding 32 channels;
+//   * a 1x1 strided conv stages only the pixels it reads (a TH x TW image, not the stride-2 span);
+//   * the product is computed transposed (A = filter taps, B = patch), so a lane holds 4
+//     consecutive output channels of one pixel: one 8-byte store per (pixel tile, channel tile)
+//     instead of four 2-byte stores, and the SE squeeze reduces over the 16 pixel lanes by DPP.
+// ------------------------------------------------------------------------------------------
+template <int TW, int KS, int ST> struct CGeo {
+  static constexpr int TH = CL_PX / TW;
+  static constexpr int PH = KS == 1 ? TH : (TH - 1) * ST + KS;  // 1x1: only the pixels read
+  static constexpr int PW = KS == 1 ? TW : (TW - 1) * ST + KS;
+  static constexpr int PS = KS == 1 ? 1 : ST;                   // patch step per output pixel
+  static constexpr int SS = KS == 1 ? ST : 1;                   // source step per patch position
+  static constexpr int TAPS = KS * KS, NPOS = PH * PW;
+  static constexpr size_t PATCH_BYTES = (size_t)NPOS * CL_CS * 2;
+};
+
+template <int NJ, int TW, int KS, int ST, typename TO>
+__global__ void __launch_bounds__(CONV_TPB) enc_conv_nhwc_kernel(ConvArgs a) {
+  using GE = CGeo<TW, KS, ST>;
+  constexpr int QP = 4;                                        // 16-byte pieces (8 bf16) per 32 channels
+  constexpr int NP8 = GE::NPOS * QP, PM = (NP8 + CONV_TPB - 1) / CONV_TPB;
+  constexpr int NW = NJ * 16 * GE::TAPS * 4, WM = (NW + CONV_TPB - 1) / CONV_TPB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const bf16_t* in = (const bf16_t*)a.in;
+  TO* out = (TO*)a.out;
+  bf16_t* patch = (bf16_t*)smem;
+  bf16_t* wl = (bf16_t*)(smem + GE::PATCH_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  const int tw_n = (a.Wo + TW - 1) / TW, th_n = (a.Ho + GE::TH - 1) / GE::TH, per = tw_n * th_n;
+  const int b = blockIdx.x / per, tix = blockIdx.x - b * per, tyi = tix / tw_n;
+  const int oh0 = tyi * GE::TH, ow0 = (tix - tyi * tw_n) * TW, n0 = blockIdx.y * (NJ * 16);
+  const int ih0 = oh0 * ST - a.pad, iw0 = ow0 * ST - a.pad;
+  int pbase[2];  // patch position of tap (0, 0) for this lane's pixel in pixel tiles 0, 1
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = wave * 32 + i * 16 + r16, ty = q / TW, tx = q % TW;
+    pbase[i] = ty * GE::PS * GE::PW + tx * GE::PS;
+  }
+  // chunk-0 element offsets of this thread's patch / filter pieces (chunk ck adds 32 ck)
+  int poff[PM], woff[WM];
+  uint32_t okm = 0;  // bit k: patch piece k lies inside the image (else it stages as zero)
+#pragma unroll
+  for (int k = 0; k < PM; ++k) {
+    const int v = tid + k * CONV_TPB, vc = min(v, NP8 - 1);
+    const int pos = vc / QP, q4 = vc % QP, py = pos / GE::PW, px = pos % GE::PW;
+    const int ih = ih0 + py * GE::SS, iw = iw0 + px * GE::SS;
+    const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+    const int ihc = min(max(ih, 0), a.H - 1), iwc = min(max(iw, 0), a.W - 1);
+    poff[k] = ((b * a.H + ihc) * a.W + iwc) * a.Cin + q4 * 8;
+    okm |= (ok && v < NP8) ? (1u << k) : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < WM; ++k) {
+    const int v = min(tid + k * CONV_TPB, NW - 1);  // clamped: every register is defined
+    const int q8 = v & 3, nt = v >> 2, n = nt / GE::TAPS, tap = nt % GE::TAPS;
+    woff[k] = ((n0 + n) * GE::TAPS + tap) * a.Cin + q8 * 8;
+  }
+  f32x4 acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bf16_t* W = (const bf16_t*)a.w;
+  const int cch = a.Cin >> 5;
+  bf16x8 xr[PM], wr[WM];
+  auto fetch = [&](int ck) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < PM; ++k) xr[k] = *(const bf16x8*)(in + poff[k] + ck * 32);
+#pragma unroll
+    for (int k = 0; k < WM; ++k) wr[k] = *(const bf16x8*)(W + woff[k] + ck * 32);
+  };
+  auto put = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < PM; ++k) {
+      const int v = tid + k * CONV_TPB;
+      if (v < NP8) {
+        const bf16x8 z = {};
+        *(bf16x8*)(patch + (v / QP) * CL_CS + (v % QP) * 8) = ((okm >> k) & 1u) ? xr[k] : z;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < WM; ++k) {
+      const int v = tid + k * CONV_TPB;
+      if (v < NW) *(bf16x8*)(wl + (v >> 2) * CL_CS + (v & 3) * 8) = wr[k];  // (n taps + tap) = v >> 2
+    }
+  };
+  fetch(0);
+  for (int ck = 0; ck < cch; ++ck) {
+    if (ck > 0) __syncthreads();  // the previous chunk's MFMAs are done with the LDS images
+    put();
+    __syncthreads();
+    if (ck + 1 < cch) fetch(ck + 1);
+#pragma unroll
+    for (int tap = 0; tap < GE::TAPS; ++tap) {
+      const int toff = (tap / KS) * GE::PW + tap % KS;
+      bf16x8 bv[2], av[NJ];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) bv[i] = *(const bf16x8*)(patch + (pbase[i] + toff) * CL_CS + g * 8);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) av[j] = *(const bf16x8*)(wl + ((j * 16 + r16) * GE::TAPS + tap) * CL_CS + g * 8);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[j], bv[i], acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue: lane (pixel r16 of tile i, group g) holds output channels 16 j + 4 g .. + 3
+  float cs[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int co = n0 + j * 16 + 4 * g;
+    const float4 bi = *(const float4*)(a.bias + co), sc = *(const float4*)(a.s + co), sh = *(const float4*)(a.t + co);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = wave * 32 + i * 16 + r16, oh = oh0 + q / TW, ow = ow0 + q % TW;
+      const bool okp = oh < a.Ho && ow < a.Wo;
+      float v[4] = {acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w};
+      if (a.mode == CONV_RELU_BN) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      v[0] = v[0] * sc.x + sh.x;
+      v[1] = v[1] * sc.y + sh.y;
+      v[2] = v[2] * sc.z + sh.z;
+      v[3] = v[3] * sc.w + sh.w;
+      if (okp) {
+        TO* dst = out + (((size_t)b * a.Ho + oh) * a.Wo + ow) * a.Cout_pad + co;
+        if constexpr (sizeof(TO) == 2) {
+          const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          *(uint2*)dst = make_uint2(lo, hi);
+        } else {
+          *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[j][r] += okp ? v[r] : 0.f;
+    }
+  }
+  if (a.se_part) {
+    // SE squeeze of this tile (ResNetBlocks.py:81-96, the mean's first stage): per output channel
+    // the sum of the tile's valid f32 outputs in a fixed order (pixel tiles, 16 pixel lanes, waves)
+    // -> one [Cout_pad] row per (image, tile); enc_se_kernel adds the tiles in tile order
+    __syncthreads();  // every wave is past the MMA loop: the patch / filter images are free
+    float* red = (float*)smem;  // [4 waves][NJ * 16]
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t = group_sum<16>(cs[j][r]);
+        if (r16 == 0) red[wave * NJ * 16 + j * 16 + 4 * g + r] = t;
+      }
+    __syncthreads();
+    if (tid < NJ * 16)
+      a.se_part[((size_t)b * per + tix) * a.Cout_pad + n0 + tid] =
+          (red[tid] + red[NJ * 16 + tid]) + (red[2 * NJ * 16 + tid] + red[3 * NJ * 16 + tid]);
+  }
+}
+
+template <int NJ, int TW, int KS, int ST, typename TO>
+hipError_t launch_conv_nhwc(const ConvArgs& a, hipStream_t s) {
+  using GE = CGeo<TW, KS, ST>;
+  constexpr size_t lds = GE::PATCH_BYTES + (size_t)NJ * 16 * GE::TAPS * CL_CS * 2;
+  static_assert(lds <= 96 * 1024, "conv tile LDS");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)enc_conv_nhwc_kernel<NJ, TW, KS, ST, TO>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    attr = true;
+  }
+  const dim3 grid(a.N * ((a.Ho + GE::TH - 1) / GE::TH) * ((a.Wo + TW - 1) / TW), a.Cout_pad / (NJ * 16));
+  hipLaunchKernelGGL((enc_conv_nhwc_kernel<NJ, TW, KS, ST, TO>), grid, dim3(CONV_TPB), lds, s, a);
+  return hipGetLastError();
+}
+
+// the compile-time-geometry kernel for this shape, or nullptr (then the runtime-geometry kernel):
+// the tower's convs (bf16 out) and the heads' (f32 out: 2x2 on the layer-2 map, 3x3 after the
+// pixel shuffles)
+typedef hipError_t (*ConvLaunch)(const ConvArgs&, hipStream_t);
+ConvLaunch conv_nhwc_for(const ConvArgs& a) {
+  if (!a.in_bf16 || a.layout != LAYOUT_NHWC || conv_no_lds || a.KH != a.KW) return nullptr;
+  const int nj = a.Cout_pad % 64 == 0 ? 4 : 2, TW = a.Wo >= 16 ? 16 : a.Wo >= 8 ? 8 : 0;
+  const int shape = a.KH * 10 + a.stride;
+#define GGD_CONV_CASE(NJ_, TW_, KS_, ST_, TO_)                                             \
+  if (nj == NJ_ && TW == TW_ && shape == KS_ * 10 + ST_ && (sizeof(TO_) == 2) == (a.out_bf16 != 0)) \
+    return launch_conv_nhwc<NJ_, TW_, KS_, ST_, TO_>;
+  GGD_CONV_CASE(4, 16, 3, 1, bf16_t) GGD_CONV_CASE(4, 8, 3, 1, bf16_t)
+  GGD_CONV_CASE(2, 16, 3, 1, bf16_t) GGD_CONV_CASE(2, 8, 3, 1, bf16_t)
+  GGD_CONV_CASE(4, 16, 3, 2, bf16_t) GGD_CONV_CASE(4, 8, 3, 2, bf16_t)
+  GGD_CONV_CASE(4, 16, 1, 2, bf16_t) GGD_CONV_CASE(4, 8, 1, 2, bf16_t)
+  GGD_CONV_CASE(4, 16, 2, 1, float) GGD_CONV_CASE(2, 16, 3, 1, float)
+#undef GGD_CONV_CASE
+  return nullptr;
+}
+
+// tile width of the LDS path for this shape, or 0 when the shape takes the direct kernel
+int conv_lds_tw(int dtype, const ConvArgs& a) {
+  if (dtype != GGD_BF16 || conv_no_lds) return 0;
+  if (conv_nhwc_for(a)) return a.Wo >= 16 ? 16 : 8;
+  const int nj = a.Cout_pad % 64 == 0 ? 4 : 2;
+  const int TW = a.Wo >= 16 ? 16 : a.Wo >= 8 ? 8 : 4;
+  const ConvLdsGeom G = conv_lds_geom(a, TW, nj);
+  const int qp = a.in_bf16 ? 4 : 8;  // input pieces per patch position
+  const bool fits = G.patch_bytes + G.w_bytes <= 96 * 1024 && G.PH * G.PW * qp <= CL_PMAX * CONV_TPB &&
+                    G.taps <= CL_TAPS_MAX;
+  return fits ? TW : 0;
+}
+
+// output tiles per image of the LDS path (the rows of ConvArgs::se_part per image)
+int conv_lds_tiles(int Ho, int Wo) {
+  const int TW = Wo >= 16 ? 16 : Wo >= 8 ? 8 : 4, TH = CL_PX / TW;
+  return ((Ho + TH - 1) / TH) * ((Wo + TW - 1) / TW);
 }
 
 template <typename TI, typename TO>
@@ -605,12 +961,15 @@ hipError_t launch_conv_t(int dtype, const ConvArgs& a, hipStream_t s) {
   const int P = a.N * a.Ho * a.Wo;
   const int nj = a.Cout_pad % 64 == 0 ? 4 : 2;
   const dim3 grid(blocks_for(P, 128), a.Cout_pad / (nj * 16));
-  if (dtype == GGD_BF16 && !conv_no_lds) {
-    const int TW = a.Wo >= 16 ? 16 : a.Wo >= 8 ? 8 : 4;
-    const ConvLdsGeom G = conv_lds_geom(a, TW, nj);
+  if (a.se_part && !conv_lds_tw(dtype, a)) return hipErrorInvalidValue;  // only the LDS paths squeeze
+  if (dtype == GGD_BF16)
+    if (const ConvLaunch f = conv_nhwc_for(a)) return f(a, s);
+  {
+    const int TW = conv_lds_tw(dtype, a);
+    const ConvLdsGeom G = conv_lds_geom(a, TW ? TW : 4, nj);
     const size_t lds = G.patch_bytes + G.w_bytes;
-    const int qp = 32 / (16 / (int)sizeof(TI));  // input pieces per patch position
-    if (lds <= 96 * 1024 && G.PH * G.PW * qp <= CL_PMAX * CONV_TPB && G.taps <= CL_TAPS_MAX) {
+    const int qp = 32 / (16 / (int)sizeof(TI));
+    if (TW) {
       static bool attr = false;
       if (!attr) {
         (void)hipFuncSetAttribute((const void*)enc_conv_lds_kernel<4, CL_PMAX, TI, TO>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
@@ -881,8 +1240,10 @@ int make_lin(ggd_enc* e, const std::string& name, int out, int in, float** w, fl
   return GGD_OK;
 }
 
+// se_S non-null: squeeze into e->se_part in the epilogue when the shape takes the LDS path, and
+// return its rows per image there (0: not squeezed, the caller runs enc_se_sum_kernel)
 int run_conv(ggd_enc* e, const EConv& cv, const void* in, int n, int H, int W, void* out, int mode, int layout,
-             hipStream_t s, bool out_act = true) {
+             hipStream_t s, bool out_act = true, int* se_S = nullptr) {
   ConvArgs a{};
   a.in = in;
   a.in_bf16 = e->asz == 2;
@@ -906,6 +1267,13 @@ int run_conv(ggd_enc* e, const EConv& cv, const void* in, int n, int H, int W, v
   a.pad = cv.pad;
   a.mode = mode;
   a.layout = layout;
+  if (se_S) {
+    *se_S = 0;
+    if (conv_lds_tw(e->dtype, a) && layout == LAYOUT_NHWC) {
+      a.se_part = e->se_part;
+      *se_S = conv_lds_tiles(a.Ho, a.Wo);
+    }
+  }
   ENC_TRY(e, launch_conv(e->dtype, a, s));
   return GGD_OK;
 }
@@ -985,8 +1353,18 @@ int ggd_enc_finalize(ggd_enc* e) {
     int r = make_conv(e, h.conv, FE + "conv_" + hn[i], FE + "bn_" + hn[i], hc[i], hc[i], hk[i], 1, 0, true);
     if (r) return r;
     h.K = hc[i] * hh[i];
-    r = make_lin(e, FE + "fc_" + hn[i], 32, h.K, &h.fc_w, &h.fc_b);
-    if (r) return r;
+    {  // fc_* columns from the reference's (c, h) flatten order to the kernel's (h, c) order
+      const std::vector<float> *pw, *pb;
+      NEED(FE + "fc_" + hn[i] + ".weight", (size_t)32 * h.K, pw);
+      NEED(FE + "fc_" + hn[i] + ".bias", 32, pb);
+      std::vector<float> wt((size_t)32 * h.K);
+      for (int j = 0; j < 32; ++j)
+        for (int c = 0; c < hc[i]; ++c)
+          for (int y = 0; y < hh[i]; ++y)
+            wt[(size_t)j * h.K + (size_t)y * hc[i] + c] = (*pw)[(size_t)j * h.K + (size_t)c * hh[i] + y];
+      ENC_TRY(e, upload(e, &h.fc_w, wt));
+      ENC_TRY(e, upload(e, &h.fc_b, *pb));
+    }
   }
   {
     int r = make_lin(e, PFX + "wav_proj_layer", e->d_model, 32, &e->proj_w, &e->proj_b);
@@ -1004,7 +1382,9 @@ int ggd_enc_finalize(ggd_enc* e) {
   for (int i = 0; i < 3; ++i)
     ENC_TRY(e, ealloc(e, &e->feat[i], e->asz * n * e->H[i + 2] * e->W[i + 2] * planes_l[i + 1]));
   ENC_TRY(e, ealloc(e, &e->se_y, sizeof(float) * n * 256));
-  ENC_TRY(e, ealloc(e, &e->se_part, sizeof(float) * n * SE_SLICES * 256));
+  int se_rows = SE_SLICES;
+  for (int l = 1; l <= 4; ++l) se_rows = std::max(se_rows, conv_lds_tiles(e->H[l], e->W[l]));
+  ENC_TRY(e, ealloc(e, &e->se_part, sizeof(float) * n * se_rows * 256));
   ENC_TRY(e, ealloc(e, &e->sbuf, e->asz * n * 32 *
                                     std::max((size_t)e->H[3] * 2 * e->W[3] * 2, (size_t)e->H[4] * 4 * e->W[4] * 4)));
   size_t hb = 0;
@@ -1040,7 +1420,7 @@ int ggd_enc_frontend(ggd_enc* e, const float* wav, int32_t n, float* img, void* 
     g.ldo = NMEL;
     g.n_valid = NMEL;
     ENC_TRY(e, launch_gemm(GGD_F32, PRO_F32, EPI_F32, g, s));
-    hipLaunchKernelGGL(enc_inorm_kernel, dim3(m), dim3(NMEL), 0, s, e->mel, img + (size_t)c0 * NMEL * F, F);
+    hipLaunchKernelGGL(enc_inorm_kernel, dim3(m), dim3(4 * NMEL), 0, s, e->mel, img + (size_t)c0 * NMEL * F, F);
     ENC_TRY(e, hipGetLastError());
   }
   return GGD_OK;
@@ -1073,7 +1453,7 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
     g.ldo = NMEL;
     g.n_valid = NMEL;
     ENC_TRY(e, launch_gemm(GGD_F32, PRO_F32, EPI_F32, g, s));
-    hipLaunchKernelGGL(enc_inorm_kernel, dim3(m), dim3(NMEL), 0, s, e->mel, e->img, F);
+    hipLaunchKernelGGL(enc_inorm_kernel, dim3(m), dim3(4 * NMEL), 0, s, e->mel, e->img, F);
     ENC_TRY(e, hipGetLastError());
     const size_t n1 = (size_t)m * e->H[1] * e->W[1] * 4;
     const bool hb = e->asz == 2;
@@ -1096,28 +1476,31 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
           if (e->buf[i] != x) sc[k++] = e->buf[i];
         void *u = sc[0], *v = sc[1], *r = sc[2];
         const int Ho = conv_out(H, 3, B.c1.stride, 1), Wo = conv_out(W, 3, B.c1.stride, 1);
+        int S = 0;  // the squeeze's partial-sum rows per image (conv2's tiles when its epilogue sums)
         int rc = run_conv(e, B.c1, x, m, H, W, u, CONV_RELU_BN, LAYOUT_NHWC, s);
-        if (!rc) rc = run_conv(e, B.c2, u, m, Ho, Wo, v, CONV_BN, LAYOUT_NHWC, s);
+        if (!rc) rc = run_conv(e, B.c2, u, m, Ho, Wo, v, CONV_BN, LAYOUT_NHWC, s, true, &S);
         const void* res = x;
         if (!rc && B.has_ds) {
           rc = run_conv(e, B.ds, x, m, H, W, r, CONV_BN, LAYOUT_NHWC, s);
           res = r;
         }
         if (rc) return rc;
-        const int S = std::max(1, std::min(SE_SLICES, Ho * Wo / 64));
-        if (hb)
-          hipLaunchKernelGGL(enc_se_sum_kernel<bf16_t>, dim3(m, S), dim3(256), 0, s, (const bf16_t*)v, Ho * Wo, B.planes,
-                             e->se_part);
-        else
-          hipLaunchKernelGGL(enc_se_sum_kernel<float>, dim3(m, S), dim3(256), 0, s, (const float*)v, Ho * Wo, B.planes,
-                             e->se_part);
-        ENC_TRY(e, hipGetLastError());
-        hipLaunchKernelGGL(enc_se_kernel, dim3(m), dim3(256), 0, s, e->se_part, S, Ho * Wo, B.planes, B.se_w0,
-                           B.se_b0, B.se_w2, B.se_b2, e->se_y);
-        ENC_TRY(e, hipGetLastError());
+        if (!S) {
+          S = std::max(1, std::min(SE_SLICES, Ho * Wo / 64));
+          if (hb)
+            hipLaunchKernelGGL(enc_se_sum_kernel<bf16_t>, dim3(m, S), dim3(256), 0, s, (const bf16_t*)v, Ho * Wo,
+                               B.planes, e->se_part);
+          else
+            hipLaunchKernelGGL(enc_se_sum_kernel<float>, dim3(m, S), dim3(256), 0, s, (const float*)v, Ho * Wo,
+                               B.planes, e->se_part);
+          ENC_TRY(e, hipGetLastError());
+        }
         // the block output goes to u (consumed by conv2 already), or to the saved feature map
         // of layers 2..4 that the heads read
         void* o = (bi == nblk[l] - 1 && l >= 1) ? e->feat[l - 1] : u;
+        hipLaunchKernelGGL(enc_se_kernel, dim3(m), dim3(256), 0, s, e->se_part, S, Ho * Wo, B.planes, B.se_w0,
+                           B.se_b0, B.se_w2, B.se_b2, e->se_y);
+        ENC_TRY(e, hipGetLastError());
         const size_t tot8 = (size_t)m * Ho * Wo * B.planes / 8;
         if (hb)
           hipLaunchKernelGGL(enc_se_apply_kernel<bf16_t>, dim3(blocks_for(tot8, 256)), dim3(256), 0, s, (const bf16_t*)v,
@@ -1140,7 +1523,7 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
       int Hh = e->H[i + 2], Wh = e->W[i + 2];
       if (h.shuffle > 1) {
         const int C = h.conv.cin, r = h.shuffle;
-        const size_t tot = (size_t)m * Hh * r * Wh * r * h.conv.cin_pad;
+        const size_t tot = (size_t)m * Hh * r * Wh * r * (h.conv.cin_pad / 8);
         if (hb)
           hipLaunchKernelGGL(enc_shuffle_kernel<bf16_t>, dim3(blocks_for(tot, 256)), dim3(256), 0, s, (const bf16_t*)fin,
                              (bf16_t*)e->sbuf, m, Hh, Wh, C, r, h.conv.cin_pad);
@@ -1152,12 +1535,14 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
         Hh *= r;
         Wh *= r;
       }
-      int rc = run_conv(e, h.conv, fin, m, Hh, Wh, e->hbuf, CONV_RELU_BN, LAYOUT_NWCH, s, false);
+      int rc = run_conv(e, h.conv, fin, m, Hh, Wh, e->hbuf, CONV_RELU_BN, LAYOUT_NHWC, s, false);
       if (rc) return rc;
       const int Wo = conv_out(Wh, h.conv.kw, 1, 0);
       if (Wo != tl[i]) return efail(e, GGD_ERR_STATE, "head length mismatch");
-      hipLaunchKernelGGL(enc_head_fc_kernel, dim3(m * Wo), dim3(256), 0, s, e->hbuf, h.K, h.fc_w, h.fc_b, e->proj_w,
-                         e->proj_b, zs[i], d);
+      const int Ho = conv_out(Hh, h.conv.kh, 1, 0), C = h.conv.cout;
+      if (h.K % 16 || h.K != C * Ho || (C & (C - 1)) || C % 4) return efail(e, GGD_ERR_STATE, "head feature shape");
+      hipLaunchKernelGGL(enc_head_fc_kernel, dim3((m * Wo + 15) / 16), dim3(64 * HFC_WAVES), 0, s, e->hbuf, m * Wo, h.K, Ho, Wo,
+                         h.conv.cout_pad, __builtin_ctz(C), h.fc_w, h.fc_b, e->proj_w, e->proj_b, zs[i], d);
       ENC_TRY(e, hipGetLastError());
     }
   }

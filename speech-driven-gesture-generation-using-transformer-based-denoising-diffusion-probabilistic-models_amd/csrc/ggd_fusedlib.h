@@ -155,6 +155,19 @@ __device__ __forceinline__ uint4 ld_16B(const void* base, uint32_t byte_off) {
   }
 }
 
+template <int CP>
+__device__ __forceinline__ uint2 ld_8B(const void* base, uint32_t byte_off) {
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  if constexpr (CP == CP_KERNEL) {
+    const u32x2 v = *G((const u32x2*)((const char*)base + byte_off));
+    return make_uint2(v.x, v.y);
+  } else {
+    const __amdgpu_buffer_rsrc_t r = uni_rsrc(base, 0x7fffffffu);
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)byte_off, 0, cp_load(CP));
+    return make_uint2(v.x, v.y);
+  }
+}
+
 // thread index as an opaque value: inside the persistent step loop (ggd_mega.hip) values derived
 // from threadIdx.x are loop invariant, and the compiler hoists them out of the loop and keeps
 // them live across every phase (spilling); an opaque index keeps them inside their phase

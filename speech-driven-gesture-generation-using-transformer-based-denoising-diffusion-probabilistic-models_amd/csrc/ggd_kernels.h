@@ -135,7 +135,7 @@ struct FusedArgs {
   float* h;          // residual rows read (f32 [N*L][256])
   float* h_out;      // KB / KC: updated residual rows written (ping-pong buffer); KD updates h in place
   void *o_sa, *o_ca, *hid;
-  float* ffp;        // KC -> KD: f32 FFN-down partial sums [N][8 chunks][L][256]
+  float* ffp;        // KC -> KD: FFN-down partial sums [N][8 chunks][L][256], as T (bf16 / f32)
   const int* t_clip; const StepRec* steps; int* step_counter; int bump_counter;
   float scale;
   // KA of layer 0 with x_emb set: h = emb_x(x) + PE is computed in the kernel (x_emb = state

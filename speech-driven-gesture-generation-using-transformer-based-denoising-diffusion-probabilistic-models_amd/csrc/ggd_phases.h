@@ -330,8 +330,9 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
 
 // ------------------------------------------------------------------------------------------
 // KC: CA out-proj + residual + LN3 + FFN-up chunk c (128 hidden) + ReLU^2 + that chunk's share of
-// FFN-down (hidden chunk x W2[:, chunk]^T, all 256 output columns): an f32 partial sum per chunk,
-// reduced by KD.  The hidden chunk never leaves LDS.                  grid (8 chunks, clips)
+// FFN-down (hidden chunk x W2[:, chunk]^T, all 256 output columns): a partial sum per chunk in T
+// (bf16 loops: bf16 partials, half the hand-off bytes of f32), reduced in f32 by KD.  The hidden
+// chunk never leaves LDS.                                                grid (8 chunks, clips)
 // ------------------------------------------------------------------------------------------
 template <typename T, int RT, int CP, typename FA>
 __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned char* smem, KCPre<T, RT>& pre) {
@@ -394,13 +395,12 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   {
     f32x4 acc[RT][2];
     gd.template run<true>(acc, Hc, SHC, lane);
-    const OutRowsP<CP> out(a.ffp + ((size_t)b * 8 + c) * L * FD, (uint32_t)(sizeof(float) * L * FD));
+    const OutRowsP<CP> out((T*)a.ffp + ((size_t)b * 8 + c) * L * FD, (uint32_t)(sizeof(T) * L * FD));
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
-        out.put4((uint32_t)((rt * 16 + c16) * FD + (2 * wave + j) * 16 + 4 * g4),
-                 make_float4(acc[rt][j][0], acc[rt][j][1], acc[rt][j][2], acc[rt][j][3]));
+        out.template put4v<T>((uint32_t)((rt * 16 + c16) * FD + (2 * wave + j) * 16 + 4 * g4), acc[rt][j]);
   }
   STAMP_END(5);
 }
@@ -423,8 +423,15 @@ __device__ __forceinline__ void kd_phase(const FA& a, int p, int b, unsigned cha
   float4 part[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    const uint4 u = ld_16B<CP>(a.ffp, (uint32_t)(sizeof(float) * ((((size_t)b * 8 + c) * L + row) * FD + col)));
-    part[c] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+    const uint32_t off = (uint32_t)(sizeof(T) * ((((size_t)b * 8 + c) * L + row) * FD + col));
+    if constexpr (sizeof(T) == 2) {
+      const uint2 u = ld_8B<CP>(a.ffp, off);
+      part[c] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                            __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+    } else {
+      const uint4 u = ld_16B<CP>(a.ffp, off);
+      part[c] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+    }
   }
   float4 res;
   if constexpr (Res<T, CP>::ON) {  // the residual rows KC left in LDS
