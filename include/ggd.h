@@ -207,7 +207,8 @@ enum {
   GGD_INFO_XL_LAUNCHES = 3,          /* last ggd_sample: XCD-local clip-group launches */
   GGD_INFO_WT_RERUNS = 4,            /* last ggd_sample: clip-group launches re-run write-through */
   GGD_INFO_CHAIN_AVAILABLE = 5,      /* 1 when the generic one-way route runs as row-block chains */
-  GGD_INFO_LONG_LAUNCHES = 6         /* last ggd_sample: long-clip loop launches (0: another route) */
+  GGD_INFO_LONG_LAUNCHES = 6,        /* last ggd_sample: long-clip loop launches (0: another route) */
+  GGD_INFO_CLIP_ATTN_LAUNCHES = 7    /* running count of whole-clip attention launches (generic routes) */
 };
 int ggd_route_info(ggd_ctx* ctx, int32_t what, double* out);
 

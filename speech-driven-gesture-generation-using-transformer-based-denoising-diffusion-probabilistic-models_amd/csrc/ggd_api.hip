@@ -109,6 +109,7 @@ struct ggd_ctx {
   bool chain = false;        // fragment-packed weights built (one-way, not fused, bf16 / fp8, d 256, FFN 1024)
   int gemm_launches = 0;     // GGD_ROUTE_GEMM_LAUNCHES: 1 = one launch per GEMM instead
   int attn_qsplit = 0;       // GGD_ROUTE_ATTN_QSPLIT: 1 = long clips on the query-split attention
+  long clip_attn_launches = 0;  // GGD_INFO_CLIP_ATTN_LAUNCHES: whole-clip attention launches (running count)
   // long-clip persistent loop (ggd_long.hip): every step of clips of >= 96 frames in one launch
   bool long_ok = false;      // the shape and dtype have a long-loop instance (needs the chain weights)
   int long_off = 0;          // GGD_ROUTE_LONG_LOOP: 1 = never
@@ -696,6 +697,12 @@ FusedLayer fused_layer(ggd_ctx* c, int li) {
   return w;
 }
 
+// every attention launch of the generic routes: counts the whole-clip kernel's launches
+hipError_t run_attention(ggd_ctx* c, int dtype, const AttnArgs& at, int n, hipStream_t s) {
+  if (attention_clip_supported(dtype, at)) ++c->clip_attn_launches;
+  return launch_attention(dtype, at, n, s);
+}
+
 // KA / KB arguments of layer li (KC runs on h2 -> h, KD on h in place)
 FusedArgs fused_args(ggd_ctx* c, int li, const int* t_clip) {
   const ggd_desc& D = c->desc;
@@ -811,7 +818,7 @@ int launch_decoder_twoway(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     at.scale = 1.0f / std::sqrt((float)dk);
     at.seq_stride = J;
     at.seq_off = sg.off;
-    HIP_TRY(c, launch_attention(dt, at, n, s));
+    HIP_TRY(c, run_attention(c, dt, at, n, s));
     GemmArgs op = gemm_args(o, M, c->attj, d, c->hj, d);
     op.a_len = op.o_len = map;
     op.a_stride = op.o_stride = J;
@@ -936,7 +943,7 @@ int launch_decoder_chain(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     const Layer& Ly = c->layers[li];
     AttnArgs at = self_attn_args(c, Ly);
     if (c->profiling && sampling && (r = prof_mark(c, s))) return r;
-    HIP_TRY(c, launch_attention(D.dtype, at, n, s));
+    HIP_TRY(c, run_attention(c, D.dtype, at, n, s));
     if (c->profiling && sampling && (r = prof_mark(c, s))) return r;
     ChainArgs ca{};
     ca.M = M;
@@ -951,7 +958,7 @@ int launch_decoder_chain(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     if ((r = chain(ca))) return r;
     cross_attn_args(c, Ly, li, t_clip, at);
     if (c->profiling && sampling && (r = prof_mark(c, s))) return r;
-    HIP_TRY(c, launch_attention(D.dtype, at, n, s));
+    HIP_TRY(c, run_attention(c, D.dtype, at, n, s));
     if (c->profiling && sampling && (r = prof_mark(c, s))) return r;
     ChainArgs cb{};
     cb.M = M;
@@ -1024,7 +1031,7 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     at.d = d;
     at.scale = 1.0f / std::sqrt((float)dk);
     if (c->profiling && sampling) { int r = prof_mark(c, s); if (r) return r; }
-    HIP_TRY(c, launch_attention(D.dtype, at, n, s));
+    HIP_TRY(c, run_attention(c, D.dtype, at, n, s));
     if (c->profiling && sampling) { int r = prof_mark(c, s); if (r) return r; }
 
     g = gemm_args(Ly.o_sa, M, c->att, d, c->h, d);
@@ -1049,7 +1056,7 @@ int launch_decoder(ggd_ctx* c, int n, bool sampling, const int* t_clip) {
     at.cw_v = Ly.ca_v.w; at.cb_v = Ly.ca_v.b;
     at.Lk = 1 + D.speech_len;
     if (c->profiling && sampling) { int r = prof_mark(c, s); if (r) return r; }
-    HIP_TRY(c, launch_attention(D.dtype, at, n, s));
+    HIP_TRY(c, run_attention(c, D.dtype, at, n, s));
     if (c->profiling && sampling) { int r = prof_mark(c, s); if (r) return r; }
 
     g = gemm_args(Ly.o_ca, M, c->att, d, c->h, d);
@@ -1733,6 +1740,7 @@ int ggd_route_info(ggd_ctx* c, int32_t what, double* out) {
     case GGD_INFO_WT_RERUNS: *out = c->mega_fallbacks; return GGD_OK;
     case GGD_INFO_CHAIN_AVAILABLE: *out = c->chain ? 1.0 : 0.0; return GGD_OK;
     case GGD_INFO_LONG_LAUNCHES: *out = c->long_launches; return GGD_OK;
+    case GGD_INFO_CLIP_ATTN_LAUNCHES: *out = (double)c->clip_attn_launches; return GGD_OK;
     default: return fail(c, GGD_ERR_ARG, "unknown route info");
   }
 }
@@ -1896,7 +1904,7 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
     at.no_qsplit = np >= 3 ? p[2] : 0;
     for (int it = 0; rc == GGD_OK && it < iters + 1; ++it) {
       if (it == 1) HIP_TRY(c, hipEventRecord(e0, s));
-      HIP_TRY(c, launch_attention(D.dtype, at, n, s));
+      HIP_TRY(c, run_attention(c, D.dtype, at, n, s));
     }
   } else if ((what == 2 || what == 3) && np >= 1) {
     const int n = p[0];

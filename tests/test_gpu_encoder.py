@@ -44,8 +44,10 @@ def test_encoder_f32_matches_oracle(pkg, sd, wav_len):
         assert err <= 2e-4 * max(1.0, b.abs().max().item()), err
 
 
-def test_encoder_bf16_matches_oracle(pkg, sd):
-    wav = wavs(3)
+@pytest.mark.parametrize("wav_len", [32000, 80000, 128000])
+def test_encoder_bf16_matches_oracle(pkg, sd, wav_len):
+    """bf16 tower (compile-time-geometry NHWC convs at these widths: 63 / 157 / 250 frames)."""
+    wav = wavs(3, wav_len)
     want = ref_denoiser.speech_encoder(sd, wav)
     got = [z.cpu() for z in encoder(pkg, sd, "bf16")(wav.cuda())]
     for a, b in zip(got, want):

@@ -17,6 +17,7 @@ D_POSE, L, WAV = 123, 40, 32000
 ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_PAIR_WT, ROUTE_PHASE_LAUNCHES = 0, 1, 2, 3   # include/ggd.h GGD_ROUTE_*
 ROUTE_GEMM_LAUNCHES, ROUTE_ATTN_QSPLIT, ROUTE_LONG_LOOP = 5, 6, 7
 INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES, INFO_CHAIN_AVAILABLE, INFO_LONG_LAUNCHES = 0, 2, 5, 6  # GGD_INFO_*
+INFO_CLIP_ATTN_LAUNCHES = 7
 
 
 def rel_rms(a, b):
@@ -575,12 +576,18 @@ def test_clip_attention_matches_query_split(pkg, beat_cfg, setup, setup_fp8, dty
     wav, x, t = inputs(n, seed=81, wav_len=wav_len, L_=Lc)
     ctx, _ = model.prepare(wav.cuda(), Lc)
     try:
+        n0 = int(_info(ctx, INFO_CLIP_ATTN_LAUNCHES))
         clip = model(x.cuda(), t.cuda(), wav=wav.cuda()).cpu()
+        n1 = int(_info(ctx, INFO_CLIP_ATTN_LAUNCHES))
         assert ctx.lib.ggd_set_route(ctx.h, ROUTE_ATTN_QSPLIT, 1) == 0
         qsplit = model(x.cuda(), t.cuda(), wav=wav.cuda()).cpu()
+        n2 = int(_info(ctx, INFO_CLIP_ATTN_LAUNCHES))
     finally:
         ctx.lib.ggd_set_route(ctx.h, ROUTE_ATTN_QSPLIT, 0)
-    assert not th.equal(clip, qsplit)          # the routes differ (exp2 vs expf): both really ran
+    # both routes really ran: 2 whole-clip launches per layer, then none.  (Their outputs may be
+    # bit-identical: the exp2 / expf difference is ~1 f32 ulp of P, which P's bf16 rounding for
+    # the PV MFMA usually absorbs -- seen at L = 100 with the r03 encoder's memory.)
+    assert n1 - n0 == 2 * 4 and n2 == n1, (n0, n1, n2)
     assert rel_rms(clip, qsplit) <= 2e-3
     ref = (setup_fp8 if dtype == "fp8" else om)(x, t, wav=wav)
     assert rel_rms(clip, ref) <= 1e-2
