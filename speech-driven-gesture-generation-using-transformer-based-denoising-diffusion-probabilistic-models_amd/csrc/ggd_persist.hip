@@ -156,8 +156,8 @@ constexpr int PK_THREADS = 512;  // 8 waves: two per SIMD, so one wave's LDS / L
 // partners meet three times per layer: after self-attention and after cross-attention each
 // hands its four heads' outputs (bf16, L x 128) to the other, which then runs the full
 // out-projection itself (a redundant 256 x 256 GEMM is cheaper than a second hand-off and keeps
-// the residual bit-identical to the one-workgroup loop); after the FFN each hands its f32
-// FFN-down partial (L x 256) and both add part 0's + part 1's.  Every other step-loop value
+// the residual bit-identical to the one-workgroup loop); after the FFN each hands its FFN-down
+// partial (L x 256, rounded to bf16) and both add part 0's + part 1's.  Every other step-loop value
 // (embedding, LayerNorms, out-projection, posterior update with its counter noise) is computed
 // identically by both, so both hold the same pose state and part 0 alone writes it.
 //
@@ -638,28 +638,49 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         }
         static_assert(2 * PL::HID <= PL::SCR, "double-buffered FFN chunk image");
         if constexpr (PAIR) {  // FFN-down partials of the two halves of K: both add part 0's + part 1's
+          // as bf16 (half the hand-off bytes of f32); each part rounds its OWN partial too, so both
+          // add the same two bf16 values and hold the same bits
           ++ep;
           const size_t sl = (size_t)(ep & 1) * PAIR_SLOT_BYTES;
+          typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+          u32x2 mine[RT][2];
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const f32x4 v = accd[rt][j];
+              mine[rt][j] = u32x2{(unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16),
+                                  (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16)};
+            }
           {
             const __amdgpu_buffer_rsrc_t r = uni_rsrc(xb + (size_t)part * 2 * PAIR_SLOT_BYTES + sl, (uint32_t)PAIR_SLOT_BYTES);
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-              for (int j = 0; j < 2; ++j)
-                pp_put16(r, (((wave * RT + rt) * 2 + j) * 64 + lane) * 16, __builtin_bit_cast(pp_u32x4, accd[rt][j]), xl);
+              for (int j = 0; j < 2; ++j) {
+                const int off = (((wave * RT + rt) * 2 + j) * 64 + lane) * 8;
+                if (xl) __builtin_amdgcn_raw_buffer_store_b64(mine[rt][j], r, off, 0, 0);
+                else __builtin_amdgcn_raw_buffer_store_b64(mine[rt][j], r, off, 0, CP_COH);
+              }
           }
           if (!pp_sync(flags, part, ep, xl, a.status, &s_ok)) return;
           const __amdgpu_buffer_rsrc_t r = uni_rsrc(xb + (size_t)(part ^ 1) * 2 * PAIR_SLOT_BYTES + sl, (uint32_t)PAIR_SLOT_BYTES);
-          pp_u32x4 o[RT][2];
+          u32x2 o[RT][2];
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-              o[rt][j] = __builtin_amdgcn_raw_buffer_load_b128(r, (((wave * RT + rt) * 2 + j) * 64 + lane) * 16, 0, CP_COH);
+              o[rt][j] = __builtin_amdgcn_raw_buffer_load_b64(r, (((wave * RT + rt) * 2 + j) * 64 + lane) * 8, 0, CP_COH);
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) accd[rt][j] += __builtin_bit_cast(f32x4, o[rt][j]);  // commutative: same bits in both
+            for (int j = 0; j < 2; ++j) {
+              const u32x2 m = mine[rt][j], q = o[rt][j];
+              accd[rt][j] = f32x4{__uint_as_float(m.x << 16) + __uint_as_float(q.x << 16),      // commutative:
+                                  __uint_as_float(m.x & 0xffff0000u) + __uint_as_float(q.x & 0xffff0000u),  // same bits
+                                  __uint_as_float(m.y << 16) + __uint_as_float(q.y << 16),      // in both parts
+                                  __uint_as_float(m.y & 0xffff0000u) + __uint_as_float(q.y & 0xffff0000u)};
+            }
         }
         const float b20 = w.ff2_b[(2 * wave) * 16 + c16], b21 = w.ff2_b[(2 * wave + 1) * 16 + c16];
 #pragma unroll
