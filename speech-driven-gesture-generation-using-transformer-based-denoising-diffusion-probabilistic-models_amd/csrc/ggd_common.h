@@ -12,6 +12,12 @@ constexpr int NT = 64;           // output columns per workgroup
 constexpr int NTHREADS = 256;    // 4 waves
 
 __device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+// two floats -> packed bf16 pair (lo in bits 0-15): one v_cvt_pk_bf16_f32, the same rounding as f2bf
+__device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  typedef __bf16 h2v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2v{lo, hi}, h2v));
+}
 __device__ __forceinline__ float bf2f(bf16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 
 template <typename T> __device__ __forceinline__ T from_f32(float v);

@@ -156,10 +156,10 @@ __global__ void enc_conv1_kernel(const float* __restrict__ img, const float* __r
   }
   if constexpr (sizeof(TA) == 2) {
     uint4 u;
-    u.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-    u.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-    u.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
-    u.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+    u.x = pk_bf16(o[0], o[1]);
+    u.y = pk_bf16(o[2], o[3]);
+    u.z = pk_bf16(o[4], o[5]);
+    u.w = pk_bf16(o[6], o[7]);
     *(uint4*)(out + p * 32 + cg * 8) = u;
   } else {
     float4* dst = (float4*)(out + p * 32 + cg * 8);
@@ -411,10 +411,10 @@ __global__ void enc_se_apply_kernel(const TA* __restrict__ v, const float* __res
   for (int i = 0; i < 8; ++i) a[i] = fmaxf(a[i] * ys[i] + r[i], 0.f);
   if constexpr (sizeof(TA) == 2) {
     uint4 u;
-    u.x = (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
-    u.y = (uint32_t)f2bf(a[2]) | ((uint32_t)f2bf(a[3]) << 16);
-    u.z = (uint32_t)f2bf(a[4]) | ((uint32_t)f2bf(a[5]) << 16);
-    u.w = (uint32_t)f2bf(a[6]) | ((uint32_t)f2bf(a[7]) << 16);
+    u.x = pk_bf16(a[0], a[1]);
+    u.y = pk_bf16(a[2], a[3]);
+    u.z = pk_bf16(a[4], a[5]);
+    u.w = pk_bf16(a[6], a[7]);
     *(uint4*)(out + e) = u;
   } else {
     *(float4*)(out + e) = make_float4(a[0], a[1], a[2], a[3]);
@@ -441,10 +441,10 @@ __global__ void enc_shuffle_kernel(const TA* __restrict__ in, TA* __restrict__ o
   TA* dst = out + p * Cp + c0;
   if constexpr (sizeof(TA) == 2) {
     uint4 o;
-    o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-    o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-    o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+    o.x = pk_bf16(v[0], v[1]);
+    o.y = pk_bf16(v[2], v[3]);
+    o.z = pk_bf16(v[4], v[5]);
+    o.w = pk_bf16(v[6], v[7]);
     *(uint4*)dst = o;
   } else {
     *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
@@ -644,8 +644,8 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int 
         if constexpr (sizeof(TI) == 2) {  // 8 bf16 channels as they are
           *(uint4*)(patch + pos * CL_CS + q4 * 8) = ok ? xr[k] : make_uint4(0u, 0u, 0u, 0u);
         } else {
-          const uint32_t lo = (uint32_t)f2bf(__uint_as_float(xr[k].x)) | ((uint32_t)f2bf(__uint_as_float(xr[k].y)) << 16);
-          const uint32_t hi = (uint32_t)f2bf(__uint_as_float(xr[k].z)) | ((uint32_t)f2bf(__uint_as_float(xr[k].w)) << 16);
+          const uint32_t lo = pk_bf16(__uint_as_float(xr[k].x), __uint_as_float(xr[k].y));
+          const uint32_t hi = pk_bf16(__uint_as_float(xr[k].z), __uint_as_float(xr[k].w));
           *(uint2*)(patch + pos * CL_CS + q4 * 4) = ok ? make_uint2(lo, hi) : make_uint2(0u, 0u);
         }
       }
@@ -870,8 +870,8 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_nhwc_kernel(ConvArgs a) {
       if (okp) {
         TO* dst = out + (((size_t)b * a.Ho + oh) * a.Wo + ow) * a.Cout_pad + co;
         if constexpr (sizeof(TO) == 2) {
-          const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          const uint32_t lo = pk_bf16(v[0], v[1]);
+          const uint32_t hi = pk_bf16(v[2], v[3]);
           *(uint2*)dst = make_uint2(lo, hi);
         } else {
           *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);

@@ -116,7 +116,7 @@ template <int CP = CP_KERNEL> struct OutRowsP {
   template <typename T> __device__ __forceinline__ void put4v(uint32_t elem, f32x4 v) const {
     if constexpr (sizeof(T) == 2) {
       typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
-      const u32x2 u = {(unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16), (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16)};
+      const u32x2 u = {pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])};
       __builtin_amdgcn_raw_buffer_store_b64(u, r, (int)(elem * 2), 0, cp_store(CP));
     } else {
       put4(elem, make_float4(v[0], v[1], v[2], v[3]));
@@ -396,8 +396,8 @@ __device__ __forceinline__ void ln_apply(const float* Hs, int L, const float2* s
     const float y2 = ok ? (v[i].z - s[i].x) * s[i].y * g.z + bb.z : 0.f;
     const float y3 = ok ? (v[i].w - s[i].x) * s[i].y * g.w + bb.w : 0.f;
     if constexpr (sizeof(T) == 2) {  // one 8-byte LDS store per row instead of four 2-byte ones
-      const uint32_t lo = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
-      const uint32_t hi = (uint32_t)f2bf(y2) | ((uint32_t)f2bf(y3) << 16);
+      const uint32_t lo = pk_bf16(y0, y1);
+      const uint32_t hi = pk_bf16(y2, y3);
       *(uint2*)(img + r * SXI + c4) = make_uint2(lo, hi);
     } else {
       *(float4*)(img + r * SXI + c4) = make_float4(y0, y1, y2, y3);
@@ -409,9 +409,14 @@ __device__ __forceinline__ void ln_apply(const float* Hs, int L, const float2* s
 // finalize, ggd_api.hip frag_from): row r of the f32 image Hs (stride SH) -> (x - mu) / sigma into
 // the T image (stride SXI).  Each row is held by 8 lanes, 32 values each, in registers: mean,
 // centred variance (two-pass, as torch) and the normalised output need no LDS round trip and no
-// barrier between them.  Rows L .. NR - 1 are written as zeros.
+// barrier between them.  Rows L .. NR - 1 are written as zeros.  The per-value arithmetic runs on
+// packed f32 pairs (v_pk_add / v_pk_fma / v_pk_mul_f32) and bf16 pairs are converted with one
+// v_cvt_pk_bf16_f32: half the VALU instructions of the scalar form (the LN segments are
+// instruction-bound on the 5 waves that hold the 40 rows; measured 0.9 us per LN before).
 template <typename T, int NT, int NR, int SXI = Frag<T>::SX>
 __device__ __forceinline__ void ln_rows(const float* Hs, int L, T* img, int tid = ltid()) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 h2 __attribute__((ext_vector_type(2)));
   constexpr int RPP = NT / 8;  // rows per pass
   const int j = tid & 7;
 #pragma unroll
@@ -419,32 +424,35 @@ __device__ __forceinline__ void ln_rows(const float* Hs, int L, T* img, int tid 
     const int r = r0 + (tid >> 3);
     if (r0 + RPP > NR && r >= NR) break;
     if (r < L) {
-      float4 v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = *(const float4*)(Hs + r * SH + (j + 8 * i) * 4);
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-      const float mu = group_sum<8>(s) * (1.0f / (float)FD);
-      float q = 0.f;
+      f2 v[16];  // columns (j + 8 i) 4 .. + 3 as the pairs v[2 i], v[2 i + 1]
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        v[i].x -= mu;
-        v[i].y -= mu;
-        v[i].z -= mu;
-        v[i].w -= mu;
-        q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+        const float4 t = *(const float4*)(Hs + r * SH + (j + 8 * i) * 4);
+        v[2 * i] = f2{t.x, t.y};
+        v[2 * i + 1] = f2{t.z, t.w};
       }
-      const float rs = __builtin_amdgcn_rsqf(group_sum<8>(q) * (1.0f / (float)FD) + 1e-5f);
+      f2 s2 = v[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) s2 += v[i];
+      const float mu = group_sum<8>(s2.x + s2.y) * (1.0f / (float)FD);
+      const f2 m2 = f2{mu, mu};
+      f2 q2 = f2{0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        v[i] -= m2;
+        q2 += v[i] * v[i];
+      }
+      const float rs = __builtin_amdgcn_rsqf(group_sum<8>(q2.x + q2.y) * (1.0f / (float)FD) + 1e-5f);
+      const f2 r2 = f2{rs, rs};
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int c4 = (j + 8 * i) * 4;
+        const f2 a = v[2 * i] * r2, b = v[2 * i + 1] * r2;
         if constexpr (sizeof(T) == 2) {
-          const uint32_t lo = (uint32_t)f2bf(v[i].x * rs) | ((uint32_t)f2bf(v[i].y * rs) << 16);
-          const uint32_t hi = (uint32_t)f2bf(v[i].z * rs) | ((uint32_t)f2bf(v[i].w * rs) << 16);
-          *(uint2*)(img + r * SXI + c4) = make_uint2(lo, hi);
+          *(uint2*)(img + r * SXI + c4) = make_uint2(__builtin_bit_cast(uint32_t, __builtin_convertvector(a, h2)),
+                                                     __builtin_bit_cast(uint32_t, __builtin_convertvector(b, h2)));
         } else {
-          *(float4*)(img + r * SXI + c4) = make_float4(v[i].x * rs, v[i].y * rs, v[i].z * rs, v[i].w * rs);
+          *(float4*)(img + r * SXI + c4) = make_float4(a.x, a.y, b.x, b.y);
         }
       }
     } else if (r < NR) {
@@ -514,8 +522,8 @@ __device__ __forceinline__ void put_tok4(T* img, int S, int i, int c0, const f32
 #pragma unroll
     for (int r = 0; r < 4; ++r) img[(c0 + r) * S + i] = from_f32<T>(v[r]);
   } else if constexpr (sizeof(T) == 2) {
-    *(uint2*)(img + i * S + c0) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
-                                             (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+    *(uint2*)(img + i * S + c0) = make_uint2(pk_bf16(v[0], v[1]),
+                                             pk_bf16(v[2], v[3]));
   } else {
     *(float4*)(img + i * S + c0) = make_float4(v[0], v[1], v[2], v[3]);
   }

@@ -178,11 +178,9 @@ __device__ __forceinline__ void lk_layernorm(const float* hs, const float* gm, c
     const float4 x = *(const float4*)(hs + r * HS_STR + k);
     const float4 g = *(const float4*)(gm + k);
     const float4 b = *(const float4*)(bt + k);
-    bf16_t* dst = xs + r * XS_STR + k;
-    dst[0] = f2bf((x.x - mu) * rs * g.x + b.x);
-    dst[1] = f2bf((x.y - mu) * rs * g.y + b.y);
-    dst[2] = f2bf((x.z - mu) * rs * g.z + b.z);
-    dst[3] = f2bf((x.w - mu) * rs * g.w + b.w);
+    // one 8-byte LDS store of the 4 bf16 values (two v_cvt_pk_bf16_f32)
+    *(uint2*)(xs + r * XS_STR + k) = make_uint2(pk_bf16((x.x - mu) * rs * g.x + b.x, (x.y - mu) * rs * g.y + b.y),
+                                                pk_bf16((x.z - mu) * rs * g.z + b.z, (x.w - mu) * rs * g.w + b.w));
   }
 }
 
@@ -541,7 +539,7 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
         const float bb = Ly.ca_vb[c];
         const float k0 = bb + w[c * 3] * 0.f + w[c * 3 + 1] * x0 + w[c * 3 + 2] * x1;
         const float k1 = bb + w[c * 3] * x0 + w[c * 3 + 1] * x1 + w[c * 3 + 2] * x2;
-        v.x = (unsigned)f2bf(k0) | ((unsigned)f2bf(k1) << 16);
+        v.x = pk_bf16(k0, k1);
       }
       *(uint4*)(Vt + c * SV + kb * 8) = v;
     }

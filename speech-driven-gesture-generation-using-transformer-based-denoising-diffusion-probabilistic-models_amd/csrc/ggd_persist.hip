@@ -649,8 +649,8 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
               const f32x4 v = accd[rt][j];
-              mine[rt][j] = u32x2{(unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16),
-                                  (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16)};
+              mine[rt][j] = u32x2{pk_bf16(v[0], v[1]),
+                                  pk_bf16(v[2], v[3])};
             }
           {
             const __amdgpu_buffer_rsrc_t r = uni_rsrc(xb + (size_t)part * 2 * PAIR_SLOT_BYTES + sl, (uint32_t)PAIR_SLOT_BYTES);
