@@ -617,28 +617,40 @@ __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float 
   }
   // softmax in the base-2 domain: exp(scale s - m) = exp2(scale log2(e) s - m'), one v_exp_f32
   // per score (and one v_rcp_f32 per row) instead of the range-reduced library expf / division
+  // The lane's 4 rows run as two packed f32 pairs (rows 0-1, 2-3: v_pk_mul / v_pk_add_f32) for
+  // the scaling, the sums and the normalisation; per element the operations and their order are
+  // the scalar ones.  A masked key is -inf after the scaling, so its exp2 is 0 without a select.
+  typedef float f2 __attribute__((ext_vector_type(2)));
   const float sl2 = scale * 1.4426950408889634f;
+  const f2 sl = f2{sl2, sl2};
+  float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float mx = -INFINITY;
+  for (int t = 0; t < LKT; ++t) {
+    const bool ok = t * 16 + c16 < Lk;
+    const f2 lo = f2{s[t][0], s[t][1]} * sl, hi = f2{s[t][2], s[t][3]} * sl;
+    s[t] = ok ? f32x4{lo.x, lo.y, hi.x, hi.y} : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-    for (int t = 0; t < LKT; ++t) {
-      const float v = t * 16 + c16 < Lk ? s[t][r] * sl2 : -INFINITY;
-      s[t][r] = v;
-      mx = fmaxf(mx, v);
-    }
-    mx = group_max<16>(mx);
-    float sum = 0.f;
+    for (int r = 0; r < 4; ++r) mx[r] = fmaxf(mx[r], s[t][r]);
+  }
 #pragma unroll
-    for (int t = 0; t < LKT; ++t) {
-      const float p = t * 16 + c16 < Lk ? __builtin_amdgcn_exp2f(s[t][r] - mx) : 0.f;
-      s[t][r] = p;
-      sum += p;
-    }
-    sum = group_sum<16>(sum);
-    const float inv = __builtin_amdgcn_rcpf(sum);
+  for (int r = 0; r < 4; ++r) mx[r] = group_max<16>(mx[r]);
+  f2 sum01 = f2{0.f, 0.f}, sum23 = f2{0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < LKT; ++t) P[(4 * g4 + r) * A::SP + t * 16 + c16] = from_f32<T>(s[t][r] * inv);
+  for (int t = 0; t < LKT; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[t][r] = __builtin_amdgcn_exp2f(s[t][r] - mx[r]);
+    sum01 += f2{s[t][0], s[t][1]};
+    sum23 += f2{s[t][2], s[t][3]};
+  }
+  const f2 inv01 = f2{__builtin_amdgcn_rcpf(group_sum<16>(sum01.x)), __builtin_amdgcn_rcpf(group_sum<16>(sum01.y))};
+  const f2 inv23 = f2{__builtin_amdgcn_rcpf(group_sum<16>(sum23.x)), __builtin_amdgcn_rcpf(group_sum<16>(sum23.y))};
+#pragma unroll
+  for (int t = 0; t < LKT; ++t) {
+    const f2 lo = f2{s[t][0], s[t][1]} * inv01, hi = f2{s[t][2], s[t][3]} * inv23;
+    P[(4 * g4 + 0) * A::SP + t * 16 + c16] = from_f32<T>(lo.x);
+    P[(4 * g4 + 1) * A::SP + t * 16 + c16] = from_f32<T>(lo.y);
+    P[(4 * g4 + 2) * A::SP + t * 16 + c16] = from_f32<T>(hi.x);
+    P[(4 * g4 + 3) * A::SP + t * 16 + c16] = from_f32<T>(hi.y);
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();

@@ -458,8 +458,9 @@ __device__ __forceinline__ void kd_phase(const FA& a, int p, int b, unsigned cha
 
 // ------------------------------------------------------------------------------------------
 // KE: LN_out + out-proj of 16 channels (eps) [+ diffusion update of those channels]
-// grid (8 channel blocks, clips).  Block p owns pose channels [16p, 16p + 16): wave w computes
-// eps for row tile w; the update of the block's L x 16 elements is one Philox quad per thread.
+// grid (8 channel blocks, clips).  Block p owns pose channels [16p, 16p + 16): wave w < RT computes
+// eps for row tile w; the update of the block's L x 16 elements is one Philox quad per thread of
+// the other waves.
 // The next step's emb_x + PE is computed by that step's first KA (x_emb).
 // ------------------------------------------------------------------------------------------
 template <typename T, int RT, int CP, typename FA>
@@ -484,8 +485,11 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
 #pragma unroll
   for (int k = 0; k < KT; ++k) go.wb[0][k] = pre.g.wb[0][k];
   const float4 bo = ld_f4(a.b_out + p * 16 + 4 * g4);
-  // the thread's quad: elements e0 + 4 tid .. + 3 (issued now, consumed after the GEMM)
-  const bool upd = a.do_update && 4 * tid < ne;
+  // the thread's quad: elements e0 + 4 ut .. + 3 (issued now, consumed after the GEMM).  The quads
+  // live on the waves the out-projection leaves idle (ut = tid - 64 RT; 64 (8 - RT) >= 4 L / 4), so
+  // their Philox normals are drawn while waves 0 .. RT-1 run the GEMM
+  const int ut = tid - 64 * RT;
+  const bool upd = a.do_update && ut >= 0 && 4 * ut < ne;
   StepRec rec{};
   float xq[4] = {0.f, 0.f, 0.f, 0.f}, zq[4] = {0.f, 0.f, 0.f, 0.f};
   float mq[4] = {0.f, 0.f, 0.f, 0.f}, pq[4] = {0.f, 0.f, 0.f, 0.f}, tq[4] = {0.f, 0.f, 0.f, 0.f};
@@ -494,7 +498,7 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
   const size_t plane = (size_t)a.n * LC;
   if (a.do_update) {
     rec = ld_rec(a.steps + k);
-    const int e = e0 + 4 * tid;  // tail threads (no valid element) only load clamped addresses
+    const int e = e0 + 4 * max(ut, 0);  // tail threads (no valid element) only load clamped addresses
     cc0 = e / L;
     l0 = e - cc0 * L;
     int cc = cc0, l = l0;
@@ -515,23 +519,24 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
   ln_rows<T, FT, RT * 16>(Hs, L, Xn);
   bar_lds();
   STAMP(1);
+  static_assert(64 * (FT / 64 - RT) * 4 >= 16 * RT * 16, "the idle waves hold every update quad");
   if (wave < RT) {
     f32x4 acc[1][1];
     go.template run<true>(acc, Xn + wave * 16 * Frag<T>::SX, Frag<T>::SX, lane);
     *(float4*)(E + (wave * 16 + c16) * SE + 4 * g4) =
         make_float4(acc[0][0][0] + bo.x, acc[0][0][1] + bo.y, acc[0][0][2] + bo.z, acc[0][0][3] + bo.w);
+  } else if (upd && !a.noise) {
+    philox_normal4(((uint64_t)rec.seed_hi << 32) | rec.seed_lo, rec.clip_offset + (uint32_t)b, (uint32_t)rec.i,
+                   TAG_STEP, (uint32_t)((e0 >> 2) + ut), zq);
   }
   bar_lds();
   STAMP(2);
   if (upd) {
     const OutRowsP<CP> xo(a.x, (uint32_t)(sizeof(float) * plane));
-    if (!a.noise)
-      philox_normal4(((uint64_t)rec.seed_hi << 32) | rec.seed_lo, rec.clip_offset + (uint32_t)b, (uint32_t)rec.i,
-                     TAG_STEP, (uint32_t)((e0 >> 2) + tid), zq);
     int cc = cc0, l = l0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = e0 + 4 * tid + u;
+      const int e = e0 + 4 * ut + u;
       if (e < e0 + ne) {
         const float ev = E[l * SE + (cc - c0)];
         const UpdOut o = upd_math(rec, a.alg, xq[u], ev, false, 0.f, inp, mq[u], pq[u], tq[u], zq[u]);
