@@ -655,17 +655,21 @@ __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float 
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   const OutRowsP<CP> dst(out, (uint32_t)(sizeof(T) * ((size_t)(Lq - 1) * ldo + FDK)));  // rows >= Lq dropped
+  // O^T = V^T P^T per 16-channel tile: lane (query c16, group g4) holds channels 4 g4 .. + 3 of its
+  // query row, so the row is written with one 8-byte (bf16) / 16-byte (f32) store per tile
 #pragma unroll
   for (int ct = 0; ct < FDK / 16; ++ct) {
     f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k0 = 0; k0 < LKT * 16; k0 += 32) att_mma16(o, P, A::SP, Vt + ct * 16 * A::SV, A::SV, k0, lane);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if constexpr (TO_LDS)
-        out[(rt * 16 + 4 * g4 + r) * ldo + ct * 16 + c16] = from_f32<T>(o[r]);
+    for (int k0 = 0; k0 < LKT * 16; k0 += 32) att_mma16(o, Vt + ct * 16 * A::SV, A::SV, P, A::SP, k0, lane);
+    const int q = rt * 16 + c16, d0 = ct * 16 + 4 * g4;
+    if constexpr (TO_LDS) {
+      if constexpr (sizeof(T) == 2)
+        *(uint2*)(out + q * ldo + d0) = make_uint2(pk_bf16(o[0], o[1]), pk_bf16(o[2], o[3]));
       else
-        dst.template put<T>((uint32_t)((rt * 16 + 4 * g4 + r) * ldo + ct * 16 + c16), o[r]);
+        *(float4*)(out + q * ldo + d0) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+      dst.template put4v<T>((uint32_t)(q * ldo + d0), o);
     }
   }
 }

@@ -106,8 +106,8 @@ __device__ int mk_role_xl(const MegaArgs& m, int nwg, int G) {
 }
 
 // barrier of the clip's 8 workgroups; epoch counts the barriers passed so far (+1).  After the
-// arrival every wave issues `prefetch` (the next phase's weight fragments); the exit barrier does
-// not wait for vector memory, so that stream stays in flight across the wait.
+// arrival the waves issue `prefetch` (the next phase's weight fragments; the polling wave after its
+// poll); the exit barrier does not wait for vector memory, so that stream stays in flight.
 // Write-through path (CP_COH): one agent-scope counter per group.  XCD-local path (CP_XL): the
 // group's 8 workgroups share one L2, so each publishes its epoch with a plain store into its own
 // word of the group's flag line (after its waves' stores have reached that L2) and wave 0 polls
@@ -126,7 +126,11 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
   } else {
     if (threadIdx.x == 0) mk_add(ctr, 1u);
   }
-  prefetch();
+  // the next phase's weight fragments: waves 1..7 now; wave 0, which polls, only after its poll --
+  // a poll load completes behind every vector load its wave issued before it (vmcnt is in order),
+  // so a prefetch issued ahead of the poll would hold the whole clip group until it had landed
+  const bool poller = threadIdx.x < 64;
+  if (!poller) prefetch();
   if constexpr (CPV == CP_XL) {
     if (threadIdx.x < 64) {
       const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
@@ -161,6 +165,7 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
       *s_ok = ok;
     }
   }
+  if (poller) prefetch();
   bar_lds();
   if (st && threadIdx.x == 0) st[2 * (epoch - 1) + 1] = __builtin_amdgcn_s_memtime();
   return *s_ok != 0;
