@@ -1,0 +1,11 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=${TAG:-r03ac}
+timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu -s tests/test_gpu_parity.py tests/test_gpu_eps_routes.py tests/test_gpu_fullsize.py -k "long or clip_attention or lk_ or fp8 or chain" > gpurun_out/${T}_pytest.txt 2>&1
+echo "pytest rc=$?"
+grep -E "PASSED|FAILED|lk_.* t=" gpurun_out/${T}_pytest.txt | cut -c1-150 | tail -30
+for w in c4 c2; do
+timeout -k 10 300 python -u bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline --no-f32-subrecord > gpurun_out/${T}_${w}_bench.json 2> gpurun_out/${T}_${w}_bench.err || { echo "bench $w failed"; tail -5 gpurun_out/${T}_${w}_bench.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/${T}_${w}_bench.json')); print('$w', d['value'], d['ms_per_step'], d['roofline']['avg_launch_us'])"
+done

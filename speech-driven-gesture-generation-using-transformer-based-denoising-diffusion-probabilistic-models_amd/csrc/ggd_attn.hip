@@ -14,6 +14,7 @@
 //             accumulator layout (DPP reductions over the 16 lanes of a row), P to the wave's
 //             LDS tile, O = P V (MFMA over 32-key steps), bf16 rows out
 #include "ggd_common.h"
+#include "ggd_cliptiles.h"
 
 namespace ggd {
 namespace {
@@ -115,63 +116,7 @@ struct AcStrip {
 template <int LKT>
 __device__ __forceinline__ void ac_tiles(const bf16_t* Qm, const bf16_t* Km, const bf16_t* Vt, bf16_t* P, int SV, int SP,
                                          int Lq, int Lk, float sl2, bf16_t* out, int ldo, int wave, int lane) {
-  const int c16 = lane & 15, g4 = lane >> 4;
-  for (int rt = wave; rt * 16 < Lq; rt += AC_NW) {
-    const bf16x8 qa = *(const bf16x8*)(Qm + (rt * 16 + c16) * AC_SQ + g4 * 8);
-    bf16x8 kb[LKT];
-#pragma unroll
-    for (int t = 0; t < LKT; ++t) kb[t] = *(const bf16x8*)(Km + (t * 16 + c16) * AC_SQ + g4 * 8);
-    f32x4 s[LKT];
-#pragma unroll
-    for (int t = 0; t < LKT; ++t)
-      s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kb[t], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < LKT; ++t) {
-        const float v = t * 16 + c16 < Lk ? s[t][r] * sl2 : -INFINITY;
-        s[t][r] = v;
-        mx = fmaxf(mx, v);
-      }
-      mx = group_max<16>(mx);
-      float sum = 0.f;
-#pragma unroll
-      for (int t = 0; t < LKT; ++t) {
-        const float p = t * 16 + c16 < Lk ? __builtin_amdgcn_exp2f(s[t][r] - mx) : 0.f;
-        s[t][r] = p;
-        sum += p;
-      }
-      sum = group_sum<16>(sum);
-      const float inv = 1.0f / sum;
-#pragma unroll
-      for (int t = 0; t < LKT; ++t) P[(4 * g4 + r) * SP + t * 16 + c16] = f2bf(s[t][r] * inv);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    constexpr int KS = LKT / 2;  // 32-key steps of P V
-    bf16x8 pa[KS], vb[2][KS];
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      pa[k] = *(const bf16x8*)(P + c16 * SP + k * 32 + g4 * 8);
-      vb[0][k] = *(const bf16x8*)(Vt + c16 * SV + k * 32 + g4 * 8);
-      vb[1][k] = *(const bf16x8*)(Vt + (16 + c16) * SV + k * 32 + g4 * 8);
-    }
-    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int k = 0; k < KS; ++k)
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) o[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[k], vb[ct][k], o[ct], 0, 0, 0);
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = rt * 16 + 4 * g4 + r;
-        if (i < Lq) out[(size_t)i * ldo + ct * 16 + c16] = f2bf(o[ct][r]);
-      }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
+  clip_attn_tiles<LKT, AC_NW, AC_SQ>(Qm, Km, Vt, P, SV, SP, Lq, Lk, sl2, out, ldo, wave, lane);
 }
 
 __global__ void __launch_bounds__(AC_NT) attn_clip_kernel(AttnArgs a) {
