@@ -218,6 +218,34 @@ __device__ __forceinline__ float group_max(float v) {
   return v;
 }
 
+// LayerNorm statistics of rows held by 4 consecutive lanes, N float4 of the row per lane (two-pass:
+// mean, then the centred sum of squares), on packed f32 pairs (v_pk_add / v_pk_mul / v_pk_fma_f32,
+// half the instructions of the scalar form) with explicit fma so that the contraction cannot
+// depend on the call site: shared by gemm_kernel's PRO_LN prologue, the row-block chains and the
+// long-clip loop, which must agree bit for bit.  k = the row length.
+template <int N>
+__device__ __forceinline__ void ln_stats4(const float4 (&v)[N], float k, float& mu, float& rs) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 s2 = f2{0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < N; ++i) s2 += f2{v[i].x, v[i].y} + f2{v[i].z, v[i].w};
+  float s = s2.x + s2.y;
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  mu = s / k;
+  const f2 m2 = f2{mu, mu};
+  f2 q2 = f2{0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const f2 a = f2{v[i].x, v[i].y} - m2, b = f2{v[i].z, v[i].w} - m2;
+    q2 += __builtin_elementwise_fma(b, b, a * a);
+  }
+  float q = q2.x + q2.y;
+  q += __shfl_xor(q, 1);
+  q += __shfl_xor(q, 2);
+  rs = 1.0f / sqrtf(q / k + 1e-5f);
+}
+
 // acc += X[xr0 + 0..15][0..K) . Y[yr0 + 0..15][0..K)^T   (both row-major with row stride S)
 template <typename T>
 __device__ __forceinline__ void att_mma(f32x4& acc, const T* X, int xr0, int SX, const T* Y, int yr0, int SY, int K,

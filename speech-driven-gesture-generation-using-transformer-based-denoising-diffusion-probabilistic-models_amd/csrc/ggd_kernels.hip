@@ -79,23 +79,7 @@ __device__ __forceinline__ void load_a(ARegs<T, MT, PRO>& R, const GemmArgs& a, 
 // LayerNorm statistics of the registers' rows (two-pass: mean, then centred sum of squares).
 template <typename T, int MT>
 __device__ __forceinline__ void ln_stats(ARegs<T, MT, PRO_LN>& R, int K) {
-  constexpr int N = ARegs<T, MT, PRO_LN>::N;
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < N; ++i) s += (R.v[i].x + R.v[i].y) + (R.v[i].z + R.v[i].w);
-  s += __shfl_xor(s, 1);
-  s += __shfl_xor(s, 2);
-  const float mu = s / (float)K;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const float d0 = R.v[i].x - mu, d1 = R.v[i].y - mu, d2 = R.v[i].z - mu, d3 = R.v[i].w - mu;
-    q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-  }
-  q += __shfl_xor(q, 1);
-  q += __shfl_xor(q, 2);
-  R.mu = mu;
-  R.rs = 1.0f / sqrtf(q / (float)K + 1e-5f);
+  ln_stats4<ARegs<T, MT, PRO_LN>::N>(R.v, (float)K, R.mu, R.rs);
 }
 
 // PRO_F32 with a dense A (lda == k_valid, identity row map, one K chunk): the tile's rows are one

@@ -153,23 +153,11 @@ __device__ __forceinline__ void lk_layernorm(const float* hs, const float* gm, c
     float4 v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = *(const float4*)(hs + r * HS_STR + (j + 4 * i) * 4);
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    const float mu = s / (float)CH_D;
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float d0 = v[i].x - mu, d1 = v[i].y - mu, d2 = v[i].z - mu, d3 = v[i].w - mu;
-      q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-    }
-    q += __shfl_xor(q, 1);
-    q += __shfl_xor(q, 2);
+    float mu, rs;
+    ln_stats4<16>(v, (float)CH_D, mu, rs);
     if (j == 0) {
       st[2 * r] = mu;
-      st[2 * r + 1] = 1.0f / sqrtf(q / (float)CH_D + 1e-5f);
+      st[2 * r + 1] = rs;
     }
   }
   ch_bar();
