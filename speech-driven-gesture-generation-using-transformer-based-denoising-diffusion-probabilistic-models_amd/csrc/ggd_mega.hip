@@ -112,10 +112,14 @@ __device__ int mk_role_xl(const MegaArgs& m, int nwg, int G) {
 // group's 8 workgroups share one L2, so each publishes its epoch with a plain store into its own
 // word of the group's flag line (after its waves' stores have reached that L2) and wave 0 polls
 // the 8 words with sc1 loads -- L2 round trips instead of memory-side atomics.
-template <int CPV, typename F>
+// VMC: vector loads the wave issued after its last hand-off store (the next phase's weights, issued
+// by the phase's hook): vmcnt completes in issue order, so waiting down to VMC outstanding drains
+// every store without waiting for those loads
+template <int CPV, int VMC = 0, typename F>
 __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part, unsigned epoch, int* status,
                                         int* s_ok, unsigned long long* st, F&& prefetch) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's hand-off stores landed
+  static_assert(VMC >= 0 && VMC < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");  // this wave's hand-off stores landed
   __syncthreads();
   if (st && threadIdx.x == 0) st[2 * (epoch - 1)] = __builtin_amdgcn_s_memtime();
   if constexpr (CPV == CP_XL) {
@@ -201,12 +205,13 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
     for (int li = 0; li < NL; ++li) {
       cfa_t f = fa0 + 4 * li;
       asm volatile("" : "+s"(f));  // per-layer arguments are re-read, not held across the loop
-      ka_phase<T, RT, CPV>(f[0], part, b, smem, pn);
+      // the out-projection fragments of KB / KC are issued by the hook behind the attention in front
       KBPre<T, RT> pb(f[1], wave);
-      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pb.load(lane); })) return;
-      kb_phase<T, RT, CPV>(f[1], part, b, it, smem, pb);
+      ka_phase<T, RT, CPV>(f[0], part, b, smem, pn, [&] { pb.load(lane); });
+      if (!mk_sync<CPV, KBPre<T, RT>::LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {})) return;
       KCPre<T, RT> pc(f[2], part, wave);
-      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pc.load(lane); })) return;
+      kb_phase<T, RT, CPV>(f[1], part, b, it, smem, pb, [&] { pc.load(lane); });
+      if (!mk_sync<CPV, KCPre<T, RT>::LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {})) return;
       kc_phase<T, RT, CPV>(f[2], part, b, smem, pc);
       KDPre<T, RT> pd(f[3], part, wave);
       if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pd.load(lane); })) return;

@@ -126,6 +126,7 @@ template <typename T, int RT> struct KBPre {  // SA out-projection, all 16 tiles
     go.tiles[1] = 2 * wave + 1;
   }
   __device__ __forceinline__ void load(int lane) { go.load(0, lane); }
+  static constexpr int LOADS = 2 * decltype(go)::G;  // vector loads per load()
 };
 template <typename T, int RT> struct KCPre {  // CA out-projection (the FFN-up tile loads in the phase)
   WGemm<T, 2, FD / Frag<T>::KF, RT> go;
@@ -136,6 +137,7 @@ template <typename T, int RT> struct KCPre {  // CA out-projection (the FFN-up t
     go.tiles[1] = 2 * wave + 1;
   }
   __device__ __forceinline__ void load(int lane) { go.load(0, lane); }
+  static constexpr int LOADS = 2 * decltype(go)::G;
 };
 template <typename T, int RT> struct KDPre {  // the FFN-down column reduce streams no weights
   template <typename FA>
@@ -143,11 +145,22 @@ template <typename T, int RT> struct KDPre {  // the FFN-down column reduce stre
   __device__ __forceinline__ void load(int) {}
 };
 
+// The persistent loop hands KA and KB a hook that issues the NEXT phase's weight fragments right
+// behind the attention: the waves the attention leaves idle (it runs on one wave per 16 query rows)
+// get there as it starts, so their share of the 128 KiB out-projection stream runs under the
+// attention instead of at the barrier (issuing the whole stream earlier, from every wave, stalls
+// the issuing waves' own work: measured).  One load site per wave keeps the registers unspilled.
+// Separate launches pass none.
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+
 // ------------------------------------------------------------------------------------------
 // KA: [emb_x + PE (layer 0)] + LN1 + QKV(head) + conv + self-attention      grid (heads, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T, int RT, int CP, typename FA>
-__device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned char* smem, KAPre<T, RT>& pre) {
+template <typename T, int RT, int CP, typename FA, typename H = NoHook>
+__device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned char* smem, KAPre<T, RT>& pre,
+                                         H&& hook = H()) {
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF, SY = 96 + 4;
   const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
@@ -238,14 +251,17 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
   STAMP(2);
   STAMP(3);
   fattn_any<T, CP>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
+  asm volatile("" ::: "memory");  // the hook's loads stay behind every store above (mk_sync counts them)
+  hook();
   STAMP_END(4);
 }
 
 // ------------------------------------------------------------------------------------------
 // KB: SA out-proj + residual + LN2 + cross-attn Q(head) + conv + cross-attention  (heads, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T, int RT, int CP, typename FA>
-__device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsigned char* smem, KBPre<T, RT>& pre) {
+template <typename T, int RT, int CP, typename FA, typename H = NoHook>
+__device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsigned char* smem, KBPre<T, RT>& pre,
+                                         H&& hook = H()) {
   using PL = Plan<T>;
   using AT = FAtt<T>;
   constexpr int KT = FD / Frag<T>::KF, SYQ = FDK + 4;
@@ -324,6 +340,8 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   bar_lds();
   STAMP(5);
   fattn_any<T, CP>(att, L, Lk, a.scale, (T*)a.o_ca + row0 * FD + h * FDK, FD);
+  asm volatile("" ::: "memory");
+  hook();
   STAMP_END(6);
   SPAN_END(span_slot);
 }
