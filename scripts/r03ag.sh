@@ -7,3 +7,6 @@ python -c "import json; d=json.load(open('gpurun_out/${T}_c2_bench.json')); prin
 timeout -k 10 300 python -u scripts/mega_stamps.py > gpurun_out/${T}_stamps.txt 2>&1
 echo "stamps rc=$?"
 grep -v amdgpu.ids gpurun_out/${T}_stamps.txt | tail -8
+timeout -k 10 300 python -u scripts/mega_arrivals.py > gpurun_out/${T}_arrivals.txt 2>&1
+echo "arrivals rc=$?"
+grep -v amdgpu.ids gpurun_out/${T}_arrivals.txt | tail -6

@@ -1750,16 +1750,21 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
   if (!c || !p || !avg_us || iters <= 0) return fail(c, GGD_ERR_ARG, "bad argument");
   HIP_TRY(c, hipSetDevice(c->device));
   if (what == 10 && np >= 1) {  // persistent-loop barrier stamps: {1} arm, {2} read, {0} off
-    const int NS = 2 * 17 * MEGA_STAMP_STEPS + 1;
+    // [0, B): workgroup 0's (done, passed) per barrier; [B]: its loop start; then raw 100 MHz
+    // real-time stamps of the arrival and exit of each of clip group 0's 8 workgroups at every
+    // barrier ([barrier][part][2], returned as ticks)
+    const int B = 2 * 17 * MEGA_STAMP_STEPS, NS = B + 1 + 16 * 17 * MEGA_STAMP_STEPS;
     if (p[0] == 1) {
       if (!c->mega_stamps) HIP_TRY(c, dalloc(c, &c->mega_stamps, NS * sizeof(unsigned long long)));
       HIP_TRY(c, hipMemset(c->mega_stamps, 0, NS * sizeof(unsigned long long)));
     }
-    if (p[0] == 2 && c->mega_stamps) {  // avg_us[j] = us from the loop start to stamp j
+    if (p[0] == 2 && c->mega_stamps) {  // avg_us[j] = us from the loop start to stamp j (j != B)
       HIP_TRY(c, hipStreamSynchronize(c->stream));
       std::vector<unsigned long long> h(NS);
       HIP_TRY(c, hipMemcpy(h.data(), c->mega_stamps, NS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-      for (int j = 0; j + 1 < NS; ++j) avg_us[j] = h[j] ? (double)(h[j] - h[NS - 1]) / 2400.0 : -1.0;
+      const int n_out = std::min(NS, np >= 2 ? p[1] : B);
+      for (int j = 0; j < n_out; ++j)
+        avg_us[j] = j > B ? (double)h[j] : j == B ? 0.0 : h[j] ? ((double)h[j] - (double)h[B]) / 2400.0 : -1.0;
     }
     if (p[0] == 0) c->mega_stamps = nullptr;  // stays owned by the ctx allocation list
     return GGD_OK;

@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(FT) kd_kernel(FusedArgs a) {
 template <typename T, int RT>
 __global__ void __launch_bounds__(FT) ke_kernel(FinalArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  KEPre<T, RT> pre = ke_pre<T, RT>(a, blockIdx.x);
+  KEPre<T, RT> pre = ke_pre<T, RT>(a, blockIdx.x, ltid() >> 6);
   pre.load(ltid() & 63);
   ke_phase<T, RT, CP_KERNEL>(a, blockIdx.x, blockIdx.y, a.do_update ? *a.step_counter : 0, smem, pre);
 }

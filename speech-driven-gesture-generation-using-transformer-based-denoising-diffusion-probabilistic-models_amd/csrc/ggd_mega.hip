@@ -117,11 +117,14 @@ __device__ int mk_role_xl(const MegaArgs& m, int nwg, int G) {
 // every store without waiting for those loads
 template <int CPV, int VMC = 0, typename F>
 __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part, unsigned epoch, int* status,
-                                        int* s_ok, unsigned long long* st, F&& prefetch) {
+                                        int* s_ok, unsigned long long* st, F&& prefetch,
+                                        unsigned long long* arr = nullptr) {
   static_assert(VMC >= 0 && VMC < 64, "vmcnt field");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");  // this wave's hand-off stores landed
   __syncthreads();
   if (st && threadIdx.x == 0) st[2 * (epoch - 1)] = __builtin_amdgcn_s_memtime();
+  // diag: arrival and exit of every workgroup of clip group 0, on the chip-wide 100 MHz clock
+  if (arr && threadIdx.x == 0) arr[2 * (8 * (epoch - 1) + part)] = __builtin_amdgcn_s_memrealtime();
   if constexpr (CPV == CP_XL) {
     if (threadIdx.x == 0) {
       const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
@@ -172,6 +175,7 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
   if (poller) prefetch();
   bar_lds();
   if (st && threadIdx.x == 0) st[2 * (epoch - 1) + 1] = __builtin_amdgcn_s_memtime();
+  if (arr && threadIdx.x == 0) arr[2 * (8 * (epoch - 1) + part) + 1] = __builtin_amdgcn_s_memrealtime();
   return *s_ok != 0;
 }
 
@@ -202,26 +206,27 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
   for (int k = 0; k < m.n_steps; ++k) {
     const int it = m.k0 + k;
     unsigned long long* st = (m.stamps && role == 0 && k < MEGA_STAMP_STEPS) ? m.stamps : nullptr;
+    unsigned long long* ar = (m.stamps && grp == 0 && k < MEGA_STAMP_STEPS) ? m.stamps + 2 * 17 * MEGA_STAMP_STEPS + 1 : nullptr;
     for (int li = 0; li < NL; ++li) {
       cfa_t f = fa0 + 4 * li;
       asm volatile("" : "+s"(f));  // per-layer arguments are re-read, not held across the loop
       // the out-projection fragments of KB / KC are issued by the hook behind the attention in front
       KBPre<T, RT> pb(f[1], wave);
       ka_phase<T, RT, CPV>(f[0], part, b, smem, pn, [&] { pb.load(lane); });
-      if (!mk_sync<CPV, KBPre<T, RT>::LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {})) return;
+      if (!mk_sync<CPV, KBPre<T, RT>::LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
       KCPre<T, RT> pc(f[2], part, wave);
       kb_phase<T, RT, CPV>(f[1], part, b, it, smem, pb, [&] { pc.load(lane); });
-      if (!mk_sync<CPV, KCPre<T, RT>::LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {})) return;
+      if (!mk_sync<CPV, KCPre<T, RT>::LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
       kc_phase<T, RT, CPV>(f[2], part, b, smem, pc);
       KDPre<T, RT> pd(f[3], part, wave);
-      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pd.load(lane); })) return;
+      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pd.load(lane); }, ar)) return;
       kd_phase<T, RT, CPV>(f[3], part, b, smem, pd);
-      pn = li + 1 < NL ? ka_pre<T, RT>(f[4], part, wave) : ke_pre<T, RT>(*fe, part);
-      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); })) return;
+      pn = li + 1 < NL ? ka_pre<T, RT>(f[4], part, wave) : ke_pre<T, RT>(*fe, part, wave);
+      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); }, ar)) return;
     }
     ke_phase<T, RT, CPV>(*fe, part, b, it, smem, pn);
     pn = ka_pre<T, RT>(fa0[0], part, wave);
-    if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); })) return;
+    if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); }, ar)) return;
   }
 }
 

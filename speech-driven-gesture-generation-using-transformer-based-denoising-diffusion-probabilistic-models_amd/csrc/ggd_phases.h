@@ -103,20 +103,27 @@ __device__ __forceinline__ void store_rows(float* dst, const float* Hs, int L, i
 // ------------------------------------------------------------------------------------------
 // one 16-column tile over K = 256 per wave: KA's QKV tile and KE's output tile share the type,
 // so the persistent loop carries ONE set of registers for "the next phase's tile" across layers
+// on = false: the wave computes nothing with the tile (KA: waves 6-7; KE: waves >= RT) and loads nothing
 template <typename T, int RT> struct Pre1 {
   WGemm<T, 1, FD / Frag<T>::KF, RT> g;
-  __device__ __forceinline__ Pre1(const void* w, int tile) : g(w, FD / Frag<T>::KF, 0) { g.tiles[0] = tile; }
-  __device__ __forceinline__ void load(int lane) { g.load(0, lane); }
+  bool on;
+  __device__ __forceinline__ Pre1(const void* w, int tile, bool on_) : g(w, FD / Frag<T>::KF, 0), on(on_) {
+    g.tiles[0] = tile;
+  }
+  __device__ __forceinline__ void load(int lane) {
+    if (on) g.load(0, lane);
+  }
+  __device__ __forceinline__ int loads() const { return on ? decltype(g)::G : 0; }  // vector loads per load()
 };
 template <typename T, int RT> using KAPre = Pre1<T, RT>;
 template <typename T, int RT> using KEPre = Pre1<T, RT>;
 template <typename T, int RT, typename FA>  // QKV of head h: waves 0-5 one tile each
 __device__ __forceinline__ KAPre<T, RT> ka_pre(const FA& a, int h, int wave) {
-  return KAPre<T, RT>(a.w.qkv, h * 6 + min(wave, 5));
+  return KAPre<T, RT>(a.w.qkv, h * 6 + min(wave, 5), wave < 6);
 }
-template <typename T, int RT, typename FA>  // output channel tile p
-__device__ __forceinline__ KEPre<T, RT> ke_pre(const FA& a, int p) {
-  return KEPre<T, RT>(a.w_out, p);
+template <typename T, int RT, typename FA>  // output channel tile p (waves 0 .. RT-1, one row tile each)
+__device__ __forceinline__ KEPre<T, RT> ke_pre(const FA& a, int p, int wave) {
+  return KEPre<T, RT>(a.w_out, p, wave < RT);
 }
 template <typename T, int RT> struct KBPre {  // SA out-projection, all 16 tiles (2 per wave)
   WGemm<T, 2, FD / Frag<T>::KF, RT> go;
