@@ -280,6 +280,14 @@ struct WGemm {
         wb[j][k] = make_uint4(v.x, v.y, v.z, v.w);
       }
   }
+  __device__ __forceinline__ void load_tile(int j, int lane) {  // group 0 of tile j only
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+      const u32x4 v = ggd::G((const u32x4*)W)[((size_t)tiles[j] * kt_total + k0 + k) * 64 + lane];
+      wb[j][k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  }
   // group 0 must have been loaded; tiles j >= nj_on are skipped (wave-uniform).  bf16: the A
   // fragments of k step k + 1 are read from LDS before the MFMAs of step k issue, so the LDS
   // latency overlaps the matrix work (one wave per SIMD hides nothing on its own).

@@ -212,11 +212,11 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
       asm volatile("" : "+s"(f));  // per-layer arguments are re-read, not held across the loop
       // the out-projection fragments of KB / KC are issued by the hook behind the attention in front
       KBPre<T, RT> pb(f[1], wave);
-      ka_phase<T, RT, CPV>(f[0], part, b, smem, pn, [&] { pb.load(lane); });
-      if (!mk_sync<CPV, KBPre<T, RT>::LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
+      ka_phase<T, RT, CPV>(f[0], part, b, smem, pn, [&] { pb.load_tile(1, lane); }, [&] { pb.load_tile(0, lane); });
+      if (!mk_sync<CPV, KBPre<T, RT>::TILE_LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
       KCPre<T, RT> pc(f[2], part, wave);
-      kb_phase<T, RT, CPV>(f[1], part, b, it, smem, pb, [&] { pc.load(lane); });
-      if (!mk_sync<CPV, KCPre<T, RT>::LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
+      kb_phase<T, RT, CPV>(f[1], part, b, it, smem, pb, [&] { pc.load_tile(1, lane); }, [&] { pc.load_tile(0, lane); });
+      if (!mk_sync<CPV, KCPre<T, RT>::TILE_LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
       kc_phase<T, RT, CPV>(f[2], part, b, smem, pc);
       KDPre<T, RT> pd(f[3], part, wave);
       if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pd.load(lane); }, ar)) return;

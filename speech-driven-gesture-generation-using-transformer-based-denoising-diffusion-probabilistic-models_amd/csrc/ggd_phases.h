@@ -133,7 +133,9 @@ template <typename T, int RT> struct KBPre {  // SA out-projection, all 16 tiles
     go.tiles[1] = 2 * wave + 1;
   }
   __device__ __forceinline__ void load(int lane) { go.load(0, lane); }
+  __device__ __forceinline__ void load_tile(int j, int lane) { go.load_tile(j, lane); }
   static constexpr int LOADS = 2 * decltype(go)::G;  // vector loads per load()
+  static constexpr int TILE_LOADS = decltype(go)::G;
 };
 template <typename T, int RT> struct KCPre {  // CA out-projection (the FFN-up tile loads in the phase)
   WGemm<T, 2, FD / Frag<T>::KF, RT> go;
@@ -144,7 +146,9 @@ template <typename T, int RT> struct KCPre {  // CA out-projection (the FFN-up t
     go.tiles[1] = 2 * wave + 1;
   }
   __device__ __forceinline__ void load(int lane) { go.load(0, lane); }
+  __device__ __forceinline__ void load_tile(int j, int lane) { go.load_tile(j, lane); }
   static constexpr int LOADS = 2 * decltype(go)::G;
+  static constexpr int TILE_LOADS = decltype(go)::G;
 };
 template <typename T, int RT> struct KDPre {  // the FFN-down column reduce streams no weights
   template <typename FA>
@@ -165,9 +169,9 @@ struct NoHook {
 // ------------------------------------------------------------------------------------------
 // KA: [emb_x + PE (layer 0)] + LN1 + QKV(head) + conv + self-attention      grid (heads, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T, int RT, int CP, typename FA, typename H = NoHook>
+template <typename T, int RT, int CP, typename FA, typename H = NoHook, typename H0 = NoHook>
 __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned char* smem, KAPre<T, RT>& pre,
-                                         H&& hook = H()) {
+                                         H&& hook = H(), H0&& hook0 = H0()) {
   using PL = Plan<T>;
   constexpr int KT = FD / Frag<T>::KF, SY = 96 + 4;
   const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
@@ -257,6 +261,7 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
   bar_lds();
   STAMP(2);
   STAMP(3);
+  hook0();  // before the attention: all waves (the attention waves issue only part of their stream here)
   fattn_any<T, CP>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
   asm volatile("" ::: "memory");  // the hook's loads stay behind every store above (mk_sync counts them)
   hook();
@@ -266,9 +271,9 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
 // ------------------------------------------------------------------------------------------
 // KB: SA out-proj + residual + LN2 + cross-attn Q(head) + conv + cross-attention  (heads, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T, int RT, int CP, typename FA, typename H = NoHook>
+template <typename T, int RT, int CP, typename FA, typename H = NoHook, typename H0 = NoHook>
 __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsigned char* smem, KBPre<T, RT>& pre,
-                                         H&& hook = H()) {
+                                         H&& hook = H(), H0&& hook0 = H0()) {
   using PL = Plan<T>;
   using AT = FAtt<T>;
   constexpr int KT = FD / Frag<T>::KF, SYQ = FDK + 4;
@@ -346,6 +351,7 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   if (wave == FT / 64 - 1) fx.store<T>(att, ck, cv, Lk, lane);
   bar_lds();
   STAMP(5);
+  hook0();
   fattn_any<T, CP>(att, L, Lk, a.scale, (T*)a.o_ca + row0 * FD + h * FDK, FD);
   asm volatile("" ::: "memory");
   hook();
