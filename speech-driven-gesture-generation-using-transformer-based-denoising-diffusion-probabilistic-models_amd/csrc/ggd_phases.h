@@ -516,11 +516,16 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
 #pragma unroll
   for (int k = 0; k < KT; ++k) go.wb[0][k] = pre.g.wb[0][k];
   const float4 bo = ld_f4(a.b_out + p * 16 + 4 * g4);
-  // the thread's quad: elements e0 + 4 ut .. + 3 (issued now, consumed after the GEMM).  The quads
+  // the thread's quad: elements e0 + 4 qi .. + 3 (issued now, consumed after the GEMM).  The quads
   // live on the waves the out-projection leaves idle (ut = tid - 64 RT; 64 (8 - RT) >= 4 L / 4), so
-  // their Philox normals are drawn while waves 0 .. RT-1 run the GEMM
+  // their Philox normals are drawn while waves 0 .. RT-1 run the GEMM.  With L % 4 == 0 a quad is 4
+  // frames of one channel and 16 consecutive threads take the block's 16 channels at the same
+  // frames (qi = channel (L / 4) + frame quad): each x store of a wave covers 4 frame rows x 64 bytes
+  // instead of 64 scattered rows.  The Philox counter stays the quad's index in (C, L) order.
   const int ut = tid - 64 * RT;
-  const bool upd = a.do_update && ut >= 0 && 4 * ut < ne;
+  const bool q4 = (L & 3) == 0;
+  const int qi = q4 ? (ut & 15) * (L >> 2) + (ut >> 4) : ut;
+  const bool upd = a.do_update && ut >= 0 && (q4 ? (ut & 15) < cn && (ut >> 4) < (L >> 2) : 4 * ut < ne);
   StepRec rec{};
   float xq[4] = {0.f, 0.f, 0.f, 0.f}, zq[4] = {0.f, 0.f, 0.f, 0.f};
   float mq[4] = {0.f, 0.f, 0.f, 0.f}, pq[4] = {0.f, 0.f, 0.f, 0.f}, tq[4] = {0.f, 0.f, 0.f, 0.f};
@@ -529,7 +534,7 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
   const size_t plane = (size_t)a.n * LC;
   if (a.do_update) {
     rec = ld_rec(a.steps + k);
-    const int e = e0 + 4 * max(ut, 0);  // tail threads (no valid element) only load clamped addresses
+    const int e = min(e0 + 4 * max(qi, 0), e0 + max(ne, 1) - 1);  // tail threads (no valid element) load clamped addresses
     cc0 = e / L;
     l0 = e - cc0 * L;
     int cc = cc0, l = l0;
@@ -558,7 +563,7 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
         make_float4(acc[0][0][0] + bo.x, acc[0][0][1] + bo.y, acc[0][0][2] + bo.z, acc[0][0][3] + bo.w);
   } else if (upd && !a.noise) {
     philox_normal4(((uint64_t)rec.seed_hi << 32) | rec.seed_lo, rec.clip_offset + (uint32_t)b, (uint32_t)rec.i,
-                   TAG_STEP, (uint32_t)((e0 >> 2) + ut), zq);
+                   TAG_STEP, (uint32_t)((e0 >> 2) + qi), zq);
   }
   bar_lds();
   STAMP(2);
@@ -567,7 +572,7 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
     int cc = cc0, l = l0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int e = e0 + 4 * ut + u;
+      const int e = e0 + 4 * qi + u;
       if (e < e0 + ne) {
         const float ev = E[l * SE + (cc - c0)];
         const UpdOut o = upd_math(rec, a.alg, xq[u], ev, false, 0.f, inp, mq[u], pq[u], tq[u], zq[u]);
