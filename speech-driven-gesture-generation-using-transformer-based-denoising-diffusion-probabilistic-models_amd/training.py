@@ -2,7 +2,9 @@
 
 Mirrors the reference's training step (models/trainer.py:131-248):
   Trainer._compute_loss: x_start = poses^T, noise ~ N(0, 1), t ~ UniformSampler (resample.py:60-68),
-      diffusion.training_losses (gaussian_diffusion.py:531-569) -> mse per clip -> mean
+      diffusion.training_losses (gaussian_diffusion.py:531-569) -> mse per clip -> mean, plus the
+      configured speed losses on pred_x_start (speed_loss / speed_l1_loss / speed_constraint_loss,
+      trainer.py:172-193; speed_losses below)
   Trainer._train_step: zero_grad, backward, compute_grad_norm (trainer.py:341-349), optional
       clip_grad_norm_ / clip_grad_value_, optimizer.step (AdamW, model_creation.py:176-178),
       lr_scheduler.step (lr_scheduler.py: ConstantLR / NoamLR "noamxf" / NoamDecayLR "noam")
@@ -707,8 +709,9 @@ def q_sample(diffusion, x_start, t, noise):
 
 
 def training_losses(diffusion, model, x_start, t, model_kwargs, noise=None):
-    """GaussianDiffusion.training_losses (gaussian_diffusion.py:531-569): returns mse (N,) with the
-    autograd graph to the parameters, and eps / x_t / pred_x_start / model_mean (detached)."""
+    """GaussianDiffusion.training_losses (gaussian_diffusion.py:531-569): returns mse (N,), eps and
+    pred_x_start with the autograd graph to the parameters (the reference's speed losses,
+    trainer.py:172-193, differentiate through pred_x_start), x_t and model_mean (detached)."""
     x_start = x_start.contiguous().float()
     if noise is None:
         noise = th.randn_like(x_start)
@@ -717,13 +720,50 @@ def training_losses(diffusion, model, x_start, t, model_kwargs, noise=None):
     eps = model(x_t, t, z=model_kwargs.get("speech_tokens"), wav=model_kwargs.get("wav"))
     assert eps.shape == noise.shape == x_start.shape
     mse = _DiffusionMSE.apply(eps, noise)
+    idx = t.cpu().numpy()
+    ext = lambda arr: th.from_numpy(arr[idx]).float().to(x_t.device).reshape(-1, 1, 1)
+    # _predict_xstart_from_eps (gaussian_diffusion.py:287-292), on the graph
+    x0 = ext(diffusion.sqrt_recip_alphas_cumprod) * x_t - ext(diffusion.sqrt_recipm1_alphas_cumprod) * eps
     with th.no_grad():
-        idx = t.cpu().numpy()
-        ext = lambda arr: th.from_numpy(arr[idx]).float().to(x_t.device).reshape(-1, 1, 1)
-        e = eps.detach()
-        x0 = ext(diffusion.sqrt_recip_alphas_cumprod) * x_t - ext(diffusion.sqrt_recipm1_alphas_cumprod) * e
-        mean = ext(diffusion.posterior_mean_coef1) * x0 + ext(diffusion.posterior_mean_coef2) * x_t
-    return {"mse": mse, "eps": e, "x_t": x_t, "pred_x_start": x0, "model_mean": mean}
+        mean = ext(diffusion.posterior_mean_coef1) * x0.detach() + ext(diffusion.posterior_mean_coef2) * x_t
+    return {"mse": mse, "eps": eps, "x_t": x_t, "pred_x_start": x0, "model_mean": mean}
+
+
+def wasserstein_distance_1d(xs, ys, eps=1e-12):
+    """trainer.py:310-322: the 2-Wasserstein distance between the Gaussians fitted to xs and ys
+    (unbiased variances), floored at sqrt(eps)."""
+    assert xs.dim() == 1 and ys.dim() == 1, "must be 1-dimensional"
+    mu1, var1, mu2, var2 = xs.mean(), xs.var(), ys.mean(), ys.var()
+    dist_quad = (mu1 - mu2) ** 2 + (var1 + var2 - 2 * th.sqrt(var1.sqrt() * var2 * var1.sqrt()))
+    if th.any(th.isnan(dist_quad)):
+        raise ValueError("[Error] Nan value in loss")
+    return th.maximum(dist_quad, th.zeros_like(dist_quad).fill_(eps)).sqrt()
+
+
+SPEED_LOSSES = ("speed_loss", "speed_l1_loss", "speed_constraint_loss")
+
+
+def speed_losses(x_start, pred_x_start, loss_params):
+    """The extra loss terms of Trainer._compute_loss (trainer.py:172-196) on (N, C, T) poses:
+    {term name: loss}, and their weighted sum.  An unknown name raises ValueError, as there."""
+    terms, total = {}, 0.0
+    for name, weight in (loss_params or {}).items():
+        if name == "speed_constraint_loss":
+            loss = th.abs(th.diff(pred_x_start, dim=2)).mean()
+            terms["speed_constraint"] = loss
+        elif name in ("speed_loss", "speed_l1_loss"):
+            speed = th.abs(th.diff(x_start, dim=2)).mean([0, 1])            # (T-1,)
+            speed_pred = th.abs(th.diff(pred_x_start, dim=2)).mean([0, 1])  # (T-1,)
+            if name == "speed_loss":
+                loss = wasserstein_distance_1d(speed, speed_pred)
+                terms["speed"] = loss
+            else:
+                loss = F.smooth_l1_loss(speed_pred, speed)
+                terms["speed_l1"] = loss
+        else:
+            raise ValueError(f"Unsupported loss: {name}")
+        total = total + weight * loss
+    return terms, total
 
 
 # ------------------------------------------------------------------------------------------
@@ -942,8 +982,10 @@ class Trainer:
 
     def __init__(self, model, diffusion, speech_encoder, lr=1e-3, weight_decay=None, scheduler_params=None,
                  grad_norm_clip_value=None, grad_clip_value=None, loss_params=None, seed=0):
-        if loss_params:
-            raise ValueError("extra losses (speed_loss, ...) are not built; beat-ours uses none")
+        for name in (loss_params or {}):
+            if name not in SPEED_LOSSES:
+                raise ValueError(f"Unsupported loss: {name}")
+        self.loss_params = dict(loss_params or {})
         broadcast_parameters(model)
         self.model = model
         self.diffusion = diffusion
@@ -970,8 +1012,9 @@ class Trainer:
         if t is None:
             t, _ = self.schedule_sampler.sample(poses.shape[0], self.model.device, self.rng)
         out = training_losses(self.diffusion, self.model, x_start, t, kw, noise=noise)
-        loss = out["mse"].mean()
-        return {"loss": loss, "denoise": loss}
+        denoise = out["mse"].mean()
+        terms, extra = speed_losses(x_start, out["pred_x_start"], self.loss_params)
+        return {"loss": denoise + extra, "denoise": denoise, **terms}
 
     def step(self, batch, noise=None, t=None):
         """zero_grad -> (buffer broadcast) -> loss -> backward -> all-reduce -> grad norm ->

@@ -189,6 +189,47 @@ def test_training_step_gradients_match_oracle(tr, train_setup):
     assert worst[0][0] <= 2e-3, worst[:6]
 
 
+def test_speed_loss_gradients_match_oracle(tr, train_setup):
+    """mse + the reference's speed losses (trainer.py:172-193) through pred_x_start: gradients of the
+    HIP model vs the oracle's torch autograd on the same loss, and Trainer accepts the terms."""
+    arch, sd, diffusion, n, g, z = train_setup
+    params = {"speed_loss": 0.5, "speed_l1_loss": 1.0, "speed_constraint_loss": 0.1}
+    model = tr.TrainableModel(arch, sd, "cuda")
+    x0 = th.randn(n, D_POSE, L, generator=g)
+    t = th.tensor([640, 201, 37])
+    noise = th.randn(n, D_POSE, L, generator=g)
+    model.zero_grad()
+    out = tr.training_losses(diffusion, model, x0.cuda(), t.cuda(), {"speech_tokens": z}, noise=noise.cuda())
+    terms, extra = tr.speed_losses(x0.cuda(), out["pred_x_start"], params)
+    loss = out["mse"].mean() + extra
+    loss.backward()
+    names = list(model.params)
+    sd_ref = {k: v.detach().float().clone() for k, v in sd.items()}
+    for k in names:
+        sd_ref[k].requires_grad_(True)
+    idx = t.numpy()
+    ext = lambda a: th.from_numpy(a[idx]).float().reshape(-1, 1, 1)
+    x_t = ext(diffusion.sqrt_alphas_cumprod) * x0 + ext(diffusion.sqrt_one_minus_alphas_cumprod) * noise
+    cfg = oracle_cfg(arch)
+    speech = ref_denoiser.speech_memory(sd_ref, cfg, tuple(a.cpu() for a in z))
+    eps = ref_denoiser.denoise(sd_ref, cfg, x_t, t, speech=speech)
+    px0 = ext(diffusion.sqrt_recip_alphas_cumprod) * x_t - ext(diffusion.sqrt_recipm1_alphas_cumprod) * eps
+    want_terms, want_extra = tr.speed_losses(x0, px0, params)
+    want = ((eps - noise) ** 2).mean(dim=(1, 2)).mean() + want_extra
+    want.backward()
+    for k in ("speed", "speed_l1", "speed_constraint"):
+        assert abs(terms[k].item() - want_terms[k].item()) <= 1e-4 * abs(want_terms[k].item()) + 1e-7, k
+    assert abs(loss.item() - want.item()) <= 1e-5 * want.item(), (loss.item(), want.item())
+    floor = 1e-4 * max(sd_ref[k].grad.abs().max().item() for k in names)
+    worst = max(((model.params[k].grad.cpu() - sd_ref[k].grad).abs().max().item()
+                 / max(sd_ref[k].grad.abs().max().item(), floor), k) for k in names)
+    print("\nworst gradient error with the speed losses:", worst)
+    assert worst[0] <= 2e-3, worst
+    trainer = tr.Trainer(model, diffusion, speech_encoder=None, lr=1e-4, loss_params=params)
+    res = trainer.step({"pose": x0.transpose(1, 2).cuda(), "speech_tokens": z}, noise=noise.cuda(), t=t.cuda())
+    assert np.isfinite(res["loss"]) and res["loss"] > 0
+
+
 def test_trainer_steps_match_torch_adamw(tr, train_setup):
     arch, sd, diffusion, n, g, z = train_setup
     sched = {"type": "noamxf", "warmup_steps": "4k", "d_model": 256}

@@ -236,3 +236,32 @@ def test_noam_decay_has_no_floor():
     for _ in range(1000):
         s.step()
     assert o.param_groups[0]["lr"] == pytest.approx(10 ** 0.5 * 1000 ** -0.5)
+
+
+def test_speed_losses_follow_trainer_py():
+    """trainer.py:172-193 and wasserstein_distance_1d (trainer.py:310-322), checked against the
+    closed forms in float64 numpy; gradients reach pred_x_start; unknown names raise."""
+    tr = _training()
+    g = th.Generator().manual_seed(4)
+    x = th.randn(3, 5, 12, generator=g, dtype=th.float64)
+    p = (x + 0.3 * th.randn(3, 5, 12, generator=g, dtype=th.float64)).requires_grad_(True)
+    params = {"speed_loss": 0.5, "speed_l1_loss": 2.0, "speed_constraint_loss": 0.25}
+    terms, total = tr.speed_losses(x, p, params)
+    xn, pn = x.numpy(), p.detach().numpy()
+    sp, sq = np.abs(np.diff(xn, axis=2)).mean((0, 1)), np.abs(np.diff(pn, axis=2)).mean((0, 1))
+    v1, v2 = sp.var(ddof=1), sq.var(ddof=1)
+    w2 = np.sqrt(max((sp.mean() - sq.mean()) ** 2 + v1 + v2 - 2 * np.sqrt(np.sqrt(v1) * v2 * np.sqrt(v1)), 1e-12))
+    d = sq - sp
+    l1 = np.where(np.abs(d) < 1.0, 0.5 * d * d, np.abs(d) - 0.5).mean()
+    sc = np.abs(np.diff(pn, axis=2)).mean()
+    assert abs(terms["speed"].item() - w2) <= 1e-12
+    assert abs(terms["speed_l1"].item() - l1) <= 1e-12
+    assert abs(terms["speed_constraint"].item() - sc) <= 1e-12
+    assert abs(total.item() - (0.5 * w2 + 2.0 * l1 + 0.25 * sc)) <= 1e-12
+    total.backward()
+    assert p.grad is not None and p.grad.abs().sum().item() > 0
+    with pytest.raises(ValueError, match="Unsupported loss"):
+        tr.speed_losses(x, p, {"foot_contact_loss": 1.0})
+    # no extra losses: nothing added
+    terms, total = tr.speed_losses(x, p, None)
+    assert terms == {} and total == 0.0
