@@ -85,3 +85,11 @@ def test_self_launch_rehearsal_matches_single_rank():
         assert res["rehearsal"] and res["world"] == n and res["global_batch"] == 2 * n
         assert res["shape"] == [2 * n, 123, 40]
         assert res["first"][:2] == one["first"]  # global clips 0, 1: same wav rows, same noise keys
+
+
+def test_headline_pmc_summary_matches_the_kernel_sources():
+    """The default (driver-run) C2 line prices its roofline traffic from a PMC summary taken on THIS
+    csrc/ tree: a kernel change has to come with a fresh summary (scripts/pmc_all.sh)."""
+    tr = bench.pmc_traffic("mk_kernel", "c2")
+    assert tr is not None and not tr.get("stale"), tr
+    assert tr["bytes_per_launch"] > 0
