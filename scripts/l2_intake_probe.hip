@@ -49,6 +49,48 @@ __global__ void __launch_bounds__(NT) probe(const uint4* src, int iters, int own
   if (acc == 0x12345678u) sink[blockIdx.x] = acc;  // keeps the loads alive
 }
 
+// the same stream through LDS-DMA (global_load_lds_dwordx4: 16 B per lane straight into LDS, no
+// result registers); D loads per wave in flight, then s_waitcnt vmcnt(0)
+typedef __attribute__((address_space(3))) void lds_void;
+template <int D>
+__global__ void __launch_bounds__(NT) probe_lds(const uint4* src, int iters, int own, unsigned* sink) {
+  __shared__ __attribute__((aligned(16))) unsigned char buf[8 * 16 * 1024];  // 16 KiB per wave
+  const uint4* base = src + (own ? (size_t)blockIdx.x * REGION_U4 : 0);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int piece = wave * 64;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      __builtin_amdgcn_global_load_lds((const void*)(base + ((piece + d * NT) % REGION_U4) + lane),
+                                       (lds_void*)(buf + wave * 16384 + (d & 15) * 1024), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    piece = (piece + D * NT) % REGION_U4;
+  }
+  __syncthreads();
+  if (buf[tid] == 0x5a) sink[blockIdx.x] = buf[tid + 1];
+}
+
+template <int D>
+static void run_lds(const uint4* src, unsigned* sink, int nwg) {
+  const int iters = (int)((16u << 20) / ((size_t)NT * 16 * D));
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  hipLaunchKernelGGL(probe_lds<D>, dim3(nwg), dim3(NT), 0, 0, src, 8, 1, sink);
+  CHECK(hipEventRecord(a));
+  hipLaunchKernelGGL(probe_lds<D>, dim3(nwg), dim3(NT), 0, 0, src, iters, 1, sink);
+  CHECK(hipGetLastError());
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  const double bytes = (double)nwg * NT * 16.0 * D * iters;
+  printf("%3d WG lds-dma D=%2d  loads in flight per CU %3d KiB  per-CU %6.1f GB/s  chip %6.2f TB/s  (%.2f ms)\n",
+         nwg, D, 8 * D, bytes / nwg / (ms * 1e-3) / 1e9, bytes / (ms * 1e-3) / 1e12, ms);
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+}
+
 template <int D>
 static void run(const uint4* src, unsigned* sink, int nwg, int own) {
   // ~64 MiB per workgroup in total
@@ -97,6 +139,10 @@ int main() {
   run<8>(src, sink, 32, 1);
   run<8>(src, sink, 64, 1);
   run<8>(src, sink, 128, 1);
+  run_lds<4>(src, sink, nwg);
+  run_lds<8>(src, sink, nwg);
+  run_lds<16>(src, sink, nwg);
+  run_lds<8>(src, sink, 8);
   CHECK(hipFree(src));
   CHECK(hipFree(sink));
   return 0;
