@@ -196,8 +196,11 @@ enum {
                                         row-block chains (ggd_chain.hip) */
   GGD_ROUTE_ATTN_QSPLIT = 6,         /* 1: clips of >= 96 frames on the query-split attention kernel
                                         instead of the whole-clip kernel (ggd_attn.hip) */
-  GGD_ROUTE_LONG_LOOP = 7            /* 1: never the long-clip persistent loop (ggd_long.hip): every
+  GGD_ROUTE_LONG_LOOP = 7,           /* 1: never the long-clip persistent loop (ggd_long.hip): every
                                         step on launches (chains + whole-clip attention) */
+  GGD_ROUTE_SIMULATE_UNRESIDENT = 8  /* test hook, 1: the clip-group and clip-pair loops report status 2
+                                        ("workgroups never all resident") without running, so the
+                                        device-gated one-workgroup-per-clip fallback runs the clips */
 };
 int ggd_set_route(ggd_ctx* ctx, int32_t knob, int32_t value);
 enum {
@@ -208,7 +211,9 @@ enum {
   GGD_INFO_WT_RERUNS = 4,            /* last ggd_sample: clip-group launches re-run write-through */
   GGD_INFO_CHAIN_AVAILABLE = 5,      /* 1 when the generic one-way route runs as row-block chains */
   GGD_INFO_LONG_LAUNCHES = 6,        /* last ggd_sample: long-clip loop launches (0: another route) */
-  GGD_INFO_CLIP_ATTN_LAUNCHES = 7    /* running count of whole-clip attention launches (generic routes) */
+  GGD_INFO_CLIP_ATTN_LAUNCHES = 7,   /* running count of whole-clip attention launches (generic routes) */
+  GGD_INFO_GATED_FALLBACKS = 8       /* last settled ggd_sample: chunks (clip-group loop) or batches
+                                        (clip pairs) the device-gated fallback loop ran instead */
 };
 int ggd_route_info(ggd_ctx* ctx, int32_t what, double* out);
 

@@ -42,8 +42,10 @@ __global__ void __launch_bounds__(NT) probe(const uint4* src, int iters, int own
     for (int d = 0; d < D; ++d) {
       v[d] = base[(piece + d * NT) % REGION_U4];
     }
+    // every component is consumed: with only .x / .w used the compiler narrows each 16-byte load
+    // into two global_load_dword (the round-3 figures of this probe measured THAT, not dwordx4)
 #pragma unroll
-    for (int d = 0; d < D; ++d) acc ^= v[d].x ^ v[d].w;
+    for (int d = 0; d < D; ++d) acc ^= (v[d].x ^ v[d].y) ^ (v[d].z ^ v[d].w);
     piece = (piece + D * NT) % REGION_U4;
   }
   if (acc == 0x12345678u) sink[blockIdx.x] = acc;  // keeps the loads alive
@@ -130,6 +132,7 @@ int main() {
     run<4>(src, sink, nwg, own);
     run<8>(src, sink, nwg, own);
     run<12>(src, sink, nwg, own);
+    run<16>(src, sink, nwg, own);
   }
   // few CUs streaming (no contention for the XCD's L2 bandwidth): 8 workgroups, one per XCD
   // under the usual round-robin dispatch, and 32 (4 per XCD)

@@ -191,12 +191,15 @@ struct ggd_ctx {
     int kind = 0;            // 1 clip-group loop (XCD-local words, then the gated write-through re-runs), 4 clip pairs
     int chunks = 0;
     bool xl = false;
+    bool fb = false;         // a device-gated fallback launch stands behind the loop (status 2 is then no error)
   };
   std::vector<Pending> pend;           // ring
   size_t pend_head = 0, pend_count = 0;
   int sticky = 0;                      // 0, or the ggd_status of a failed earlier loop
   std::string sticky_msg;
   bool mega_none_ran = false;          // settled clip-group check: every chunk reported 2 (nothing ran)
+  int gated_ran = 0;                   // settled check: chunks the device-gated fallback loop ran instead
+  bool sim_unresident = false;         // GGD_ROUTE_SIMULATE_UNRESIDENT
 
   // Per-call uploads (step records, the loop's argument blocks): from pageable memory a small
   // hipMemcpyAsync is staged by the runtime in pieces (several blit kernels and host waits per
@@ -236,6 +239,7 @@ constexpr size_t PEND_RING = 8;
 
 // Read the status words of a finished deferred check (see ggd_ctx::Pending).
 void settle(ggd_ctx* c, const ggd_ctx::Pending& p) {
+  c->gated_ran = 0;
   if (p.kind == 1) {
     int worst = 0, unrun = 0;
     c->mega_xl_launches = 0;
@@ -248,6 +252,11 @@ void settle(ggd_ctx* c, const ggd_ctx::Pending& p) {
       } else if (p.xl) {
         ++c->mega_xl_launches;
       }
+      if (st == 2 && p.fb) {  // never all resident: the gated one-workgroup-per-clip loop ran the chunk
+        ++c->mega_fallbacks;
+        ++c->gated_ran;
+        st = 0;
+      }
       worst = std::max(worst, st);
       unrun += st == 2 ? 1 : 0;
     }
@@ -259,7 +268,8 @@ void settle(ggd_ctx* c, const ggd_ctx::Pending& p) {
                                  : "persistent loop (earlier ggd_sample): a clip-group barrier timed out";
     }
   } else if (p.kind == 4) {
-    if (p.host[0] && !c->sticky) {
+    if (p.host[0] == 2 && p.fb) c->gated_ran = 1;
+    if (p.host[0] && !(p.host[0] == 2 && p.fb) && !c->sticky) {
       c->sticky = GGD_ERR_HIP;
       c->sticky_msg = p.host[0] == 2 ? "clip-pair loop (earlier ggd_sample): workgroups were not all resident"
                                      : "clip-pair loop (earlier ggd_sample): a pair barrier timed out";
@@ -285,8 +295,20 @@ int poll_pending(ggd_ctx* c, bool wait) {
   return GGD_OK;
 }
 
+// Settle every deferred check except the newest (blocking): the checks of earlier calls.
+int poll_pending_before_last(ggd_ctx* c) {
+  while (c->pend_count > 1) {
+    ggd_ctx::Pending& p = c->pend[c->pend_head];
+    HIP_TRY(c, hipEventSynchronize(p.ev));
+    settle(c, p);
+    c->pend_head = (c->pend_head + 1) % PEND_RING;
+    --c->pend_count;
+  }
+  return GGD_OK;
+}
+
 // Queue a deferred check of `nwords` device status words (stream-ordered behind the loop).
-int defer_check(ggd_ctx* c, const int* dev_words, int nwords, int kind, int chunks, bool xl, hipStream_t s) {
+int defer_check(ggd_ctx* c, const int* dev_words, int nwords, int kind, int chunks, bool xl, bool fb, hipStream_t s) {
   if (c->pend.empty()) {
     c->pend.resize(PEND_RING);
     for (auto& p : c->pend) {
@@ -305,6 +327,7 @@ int defer_check(ggd_ctx* c, const int* dev_words, int nwords, int kind, int chun
   p.kind = kind;
   p.chunks = chunks;
   p.xl = xl;
+  p.fb = fb;
   HIP_TRY(c, hipMemcpyAsync(p.host, dev_words, sizeof(int) * nwords, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipEventRecord(p.ev, s));
   ++c->pend_count;
@@ -1657,6 +1680,10 @@ int ggd_kernel_time(ggd_ctx* c, int32_t which, double* avg_us, int64_t* launches
     float ms = 0;
     HIP_TRY(c, hipEventElapsedTime(&ms, c->prof.ev[0], c->prof.ev[1]));
     c->prof_avg_us = ms * 1000.0 / std::max(1, c->prof_lazy_div);
+    int r = poll_pending(c, true);
+    if (r) return r;
+    if (c->gated_ran)  // the timed span holds a loop that never ran; its untimed fallback made the result
+      return fail(c, GGD_ERR_STATE, "profiled loop did not run (workgroups not all resident): no kernel time");
   }
   if (c->span_pending) {  // launch span = latest workgroup end - earliest workgroup start
     const size_t n = c->span_pending, wg = c->span_wg;
@@ -1719,6 +1746,9 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
     case GGD_ROUTE_LONG_LOOP:       // 1: never the long-clip persistent loop
       c->long_off = value != 0;
       return GGD_OK;
+    case GGD_ROUTE_SIMULATE_UNRESIDENT:  // test hook: co-resident loops report status 2, run nothing
+      c->sim_unresident = value != 0;
+      return GGD_OK;
     default:
       break;
   }
@@ -1727,7 +1757,8 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
 
 int ggd_route_info(ggd_ctx* c, int32_t what, double* out) {
   if (!c || !out) return GGD_ERR_ARG;
-  if (what == GGD_INFO_XL_LAUNCHES || what == GGD_INFO_WT_RERUNS) {  // counters of a deferred check
+  if (what == GGD_INFO_XL_LAUNCHES || what == GGD_INFO_WT_RERUNS || what == GGD_INFO_GATED_FALLBACKS) {
+    // counters of a deferred check
     HIP_TRY(c, hipSetDevice(c->device));
     int r = poll_pending(c, true);
     if (r) return r;
@@ -1741,6 +1772,7 @@ int ggd_route_info(ggd_ctx* c, int32_t what, double* out) {
     case GGD_INFO_CHAIN_AVAILABLE: *out = c->chain ? 1.0 : 0.0; return GGD_OK;
     case GGD_INFO_LONG_LAUNCHES: *out = c->long_launches; return GGD_OK;
     case GGD_INFO_CLIP_ATTN_LAUNCHES: *out = (double)c->clip_attn_launches; return GGD_OK;
+    case GGD_INFO_GATED_FALLBACKS: *out = (double)c->gated_ran; return GGD_OK;
     default: return fail(c, GGD_ERR_ARG, "unknown route info");
   }
 }
@@ -2187,6 +2219,55 @@ int run_long(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
   return GGD_OK;
 }
 
+// Arguments of the one-workgroup-per-clip loop (ggd_persist.hip) for this sampling call.
+PersistArgs persist_args(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
+  const ggd_desc& D = c->desc;
+  PersistArgs p{};
+  p.layers = c->d_layers;
+  p.n_layers = D.n_layers;
+  p.n = a.n;
+  p.L = D.seq_len;
+  p.Ts = D.speech_len;
+  p.C = D.d_pose;
+  p.alg = a.alg;
+  p.ln_g = c->out_ln_g;
+  p.ln_b = c->out_ln_b;
+  p.w_out = c->f_out.w;
+  p.b_out = c->f_out.b;
+  p.w_emb = c->f_emb.w;
+  p.b_emb = c->f_emb.b;
+  p.pe = c->pe;
+  p.x = c->x;
+  p.steps = c->d_steps;
+  p.k0 = 0;
+  p.n_steps = nsteps;
+  p.noise = a.noise;
+  p.seed = a.seed;
+  p.clip_offset = a.clip_offset;
+  p.inp_pose = a.inpaint_poses;
+  p.inp_mask = a.inpaint_masks;
+  p.trans = a.trans;
+  p.extras = a.extras;
+  p.scale = 1.0f / std::sqrt((float)(D.d_model / D.heads));
+  return p;
+}
+
+// Behind a persistent loop that needs every workgroup resident at once: the same clips re-initialised
+// and run on the one-workgroup-per-clip loop (no co-residency needed), both launches gated on the
+// device by the loop's status word, so a non-blocking call never hands back an unrun x
+int launch_gated_fallback(ggd_ctx* c, const ggd_sample_args& a, int nsteps, int clip0, int clips, const int* gate,
+                          int gate_xl, hipStream_t s) {
+  const ggd_desc& D = c->desc;
+  PersistArgs p = persist_args(c, a, nsteps);
+  p.clip0 = clip0;
+  p.gate = gate;
+  p.gate_xl = gate_xl;
+  HIP_TRY(c, launch_init_state_gated(c->x, a.x_T, a.seed, a.clip_offset, clip0, clips, D.d_pose, D.seq_len, gate,
+                                     gate_xl, s));
+  HIP_TRY(c, launch_persist_range(p, clips, s));
+  return GGD_OK;
+}
+
 // The first `nsteps` iterations as ONE persistent launch (ggd_mega.hip) per chunk of clips.
 // The XCD-local variant runs first; a chunk it cannot place (status 3: nothing ran) is re-run on the
 // write-through variant by a second launch that the device gates on that status word, so the host
@@ -2240,6 +2321,11 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
   if (chunks > MEGA_MAX_CHUNKS) return fail(c, GGD_ERR_ARG, "batch too large for the persistent loop");
   HIP_TRY(c, hipMemsetAsync(c->mega_status, 0, sizeof(int) * 2 * MEGA_MAX_CHUNKS, s));
   const bool xl = c->mega_place == 0;
+  // bf16 clips the one-workgroup-per-clip loop can run get a device-gated fallback; otherwise (f32
+  // parity mode) the call checks the status itself before returning (blocking) and, when nothing
+  // ran, re-initialises x and hands the call to the launch route
+  const bool fb = c->persist;
+  if (!fb) sync = true;
   if (c->profiling) {
     c->prof.next = 0;
     int r = prof_mark(c, s);
@@ -2247,11 +2333,11 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
   }
   for (int c0 = 0, ci = 0; c0 < a.n; c0 += cap, ++ci) {
     MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + ci,
-               c0 == 0 ? c->mega_stamps : nullptr, c0, c->mega_place == 1 ? 1 : 0, nullptr};
+               c0 == 0 ? c->mega_stamps : nullptr, c0, c->mega_place == 1 ? 1 : 0, nullptr, c->sim_unresident ? 1 : 0};
     HIP_TRY(c, launch_mega(D.dtype, D.seq_len, m, std::min(cap, a.n - c0), xl, s));
     if (xl) {  // the write-through re-run of this chunk, live only if the launch above reported 3
       MegaArgs g{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + MEGA_MAX_CHUNKS + ci,
-                 nullptr, c0, 0, c->mega_status + ci};
+                 nullptr, c0, 0, c->mega_status + ci, c->sim_unresident ? 1 : 0};
       HIP_TRY(c, launch_mega(D.dtype, D.seq_len, g, std::min(cap, a.n - c0), false, s));
     }
   }
@@ -2264,14 +2350,24 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
     c->prof_kind = 1;
     c->span_pending = 0;
   }
-  int r = defer_check(c, c->mega_status, 2 * MEGA_MAX_CHUNKS, 1, chunks, xl, s);
+  // each chunk on the one-workgroup-per-clip loop, live only if it never ran (status 2); outside the
+  // profiled span (the gated launches exit at once when the loop ran)
+  for (int c0 = 0, ci = 0; fb && c0 < a.n; c0 += cap, ++ci) {
+    int r = launch_gated_fallback(c, a, nsteps, c0, std::min(cap, a.n - c0), c->mega_status + ci, xl ? 1 : 0, s);
+    if (r) return r;
+  }
+  int r = defer_check(c, c->mega_status, 2 * MEGA_MAX_CHUNKS, 1, chunks, xl, fb, s);
   if (r) return r;
   if (!sync) return GGD_OK;
+  // earlier calls' checks first: an error they left is reported, not taken for this loop's
+  if ((r = poll_pending_before_last(c))) return r;
+  if ((r = take_sticky(c))) return r;
   if ((r = poll_pending(c, true))) return r;
-  if (c->sticky && c->mega_none_ran) {  // nothing ran (status 2 everywhere): the caller takes the launch route
+  if (c->sticky && c->mega_none_ran && !fb) {  // nothing ran (status 2 everywhere): the launch route runs it
     c->sticky = 0;
     c->sticky_msg.clear();
     ++c->mega_fallbacks;
+    HIP_TRY(c, launch_init_state(c->x, a.x_T, a.seed, a.clip_offset, a.n, D.d_pose, D.seq_len, s));
     return 1;
   }
   return take_sticky(c);
@@ -2319,33 +2415,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   if (use_persist) {
     // ONE launch: a workgroup per clip runs all nsteps iterations (ggd_persist.hip); in
     // profiling mode that launch is the timed kernel
-    PersistArgs p{};
-    p.layers = c->d_layers;
-    p.n_layers = D.n_layers;
-    p.n = a->n;
-    p.L = D.seq_len;
-    p.Ts = D.speech_len;
-    p.C = D.d_pose;
-    p.alg = a->alg;
-    p.ln_g = c->out_ln_g;
-    p.ln_b = c->out_ln_b;
-    p.w_out = c->f_out.w;
-    p.b_out = c->f_out.b;
-    p.w_emb = c->f_emb.w;
-    p.b_emb = c->f_emb.b;
-    p.pe = c->pe;
-    p.x = c->x;
-    p.steps = c->d_steps;
-    p.k0 = 0;
-    p.n_steps = nsteps;
-    p.noise = a->noise;
-    p.seed = a->seed;
-    p.clip_offset = a->clip_offset;
-    p.inp_pose = a->inpaint_poses;
-    p.inp_mask = a->inpaint_masks;
-    p.trans = a->trans;
-    p.extras = a->extras;
-    p.scale = 1.0f / std::sqrt((float)(D.d_model / D.heads));
+    PersistArgs p = persist_args(c, *a, nsteps);
     p.stamps = c->stamps;
     // clip pairs (two workgroups per clip) when the one-workgroup loop would leave CUs idle:
     // chunks of <= pcap clips, each filling the chip, vs rounds of 2 pcap clips at one per CU
@@ -2367,6 +2437,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
       p.status = c->pair_status;
       p.xbuf = c->pair_xbuf;
       p.force_coh = c->pair_force_coh;
+      p.sim_unresident = c->sim_unresident ? 1 : 0;
       HIP_TRY(c, hipMemsetAsync(c->pair_status, 0, sizeof(int), s));
     }
     if (c->profiling) {
@@ -2392,22 +2463,17 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
       c->prof_kind = pair ? 4 : 3;
       c->span_pending = 0;
     }
-    if (pair) {  // status words checked later (or now, with sync; then status 2 -- nothing ran -- re-runs
-                 // on the one-workgroup-per-clip loop, which needs no co-residency)
-      int r = defer_check(c, c->pair_status, 1, 4, 1, false, s);
+    if (pair) {  // status 2 (the pairs were never all resident): the whole batch re-runs on the
+                 // one-workgroup-per-clip loop, which needs no co-residency, gated on the device; the
+                 // status word is checked later (or now, with sync)
+      int r = launch_gated_fallback(c, *a, nsteps, 0, a->n, c->pair_status, 0, s);
       if (r) return r;
+      if ((r = defer_check(c, c->pair_status, 1, 4, 1, false, true, s))) return r;
       if (sync) {
+        if ((r = poll_pending_before_last(c))) return r;
+        if ((r = take_sticky(c))) return r;
         if ((r = poll_pending(c, true))) return r;
-        if (c->sticky) {
-          int st = 0;
-          HIP_TRY(c, hipMemcpy(&st, c->pair_status, sizeof(int), hipMemcpyDeviceToHost));
-          if (st != 2) return take_sticky(c);
-          c->sticky = 0;
-          c->sticky_msg.clear();
-          HIP_TRY(c, launch_init_state(c->x, a->x_T, a->seed, a->clip_offset, a->n, D.d_pose, D.seq_len, s));
-          HIP_TRY(c, launch_persist(p, s));
-          c->pair_launches = 0;
-        }
+        if ((r = take_sticky(c))) return r;
       }
     }
     HIP_TRY(c, launch_nlc_to_ncl(a->out, c->x, a->n, D.d_pose, D.seq_len, D.d_pose, s));

@@ -187,6 +187,13 @@ struct PersistArgs {
   unsigned char* xbuf;         // hand-off slots [pairs][2 parts][2 epochs][PAIR_SLOT_BYTES]
   int clip0;                   // first clip of this launch (batches above the capacity run as chunks)
   int force_coh;               // diagnostics: take the write-through placement even when XCD-local fits
+  // device-gated fallback (one workgroup per clip, clips clip0 ..): non-null -> the launch runs only
+  // if the loop it stands in for reported status 2 (its workgroups were never all resident).
+  // gate_xl = 0: *gate is that loop's status word; 1: gate[0] is an XCD-local clip-group launch's word
+  // and gate[MEGA_MAX_CHUNKS] its gated write-through re-run's (used when gate[0] == 3)
+  const int* gate;
+  int gate_xl;
+  int sim_unresident;          // test hook (GGD_ROUTE_SIMULATE_UNRESIDENT): the clip-pair loop reports 2, runs nothing
 };
 constexpr int PAIR_MAX = 128;                              // clip pairs per launch (ctl words)
 constexpr int PAIR_CTL_WORDS = 256 + PAIR_MAX * 32;        // tickets / arrival, one flag line per pair
@@ -210,9 +217,16 @@ struct MegaArgs {
   const int* gate;       // non-null: the launch runs only if *gate == 3 (the XCD-local launch of the same
                          // chunk could not place its clip groups) -- the write-through re-run, decided on
                          // the device so the host never waits for the first launch's status
+  int sim_unresident;    // test hook (GGD_ROUTE_SIMULATE_UNRESIDENT): report status 2 and run nothing
 };
 constexpr int MEGA_STAMP_STEPS = 2;
 constexpr int MEGA_MAX_CHUNKS = 16;  // status words: one per launch of up to mega_capacity() clips
+// PersistArgs::gate: open when the stood-in loop reported status 2 (nothing of it may be trusted)
+__device__ __forceinline__ bool gate_open(const int* g, int xl) {
+  if (!g) return true;
+  const int s0 = g[0];
+  return xl ? (s0 == 2 || (s0 == 3 && g[MEGA_MAX_CHUNKS] == 2)) : s0 == 2;
+}
 constexpr int MEGA_CTL_WORDS = 256 + 32 * 16 + 32 * 32;  // tickets/arrival, group counters, group flag lines
 
 // Row-block chains of the one-way decoder (ggd_chain.hip): one launch runs, on 32-row blocks of
@@ -295,6 +309,8 @@ hipError_t launch_ca_kv_conv(int dtype, const float* kv_mem, const float* kw, co
                              const float* vb, int n, int Ts, void* out, hipStream_t s);
 bool fused_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s);
+// clips [a.clip0, a.clip0 + clips) of a batch of a.n, one workgroup per clip (the gated fallback)
+hipError_t launch_persist_range(const PersistArgs& a, int clips, hipStream_t s);
 // clip pairs: clips [a.clip0, a.clip0 + pairs) with two co-resident workgroups each (pairs <=
 // persist_pair_capacity()); a.ctl must hold PAIR_CTL_WORDS words (zeroed here)
 hipError_t launch_persist_pair(const PersistArgs& a, int pairs, hipStream_t s);
@@ -315,6 +331,10 @@ hipError_t launch_posterior(const PostArgs& a, hipStream_t s);
 hipError_t launch_step_embed(float* out, int T, int d, hipStream_t s);
 hipError_t launch_init_state(float* x, const float* x_T_ncl, uint64_t seed, int64_t clip_offset,
                              int n, int C, int L, hipStream_t s);
+// the same for clips [clip0, clip0 + n) of the batch, run only if the gate (PersistArgs::gate) is open:
+// a loop that did not run re-initialises the clips it stood for before its fallback runs them
+hipError_t launch_init_state_gated(float* x, const float* x_T_ncl, uint64_t seed, int64_t clip_offset, int clip0,
+                                   int n, int C, int L, const int* gate, int gate_xl, hipStream_t s);
 hipError_t launch_nlc_to_ncl(float* dst, const float* src, int n, int C, int L, int ld_src,
                              hipStream_t s);
 hipError_t launch_set_int(int* p, int v, hipStream_t s);

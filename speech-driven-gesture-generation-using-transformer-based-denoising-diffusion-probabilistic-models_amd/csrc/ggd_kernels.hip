@@ -878,6 +878,23 @@ hipError_t launch_init_state(float* x, const float* x_T_ncl, uint64_t seed, int6
   return hipGetLastError();
 }
 
+__global__ void init_state_gated_kernel(float* x, const float* xT, uint64_t seed, int64_t clip_offset, int clip0,
+                                        int n, int C, int L, const int* gate, int gate_xl) {
+  if (!gate_open(gate, gate_xl)) return;
+  const int idx = blockIdx.x * NTHREADS + threadIdx.x;
+  if (idx >= n * L * C) return;
+  const int c = idx % C, bl = idx / C, l = bl % L, b = clip0 + bl / L;
+  x[(size_t)clip0 * L * C + idx] = xT ? xT[((size_t)b * C + c) * L + l]
+                                      : philox_normal(seed, (uint32_t)(clip_offset + b), 0u, TAG_XT, (uint32_t)(c * L + l));
+}
+
+hipError_t launch_init_state_gated(float* x, const float* x_T_ncl, uint64_t seed, int64_t clip_offset, int clip0,
+                                   int n, int C, int L, const int* gate, int gate_xl, hipStream_t s) {
+  hipLaunchKernelGGL(init_state_gated_kernel, dim3((n * L * C + NTHREADS - 1) / NTHREADS), dim3(NTHREADS), 0, s,
+                     x, x_T_ncl, seed, clip_offset, clip0, n, C, L, gate, gate_xl);
+  return hipGetLastError();
+}
+
 __global__ void nlc_to_ncl_kernel(float* dst, const float* src, int n, int C, int L, int ld) {
   const int idx = blockIdx.x * NTHREADS + threadIdx.x;
   if (idx >= n * C * L) return;

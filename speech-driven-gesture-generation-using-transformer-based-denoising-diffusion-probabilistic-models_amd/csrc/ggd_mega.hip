@@ -184,6 +184,10 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_role, s_ok;
   if (m.gate && ggd::G(m.gate)[0] != 3) return;  // gated re-run: the XCD-local launch placed (or failed otherwise)
+  if (m.sim_unresident) {  // test hook: as if the workgroups were never all resident
+    if (threadIdx.x == 0) atomicMax(m.status, 2);
+    return;
+  }
   if (threadIdx.x == 0) s_role = CPV == CP_XL ? mk_role_xl(m, gridDim.x, G) : mk_role(m, gridDim.x);
   __syncthreads();
   const int role = s_role;

@@ -284,6 +284,7 @@ template <int RT, bool PAIR>
 __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_role, s_ok;
+  if (a.gate && !gate_open(a.gate, a.gate_xl)) return;  // the loop this launch stands in for ran
   using PL = PPlan<RT>;
   using T = bf16_t;
   using AT = FAtt<T, PL::R>;
@@ -304,12 +305,16 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
 
   // clip b; PAIR: this workgroup's part (heads 4 part .., FFN chunks 4 part ..), its pair's flag
   // line and hand-off slots [part][epoch & 1]
-  int b = blockIdx.x, part = 0;
+  int b = a.clip0 + (int)blockIdx.x, part = 0;
   bool xl = false;
   unsigned* flags = nullptr;
   unsigned char* xb = nullptr;
   unsigned ep = 0;
   if constexpr (PAIR) {
+    if (a.sim_unresident) {  // test hook: as if the pairs were never all resident
+      if (threadIdx.x == 0) atomicMax(a.status, 2);
+      return;
+    }
     if (threadIdx.x == 0) s_role = pp_role(a, gridDim.x, P);
     __syncthreads();
     const int role = __builtin_amdgcn_readfirstlane(s_role);
@@ -810,7 +815,15 @@ static hipError_t launch_psk(const PersistArgs& a, int P, dim3 grid, hipStream_t
 
 hipError_t launch_persist(const PersistArgs& a, hipStream_t s) {
   persist_attrs();
-  return launch_psk<false>(a, a.n, dim3(a.n), s);
+  PersistArgs b = a;
+  b.clip0 = 0;
+  return launch_psk<false>(b, b.n, dim3(b.n), s);
+}
+
+hipError_t launch_persist_range(const PersistArgs& a, int clips, hipStream_t s) {
+  if (clips < 1 || a.clip0 < 0 || a.clip0 + clips > a.n) return hipErrorInvalidValue;
+  persist_attrs();
+  return launch_psk<false>(a, clips, dim3(clips), s);
 }
 
 // pairs per launch: the grid (16 workgroups per 8 pairs, one per CU) must be co-resident

@@ -841,6 +841,13 @@ class AdamW:
             self.exp_avg_sq.copy_(st["exp_avg_sq"])
         g = st["param_groups"][0]
         self.param_groups = [{"lr": float(g["lr"]), "initial_lr": float(g.get("initial_lr", g["lr"]))}]
+        # torch.optim.Optimizer.load_state_dict (trainer.py:218) restores every group hyperparameter
+        if "betas" in g:
+            self.betas = tuple(float(b) for b in g["betas"])
+        if "eps" in g:
+            self.eps = float(g["eps"])
+        if "weight_decay" in g:
+            self.weight_decay = float(g["weight_decay"])
 
 
 def parse_steps(s):

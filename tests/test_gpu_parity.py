@@ -15,9 +15,9 @@ pytestmark = pytest.mark.gpu
 
 D_POSE, L, WAV = 123, 40, 32000
 ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_PAIR_WT, ROUTE_PHASE_LAUNCHES = 0, 1, 2, 3   # include/ggd.h GGD_ROUTE_*
-ROUTE_GEMM_LAUNCHES, ROUTE_ATTN_QSPLIT, ROUTE_LONG_LOOP = 5, 6, 7
+ROUTE_GEMM_LAUNCHES, ROUTE_ATTN_QSPLIT, ROUTE_LONG_LOOP, ROUTE_SIM_UNRESIDENT = 5, 6, 7, 8
 INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES, INFO_CHAIN_AVAILABLE, INFO_LONG_LAUNCHES = 0, 2, 5, 6  # GGD_INFO_*
-INFO_CLIP_ATTN_LAUNCHES = 7
+INFO_CLIP_ATTN_LAUNCHES, INFO_GATED_FALLBACKS = 7, 8
 
 
 def rel_rms(a, b):
@@ -528,6 +528,79 @@ def test_clip_pair_batches_ddim_bf16(pkg, beat_cfg, setup, n):
         _route(ctx, 2)
     assert bool(th.isfinite(pair).all())
     assert rel_rms(pair, psk) <= 1e-2
+
+
+# ------------------------------------------------------------------------------------------
+# The persistent loops that need every workgroup resident at once (clip groups, clip pairs) stand
+# behind a device-gated fallback: when a loop reports status 2 (never all resident, nothing trusted)
+# the clips are re-initialised and run on the one-workgroup-per-clip loop, decided on the device, so
+# a non-blocking ggd_sample never hands back an unrun x.  GGD_ROUTE_SIMULATE_UNRESIDENT makes the
+# loops report 2 without running.
+# ------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("sync", [False, True])
+def test_unresident_loops_fall_back_on_device_bf16(pkg, beat_cfg, setup, sync):
+    _, sd, om = setup
+    model, diffusion = make_model(pkg, beat_cfg, sd, "bf16")
+    n, steps = 4, 6
+    wav, x, _ = inputs(n, seed=71)
+    zs = th.randn(steps, n, D_POSE, L, generator=th.Generator().manual_seed(72))
+    ctx, _ = model.prepare(wav.cuda(), L)
+    run = lambda: diffusion.p_sample_loop(model, (n, D_POSE, L), {"wav": wav.cuda()}, noise=x.cuda(),
+                                          step_noise=zs.cuda(), n_steps=steps, sync=sync)
+    outs = {}
+    try:
+        _route(ctx, 0)
+        _pair(ctx, 1)
+        outs["psk"] = run()                                   # the fallback loop itself
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_SIM_UNRESIDENT, 1) == 0
+        _route(ctx, 1)                                        # clip-group loop (mk_kernel), never resident
+        outs["mk_sim"] = run()
+        model.sync()                                          # no error: the fallback ran the clips
+        assert _info(ctx, INFO_GATED_FALLBACKS) == 1
+        _route(ctx, 0)
+        _pair(ctx, 2)                                         # clip pairs, never resident
+        outs["pair_sim"] = run()
+        model.sync()
+        assert _info(ctx, INFO_GATED_FALLBACKS) == 1
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_SIM_UNRESIDENT, 0) == 0
+        _route(ctx, 1)
+        outs["mk"] = run()                                    # the loop itself again: fallback idle
+        model.sync()
+        assert _info(ctx, INFO_GATED_FALLBACKS) == 0
+    finally:
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_SIM_UNRESIDENT, 0)
+        _pair(ctx, 0)
+        _route(ctx, 2)
+    for k in ("mk_sim", "pair_sim"):
+        for key in ("sample", "eps", "pred_x_start", "mean"):
+            assert th.equal(outs[k][key].cpu(), outs["psk"][key].cpu()), (k, key)
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    want = ref_diffusion.sample_loop(sch, om, (n, D_POSE, L), {"wav": wav}, ref_diffusion.InjectedNoise(x, zs),
+                                     "ddpm", x_T=x, n_steps=steps)["sample"]
+    assert rel_rms(outs["mk_sim"]["sample"].cpu(), want) <= 5e-2
+    assert rel_rms(outs["mk"]["sample"].cpu(), outs["psk"]["sample"].cpu()) <= 1e-2
+
+
+def test_unresident_f32_loop_checks_before_returning(pkg, beat_cfg, setup):
+    """f32 (parity mode) has no one-workgroup-per-clip loop: the call checks the clip-group loop's
+    status itself and runs a loop that never ran on the per-phase launches, from a re-initialised x."""
+    _, sd, om = setup
+    model, diffusion = make_model(pkg, beat_cfg, sd, "f32")
+    n, steps = 2, 3
+    wav, x, _ = inputs(n, seed=73)
+    zs = th.randn(steps, n, D_POSE, L, generator=th.Generator().manual_seed(74))
+    ctx, _ = model.prepare(wav.cuda(), L)
+    try:
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_SIM_UNRESIDENT, 1) == 0
+        got = diffusion.p_sample_loop(model, (n, D_POSE, L), {"wav": wav.cuda()}, noise=x.cuda(),
+                                      step_noise=zs.cuda(), n_steps=steps)["sample"].cpu()
+        model.sync()
+    finally:
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_SIM_UNRESIDENT, 0)
+    sch = ref_diffusion.make_schedule("linear", 1000, "")
+    want = ref_diffusion.sample_loop(sch, om, (n, D_POSE, L), {"wav": wav}, ref_diffusion.InjectedNoise(x, zs),
+                                     "ddpm", x_T=x, n_steps=steps)["sample"]
+    assert (got - want).abs().max().item() <= 1e-3
 
 
 # ------------------------------------------------------------------------------------------

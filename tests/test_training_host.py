@@ -265,3 +265,23 @@ def test_speed_losses_follow_trainer_py():
     # no extra losses: nothing added
     terms, total = tr.speed_losses(x, p, None)
     assert terms == {} and total == 0.0
+
+
+def test_adamw_load_state_dict_restores_group_hyperparameters():
+    """torch.optim.Optimizer.load_state_dict (trainer.py:218) restores lr, betas, eps and
+    weight_decay of the saved group; a resumed run then steps with the checkpoint's values."""
+    import types
+    tr = _training()
+    params = {"a": th.zeros(3, 2), "b": th.zeros(4)}
+    model = types.SimpleNamespace(flat=th.zeros(10), params=params)
+    saved = tr.AdamW(model, lr=2e-4, betas=(0.8, 0.95), eps=1e-6, weight_decay=0.05)
+    st = saved.state_dict()
+    opt = tr.AdamW(model, lr=1e-3)
+    opt.load_state_dict(st)
+    assert opt.param_groups[0]["lr"] == pytest.approx(2e-4)
+    assert opt.betas == (0.8, 0.95) and opt.eps == 1e-6 and opt.weight_decay == 0.05
+    # the same checkpoint restored into torch's AdamW carries the same hyperparameters
+    ref = th.optim.AdamW([th.nn.Parameter(th.zeros(3, 2)), th.nn.Parameter(th.zeros(4))], lr=1e-3)
+    ref.load_state_dict(st)
+    g = ref.param_groups[0]
+    assert tuple(g["betas"]) == opt.betas and g["eps"] == opt.eps and g["weight_decay"] == opt.weight_decay
