@@ -348,21 +348,40 @@ def rehearse(args, rank, world):
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    out = sharding.sample_sharded(fn, wav_all, n_total, rank, world, th.device("cpu"))
+    stats = {}
+    out = sharding.sample_sharded(fn, wav_all, n_total, rank, world, th.device("cpu"), stats)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    dist_rec = None
     if world > 1:
         t = th.tensor([elapsed], dtype=th.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        dist_rec = distributed_record(dist, args, stats, stats.get("gather_ms", 0.0), 0.0, "cpu")
     if rank == 0:
         print(json.dumps({"metric": "rehearsal (not a measurement)", "rehearsal": True, "n_gpus": world,
                           "world": world, "global_batch": n_total, "elapsed_s": elapsed,
                           "checksum": float(out.double().sum()), "shape": list(out.shape),
-                          "first": out[:, 0, 0].tolist()}), flush=True)
+                          "first": out[:, 0, 0].tolist(), "distributed": dist_rec}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def distributed_record(dist, args, stats, gather_ms, kernel_us, device):
+    """The N > 1 fields of the bench line, each reduced over ranks (MAX): the backend and world the
+    ranks actually run (checked against --gpus), the final all-gather's payload and its own event
+    time in the last timed pass, and the dominant kernel's average launch time."""
+    world = dist.get_world_size()
+    assert world == args.gpus, f"--gpus {args.gpus} but the process group has {world} ranks"
+    t = th.tensor([gather_ms, kernel_us], dtype=th.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"backend": dist.get_backend() + (" (RCCL)" if dist.get_backend() == "nccl" else ""),
+            "world_size": world, "all_gather_bytes": stats.get("gather_bytes"),
+            "all_gather_ms_max_over_ranks": round(float(t[0]), 4),
+            "kernel_avg_launch_us_max_over_ranks": round(float(t[1]), 3) if kernel_us else None,
+            "timing": "hipEvent pair on the sampling stream around all_gather_into_tensor (includes the wait "
+                      "for the slowest rank), last timed pass" if device != "cpu" else "perf_counter around the gather"}
 
 
 def main():
@@ -415,13 +434,15 @@ def main():
     wavs = [th.randn(n_total, wav_len, device=dev, generator=g) * 0.1 for _ in range(n_batches)]
     start, stop = sharding.shard_range(n_total, rank, world)
 
+    gather_stats = {}
+
     def one_pass(wav_all, seed, wav_next=None):
         def fn(wav_local, offset):
             out = loop(model, (wav_local.shape[0], d_pose, L), model_kwargs={"wav": wav_local}, seed=seed,
                        clip_offset=offset, use_graph=args.graph, extras=False,
                        prefetch_wav=None if wav_next is None else wav_next[start:stop])
             return out["sample"]
-        return sharding.sample_sharded(fn, wav_all, n_total, rank, world, dev)
+        return sharding.sample_sharded(fn, wav_all, n_total, rank, world, dev, gather_stats)
 
     # warm-up (graph capture, encoder kernels, allocator)
     enc = __import__(ge.PKG_NAME + ".encoder", fromlist=["x"])
@@ -464,10 +485,17 @@ def main():
         prof_kind = lib.ggd_profile_kind(ctx.h)
         prof_us.append(avg.value * cnt.value)
         prof_n += cnt.value
+    dist_rec = None
     if dist is not None:
         t = th.tensor([elapsed], device=dev, dtype=th.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        ev = gather_stats.get("gather_events")
+        gather_ms = ev[0].elapsed_time(ev[1]) if ev else 0.0
+        own_us = prof_us[0] / prof_n if prof and prof_n else 0.0
+        dist_rec = distributed_record(dist, args, gather_stats, gather_ms, own_us, dev)
+        if dist_rec["kernel_avg_launch_us_max_over_ranks"]:   # the roofline of the slowest rank
+            prof_us = [dist_rec["kernel_avg_launch_us_max_over_ranks"] * prof_n]
     log(f"timed region done: {elapsed:.3f} s")
     assert out.shape == (n_total, d_pose, L) and bool(th.isfinite(out).all())
 
@@ -548,6 +576,7 @@ def main():
                    "speech_encoder": "inline per pass" if not overlap else
                    "per pass, pass k+1's beside pass k's loop on a second HIP stream"},
         "roofline": roof,
+        "distributed": dist_rec,
         "whole_job": {"gflop_per_frame": round(frame_flop / 1e9, 4), "clip_step_mflop": round(clip_step / 1e6, 2),
                       "achieved_tflops_per_gpu": round(value * frame_flop / world / 1e12, 3),
                       "frac_of_peak": round(value * frame_flop / world / 1e12 / peak, 5)},

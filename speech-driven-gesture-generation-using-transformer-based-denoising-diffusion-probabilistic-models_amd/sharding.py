@@ -19,9 +19,14 @@ def shard_range(n_total, rank, world):
     return start, start + base + (1 if rank < extra else 0)
 
 
-def sample_sharded(sample_fn, wavs, n_total, rank, world, device):
+def sample_sharded(sample_fn, wavs, n_total, rank, world, device, stats=None):
     """Run ``sample_fn(wav_shard, clip_offset) -> (n_local, ...)`` on this rank's clips and
-    all-gather the results in global clip order on every rank."""
+    all-gather the results in global clip order on every rank.
+
+    ``stats`` (a dict, optional) receives the all-gather's payload bytes and its timing: on a GPU a
+    pair of events on the current stream around the collective (``gather_events``: the stream waits
+    for RCCL there, so the span also holds the wait for the slowest rank), on CPU ``gather_ms``."""
+    import time
     start, stop = shard_range(n_total, rank, world)
     local = sample_fn(wavs[start:stop], start).contiguous()
     if world == 1:
@@ -32,6 +37,19 @@ def sample_sharded(sample_fn, wavs, n_total, rank, world, device):
     pad = th.zeros((maxn,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local
     gathered = th.empty((world * maxn,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(gathered, pad)
+    if stats is None:
+        dist.all_gather_into_tensor(gathered, pad)
+    elif gathered.is_cuda:
+        e0, e1 = th.cuda.Event(enable_timing=True), th.cuda.Event(enable_timing=True)
+        e0.record()
+        dist.all_gather_into_tensor(gathered, pad)
+        e1.record()
+        stats["gather_events"] = (e0, e1)
+    else:
+        t0 = time.perf_counter()
+        dist.all_gather_into_tensor(gathered, pad)
+        stats["gather_ms"] = (time.perf_counter() - t0) * 1e3
+    if stats is not None:
+        stats["gather_bytes"] = gathered.numel() * gathered.element_size()
     parts = [gathered[r * maxn: r * maxn + sizes[r]] for r in range(world)]
     return th.cat(parts, dim=0)

@@ -85,6 +85,11 @@ def test_self_launch_rehearsal_matches_single_rank():
         assert res["rehearsal"] and res["world"] == n and res["global_batch"] == 2 * n
         assert res["shape"] == [2 * n, 123, 40]
         assert res["first"][:2] == one["first"]  # global clips 0, 1: same wav rows, same noise keys
+        d = res["distributed"]   # the fields a GPU run at N > 1 reports (max over ranks)
+        assert d["backend"] == "gloo" and d["world_size"] == n
+        assert d["all_gather_bytes"] == 2 * n * 123 * 40 * 4
+        assert d["all_gather_ms_max_over_ranks"] >= 0.0
+    assert one["distributed"] is None
 
 
 def test_headline_pmc_summary_matches_the_kernel_sources():

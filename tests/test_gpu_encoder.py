@@ -66,3 +66,27 @@ def test_encoder_batch_invariant(pkg, sd, dtype):
     part = enc(wav[2:4].contiguous())
     for a, b in zip(full, part):
         assert th.equal(a[2:4], b)
+
+
+@pytest.mark.parametrize("wav_len", [32000, 128000])
+def test_encoder_frontend_matches_scipy_mel(pkg, sd, wav_len):
+    """The HIP front end (pre-emphasis, STFT power, HTK mel, +1e-6, InstanceNorm1d;
+    speech_encoder.py:18-34,53-58) against the scipy / float64 pipeline of tests/test_mel_pin.py,
+    which shares no code with the oracle or the kernels.  Bound: max|diff| <= 1e-3 on the
+    normalised image (O(1) values)."""
+    import numpy as np
+    from tests.test_mel_pin import htk_filterbank_f64, scipy_power_f64
+    wav = wavs(2, wav_len, seed=9)
+    got = encoder(pkg, sd, "f32").frontend(wav.cuda()).cpu().double().numpy()
+    fb = htk_filterbank_f64()
+    for i in range(wav.shape[0]):
+        x = wav[i].double().numpy()
+        y = np.empty_like(x)
+        y[0] = x[0] - 0.97 * x[1]
+        y[1:] = x[1:] - 0.97 * x[:-1]
+        mel = fb.T @ scipy_power_f64(y) + 1e-6
+        want = (mel - mel.mean(axis=1, keepdims=True)) / np.sqrt(mel.var(axis=1, keepdims=True) + 1e-5)
+        assert got[i].shape == want.shape
+        err = np.abs(got[i] - want).max()
+        print(f"frontend {wav_len}: max|diff| {err:.3e}")
+        assert err <= 1e-3, err
