@@ -601,11 +601,93 @@ __device__ __forceinline__ void att_mma16(f32x4& acc, const float* X, int SX, co
   }
 }
 
+// Whole 16-lane rows of a wave exchanged by gfx950's v_permlane16_swap / v_permlane32_swap (one
+// VALU instruction each; lane semantics checked by scripts/permlane_probe.hip): the max / sum of
+// x over the wave's 4 lane rows at the same column c16, identical bits in every lane.
+__device__ __forceinline__ float lanerow_max4(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  const float m = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float lanerow_sum4(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// bf16 attention of one 16-query tile with the probabilities kept in registers.  S^T = K Q^T (the
+// K tile as the MFMA A operand), so lane (c16, g4) holds the scores of query c16 against keys
+// 16 t + 4 g4 .. + 3: the softmax reduces over keys in-lane and across the 4 lane rows, and the
+// bf16 P values of key tile t are exactly the B operand (k = 4 g4 .. + 3, n = c16) of
+// O^T = V^T P^T on v_mfma_f32_16x16x16_bf16 -- no P tile through LDS, no per-element P stores.
+// Output lane map as fattn's: query c16, channels 4 g4 .. + 3 of each 16-channel tile.
+template <int LKT, int QR, bool TO_LDS, int CP>
+__device__ __forceinline__ void fattn_regp(unsigned char* att, int Lk, float scale, bf16_t* out, int ldo,
+                                           const OutRowsP<CP>& dst, int rt, int lane) {
+  using A = FAtt<bf16_t, QR>;
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  const bf16_t* Qm = (const bf16_t*)(att + A::OQ);
+  const bf16_t* Km = (const bf16_t*)(att + A::OK);
+  const bf16_t* Vt = (const bf16_t*)(att + A::OV);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  const bf16x8 qf = *(const bf16x8*)(Qm + (rt * 16 + c16) * A::SQ + g4 * 8);
+  f32x4 s[LKT];
+#pragma unroll
+  for (int t = 0; t < LKT; ++t) {
+    const bf16x8 kf = *(const bf16x8*)(Km + (t * 16 + c16) * A::SQ + g4 * 8);
+    s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  }
+  // base-2 softmax (as fattn): a masked key is -inf after the scaling, its exp2 is 0
+  const float sl2 = scale * 1.4426950408889634f;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < LKT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float v = t * 16 + 4 * g4 + i < Lk ? s[t][i] * sl2 : -INFINITY;
+      s[t][i] = v;
+      mx = fmaxf(mx, v);
+    }
+  mx = lanerow_max4(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < LKT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s[t][i] = __builtin_amdgcn_exp2f(s[t][i] - mx);
+      sum += s[t][i];
+    }
+  const float inv = __builtin_amdgcn_rcpf(lanerow_sum4(sum));
+  s16x4 pb[LKT];
+#pragma unroll
+  for (int t = 0; t < LKT; ++t) {
+    const uint2 u = make_uint2(pk_bf16(s[t][0] * inv, s[t][1] * inv), pk_bf16(s[t][2] * inv, s[t][3] * inv));
+    pb[t] = __builtin_bit_cast(s16x4, u);
+  }
+#pragma unroll
+  for (int ct = 0; ct < FDK / 16; ++ct) {
+    f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < LKT; ++t) {
+      const s16x4 vf = *(const s16x4*)(Vt + (ct * 16 + c16) * A::SV + t * 16 + 4 * g4);
+      o = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf, pb[t], o, 0, 0, 0);
+    }
+    const int q = rt * 16 + c16, d0 = ct * 16 + 4 * g4;
+    if constexpr (TO_LDS)
+      *(uint2*)(out + q * ldo + d0) = make_uint2(pk_bf16(o[0], o[1]), pk_bf16(o[2], o[3]));
+    else
+      dst.template put4v<bf16_t>((uint32_t)(q * ldo + d0), o);
+  }
+}
+
 // O[Lq][32] = softmax(scale Q K^T) V for one head; wave w owns query rows 16w..16w+15.
 // LKT = key tiles of 16 (Lk <= 16 LKT, LKT even).  Keys >= Lk are masked by select (their K
 // rows may hold anything); V^T columns >= Lk must be finite (zeroed by the caller).
 // TO_LDS: `out` is an LDS operand image and every query row (padding included) is written;
 // otherwise `out` is global and rows >= Lq are dropped by the bounded buffer stores.
+// bf16 runs fattn_regp (P in registers); f32 (the parity precision) keeps the P tile in LDS.
 template <typename T, int LKT, int QR = FR, bool TO_LDS = false, int CP = CP_KERNEL>
 __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float scale, T* out, int ldo,
                                       int tid = ltid()) {
@@ -617,6 +699,11 @@ __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float 
   T* P = (T*)(att + A::OP) + wave * 16 * A::SP;
   const int rt = wave;
   if (rt * 16 >= Lq) return;
+  if constexpr (sizeof(T) == 2) {
+    const OutRowsP<CP> dst(out, (uint32_t)(sizeof(T) * ((size_t)(Lq - 1) * ldo + FDK)));  // rows >= Lq dropped
+    fattn_regp<LKT, QR, TO_LDS, CP>(att, Lk, scale, out, ldo, dst, rt, lane);
+    return;
+  }
   f32x4 s[LKT];
 #pragma unroll
   for (int t = 0; t < LKT; ++t) {
