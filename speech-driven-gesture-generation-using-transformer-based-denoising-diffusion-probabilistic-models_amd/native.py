@@ -17,6 +17,9 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 PRODUCT_LIB = os.path.join(PKG_DIR, "libggd.so")
 DIAG_LIB = os.path.join(PKG_DIR, "libggd_diag.so")
 LIB_PATH = DIAG_LIB if os.environ.get("GGD_DIAG") == "1" else PRODUCT_LIB
+# A/B experiments (scripts/ab.sh): another build of the same library, same ABI
+if os.environ.get("GGD_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["GGD_LIB"])
 SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_encoder.hip", "ggd_train.hip", "ggd_chain.hip", "ggd_attn.hip", "ggd_long.hip",
            "ggd_api.hip"]
 DIAG_SOURCES = ["ggd_diag.hip"]   # + ggd_api.hip again with -DGGD_DIAG
