@@ -2287,8 +2287,8 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
   c->mega_fa_host.assign(4 * NL, FusedArgs{});
   for (int li = 0; li < NL; ++li) {
     FusedArgs f = fused_args(c, li, nullptr);
-    c->mega_fa_host[4 * li] = f;      // KA (layer 0: emb of x)
-    f.x_emb = nullptr;
+    f.x_emb = nullptr;                // layer 0's h rows come from the loop's KE rows phase
+    c->mega_fa_host[4 * li] = f;      // KA
     c->mega_fa_host[4 * li + 1] = f;  // KB: h -> h2
     f.h = c->h2;
     f.h_out = c->h;
@@ -2310,6 +2310,8 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
   fe.extras = a.extras;             // written by the loop's own last iteration
   fe.extras_k = nsteps - 1;
   fe.stamps = c->mega_phase_stamps ? c->mega_phase_stamps + 64 : nullptr;
+  fe.ffp = c->ffp;                               // the last layer's KD runs in the KE rows phase
+  fe.ff2_b = fused_layer(c, NL - 1).ff2_b;
   {
     int r = upload_cached(c, c->mega_fa, c->mega_fa_host.data(), sizeof(FusedArgs) * 4 * NL, s);
     if (!r) r = upload_cached(c, c->mega_fe, &fe, sizeof(FinalArgs), s);

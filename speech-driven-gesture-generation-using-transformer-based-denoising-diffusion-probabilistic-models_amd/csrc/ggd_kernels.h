@@ -163,6 +163,9 @@ struct FinalArgs {
   int extras_k;            // extras are written at iteration extras_k only (< 0: at every iteration)
   int do_out, do_update;
   unsigned long long* stamps;  // diagnostics
+  // the persistent loop's KE rows phase also runs the last layer's FFN-down reduction for its rows
+  const void* ffp;             // FFN-down partials [N][8 chunks][L][d] (the loop's dtype)
+  const float* ff2_b;          // the last layer's FFN-down bias
 };
 
 // Persistent per-clip sampler (ggd_persist.hip): one workgroup per clip runs iterations

@@ -115,6 +115,11 @@ __device__ int mk_role_xl(const MegaArgs& m, int nwg, int G) {
 // VMC: vector loads the wave issued after its last hand-off store (the next phase's weights, issued
 // by the phase's hook): vmcnt completes in issue order, so waiting down to VMC outstanding drains
 // every store without waiting for those loads
+// (stamps are indexed by epoch - 2: the prologue's barrier is epoch 1 and is not stamped)
+// GGD_MK_SPOLL (round-4 A/B switch): the XCD-local barrier polls with scalar loads (below)
+#ifndef GGD_MK_SPOLL
+#define GGD_MK_SPOLL 0
+#endif
 template <int CPV, int VMC = 0, typename F>
 __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part, unsigned epoch, int* status,
                                         int* s_ok, unsigned long long* st, F&& prefetch,
@@ -122,9 +127,9 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
   static_assert(VMC >= 0 && VMC < 64, "vmcnt field");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");  // this wave's hand-off stores landed
   __syncthreads();
-  if (st && threadIdx.x == 0) st[2 * (epoch - 1)] = __builtin_amdgcn_s_memtime();
+  if (st && threadIdx.x == 0) st[2 * (epoch - 2)] = __builtin_amdgcn_s_memtime();
   // diag: arrival and exit of every workgroup of clip group 0, on the chip-wide 100 MHz clock
-  if (arr && threadIdx.x == 0) arr[2 * (8 * (epoch - 1) + part)] = __builtin_amdgcn_s_memrealtime();
+  if (arr && threadIdx.x == 0) arr[2 * (8 * (epoch - 2) + part)] = __builtin_amdgcn_s_memrealtime();
   if constexpr (CPV == CP_XL) {
     if (threadIdx.x == 0) {
       const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
@@ -133,13 +138,37 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
   } else {
     if (threadIdx.x == 0) mk_add(ctr, 1u);
   }
-  // the next phase's weight fragments: waves 1..7 now; wave 0, which polls, only after its poll --
-  // a poll load completes behind every vector load its wave issued before it (vmcnt is in order),
-  // so a prefetch issued ahead of the poll would hold the whole clip group until it had landed
+  // XCD-local path: wave 0 polls the group's 8 flag words with SCALAR loads (s_load glc: past the
+  // scalar cache, from the shared L2), which count in lgkmcnt -- a vector poll load would complete
+  // only behind every vector load its wave issued before it (vmcnt retires in order), i.e. behind
+  // the weight fragments the hooks issued under the attention.  So every wave, the poller
+  // included, issues the next phase's fragments at once.
   const bool poller = threadIdx.x < 64;
-  if (!poller) prefetch();
-  if constexpr (CPV == CP_XL) {
-    if (threadIdx.x < 64) {
+  constexpr bool SP = CPV == CP_XL && GGD_MK_SPOLL != 0;
+  if (SP || !poller) prefetch();
+  if constexpr (SP) {
+    if (poller) {
+      typedef unsigned u32x8 __attribute__((ext_vector_type(8)));
+      const unsigned* fp = (const unsigned*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)flags)) |
+                                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)flags >> 32)) << 32));
+      int ok = 1;
+      for (int spin = 0;; ++spin) {
+        u32x8 v;
+        asm volatile("s_load_dwordx8 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(fp) : "memory");
+        const unsigned lo = min(min(min(v[0], v[1]), min(v[2], v[3])), min(min(v[4], v[5]), min(v[6], v[7])));
+        if (lo >= epoch) break;
+        if ((spin & 255) == 255 && (spin > MK_SPIN_LIMIT || __hip_atomic_load(status, __ATOMIC_RELAXED,
+                                                                               __HIP_MEMORY_SCOPE_AGENT))) {
+          if (threadIdx.x == 0) atomicMax(status, 1);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (threadIdx.x == 0) *s_ok = ok;
+    }
+  } else if constexpr (CPV == CP_XL) {  // vector poll (a poll load retires behind the wave's earlier loads:
+    if (threadIdx.x < 64) {             // the poller issues its prefetch after it)
       const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
       const int off = (threadIdx.x & 7) * 4;
       int ok = 1;
@@ -172,10 +201,10 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
       *s_ok = ok;
     }
   }
-  if (poller) prefetch();
+  if (!SP && poller) prefetch();
   bar_lds();
-  if (st && threadIdx.x == 0) st[2 * (epoch - 1) + 1] = __builtin_amdgcn_s_memtime();
-  if (arr && threadIdx.x == 0) arr[2 * (8 * (epoch - 1) + part) + 1] = __builtin_amdgcn_s_memrealtime();
+  if (st && threadIdx.x == 0) st[2 * (epoch - 2) + 1] = __builtin_amdgcn_s_memtime();
+  if (arr && threadIdx.x == 0) arr[2 * (8 * (epoch - 2) + part) + 1] = __builtin_amdgcn_s_memrealtime();
   return *s_ok != 0;
 }
 
@@ -203,10 +232,13 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
   const int NL = m.n_layers;
   cfa_t fa0 = (cfa_t)m.fa;
   cfe_t fe = (cfe_t)m.fe;
-  // weights of the next phase, issued at the barrier in front of it (the first one here); KA's
-  // and KE's tiles share one register set (Pre1)
+  // prologue: the first step's layer-0 residual rows from the initial x (every later step's come
+  // from the KE rows phase of the step before)
+  emb_prologue<T, CPV>(*fe, part, b, smem);
+  // weights of the next phase, issued at the barrier in front of it; KA's and KE's tiles share one
+  // register set (Pre1)
   Pre1<T, RT> pn = ka_pre<T, RT>(fa0[0], part, wave);
-  pn.load(lane);
+  if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, nullptr, [&] { pn.load(lane); })) return;
   for (int k = 0; k < m.n_steps; ++k) {
     const int it = m.k0 + k;
     unsigned long long* st = (m.stamps && role == 0 && k < MEGA_STAMP_STEPS) ? m.stamps : nullptr;
@@ -216,19 +248,23 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
       asm volatile("" : "+s"(f));  // per-layer arguments are re-read, not held across the loop
       // the out-projection fragments of KB / KC are issued by the hook behind the attention in front
       KBPre<T, RT> pb(f[1], wave);
-      ka_phase<T, RT, CPV>(f[0], part, b, smem, pn, [&] { pb.load_tile(1, lane); }, [&] { pb.load_tile(0, lane); });
+      ka_phase<T, RT, CPV, false>(f[0], part, b, smem, pn, [&] { pb.load_tile(1, lane); }, [&] { pb.load_tile(0, lane); });
       if (!mk_sync<CPV, KBPre<T, RT>::TILE_LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
       KCPre<T, RT> pc(f[2], part, wave);
       kb_phase<T, RT, CPV>(f[1], part, b, it, smem, pb, [&] { pc.load_tile(1, lane); }, [&] { pc.load_tile(0, lane); });
       if (!mk_sync<CPV, KCPre<T, RT>::TILE_LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
       kc_phase<T, RT, CPV>(f[2], part, b, smem, pc);
-      KDPre<T, RT> pd(f[3], part, wave);
-      if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pd.load(lane); }, ar)) return;
-      kd_phase<T, RT, CPV>(f[3], part, b, smem, pd);
-      pn = li + 1 < NL ? ka_pre<T, RT>(f[4], part, wave) : ke_pre<T, RT>(*fe, part, wave);
+      if (li + 1 < NL || !GGD_MK_FUSE_KD) {
+        KDPre<T, RT> pd(f[3], part, wave);
+        if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pd.load(lane); }, ar)) return;
+        kd_phase<T, RT, CPV>(f[3], part, b, smem, pd);
+        pn = li + 1 < NL ? ka_pre<T, RT>(f[4], part, wave) : ker_pre<T, RT>(*fe, wave);
+      } else {  // the last layer's KD runs inside the KE rows phase, for each block's rows
+        pn = ker_pre<T, RT>(*fe, wave);
+      }
       if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); }, ar)) return;
     }
-    ke_phase<T, RT, CPV>(*fe, part, b, it, smem, pn);
+    ker_phase<T, RT, CPV>(*fe, part, b, it, smem, pn);
     pn = ka_pre<T, RT>(fa0[0], part, wave);
     if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pn.load(lane); }, ar)) return;
   }

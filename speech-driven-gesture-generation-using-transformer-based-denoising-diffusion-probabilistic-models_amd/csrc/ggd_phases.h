@@ -32,6 +32,16 @@
 #pragma once
 #include "ggd_fusedlib.h"
 
+// Round-4 switches of the persistent loop's KE rows phase (A/B builds: -DGGD_MK_...=0/1):
+//   GGD_MK_FUSE_KD  the last layer's FFN-down reduction runs inside KE, for each block's rows
+//   GGD_MK_CMAP     KE update threads take channel t % 128 (coalesced x access) instead of t / 3
+#ifndef GGD_MK_FUSE_KD
+#define GGD_MK_FUSE_KD 0
+#endif
+#ifndef GGD_MK_CMAP
+#define GGD_MK_CMAP 0
+#endif
+
 namespace ggd {
 
 constexpr int FT = 512;  // threads of the fused kernels: 8 waves, two per SIMD
@@ -169,7 +179,9 @@ struct NoHook {
 // ------------------------------------------------------------------------------------------
 // KA: [emb_x + PE (layer 0)] + LN1 + QKV(head) + conv + self-attention      grid (heads, clips)
 // ------------------------------------------------------------------------------------------
-template <typename T, int RT, int CP, typename FA, typename H = NoHook, typename H0 = NoHook>
+// EMB = false (the persistent loop): layer 0's residual rows come from the KE rows phase, the x ->
+// emb path is not compiled in
+template <typename T, int RT, int CP, bool EMB = true, typename FA, typename H = NoHook, typename H0 = NoHook>
 __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned char* smem, KAPre<T, RT>& pre,
                                          H&& hook = H(), H0&& hook0 = H0()) {
   using PL = Plan<T>;
@@ -188,7 +200,7 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
   const auto& w = a.w;
 
   STAMP(0);
-  const bool emb = a.x_emb != nullptr;  // layer 0: h = emb_x(x) + PE computed here
+  const bool emb = EMB && a.x_emb != nullptr;  // layer 0: h = emb_x(x) + PE computed here
   glds_rows<FT, CP>(Hs, sizeof(float) * SH, emb ? a.pe : a.h + (size_t)b * L * FD, sizeof(float) * FD, L, 1);
   constexpr int KTE = 128 / Frag<T>::KF, SB = 128 + Frag<T>::PT, NXV = FR * 128 / FT;
   WGemm<T, 2, KTE, RT> ge(a.w_emb, KTE, 0);
@@ -596,6 +608,269 @@ __device__ __forceinline__ void ke_phase(const FA& a, int p, int b, int k, unsig
     }
   }
   STAMP_END(3);
+}
+
+// ------------------------------------------------------------------------------------------
+// KE by frame rows (the persistent loop, round 4).  Workgroup p of clip b owns frames
+// [r0, r1) = [p L / 8, (p + 1) L / 8) (<= 8 rows: one MFMA row tile) and runs, for those rows,
+//   the last layer's FFN-down reduction (KD) for its rows: no KD phase and barrier in front of KE;
+//   LN_out + eps of all C channels (wave w: channel tile w) -> E (LDS);
+//   the DDPM / DDIM update of every element of its frames: the Philox quads keep the reference's
+//   (C, L) element order (a quad is 4 consecutive elements of a channel's frames), one quad per
+//   thread -- thread (channel c = t % 128, k = t / 128 < 3) draws quad (c L + r0) / 4 + k and updates the elements of
+//   it that are channel c's frames in [r0, r1) (a quad that straddles two blocks is drawn by both,
+//   each keeping its own elements; a quad that straddles two channels by both channels' threads);
+//   emb_x + PE of the updated rows -> the next step's layer-0 residual rows h.
+// The next step's KA of layer 0 then stages h like every other layer (no x -> emb path in front
+// of it: 16 dword loads per thread, the operand image, a 3-row-tile GEMM and two barriers).
+// ------------------------------------------------------------------------------------------
+template <typename T> struct KerPlan {
+  static constexpr int SE = 128 + 4, SB = 128 + Frag<T>::PT;
+  static constexpr size_t HS = al16(sizeof(float) * 8 * SH);                  // the block's h rows
+  static constexpr size_t XN = al16(sizeof(T) * 16 * Frag<T>::SX);            // LN_out image
+  static constexpr size_t E = al16(sizeof(float) * 16 * SE);                  // eps [row][channel]
+  static constexpr size_t XB = al16(sizeof(T) * 16 * SB);                     // emb operand
+  static constexpr size_t BYTES = HS + XN + E + XB;
+};
+template <typename T, int RT, typename FA>  // channel tile = wave (the tiles past C load nothing)
+__device__ __forceinline__ KEPre<T, RT> ker_pre(const FA& a, int wave) {
+  return KEPre<T, RT>(a.w_out, wave, 16 * wave < a.C);
+}
+
+// h rows [r0, r0 + R) of clip b = PE + b_emb + Xb W_emb^T (Xb: the rows' x in bf16 / f32, 16 x 128,
+// zero past C and R); wave w owns columns 32 w .. 32 w + 31.  ge: the wave's two W_emb tiles (loaded).
+template <typename T, int CP, typename FA>
+__device__ __forceinline__ void emb_rows_store(const FA& a, int b, int r0, int R, const T* Xb,
+                                               WGemm<T, 2, 128 / Frag<T>::KF, 1>& ge, const float4 (&pe)[2],
+                                               int lane, int wave) {
+  const int c16 = lane & 15, g4 = lane >> 4;
+  f32x4 acc[1][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) acc[0][j] = f32x4{pe[j].x, pe[j].y, pe[j].z, pe[j].w};
+  ge.template run<true>(acc, Xb, KerPlan<T>::SB, lane, 2, false);
+  const OutRowsP<CP> ho(a.h + ((size_t)b * a.L + r0) * FD, (uint32_t)(sizeof(float) * R * FD));  // rows >= R dropped
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    ho.put4((uint32_t)(c16 * FD + (2 * wave + j) * 16 + 4 * g4),
+            make_float4(acc[0][j][0], acc[0][j][1], acc[0][j][2], acc[0][j][3]));
+}
+
+// LayerNorm (no affine, as ln_rows) of R <= 8 f32 rows Hs (stride SH) into the 16-row T image:
+// wave w normalises row w with all 64 lanes (4 columns each; sums over 16 lanes by DPP, then across
+// the wave's 4 lane rows), so the few rows of a block cost one short pass instead of 32 values per
+// lane on one wave; rows R .. 15 are written as zeros (waves w and w + 8)
+template <typename T>
+__device__ __forceinline__ void ln_rows_wave(const float* Hs, int R, T* img, int lane, int wave) {
+  const int c4 = 4 * lane;
+  const float4 v = *(const float4*)(Hs + min(wave, 7) * SH + c4);
+  const float mu = lanerow_sum4(group_sum<16>((v.x + v.y) + (v.z + v.w))) * (1.0f / (float)FD);
+  const float d0 = v.x - mu, d1 = v.y - mu, d2 = v.z - mu, d3 = v.w - mu;
+  const float q = lanerow_sum4(group_sum<16>((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3)));
+  const float rs = __builtin_amdgcn_rsqf(q * (1.0f / (float)FD) + 1e-5f);
+  const bool on = wave < R;  // a row past R holds stale LDS (maybe a NaN pattern): zeros, not 0 * x
+  const float y0 = on ? d0 * rs : 0.f, y1 = on ? d1 * rs : 0.f, y2 = on ? d2 * rs : 0.f, y3 = on ? d3 * rs : 0.f;
+  constexpr int SXI = Frag<T>::SX;
+  if constexpr (sizeof(T) == 2) {
+    *(uint2*)(img + wave * SXI + c4) = make_uint2(pk_bf16(y0, y1), pk_bf16(y2, y3));
+    *(uint2*)(img + (wave + 8) * SXI + c4) = make_uint2(0u, 0u);
+  } else {
+    *(float4*)(img + wave * SXI + c4) = make_float4(y0, y1, y2, y3);
+    *(float4*)(img + (wave + 8) * SXI + c4) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// the lane's PE + b_emb initial accumulators of emb_rows_store (row r0 + c16, clamped)
+template <typename FA>
+__device__ __forceinline__ void emb_init(const FA& a, int r0, int lane, int wave, float4 (&pe)[2]) {
+  const int c16 = lane & 15, g4 = lane >> 4, r = min(r0 + c16, a.L - 1);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = (2 * wave + j) * 16 + 4 * g4;
+    const float4 p = ld_f4(a.pe + (size_t)r * FD + col), bb = ld_f4(a.b_emb + col);
+    pe[j] = make_float4(p.x + bb.x, p.y + bb.y, p.z + bb.z, p.w + bb.w);
+  }
+}
+
+// the persistent loop's prologue: the first step's layer-0 residual rows from the initial x
+template <typename T, int CP, typename FA>
+__device__ __forceinline__ void emb_prologue(const FA& a, int p, int b, unsigned char* smem) {
+  using KP = KerPlan<T>;
+  constexpr int KTE = 128 / Frag<T>::KF;
+  const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
+  const int L = a.L, C = a.C, r0 = p * L / 8, R = (p + 1) * L / 8 - r0;
+  T* Xb = (T*)(smem + KP::HS + KP::XN + KP::E);
+  WGemm<T, 2, KTE, 1> ge(a.w_emb, KTE, 0);
+  ge.tiles[0] = 2 * wave;
+  ge.tiles[1] = 2 * wave + 1;
+  ge.load(0, lane);
+  float4 pe[2];
+  emb_init(a, r0, lane, wave, pe);
+  float xv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // 16 rows x 128 channels, 4 per thread
+    const int idx = tid + i * FT, l = idx >> 7, c = idx & 127;
+    xv[i] = ld_f32<CP>(a.x, (uint32_t)(((size_t)b * L + r0 + min(l, R - 1)) * C + min(c, C - 1)));
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + i * FT, l = idx >> 7, c = idx & 127;
+    Xb[l * KP::SB + c] = from_f32<T>(l < R && c < C ? xv[i] : 0.f);
+  }
+  __syncthreads();
+  emb_rows_store<T, CP>(a, b, r0, R, Xb, ge, pe, lane, wave);
+}
+
+template <typename T, int RT, int CP, typename FA>
+__device__ __forceinline__ void ker_phase(const FA& a, int p, int b, int k, unsigned char* smem, KEPre<T, RT>& pre) {
+  using KP = KerPlan<T>;
+  constexpr int KT = FD / Frag<T>::KF, KTE = 128 / Frag<T>::KF, SE = KP::SE, SB = KP::SB;
+  const int tid = ltid(), lane = tid & 63, wave = tid >> 6;
+  const int L = a.L, C = a.C, c16 = lane & 15, g4 = lane >> 4, LC = L * C;
+  const int r0 = p * L / 8, R = (p + 1) * L / 8 - r0;
+  using RS = Res<T, CP>;
+  unsigned char* kb = smem + RS::BASE;  // behind the resident residual rows (KC left them there)
+  float* Hs = (float*)kb;
+  T* Xn = (T*)(kb + KP::HS);
+  float* E = (float*)(kb + KP::HS + KP::XN);
+  T* Xb = (T*)(kb + KP::HS + KP::XN + KP::E);
+  static_assert(RS::BASE + KP::BYTES <= 160 * 1024 - 256, "KE rows LDS");
+  const size_t row0 = (size_t)b * L;
+  const int h = p;  // STAMP uses (h, b)
+
+  STAMP(0);
+  // the last layer's KD for the block's rows only: h = h_KC + (sum of the 8 FFN-down partials in
+  // chunk order + b2), kd_phase's arithmetic; thread (row i = tid / 64, columns 4 (tid % 64) ..)
+  // (without GGD_MK_FUSE_KD: the KD phase ran, the rows are staged from h)
+  const int si = tid >> 6, sc = 4 * (tid & 63), srow = min(r0 + max(min(si, R - 1), 0), L - 1);  // R = 0 when L < 8
+  if constexpr (!GGD_MK_FUSE_KD) glds_rows<FT, CP>(Hs, sizeof(float) * SH, a.h + (row0 + r0) * FD, sizeof(float) * FD, R, 1);
+  float4 part[8];
+#pragma unroll
+  for (int c = 0; c < (GGD_MK_FUSE_KD ? 8 : 0); ++c) {
+    const uint32_t off = (uint32_t)(sizeof(T) * ((((size_t)b * 8 + c) * L + srow) * FD + sc));
+    if constexpr (sizeof(T) == 2) {
+      const uint2 u = ld_8B<CP>(a.ffp, off);
+      part[c] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                            __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+    } else {
+      const uint4 u = ld_16B<CP>(a.ffp, off);
+      part[c] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+    }
+  }
+  float4 sres = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (!GGD_MK_FUSE_KD) {
+  } else if constexpr (RS::ON) {
+    sres = *(const float4*)((const float*)smem + srow * SH + sc);
+  } else {
+    const uint4 u = ld_16B<CP>(a.h, (uint32_t)(sizeof(float) * ((row0 + srow) * FD + sc)));
+    sres = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+  }
+  const float4 sb2 = GGD_MK_FUSE_KD ? ld_f4(a.ff2_b + sc) : make_float4(0.f, 0.f, 0.f, 0.f);
+  WGemm<T, 1, KT, 1> go(a.w_out, KT, 0);  // wave w: channel tile w (prefetched at the barrier)
+  go.tiles[0] = wave;
+#pragma unroll
+  for (int kk = 0; kk < KT; ++kk) go.wb[0][kk] = pre.g.wb[0][kk];
+  const float4 bo = ld_f4(a.b_out + wave * 16 + 4 * g4);
+  // the thread's quad (see above); its elements' state / noise loads are issued now.  Thread t
+  // takes channel t % 128 and the (t / 128)-th quad of it: with L % 4 == 0 every lane of a wave
+  // then holds the same frames, so each x store / load of the wave covers one frame row's
+  // consecutive channels (a few cache lines) instead of 64 scattered rows (C <= 128, E's rows)
+#if GGD_MK_CMAP
+  const int uc = tid & 127, qi = ((uc * L + r0) >> 2) + (tid >> 7);
+  const bool qon = uc < C && tid < 3 * 128;
+#else
+  const int uc = tid / 3, qi = ((uc * L + r0) >> 2) + (tid - 3 * uc);
+  const bool qon = uc < C;
+#endif
+  StepRec rec = ld_rec(a.steps + k);
+  float xq[4] = {0.f, 0.f, 0.f, 0.f}, zq[4] = {0.f, 0.f, 0.f, 0.f};
+  float mq[4] = {0.f, 0.f, 0.f, 0.f}, pq[4] = {0.f, 0.f, 0.f, 0.f}, tq[4] = {0.f, 0.f, 0.f, 0.f};
+  int ul[4];
+  bool uok[4];
+  const bool inp = a.inp_mask != nullptr;
+  const size_t plane = (size_t)a.n * LC;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    // element e = 4 qi + u is frame e - uc L of channel uc when that lies in [r0, r0 + R) (the quad
+    // starts at most 3 elements before the channel's frame r0: no division needed)
+    const int e = 4 * qi + u, lr = e - uc * L, l = min(max(lr, 0), L - 1);
+    ul[u] = l;
+    uok[u] = qon && lr >= r0 && lr < r0 + R;
+    const size_t gi = (row0 + l) * C + min(uc, C - 1);
+    xq[u] = ld_f32<CP>(a.x, (uint32_t)gi);
+    if (a.noise) zq[u] = G(a.noise)[(size_t)k * plane + (size_t)b * LC + min(e, LC - 1)];
+    if (inp) {
+      mq[u] = G(a.inp_mask)[row0 + l];
+      pq[u] = G(a.inp_pose)[gi];
+      tq[u] = G(a.trans)[l];
+    }
+  }
+  // emb operand pads: channels C..127 of every row and rows R..15 (the update fills the rest)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + i * FT, l = idx >> 7, c = idx & 127;
+    if (l >= R || c >= C) Xb[l * SB + c] = from_f32<T>(0.f);
+  }
+  __syncthreads();  // every operand above has landed
+  if (GGD_MK_FUSE_KD && si < R) {
+    float4 y = part[0];
+#pragma unroll
+    for (int c = 1; c < 8; ++c) {
+      y.x += part[c].x;
+      y.y += part[c].y;
+      y.z += part[c].z;
+      y.w += part[c].w;
+    }
+    *(float4*)(Hs + si * SH + sc) =
+        make_float4(sres.x + (y.x + sb2.x), sres.y + (y.y + sb2.y), sres.z + (y.z + sb2.z), sres.w + (y.w + sb2.w));
+  }
+  if constexpr (GGD_MK_FUSE_KD) bar_lds();
+  // the emb operands, in flight across LN_out, eps and the update (issued after the wait above, so
+  // that it does not hold for them)
+  WGemm<T, 2, KTE, 1> ge(a.w_emb, KTE, 0);
+  ge.tiles[0] = 2 * wave;
+  ge.tiles[1] = 2 * wave + 1;
+  ge.load(0, lane);
+  float4 pe[2];
+  emb_init(a, r0, lane, wave, pe);
+  ln_rows_wave<T>(Hs, R, Xn, lane, wave);
+  bar_lds();
+  STAMP(1);
+  if (16 * wave < C) {
+    f32x4 acc[1][1];
+    go.template run<true>(acc, Xn, Frag<T>::SX, lane);
+    *(float4*)(E + c16 * SE + 16 * wave + 4 * g4) =
+        make_float4(acc[0][0][0] + bo.x, acc[0][0][1] + bo.y, acc[0][0][2] + bo.z, acc[0][0][3] + bo.w);
+  }
+  if (qon && !a.noise)
+    philox_normal4(((uint64_t)rec.seed_hi << 32) | rec.seed_lo, rec.clip_offset + (uint32_t)b, (uint32_t)rec.i,
+                   TAG_STEP, (uint32_t)qi, zq);
+  bar_lds();
+  STAMP(2);
+  {
+    const OutRowsP<CP> xo(a.x, (uint32_t)(sizeof(float) * plane));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!uok[u]) continue;
+      const int l = ul[u], e = 4 * qi + u;
+      const float ev = E[(l - r0) * SE + uc];
+      const UpdOut o = upd_math(rec, a.alg, xq[u], ev, false, 0.f, inp, mq[u], pq[u], tq[u], zq[u]);
+      xo.template put<float>((uint32_t)((row0 + l) * C + uc), o.xn);
+      Xb[(l - r0) * SB + uc] = from_f32<T>(o.xn);
+      if (a.extras && (a.extras_k < 0 || k == a.extras_k)) {
+        const size_t ncl = (size_t)b * LC + e;
+        a.extras[0 * plane + ncl] = o.mean;
+        a.extras[1 * plane + ncl] = rec.var;
+        a.extras[2 * plane + ncl] = rec.logvar;
+        a.extras[3 * plane + ncl] = ev;
+        a.extras[4 * plane + ncl] = o.x0;
+        a.extras[5 * plane + ncl] = o.raw;
+      }
+    }
+  }
+  bar_lds();
+  STAMP(3);
+  emb_rows_store<T, CP>(a, b, r0, R, Xb, ge, pe, lane, wave);
+  STAMP_END(4);
 }
 
 }  // namespace ggd
