@@ -198,9 +198,13 @@ enum {
                                         instead of the whole-clip kernel (ggd_attn.hip) */
   GGD_ROUTE_LONG_LOOP = 7,           /* 1: never the long-clip persistent loop (ggd_long.hip): every
                                         step on launches (chains + whole-clip attention) */
-  GGD_ROUTE_SIMULATE_UNRESIDENT = 8  /* test hook, 1: the clip-group and clip-pair loops report status 2
+  GGD_ROUTE_SIMULATE_UNRESIDENT = 8, /* test hook, 1: the clip-group and clip-pair loops report status 2
                                         ("workgroups never all resident") without running, so the
                                         device-gated one-workgroup-per-clip fallback runs the clips */
+  GGD_ROUTE_FP8_MFMA = 9             /* GGD_FP8W long-clip loop: 0 the FFN and LayerNorm-projection GEMMs
+                                        on block-scaled fp8 MFMA (e4m3 activations, one e8m0 scale per
+                                        32 values), 1 the e4m3 weights widened into bf16 MFMAs (the
+                                        launch route's arithmetic, bit-equal to it) */
 };
 int ggd_set_route(ggd_ctx* ctx, int32_t knob, int32_t value);
 enum {

@@ -28,6 +28,7 @@ struct Lin {            // packed Linear: T [npad][kpad] (or e4m3 bytes + scale)
   float* b = nullptr;
   float* scale = nullptr;  // GGD_FP8W per-step Linears: per-output-channel dequantization scale
   void* wf = nullptr;      // row-block chain route: fragment-packed copy of w (ggd_chain.hip)
+  void* wmx = nullptr;     // GGD_FP8W long loop: e4m3 copy in the block-scaled fp8 MFMA's B order
   int n = 0, k = 0, npad = 0, kpad = 0;
 };
 
@@ -113,6 +114,8 @@ struct ggd_ctx {
   // long-clip persistent loop (ggd_long.hip): every step of clips of >= 96 frames in one launch
   bool long_ok = false;      // the shape and dtype have a long-loop instance (needs the chain weights)
   int long_off = 0;          // GGD_ROUTE_LONG_LOOP: 1 = never
+  int fp8_mfma_off = 0;      // GGD_ROUTE_FP8_MFMA: 1 = the long loop's fp8 weights widened into bf16 MFMAs
+  ChainStage* long_stages_mx = nullptr;  // the stage table with the F1 / F2 / P / P2 weights' MX copies
   LongLayer* long_layers = nullptr;
   bf16_t* long_kvc = nullptr;  // [layers][max_batch] convolved memory K / V^T (ggd_set_memory)
   ChainStage* long_stages = nullptr;
@@ -1481,6 +1484,12 @@ int ggd_finalize_weights(ggd_ctx* c) {
                  long_loop_supported(D.dtype, d, D.heads, D.seq_len, D.speech_len, C, c->out_lin.npad);
     if (c->long_ok) {
       TRY(pack(c->emb_x));
+      if (D.dtype == GGD_FP8W)  // the FFN / LN-projection weights the block-scaled stages read
+        for (Layer& Ly : c->layers)
+          for (Lin* L : {&Ly.qkv, &Ly.q_ca, &Ly.ff1, &Ly.ff2}) {
+            HIP_TRY(c, dalloc(c, &L->wmx, chain_pack_bytes(1, L->npad, L->kpad)));
+            HIP_TRY(c, launch_chain_pack(2, L->w, L->wmx, L->npad, L->kpad, c->stream));
+          }
       HIP_TRY(c, dalloc(c, &c->long_kvc, D.n_layers * long_kv_cache_bytes(D.max_batch, D.speech_len, D.heads)));
     }
   }
@@ -1746,6 +1755,9 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
     case GGD_ROUTE_LONG_LOOP:       // 1: never the long-clip persistent loop
       c->long_off = value != 0;
       return GGD_OK;
+    case GGD_ROUTE_FP8_MFMA:        // 1: the long loop's e4m3 weights widened into bf16 MFMAs
+      c->fp8_mfma_off = value != 0;
+      break;
     case GGD_ROUTE_SIMULATE_UNRESIDENT:  // test hook: co-resident loops report status 2, run nothing
       c->sim_unresident = value != 0;
       return GGD_OK;
@@ -2119,6 +2131,23 @@ int long_tables(ggd_ctx* c) {
       stage(b0 + 7, c->layers[0].qkv, c->layers[0].ln1_g, c->layers[0].ln1_b, c->qkv, 3 * d);
     }
   }
+  if (D.dtype == GGD_FP8W) {  // the same table with the block-scaled stages' weights on their MX copies
+    std::vector<ChainStage> mx = st;
+    auto use = [&](int i, const Lin& w) { mx[i].w.w = w.wmx; };
+    use(1, c->layers[0].qkv);
+    for (int li = 0; li < NL; ++li) {
+      const int b0 = 2 + LONG_STAGES_PER_LAYER * li;
+      use(b0 + 1, c->layers[li].q_ca);
+      use(b0 + 3, c->layers[li].ff1);
+      use(b0 + 4, c->layers[li].ff2);
+      if (li + 1 < NL) use(b0 + 5, c->layers[li + 1].qkv);
+      else use(b0 + 7, c->layers[0].qkv);
+    }
+    for (const ChainStage& x : mx)
+      if (x.w.scale && !x.w.w) return fail(c, GGD_ERR_STATE, "long-clip loop: missing block-scaled weight copy");
+    HIP_TRY(c, dalloc(c, &c->long_stages_mx, sizeof(ChainStage) * mx.size()));
+    HIP_TRY(c, hipMemcpy(c->long_stages_mx, mx.data(), sizeof(ChainStage) * mx.size(), hipMemcpyHostToDevice));
+  }
   HIP_TRY(c, dalloc(c, &c->long_layers, sizeof(LongLayer) * NL));
   HIP_TRY(c, dalloc(c, &c->long_stages, sizeof(ChainStage) * st.size()));
   HIP_TRY(c, dalloc(c, &c->long_ctl, sizeof(unsigned) * LONG_CTL_WORDS));
@@ -2162,7 +2191,8 @@ int run_long(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
   for (int c0i = 0, ci = 0; c0i < a.n; c0i += cap, ++ci) {
     LongArgs la{};
     la.layers = c->long_layers;
-    la.stages = c->long_stages;
+    const bool mx = D.dtype == GGD_FP8W && !c->fp8_mfma_off;
+    la.stages = mx ? c->long_stages_mx : c->long_stages;
     la.n_layers = D.n_layers;
     la.n = a.n;
     la.L = L;
@@ -2189,7 +2219,7 @@ int run_long(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
     la.ctl = c->long_ctl;
     la.status = c->long_status + ci;
     la.stamps = ci == 0 ? c->long_stamps : nullptr;
-    HIP_TRY(c, launch_long_loop(D.dtype == GGD_FP8W, la, std::min(cap, a.n - c0i), s));
+    HIP_TRY(c, launch_long_loop(mx ? 2 : D.dtype == GGD_FP8W ? 1 : 0, la, std::min(cap, a.n - c0i), s));
   }
   if (c->profiling && (r = prof_mark(c, s))) return r;
   int st[MEGA_MAX_CHUNKS];

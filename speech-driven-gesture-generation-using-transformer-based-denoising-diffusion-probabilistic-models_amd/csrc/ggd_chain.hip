@@ -243,7 +243,8 @@ __global__ void __launch_bounds__(CH_NT) chain_kernel(ChainArgs a) {
 }
 
 // row-major W [npad][kpad] (bf16 or e4m3 bytes) -> the fragment-packed copy, one 16-byte unit per thread
-template <bool W8>
+// MX: the block-scaled MFMA's B order (ggd_chainlib.h: unit u of chunk c = step u / 2, half u % 2)
+template <bool W8, bool MX = false>
 __global__ void chain_pack_kernel(const unsigned char* __restrict__ src, unsigned char* __restrict__ dst, int npad,
                                   int kpad) {
   const int upt = W8 ? kpad / 64 : kpad / 32;
@@ -253,7 +254,10 @@ __global__ void chain_pack_kernel(const unsigned char* __restrict__ src, unsigne
   const int lane = (int)(e % 64), u = (int)((e / 64) % upt), nt = (int)(e / (64 * upt));
   const int row = nt * 16 + (lane & 15), g = lane >> 4;
   uint4 out;
-  if constexpr (W8) {
+  if constexpr (MX) {
+    const int c = u >> 2, st = (u >> 1) & 1, hf = u & 1;
+    out = *(const uint4*)(src + (size_t)row * kpad + 256 * c + 128 * st + 32 * g + 16 * hf);
+  } else if constexpr (W8) {
     const unsigned char* r = src + (size_t)row * kpad + 64 * u + 8 * g;
     const uint2 lo = *(const uint2*)r, hi = *(const uint2*)(r + 32);
     out = make_uint4(lo.x, lo.y, hi.x, hi.y);
@@ -275,7 +279,10 @@ hipError_t launch_chain_pack(int w8, const void* src, void* dst, int npad, int k
   if (!src || !dst || npad <= 0 || npad % 64 || kpad <= 0 || kpad % 256) return hipErrorInvalidValue;
   const long units = (long)npad * kpad * (w8 ? 1 : 2) / 16;
   const int blocks = (int)((units + 255) / 256);
-  if (w8)
+  if (w8 == 2)  // e4m3 in the block-scaled MFMA's B order
+    hipLaunchKernelGGL((chain_pack_kernel<true, true>), dim3(blocks), dim3(256), 0, s, (const unsigned char*)src,
+                       (unsigned char*)dst, npad, kpad);
+  else if (w8)
     hipLaunchKernelGGL(chain_pack_kernel<true>, dim3(blocks), dim3(256), 0, s, (const unsigned char*)src,
                        (unsigned char*)dst, npad, kpad);
   else

@@ -115,6 +115,72 @@ __device__ __forceinline__ void ch_layernorm(const float* hs, const float* gm, c
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Block-scaled fp8 MFMA (long-clip loop, GGD_ROUTE_FP8_MFMA): v_mfma_scale_f32_16x16x128_f8f6f4
+// with e4m3 activations AND e4m3 weights -- K = 128 per instruction at twice the cycles of the
+// bf16 16x16x32 form, i.e. 2x the bf16 rate (MI355X_MICROARCH.md:432), and no fp8 -> bf16
+// widening of the weights.  Lane map (scripts/mx_probe.hip, checked on the GPU with exact
+// integers and non-unit scales): lane l holds A[l & 15][32 (l >> 4) + j] and B[32 (l >> 4) + j][l & 15],
+// j < 32, and its e8m0 scale operand scales exactly that 32-value block.
+//   Activations: one e8m0 scale per (row, 32 consecutive k) -- the MX block -- chosen from the
+//   block's max |v| = 1.f 2^E as 2^(E - 7), so the block's values land below 256 < 448 (no
+//   saturation) and keep e4m3's relative precision down to max / 2^13.
+//   Weights: the context's per-output-channel e4m3 quantisation (scale amax / 448, applied in
+//   the epilogue exactly as the bf16-widened route), MFMA scale operand 2^0.
+// MX weight packing (chain_pack_kernel<true, true>): unit u of a 256-k chunk = MFMA step s = u / 2,
+// half h = u % 2: lane (g, r16) bytes e < 16 = W[16 nt + r16][256 c + 128 s + 32 g + 16 h + e], so
+// units 2s, 2s + 1 of a lane are its 32 B operand bytes of step s, in k order.
+constexpr int XS8_STR = CH_D + 16;   // fp8 A rows (bytes; 68 dwords: consecutive rows 4 banks apart)
+constexpr int HH8_STR = CH_FF + 16;  // fp8 hidden rows (bytes)
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// e8m0 block scale byte of a block whose max |v| is m (>= 0): 2^(E - 7) for m = 1.f 2^E, clamped so
+// that the quantisation multiplier 2^(7 - E) stays a normal f32
+__device__ __forceinline__ unsigned mx_scale_byte(float m) {
+  const int be = (int)((__float_as_uint(m) >> 23) & 0xff);
+  return (unsigned)min(max(be - 7, 2), 253);
+}
+// the multiplier that maps the block into e4m3: 2^-(sb - 127)
+__device__ __forceinline__ float mx_mul(unsigned sb) { return __uint_as_float((254u - sb) << 23); }
+// 4 f32 -> 4 e4m3 bytes (round to nearest even), byte i = value i
+__device__ __forceinline__ unsigned mx_pack4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (unsigned)w;
+}
+// max over lanes l ^ 1, l ^ 2, ..., l ^ (N / 2) (N lanes: a power of two <= 16)
+template <int N>
+__device__ __forceinline__ float mx_group_max(float v) {
+#pragma unroll
+  for (int o = 1; o < N; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// acc[i][j] += A8[16 i + .][256 c + .] . W[16 (nt0 + j) + .][256 c + .]^T over the chunk's 256 k:
+// two block-scaled MFMAs per (row tile, column tile).  A8: fp8 rows (stride sa bytes), As8: their
+// e8m0 scale bytes [32 rows][nb blocks]
+template <int TGB>
+__device__ __forceinline__ void ch_mma_mx(const BBuf<true, TGB>& B, const unsigned char* A8, int sa,
+                                          const unsigned char* As8, int nb, int c, int lane, f32x4 (&acc)[2][TGB],
+                                          int tg) {
+  const int r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int k = 256 * c + 128 * s + 32 * g, blk = 8 * c + 4 * s + g;
+    const i32x8 a0 = *(const i32x8*)(A8 + r16 * sa + k);
+    const i32x8 a1 = *(const i32x8*)(A8 + (16 + r16) * sa + k);
+    const int s0 = As8[r16 * nb + blk], s1 = As8[(16 + r16) * nb + blk];
+#pragma unroll
+    for (int j = 0; j < TGB; ++j) {
+      if (j >= tg) continue;
+      const uint4 u0 = B.v[j][2 * s], u1 = B.v[j][2 * s + 1];
+      const i32x8 bw = {(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
+      acc[0][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a0, bw, acc[0][j], 0, 0, 0, s0, 0, 127);
+      acc[1][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a1, bw, acc[1][j], 0, 0, 0, s1, 0, 127);
+    }
+  }
+}
+
 // acc + bias (and the fp8 per-channel scale) of column n: gemm_kernel's expression; prm = the
 // stage's LDS parameters [bias[npad] | scale[npad]]
 template <bool W8>

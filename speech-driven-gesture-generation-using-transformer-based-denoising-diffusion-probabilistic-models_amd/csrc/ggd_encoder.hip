@@ -830,18 +830,32 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_nhwc_kernel(ConvArgs a) {
     put();
     __syncthreads();
     if (ck + 1 < cch) fetch(ck + 1);
+    // the LDS operands of tap + 1 are read before the MFMAs of tap issue (a fence keeps the
+    // scheduler from sinking each read next to its MFMA): the LDS latency overlaps the matrix work
+    bf16x8 bv[2], av[NJ], bn[2], an[NJ];
+    auto rd = [&](int tap, bf16x8(&b)[2], bf16x8(&w)[NJ]) __attribute__((always_inline)) {
+      const int toff = (tap / KS) * GE::PW + tap % KS;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) b[i] = *(const bf16x8*)(patch + (pbase[i] + toff) * CL_CS + g * 8);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) w[j] = *(const bf16x8*)(wl + ((j * 16 + r16) * GE::TAPS + tap) * CL_CS + g * 8);
+    };
+    rd(0, bv, av);
 #pragma unroll
     for (int tap = 0; tap < GE::TAPS; ++tap) {
-      const int toff = (tap / KS) * GE::PW + tap % KS;
-      bf16x8 bv[2], av[NJ];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) bv[i] = *(const bf16x8*)(patch + (pbase[i] + toff) * CL_CS + g * 8);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) av[j] = *(const bf16x8*)(wl + ((j * 16 + r16) * GE::TAPS + tap) * CL_CS + g * 8);
+      if (tap + 1 < GE::TAPS) rd(tap + 1, bn, an);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[j], bv[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (tap + 1 < GE::TAPS) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) bv[i] = bn[i];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) av[j] = an[j];
+      }
     }
   }
   // epilogue: lane (pixel r16 of tile i, group g) holds output channels 16 j + 4 g .. + 3

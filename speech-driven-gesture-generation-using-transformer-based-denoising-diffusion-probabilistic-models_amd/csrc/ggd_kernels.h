@@ -296,12 +296,16 @@ constexpr int LONG_STAMPS = 64;
 // launchers (return hipError_t of the launch)
 bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C, int out_npad);
 int long_loop_capacity();   // clips per launch
+// w8: 0 bf16 weights, 1 e4m3 weights widened into bf16 MFMAs, 2 e4m3 weights AND activations on
+// block-scaled fp8 MFMA in the FFN / LayerNorm-projection stages (a.stages' F1 / F2 / P / P2 weights
+// then hold launch_chain_pack(2, ...) copies)
 hipError_t launch_long_loop(int w8, const LongArgs& a, int G, hipStream_t s);
 // step-invariant convolved memory K / V^T of one layer for the long loop (keys 0, 1 and >= 1 + Ts zero)
 hipError_t launch_long_kv_cache(const float* kv_mem, const float* kw, const float* kb, const float* vw, const float* vb,
                                 int n, int Ts, int heads, bf16_t* out, hipStream_t s);
 size_t long_kv_cache_bytes(int n, int Ts, int heads);
 hipError_t launch_chain(int w8, const ChainArgs& a, hipStream_t s);
+// w8: 0 bf16, 1 e4m3 (bf16-widened chain order), 2 e4m3 in the block-scaled fp8 MFMA's B order
 hipError_t launch_chain_pack(int w8, const void* src, void* dst, int npad, int kpad, hipStream_t s);
 size_t chain_pack_bytes(int w8, int npad, int kpad);
 bool chain_p_supported(int npad);   // P stage widths with a kernel instance

@@ -173,6 +173,43 @@ __device__ __forceinline__ void lk_layernorm(const float* hs, const float* gm, c
   }
 }
 
+// lk_layernorm into the block-scaled fp8 A image (MX stages): the same statistics and normalised
+// values, then per (row, 32 columns) the e8m0 block scale over the 8 lanes that hold the block
+// (a wave covers one row per pass) and 4 e4m3 bytes per lane.  xs8: [32][XS8_STR] bytes, sc: [32][8]
+__device__ __forceinline__ void lk_layernorm_mx(const float* hs, const float* gm, const float* bt, unsigned char* xs8,
+                                                unsigned char* sc, float* st) {
+  const int tid = ltid();
+  if (tid < CH_MT * 4) {
+    const int r = tid >> 2, j = tid & 3;
+    float4 v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = *(const float4*)(hs + r * HS_STR + (j + 4 * i) * 4);
+    float mu, rs;
+    ln_stats4<16>(v, (float)CH_D, mu, rs);
+    if (j == 0) {
+      st[2 * r] = mu;
+      st[2 * r + 1] = rs;
+    }
+  }
+  ch_bar();
+  static_assert(CH_MT * CH_D / 4 % CH_NT == 0 && CH_NT % (CH_D / 4) == 0, "a wave pass is one whole row");
+#pragma unroll
+  for (int i = 0; i < CH_MT * CH_D / 4 / CH_NT; ++i) {
+    const int e = tid + i * CH_NT, r = e / (CH_D / 4), k = (e % (CH_D / 4)) * 4;
+    const float mu = st[2 * r], rs = st[2 * r + 1];
+    const float4 x = *(const float4*)(hs + r * HS_STR + k);
+    const float4 g = *(const float4*)(gm + k);
+    const float4 b = *(const float4*)(bt + k);
+    const float y0 = (x.x - mu) * rs * g.x + b.x, y1 = (x.y - mu) * rs * g.y + b.y;
+    const float y2 = (x.z - mu) * rs * g.z + b.z, y3 = (x.w - mu) * rs * g.w + b.w;
+    const float m = mx_group_max<8>(fmaxf(fmaxf(fabsf(y0), fabsf(y1)), fmaxf(fabsf(y2), fabsf(y3))));
+    const unsigned sb = mx_scale_byte(m);
+    const float mul = mx_mul(sb);
+    *(unsigned*)(xs8 + r * XS8_STR + k) = mx_pack4(y0 * mul, y1 * mul, y2 * mul, y3 * mul);
+    if ((tid & 7) == 0) sc[r * (CH_D / 32) + k / 32] = (unsigned char)sb;
+  }
+}
+
 // stage arguments and layers live in constant memory: field reads are scalar loads
 typedef const __attribute__((address_space(4))) ChainStage* cst_t;
 typedef const __attribute__((address_space(4))) LongArgs cla_T;  // the kernel's argument block, in place
@@ -246,18 +283,39 @@ __device__ __forceinline__ void lk_update(X& x, bool to_xs) {
     }
 }
 
-template <bool W8, int KIND, int IT, class X>
+// MX (w8 = 2): the FFN and LayerNorm-projection stages run on block-scaled fp8 MFMA; their A images
+// live in the xs / hh regions as e4m3 bytes, the e8m0 block scales behind the fp8 hidden rows
+// (the attention output projections, out_layers and emb_x keep the bf16-widened route)
+constexpr size_t LK_HSC = (size_t)CH_MT * HH8_STR;           // hh region: hidden block scales [32][32]
+constexpr size_t LK_XSC = LK_HSC + (size_t)CH_MT * (CH_FF / 32);  //            LN block scales [32][8]
+static_assert(LK_XSC + CH_MT * (CH_D / 32) <= sizeof(bf16_t) * CH_MT * HH_STR, "MX images fit the hh region");
+static_assert(CH_MT * XS8_STR <= sizeof(bf16_t) * CH_MT * XS_STR, "fp8 A rows fit the xs region");
+static_assert(LK_XSC >= sizeof(float) * CH_MT * EPS_STR, "eps rows (out_layers) stay clear of the LN scales");
+template <int KIND, int si, bool MX>
+constexpr bool lk_mx() {
+  constexpr int k = LkPlan<KIND>::s[si].kind;
+  return MX && (k == SK_F1 || k == SK_F2 || k == SK_P || k == SK_P2);
+}
+
+template <bool W8, int KIND, int IT, bool MX, class X>
 __device__ __forceinline__ void lk_iter(X& x) {
   using GE = LkGeo<W8, KIND>;
   using PL = LkPlan<KIND>;
   constexpr int TGB = GE::TGB, D1 = LK_DEPTH - 1;
   constexpr int si = GE::stage_of(IT), l = IT - GE::first(si), tg = GE::tg(si), nch = PL::s[si].nch;
   constexpr int kind = PL::s[si].kind;
+  constexpr bool mx = lk_mx<KIND, si, MX>();
+  static_assert(!MX || W8, "block-scaled fp8 needs e4m3 weights");
+  unsigned char* const xs8 = (unsigned char*)x.xs;
+  unsigned char* const hh8 = (unsigned char*)x.hh;
   if constexpr (IT + D1 < GE::TOTAL) lk_issue<W8, KIND, IT + D1>(x);
   if constexpr (l == 0 && si > 0) {  // stage hand-offs (LDS); the prefetched weights stay in flight
     ch_bar();
     if constexpr (kind == SK_F1 || kind == SK_P || kind == SK_PO || kind == SK_P2) {
-      lk_layernorm(x.hs, x.prm + GE::ln(si), x.prm + GE::ln(si) + CH_D, x.xs, x.prm + GE::PRM_TOTAL);
+      if constexpr (mx)
+        lk_layernorm_mx(x.hs, x.prm + GE::ln(si), x.prm + GE::ln(si) + CH_D, xs8, hh8 + LK_XSC, x.prm + GE::PRM_TOTAL);
+      else
+        lk_layernorm(x.hs, x.prm + GE::ln(si), x.prm + GE::ln(si) + CH_D, x.xs, x.prm + GE::PRM_TOTAL);
       ch_bar();
     } else if constexpr (kind == SK_E) {  // after out_layers: the update, its x rows feed emb_x
       lk_update(x, true);
@@ -272,11 +330,37 @@ __device__ __forceinline__ void lk_iter(X& x) {
 #pragma unroll
       for (int j = 0; j < TGB; ++j) x.acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  if constexpr (kind == SK_F2)
+  if constexpr (mx) {
+    if constexpr (kind == SK_F2)
+      ch_mma_mx<TGB>(x.bb[IT % LK_DEPTH], hh8, HH8_STR, hh8 + LK_HSC, CH_FF / 32, c, x.lane, x.acc, tg);
+    else
+      ch_mma_mx<TGB>(x.bb[IT % LK_DEPTH], xs8, XS8_STR, hh8 + LK_XSC, CH_D / 32, c, x.lane, x.acc, tg);
+  } else if constexpr (kind == SK_F2) {
     ch_mma<W8, TGB>(x.bb[IT % LK_DEPTH], x.hh, HH_STR, c, x.lane, x.acc, tg);
-  else
+  } else {
     ch_mma<W8, TGB>(x.bb[IT % LK_DEPTH], x.xs, XS_STR, c, x.lane, x.acc, tg);
-  if constexpr (c == nch - 1) {
+  }
+  if constexpr (c == nch - 1 && mx && kind == SK_F1) {  // ReLU^2 hidden rows -> e4m3 + block scales
+    static_assert(tg == 2, "a lane's two column tiles are one 32-column block");
+    constexpr int np = PL::s[si].ncols;
+    const float* pp = x.prm + GE::prm(si);
+    const int n0 = nt0 * 16 + x.c16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i * 16 + x.g4 + r;
+        const float v0 = fmaxf(ch_val<W8>(pp, np, x.acc[i][0][r], n0), 0.f);
+        const float v1 = fmaxf(ch_val<W8>(pp, np, x.acc[i][1][r], n0 + 16), 0.f);
+        const float y0 = v0 * v0, y1 = v1 * v1;
+        const unsigned sb = mx_scale_byte(mx_group_max<16>(fmaxf(y0, y1)));
+        const float mul = mx_mul(sb);
+        const int w = __builtin_amdgcn_cvt_pk_fp8_f32(y0 * mul, y1 * mul, 0, false);
+        hh8[row * HH8_STR + n0] = (unsigned char)(w & 0xff);
+        hh8[row * HH8_STR + n0 + 16] = (unsigned char)((w >> 8) & 0xff);
+        if (x.c16 == 0) hh8[LK_HSC + row * (CH_FF / 32) + nt0 / 2] = (unsigned char)sb;
+      }
+  } else if constexpr (c == nch - 1) {
     constexpr int np = PL::s[si].ncols;
     const float* pp = x.prm + GE::prm(si);
     const int L = x.a.L, l0 = x.part * CH_MT;
@@ -305,11 +389,11 @@ __device__ __forceinline__ void lk_iter(X& x) {
         }
       }
   }
-  if constexpr (IT + 1 < GE::TOTAL) lk_iter<W8, KIND, IT + 1>(x);
+  if constexpr (IT + 1 < GE::TOTAL) lk_iter<W8, KIND, IT + 1, MX>(x);
 }
 
 // one chain phase of row block `part` of clip b
-template <bool W8, int KIND>
+template <bool W8, int KIND, bool MX>
 __device__ __forceinline__ void lk_chain(cla_T& a, cst_t sa, int b, int part, int it,
                                                    unsigned char* smem) {
   using GE = LkGeo<W8, KIND>;
@@ -357,7 +441,7 @@ __device__ __forceinline__ void lk_chain(cla_T& a, cst_t sa, int b, int part, in
     }
   }
   ch_bar();
-  lk_iter<W8, KIND, 0>(x);
+  lk_iter<W8, KIND, 0, MX>(x);
   if constexpr (KIND == K_BLL) {  // the last step: update only
     ch_bar();
     lk_update(x, false);
@@ -558,7 +642,7 @@ size_t lk_attn_lds(int L, int Lk) {
 // ------------------------------------------------------------------------------------------
 // the persistent loop
 // ------------------------------------------------------------------------------------------
-template <bool W8>
+template <bool W8, bool MX>
 __global__ void __launch_bounds__(CH_NT) lk_kernel(LongArgs args, int G) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_role, s_ok;
@@ -595,7 +679,7 @@ __global__ void __launch_bounds__(CH_NT) lk_kernel(LongArgs args, int G) {
       lk_attn<false>(a, lay + li, b, part, t_orig, smem + LK_HS, stamps && k == 1 && li == 0 ? stamps + 56 : nullptr);
       if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
       stamp();
-      if (rows) lk_chain<W8, K_A>(a, sl, b, part, it, smem);         // R(o_sa) + P(LN2, q_ca)
+      if (rows) lk_chain<W8, K_A, MX>(a, sl, b, part, it, smem);         // R(o_sa) + P(LN2, q_ca)
       if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
       stamp();
       lk_attn<true>(a, lay + li, b, part, t_orig, smem + LK_HS, stamps && k == 1 && li == 0 ? stamps + 60 : nullptr);
@@ -603,11 +687,11 @@ __global__ void __launch_bounds__(CH_NT) lk_kernel(LongArgs args, int G) {
       stamp();
       if (rows) {
         if (li + 1 < NL)
-          lk_chain<W8, K_B>(a, sl + 2, b, part, it, smem);             // R(o_ca) + F + P(next LN1, QKV)
+          lk_chain<W8, K_B, MX>(a, sl + 2, b, part, it, smem);             // R(o_ca) + F + P(next LN1, QKV)
         else if (k + 1 < a.n_steps)
-          lk_chain<W8, K_BL>(a, sl + 2, b, part, it, smem);            // ... + out_layers, update, emb_x, LN1 + QKV
+          lk_chain<W8, K_BL, MX>(a, sl + 2, b, part, it, smem);            // ... + out_layers, update, emb_x, LN1 + QKV
         else
-          lk_chain<W8, K_BLL>(a, sl + 2, b, part, it, smem);           // ... + out_layers, update
+          lk_chain<W8, K_BLL, MX>(a, sl + 2, b, part, it, smem);           // ... + out_layers, update
       }
       if (k + 1 < a.n_steps || li + 1 < NL)
         if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
@@ -660,14 +744,16 @@ hipError_t launch_long_loop(int w8, const LongArgs& a, int G, hipStream_t s) {
   const size_t lds = w8 ? lk_lds<true>(a.L, 1 + a.Ts) : lk_lds<false>(a.L, 1 + a.Ts);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)lk_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
-    (void)hipFuncSetAttribute((const void*)lk_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+    (void)hipFuncSetAttribute((const void*)lk_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+    (void)hipFuncSetAttribute((const void*)lk_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+    (void)hipFuncSetAttribute((const void*)lk_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
     (void)hipGetLastError();
     attr = true;
   }
   const int nwg = 64 * ((G + 7) / 8);
-  if (w8) hipLaunchKernelGGL(lk_kernel<true>, dim3(nwg), dim3(CH_NT), lds, s, a, G);
-  else hipLaunchKernelGGL(lk_kernel<false>, dim3(nwg), dim3(CH_NT), lds, s, a, G);
+  if (w8 == 2) hipLaunchKernelGGL((lk_kernel<true, true>), dim3(nwg), dim3(CH_NT), lds, s, a, G);
+  else if (w8) hipLaunchKernelGGL((lk_kernel<true, false>), dim3(nwg), dim3(CH_NT), lds, s, a, G);
+  else hipLaunchKernelGGL((lk_kernel<false, false>), dim3(nwg), dim3(CH_NT), lds, s, a, G);
   return hipGetLastError();
 }
 

@@ -16,6 +16,7 @@ pytestmark = pytest.mark.gpu
 D_POSE, L, WAV = 123, 40, 32000
 ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_PAIR_WT, ROUTE_PHASE_LAUNCHES = 0, 1, 2, 3   # include/ggd.h GGD_ROUTE_*
 ROUTE_GEMM_LAUNCHES, ROUTE_ATTN_QSPLIT, ROUTE_LONG_LOOP, ROUTE_SIM_UNRESIDENT = 5, 6, 7, 8
+ROUTE_FP8_MFMA = 9
 INFO_PER_CLIP_AVAILABLE, INFO_PAIR_LAUNCHES, INFO_CHAIN_AVAILABLE, INFO_LONG_LAUNCHES = 0, 2, 5, 6  # GGD_INFO_*
 INFO_CLIP_ATTN_LAUNCHES, INFO_GATED_FALLBACKS = 7, 8
 
@@ -332,19 +333,31 @@ def test_denoise_fp8_weights(pkg, beat_cfg, setup, setup_fp8, Lc, wav_len, n):
     assert err_f <= 1e-1, err_f
 
 
-def test_sample_fp8_weights_long_clip(pkg, beat_cfg, setup, setup_fp8):
-    """C4: L = 160 DDPM steps on injected noise vs the oracle loop on the dequantized weights."""
+@pytest.mark.parametrize("mfma,eps_bound", [(0, 1e-1), (1, 2e-2)])
+def test_sample_fp8_weights_long_clip(pkg, beat_cfg, setup, setup_fp8, mfma, eps_bound):
+    """C4: L = 160 DDPM steps on injected noise vs the oracle loop on the dequantized weights.
+    mfma 0 (default): the long loop's FFN / LN-projection GEMMs on block-scaled fp8 MFMA (e4m3
+    activations: SURVEY.md 8d's fp8 bound, eps rel-RMS <= 1e-1); 1: e4m3 weights widened into bf16
+    MFMAs (only bf16 activation rounding: 2e-2)."""
     model, diffusion = make_model(pkg, beat_cfg, setup[1], "fp8")
     n, steps, Lc = 2, 5, 160
     wav, x, _ = inputs(n, seed=33, wav_len=128000, L_=Lc)
     zs = th.randn(steps, n, D_POSE, Lc, generator=th.Generator().manual_seed(34))
-    out = diffusion.p_sample_loop(model, (n, D_POSE, Lc), model_kwargs={"wav": wav.cuda()}, noise=x.cuda(),
-                                  step_noise=zs.cuda(), n_steps=steps)
+    ctx, _ = model.prepare(wav.cuda(), Lc)
+    try:
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, mfma) == 0
+        out = diffusion.p_sample_loop(model, (n, D_POSE, Lc), model_kwargs={"wav": wav.cuda()}, noise=x.cuda(),
+                                      step_noise=zs.cuda(), n_steps=steps, sync=True)
+        assert int(_info(ctx, INFO_LONG_LAUNCHES)) == 1
+    finally:
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0)
     sch = ref_diffusion.make_schedule("linear", 1000, "")
     want = ref_diffusion.sample_loop(sch, setup_fp8, (n, D_POSE, Lc), {"wav": wav},
                                      ref_diffusion.InjectedNoise(x, zs), "ddpm", x_T=x, n_steps=steps)
-    assert rel_rms(out["sample"].cpu(), want["sample"]) <= 5e-2
-    assert rel_rms(out["eps"].cpu(), want["eps"]) <= 2e-2
+    e_s, e_e = rel_rms(out["sample"].cpu(), want["sample"]), rel_rms(out["eps"].cpu(), want["eps"])
+    print(f"fp8 long clip, GGD_ROUTE_FP8_MFMA {mfma}: sample rel-RMS {e_s:.2e}, last eps rel-RMS {e_e:.2e}")
+    assert e_s <= 5e-2
+    assert e_e <= eps_bound
 
 
 # ------------------------------------------------------------------------------------------
@@ -694,6 +707,9 @@ def test_long_loop_equals_launch_route(pkg, beat_cfg, setup, setup_fp8, dtype, n
         return loop(model, (n, D_POSE, Lc), model_kwargs={"wav": wav.cuda()}, **kw)
 
     try:
+        # fp8: the loop with its e4m3 weights widened into bf16 MFMAs -- the launch route's arithmetic
+        # (the default block-scaled fp8 stages have no launch-route twin; checked against the oracle)
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 1) == 0
         out_l = run()
         launches = int(_info(ctx, INFO_LONG_LAUNCHES))
         assert ctx.lib.ggd_set_route(ctx.h, ROUTE_LONG_LOOP, 1) == 0
@@ -701,6 +717,7 @@ def test_long_loop_equals_launch_route(pkg, beat_cfg, setup, setup_fp8, dtype, n
         assert int(_info(ctx, INFO_LONG_LAUNCHES)) == 0
     finally:
         ctx.lib.ggd_set_route(ctx.h, ROUTE_LONG_LOOP, 0)
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0)
     assert launches == (n + 31) // 32
     for k in ("sample", "eps"):
         assert th.equal(out_l[k].cpu(), out_r[k].cpu()), k
