@@ -453,7 +453,8 @@ def main():
     ctx = model.context(L, enc.speech_len(arch["type"], wav_len), B)
     lib = ctx.lib
     mx = args.dtype == "fp8" and not args.no_fp8_mfma   # block-scaled fp8 MFMA in the long loop (default)
-    assert lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0 if mx else 1) == 0
+    if args.dtype == "fp8":
+        assert lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0 if mx else 1) == 0
     prof = not args.no_profile
     for w in range(args.warmup):
         log(f"warm-up pass {w}")

@@ -1757,7 +1757,7 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
       return GGD_OK;
     case GGD_ROUTE_FP8_MFMA:        // 1: the long loop's e4m3 weights widened into bf16 MFMAs
       c->fp8_mfma_off = value != 0;
-      break;
+      return GGD_OK;
     case GGD_ROUTE_SIMULATE_UNRESIDENT:  // test hook: co-resident loops report status 2, run nothing
       c->sim_unresident = value != 0;
       return GGD_OK;

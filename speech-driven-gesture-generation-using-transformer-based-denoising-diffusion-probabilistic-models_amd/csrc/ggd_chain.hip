@@ -256,7 +256,7 @@ __global__ void chain_pack_kernel(const unsigned char* __restrict__ src, unsigne
   uint4 out;
   if constexpr (MX) {
     const int c = u >> 2, st = (u >> 1) & 1, hf = u & 1;
-    out = *(const uint4*)(src + (size_t)row * kpad + 256 * c + 128 * st + 32 * g + 16 * hf);
+    out = *(const uint4*)(src + (size_t)row * kpad + 256 * c + 128 * st + 64 * hf + 16 * g);
   } else if constexpr (W8) {
     const unsigned char* r = src + (size_t)row * kpad + 64 * u + 8 * g;
     const uint2 lo = *(const uint2*)r, hi = *(const uint2*)(r + 32);

@@ -119,17 +119,19 @@ __device__ __forceinline__ void ch_layernorm(const float* hs, const float* gm, c
 // Block-scaled fp8 MFMA (long-clip loop, GGD_ROUTE_FP8_MFMA): v_mfma_scale_f32_16x16x128_f8f6f4
 // with e4m3 activations AND e4m3 weights -- K = 128 per instruction at twice the cycles of the
 // bf16 16x16x32 form, i.e. 2x the bf16 rate (MI355X_MICROARCH.md:432), and no fp8 -> bf16
-// widening of the weights.  Lane map (scripts/mx_probe.hip, checked on the GPU with exact
-// integers and non-unit scales): lane l holds A[l & 15][32 (l >> 4) + j] and B[32 (l >> 4) + j][l & 15],
-// j < 32, and its e8m0 scale operand scales exactly that 32-value block.
+// widening of the weights.  Lane map (scripts/mx_probe.hip, profiles/r04l_mx_probe.txt: the one of
+// four hypotheses that reproduces exact integer products with non-unit A and B scales): lane l,
+// g = l >> 4, holds bytes j < 16 = k 16 g + j and bytes 16 + j = k 64 + 16 g + j of row l & 15 (A)
+// / column l & 15 (B); its e8m0 scale operand scales the 32-value block k 32 g .. 32 g + 31 of
+// that row / column -- a block whose values other lanes hold.
 //   Activations: one e8m0 scale per (row, 32 consecutive k) -- the MX block -- chosen from the
 //   block's max |v| = 1.f 2^E as 2^(E - 7), so the block's values land below 256 < 448 (no
 //   saturation) and keep e4m3's relative precision down to max / 2^13.
 //   Weights: the context's per-output-channel e4m3 quantisation (scale amax / 448, applied in
 //   the epilogue exactly as the bf16-widened route), MFMA scale operand 2^0.
 // MX weight packing (chain_pack_kernel<true, true>): unit u of a 256-k chunk = MFMA step s = u / 2,
-// half h = u % 2: lane (g, r16) bytes e < 16 = W[16 nt + r16][256 c + 128 s + 32 g + 16 h + e], so
-// units 2s, 2s + 1 of a lane are its 32 B operand bytes of step s, in k order.
+// half h = u % 2: lane (g, r16) bytes e < 16 = W[16 nt + r16][256 c + 128 s + 64 h + 16 g + e], so
+// units 2s, 2s + 1 of a lane are its 32 B operand bytes of step s in the MFMA's order.
 constexpr int XS8_STR = CH_D + 16;   // fp8 A rows (bytes; 68 dwords: consecutive rows 4 banks apart)
 constexpr int HH8_STR = CH_FF + 16;  // fp8 hidden rows (bytes)
 typedef int i32x8 __attribute__((ext_vector_type(8)));
@@ -166,9 +168,11 @@ __device__ __forceinline__ void ch_mma_mx(const BBuf<true, TGB>& B, const unsign
   const int r16 = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const int k = 256 * c + 128 * s + 32 * g, blk = 8 * c + 4 * s + g;
-    const i32x8 a0 = *(const i32x8*)(A8 + r16 * sa + k);
-    const i32x8 a1 = *(const i32x8*)(A8 + (16 + r16) * sa + k);
+    const int k = 256 * c + 128 * s + 16 * g, blk = 8 * c + 4 * s + g;
+    const uint4 p0 = *(const uint4*)(A8 + r16 * sa + k), q0 = *(const uint4*)(A8 + r16 * sa + k + 64);
+    const uint4 p1 = *(const uint4*)(A8 + (16 + r16) * sa + k), q1 = *(const uint4*)(A8 + (16 + r16) * sa + k + 64);
+    const i32x8 a0 = {(int)p0.x, (int)p0.y, (int)p0.z, (int)p0.w, (int)q0.x, (int)q0.y, (int)q0.z, (int)q0.w};
+    const i32x8 a1 = {(int)p1.x, (int)p1.y, (int)p1.z, (int)p1.w, (int)q1.x, (int)q1.y, (int)q1.z, (int)q1.w};
     const int s0 = As8[r16 * nb + blk], s1 = As8[(16 + r16) * nb + blk];
 #pragma unroll
     for (int j = 0; j < TGB; ++j) {

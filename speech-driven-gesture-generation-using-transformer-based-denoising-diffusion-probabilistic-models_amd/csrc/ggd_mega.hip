@@ -116,10 +116,6 @@ __device__ int mk_role_xl(const MegaArgs& m, int nwg, int G) {
 // by the phase's hook): vmcnt completes in issue order, so waiting down to VMC outstanding drains
 // every store without waiting for those loads
 // (stamps are indexed by epoch - 2: the prologue's barrier is epoch 1 and is not stamped)
-// GGD_MK_SPOLL (round-4 A/B switch): the XCD-local barrier polls with scalar loads (below)
-#ifndef GGD_MK_SPOLL
-#define GGD_MK_SPOLL 0
-#endif
 template <int CPV, int VMC = 0, typename F>
 __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part, unsigned epoch, int* status,
                                         int* s_ok, unsigned long long* st, F&& prefetch,
@@ -138,37 +134,10 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
   } else {
     if (threadIdx.x == 0) mk_add(ctr, 1u);
   }
-  // XCD-local path: wave 0 polls the group's 8 flag words with SCALAR loads (s_load glc: past the
-  // scalar cache, from the shared L2), which count in lgkmcnt -- a vector poll load would complete
-  // only behind every vector load its wave issued before it (vmcnt retires in order), i.e. behind
-  // the weight fragments the hooks issued under the attention.  So every wave, the poller
-  // included, issues the next phase's fragments at once.
   const bool poller = threadIdx.x < 64;
-  constexpr bool SP = CPV == CP_XL && GGD_MK_SPOLL != 0;
-  if (SP || !poller) prefetch();
-  if constexpr (SP) {
-    if (poller) {
-      typedef unsigned u32x8 __attribute__((ext_vector_type(8)));
-      const unsigned* fp = (const unsigned*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)flags)) |
-                                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)flags >> 32)) << 32));
-      int ok = 1;
-      for (int spin = 0;; ++spin) {
-        u32x8 v;
-        asm volatile("s_load_dwordx8 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(fp) : "memory");
-        const unsigned lo = min(min(min(v[0], v[1]), min(v[2], v[3])), min(min(v[4], v[5]), min(v[6], v[7])));
-        if (lo >= epoch) break;
-        if ((spin & 255) == 255 && (spin > MK_SPIN_LIMIT || __hip_atomic_load(status, __ATOMIC_RELAXED,
-                                                                               __HIP_MEMORY_SCOPE_AGENT))) {
-          if (threadIdx.x == 0) atomicMax(status, 1);
-          ok = 0;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (threadIdx.x == 0) *s_ok = ok;
-    }
-  } else if constexpr (CPV == CP_XL) {  // vector poll (a poll load retires behind the wave's earlier loads:
-    if (threadIdx.x < 64) {             // the poller issues its prefetch after it)
+  if (!poller) prefetch();
+  if constexpr (CPV == CP_XL) {  // vector poll (a poll load retires behind the wave's earlier loads:
+    if (threadIdx.x < 64) {      // the poller issues its prefetch after it)
       const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
       const int off = (threadIdx.x & 7) * 4;
       int ok = 1;
@@ -201,7 +170,7 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
       *s_ok = ok;
     }
   }
-  if (!SP && poller) prefetch();
+  if (poller) prefetch();
   bar_lds();
   if (st && threadIdx.x == 0) st[2 * (epoch - 2) + 1] = __builtin_amdgcn_s_memtime();
   if (arr && threadIdx.x == 0) arr[2 * (8 * (epoch - 2) + part) + 1] = __builtin_amdgcn_s_memrealtime();

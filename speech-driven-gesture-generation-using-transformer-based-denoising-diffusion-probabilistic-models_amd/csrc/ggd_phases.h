@@ -32,14 +32,17 @@
 #pragma once
 #include "ggd_fusedlib.h"
 
-// Round-4 switches of the persistent loop's KE rows phase (A/B builds: -DGGD_MK_...=0/1):
-//   GGD_MK_FUSE_KD  the last layer's FFN-down reduction runs inside KE, for each block's rows
+// Round-4 switches of the persistent loop's KE rows phase (A/B builds: -DGGD_MK_...=0/1; both
+// bit-identical, both on: scripts/ab.sh on one box, profiles/r04m_c2_ab.txt, C2 mk_kernel 75.07 ->
+// 74.21 ms (FUSE_KD) and 74.85 ms (CMAP))
+//   GGD_MK_FUSE_KD  the last layer's FFN-down reduction runs inside KE, for each block's rows (one
+//                   clip-group barrier and the KD phase fewer per step: 15 instead of 16)
 //   GGD_MK_CMAP     KE update threads take channel t % 128 (coalesced x access) instead of t / 3
 #ifndef GGD_MK_FUSE_KD
-#define GGD_MK_FUSE_KD 0
+#define GGD_MK_FUSE_KD 1
 #endif
 #ifndef GGD_MK_CMAP
-#define GGD_MK_CMAP 0
+#define GGD_MK_CMAP 1
 #endif
 
 namespace ggd {

@@ -162,7 +162,18 @@ def test_route_eps_check_sees_one_cross_attention_weight(pkg, beat_cfg, weights,
     e_ref, _ = reference_step(om, wav, x, 402)
     err = rel_rms(eps, e_ref)
     print(f"{route}: eps rel-RMS with the perturbed weight {err:.2e}")
-    assert err > ROUTES[route][6], err
+    if route != "lk_fp8":
+        assert err > ROUTES[route][6], err
+        return
+    # block-scaled fp8 MFMA: e4m3 activations put the route's own eps error at a few % (inside
+    # SURVEY.md 8d's fp8 bound of 1e-1, which a 1.7 % model change cannot fail); the check is then
+    # that the perturbation moves the error measurably above the same route's unperturbed error
+    wav0, out0 = run_route(pkg, beat_cfg, sd, route, (402,))
+    x0, eps0, _ = out0[402]
+    assert th.equal(wav0, wav) and th.equal(x0, x)
+    clean = rel_rms(eps0, e_ref)
+    print(f"{route}: eps rel-RMS unperturbed {clean:.2e}")
+    assert err > 1.05 * clean and err - clean > 2e-3, (clean, err)
 
 
 def test_speech_driven_weights_make_eps_depend_on_speech(pkg, beat_cfg):

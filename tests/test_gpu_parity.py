@@ -630,6 +630,8 @@ def test_chain_route_equals_gemm_launches(pkg, beat_cfg, setup, setup_fp8, dtype
     wav, x, t = inputs(n, seed=71, wav_len=wav_len, L_=Lc)
     ctx, _ = model.prepare(wav.cuda(), Lc)
     assert _info(ctx, INFO_CHAIN_AVAILABLE) == 1.0
+    # fp8: the long loop (which the chain route's sample takes) with the launch route's arithmetic
+    assert ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 1) == 0
     zs = th.randn(3, n, D_POSE, Lc, generator=th.Generator().manual_seed(72))
 
     def run():
@@ -644,6 +646,7 @@ def test_chain_route_equals_gemm_launches(pkg, beat_cfg, setup, setup_fp8, dtype
         gemm = run()
     finally:
         ctx.lib.ggd_set_route(ctx.h, ROUTE_GEMM_LAUNCHES, 0)
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0)
     assert th.equal(chain[0], gemm[0])
     assert th.equal(chain[1], gemm[1])
     ref = (setup_fp8 if dtype == "fp8" else om)(x, t, wav=wav)
