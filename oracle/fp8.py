@@ -92,3 +92,50 @@ def dequantized_state_dict(sd, twoway=False):
         _, _, deq = quantize_rows(sd[k].detach().cpu().float().numpy())
         out[k] = th.from_numpy(deq)
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# Block-scaled (MX) e4m3 activations of the long-clip loop's fp8-MFMA stages (GGD_ROUTE_FP8_MFMA,
+# csrc/ggd_chainlib.h mx_scale_byte / mx_mul): blocks of 32 consecutive values along the last dim,
+# scale 2^(E - 7) for the block max 1.f 2^E (biased exponent clamped to [2, 253]), values rounded to
+# e4m3 (nearest even) after the exact power-of-two division.
+# ------------------------------------------------------------------------------------------
+def mx_e4m3(x):
+    """fp32 tensor (last dim a multiple of 32) -> its MX-e4m3 dequantization, same shape."""
+    shp = x.shape
+    xb = x.detach().float().reshape(-1, shp[-1] // 32, 32).contiguous()
+    m = xb.abs().amax(-1, keepdim=True)
+    be = (m.view(th.int32) >> 23) & 0xFF
+    sb = (be - 7).clamp(2, 253)
+    mul = ((254 - sb) << 23).view(th.float32)     # 2^-(sb - 127): exact
+    scale = ((sb) << 23).view(th.float32)         # 2^(sb - 127)
+    q = e4m3_decode(e4m3_encode((xb * mul).numpy()))
+    return (th.from_numpy(q) * scale).reshape(shp)
+
+
+# the Linears whose INPUT the fp8-MFMA long loop quantises (self-attention Q / K / V of LN1, the
+# cross-attention query of LN2, both FFN Linears); OUT_PROJ adds the attention out-projections
+_MX_INPUTS = [r"pose_decoder\.layers\.\d+\.self_attn\.(query|key|value)\.0\.linear",
+              r"pose_decoder\.layers\.\d+\.cross_attn\.query\.0\.linear",
+              r"pose_decoder\.layers\.\d+\.feed_forward\.layer[12]"]
+_MX_OUT_PROJ = [r"pose_decoder\.layers\.\d+\.(self_attn|cross_attn)\.output"]
+
+
+class mx_activations:
+    """Context manager: while active, oracle.ref_denoiser quantises the inputs of the Linears the
+    fp8-MFMA long loop runs on block-scaled MFMA to MX-e4m3 (``out_proj``: the attention
+    out-projections too).  Test infrastructure: the oracle of that route's exact arithmetic."""
+
+    def __init__(self, out_proj=False):
+        self.pats = [re.compile(p) for p in _MX_INPUTS + (_MX_OUT_PROJ if out_proj else [])]
+
+    def __enter__(self):
+        from oracle import ref_denoiser
+        self._prev = ref_denoiser.ACT_QUANT
+        ref_denoiser.ACT_QUANT = lambda name, x: mx_e4m3(x) if any(p.fullmatch(name) for p in self.pats) else x
+        return self
+
+    def __exit__(self, *exc):
+        from oracle import ref_denoiser
+        ref_denoiser.ACT_QUANT = self._prev
+        return False

@@ -18,8 +18,14 @@ import torch.nn.functional as F
 # small building blocks
 # ----------------------------------------------------------------------------
 
+# activation quantisation hook (oracle/fp8.py mx_activations): (linear name, input) -> input
+ACT_QUANT = None
+
+
 def _lin(sd, name, x):
     """nn.Linear: models/modules/transformer.py:51,73; models/nn.py:189-190,213."""
+    if ACT_QUANT is not None:
+        x = ACT_QUANT(name, x)
     return F.linear(x, sd[name + ".weight"], sd.get(name + ".bias"))
 
 

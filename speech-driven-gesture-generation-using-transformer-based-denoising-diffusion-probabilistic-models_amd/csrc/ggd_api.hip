@@ -1486,7 +1486,7 @@ int ggd_finalize_weights(ggd_ctx* c) {
       TRY(pack(c->emb_x));
       if (D.dtype == GGD_FP8W)  // the FFN / LN-projection weights the block-scaled stages read
         for (Layer& Ly : c->layers)
-          for (Lin* L : {&Ly.qkv, &Ly.q_ca, &Ly.ff1, &Ly.ff2}) {
+          for (Lin* L : {&Ly.qkv, &Ly.q_ca, &Ly.ff1, &Ly.ff2, &Ly.o_sa, &Ly.o_ca}) {
             HIP_TRY(c, dalloc(c, &L->wmx, chain_pack_bytes(1, L->npad, L->kpad)));
             HIP_TRY(c, launch_chain_pack(2, L->w, L->wmx, L->npad, L->kpad, c->stream));
           }
@@ -2137,6 +2137,10 @@ int long_tables(ggd_ctx* c) {
     use(1, c->layers[0].qkv);
     for (int li = 0; li < NL; ++li) {
       const int b0 = 2 + LONG_STAGES_PER_LAYER * li;
+      if (long_mx_out_proj()) {
+        use(b0 + 0, c->layers[li].o_sa);
+        use(b0 + 2, c->layers[li].o_ca);
+      }
       use(b0 + 1, c->layers[li].q_ca);
       use(b0 + 3, c->layers[li].ff1);
       use(b0 + 4, c->layers[li].ff2);

@@ -291,10 +291,15 @@ constexpr size_t LK_XSC = LK_HSC + (size_t)CH_MT * (CH_FF / 32);  //            
 static_assert(LK_XSC + CH_MT * (CH_D / 32) <= sizeof(bf16_t) * CH_MT * HH_STR, "MX images fit the hh region");
 static_assert(CH_MT * XS8_STR <= sizeof(bf16_t) * CH_MT * XS_STR, "fp8 A rows fit the xs region");
 static_assert(LK_XSC >= sizeof(float) * CH_MT * EPS_STR, "eps rows (out_layers) stay clear of the LN scales");
+// GGD_LK_MX_R (A/B switch): the attention out-projections (stage R, A = the hand-off rows,
+// quantised as they are staged) on block-scaled fp8 MFMA too
+#ifndef GGD_LK_MX_R
+#define GGD_LK_MX_R 0
+#endif
 template <int KIND, int si, bool MX>
 constexpr bool lk_mx() {
   constexpr int k = LkPlan<KIND>::s[si].kind;
-  return MX && (k == SK_F1 || k == SK_F2 || k == SK_P || k == SK_P2);
+  return MX && (k == SK_F1 || k == SK_F2 || k == SK_P || k == SK_P2 || (GGD_LK_MX_R && k == SK_R));
 }
 
 template <bool W8, int KIND, int IT, bool MX, class X>
@@ -434,10 +439,38 @@ __device__ __forceinline__ void lk_chain(cla_T& a, cst_t sa, int b, int part, in
   static_assert(PL::s[0].kind == SK_R, "every chain phase opens with the attention output projection");
   {  // attention output rows of the block (written by the head parts)
     const bf16_t* src = (const bf16_t*)a.att + ((size_t)b * a.L + part * CH_MT) * CH_D;
+    uint4 v[CH_MT * CH_D / 8 / CH_NT];
 #pragma unroll
     for (int i = 0; i < CH_MT * CH_D / 8 / CH_NT; ++i) {
       const int e = tid + i * CH_NT, r = e / (CH_D / 8), cv = e % (CH_D / 8);
-      *(uint4*)(x.xs + r * XS_STR + 8 * cv) = ld_16B<CP_XL>(src, (uint32_t)((r * CH_D + 8 * cv) * 2));
+      v[i] = ld_16B<CP_XL>(src, (uint32_t)((r * CH_D + 8 * cv) * 2));
+    }
+#pragma unroll
+    for (int i = 0; i < CH_MT * CH_D / 8 / CH_NT; ++i) {
+      const int e = tid + i * CH_NT, r = e / (CH_D / 8), cv = e % (CH_D / 8);
+      if constexpr (lk_mx<KIND, 0, MX>()) {  // e4m3 rows + the block scales: a block is 4 lanes' pieces
+        // max |v| on the bf16 bits (non-negative bf16 order as integers: v_pk_max_u16), then two
+        // values at a time into e4m3 (few live registers beside the weight groups in flight)
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        const unsigned w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        u16x2 mm = {0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mm = __builtin_elementwise_max(mm, __builtin_bit_cast(u16x2, w[q] & 0x7fff7fffu));
+        const unsigned mb = (unsigned)max(mm.x, mm.y) << 16;
+        const unsigned sb = mx_scale_byte(mx_group_max<4>(__uint_as_float(mb)));
+        const float mul = mx_mul(sb);
+        auto lo = [&](int q) { return __uint_as_float(w[q] << 16) * mul; };
+        auto hi = [&](int q) { return __uint_as_float(w[q] & 0xffff0000u) * mul; };
+        int o0 = __builtin_amdgcn_cvt_pk_fp8_f32(lo(0), hi(0), 0, false);
+        o0 = __builtin_amdgcn_cvt_pk_fp8_f32(lo(1), hi(1), o0, true);
+        int o1 = __builtin_amdgcn_cvt_pk_fp8_f32(lo(2), hi(2), 0, false);
+        o1 = __builtin_amdgcn_cvt_pk_fp8_f32(lo(3), hi(3), o1, true);
+        unsigned char* xs8 = (unsigned char*)x.xs;
+        *(uint2*)(xs8 + r * XS8_STR + 8 * cv) = make_uint2((unsigned)o0, (unsigned)o1);
+        if ((cv & 3) == 0) ((unsigned char*)x.hh)[LK_XSC + r * (CH_D / 32) + cv / 4] = (unsigned char)sb;
+      } else {
+        *(uint4*)(x.xs + r * XS_STR + 8 * cv) = v[i];
+      }
     }
   }
   ch_bar();
@@ -715,6 +748,8 @@ bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C
   return dtype != 0 && d_model == CH_D && heads == 8 && L % CH_MT == 0 && L / CH_MT <= 8 && L >= 96 &&
          L <= ATT_LMAX && lkp >= 96 && lkp <= ATT_LMAX && C <= 128 && out_npad == 128 && lds <= 160 * 1024 - 256;
 }
+
+bool long_mx_out_proj() { return GGD_LK_MX_R != 0; }
 
 size_t long_kv_cache_bytes(int n, int Ts, int heads) {
   const int Lkp = (1 + Ts + 31) / 32 * 32;

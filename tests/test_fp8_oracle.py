@@ -54,3 +54,26 @@ def test_step_linear_selection(pkg, beat_cfg):
     assert set(dq) == set(sd)
     for k in names:
         assert not th.equal(dq[k], sd[k])
+
+
+def test_mx_e4m3_blocks():
+    """MX activations (the fp8-MFMA long loop's quantiser, ggd_chainlib.h mx_scale_byte / mx_mul):
+    per 32-value block the max lands in [128, 256) (scale 2^(E - 7)), powers of two and small
+    integers times the scale survive exactly, every value keeps e4m3's 2^-4 relative step, an
+    all-zero block stays zero and blocks do not see each other's scale."""
+    g = th.Generator().manual_seed(3)
+    x = th.randn(6, 96, generator=g) * th.tensor([1e-3, 1.0, 300.0]).repeat_interleave(32)
+    y = fp8.mx_e4m3(x)
+    rel = ((y - x).abs() / x.abs().clamp_min(1e-30))
+    # normals of the block keep a 3-bit mantissa (round to nearest: <= 2^-4 relative); values below
+    # max / 2^13 may go subnormal, the random data here has none
+    assert float(rel.max()) <= 2.0 ** -4 + 1e-7
+    blocks = x.reshape(6, 3, 32)
+    m = blocks.abs().amax(-1)
+    e = th.floor(th.log2(m))
+    scaled = (blocks / (2.0 ** (e - 7))[..., None]).abs().amax(-1)
+    assert bool(((scaled >= 128) & (scaled < 256)).all())
+    z = th.zeros(2, 64)
+    z[1, 32:] = th.tensor([2.0 ** k for k in range(-8, 24)])
+    assert th.equal(fp8.mx_e4m3(z)[0], z[0])
+    assert th.equal(fp8.mx_e4m3(z)[1, 32:][-14:], z[1, 32:][-14:])   # within 2^13 of the block max: exact

@@ -200,3 +200,24 @@ def test_speech_driven_weights_make_eps_depend_on_speech(pkg, beat_cfg):
         print(f"t={t}: speech moves eps by {speech:.3f}; GPU difference vs oracle rel-RMS {d_err:.3e}")
         assert speech >= 0.05
         assert d_err <= 0.1, d_err
+
+
+def test_fp8_mfma_route_is_the_mx_oracle(pkg, beat_cfg, weights):
+    """The block-scaled fp8 route against an oracle that applies the SAME arithmetic: dequantised
+    e4m3 weights AND MX-e4m3 activations (oracle/fp8.py mx_activations: blocks of 32 values, scale
+    2^(E - 7)) at the inputs of the Linears the loop runs on fp8 MFMA.  It must sit much closer to
+    that oracle than to the plain dequantised-weight oracle (whose gap is the activation rounding):
+    the loop quantises what, where and how it says.  (Layer 0's first-step QKV is computed in front
+    of the loop by the bf16 chain launch, so that Linear's input is not quantised on the GPU.)"""
+    from oracle import fp8
+    arch, sd = weights
+    wav, out = run_route(pkg, beat_cfg, sd, "lk_fp8", (999, 402, 118))
+    om = oracle_for("lk_fp8", arch, sd)
+    for t, (x, eps, _) in out.items():
+        e_plain, _ = reference_step(om, wav, x, t)
+        with fp8.mx_activations():
+            e_mx, _ = reference_step(om, wav, x, t)
+        err_mx, err_plain = rel_rms(eps, e_mx), rel_rms(eps, e_plain)
+        print(f"lk_fp8 t={t}: eps rel-RMS vs MX oracle {err_mx:.2e}, vs dequantised-weight oracle {err_plain:.2e}")
+        assert err_mx <= 1.5e-2, (t, err_mx)
+        assert err_mx < 0.6 * err_plain, (t, err_mx, err_plain)
