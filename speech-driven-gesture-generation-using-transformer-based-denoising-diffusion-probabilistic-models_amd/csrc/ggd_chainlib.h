@@ -150,18 +150,12 @@ __device__ __forceinline__ unsigned mx_pack4(float a, float b, float c, float d)
   w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
   return (unsigned)w;
 }
-// max over lanes l ^ 1, l ^ 2, ..., l ^ (N / 2) (N lanes: a power of two <= 16)
-template <int N>
-__device__ __forceinline__ float mx_group_max(float v) {
-#pragma unroll
-  for (int o = 1; o < N; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
 // acc[i][j] += A8[16 i + .][256 c + .] . W[16 (nt0 + j) + .][256 c + .]^T over the chunk's 256 k:
 // two block-scaled MFMAs per (row tile, column tile).  A8: fp8 rows (stride sa bytes), As8: their
-// e8m0 scale bytes [32 rows][nb blocks]
-template <int TGB>
+// e8m0 scale bytes [32 rows][nb blocks].  TR: computed transposed (the weights as the MFMA A
+// operand), so lane (c16, g4) holds row 16 i + c16, columns 16 (nt0 + j) + 4 g4 .. + 3 -- four
+// consecutive columns of one row, what a packed epilogue store wants
+template <int TGB, bool TR = false>
 __device__ __forceinline__ void ch_mma_mx(const BBuf<true, TGB>& B, const unsigned char* A8, int sa,
                                           const unsigned char* As8, int nb, int c, int lane, f32x4 (&acc)[2][TGB],
                                           int tg) {
@@ -179,8 +173,13 @@ __device__ __forceinline__ void ch_mma_mx(const BBuf<true, TGB>& B, const unsign
       if (j >= tg) continue;
       const uint4 u0 = B.v[j][2 * s], u1 = B.v[j][2 * s + 1];
       const i32x8 bw = {(int)u0.x, (int)u0.y, (int)u0.z, (int)u0.w, (int)u1.x, (int)u1.y, (int)u1.z, (int)u1.w};
-      acc[0][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a0, bw, acc[0][j], 0, 0, 0, s0, 0, 127);
-      acc[1][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a1, bw, acc[1][j], 0, 0, 0, s1, 0, 127);
+      if constexpr (TR) {
+        acc[0][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw, a0, acc[0][j], 0, 0, 0, 127, 0, s0);
+        acc[1][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bw, a1, acc[1][j], 0, 0, 0, 127, 0, s1);
+      } else {
+        acc[0][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a0, bw, acc[0][j], 0, 0, 0, s0, 0, 127);
+        acc[1][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a1, bw, acc[1][j], 0, 0, 0, s1, 0, 127);
+      }
     }
   }
 }

@@ -201,7 +201,6 @@ struct ConvArgs {
   int N, H, W, Cin, Ho, Wo, Cout_pad, Cvalid, KH, KW, stride, pad, mode, layout, in_bf16, out_bf16;
   float* se_part;           // LDS kernel, non-null: the SE squeeze's partial sums of the f32 outputs,
                             // one row of Cout_pad per (image, output tile): [N][tiles][Cout_pad]
-  int tpw;                  // enc_conv_nhwc_kernel: output tiles per workgroup (set by its launcher)
 };
 
 template <typename T> struct ConvB;
@@ -902,200 +901,6 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_nhwc_kernel(ConvArgs a) {
   }
 }
 
-// enc_conv_nhwc_kernel with several output tiles per workgroup (3x3 stride 1 only -- the tower's
-// bulk; the strided and 1x1 convs keep the one-tile kernel and its register budget): the
-template <int NJ, int TW, int KS, int ST, typename TO>
-__global__ void __launch_bounds__(CONV_TPB) enc_conv_mt_kernel(ConvArgs a) {
-  using GE = CGeo<TW, KS, ST>;
-  constexpr int QP = 4;                                        // 16-byte pieces (8 bf16) per 32 channels
-  constexpr int NP8 = GE::NPOS * QP, PM = (NP8 + CONV_TPB - 1) / CONV_TPB;
-  constexpr int NW = NJ * 16 * GE::TAPS * 4, WM = (NW + CONV_TPB - 1) / CONV_TPB;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const bf16_t* in = (const bf16_t*)a.in;
-  TO* out = (TO*)a.out;
-  bf16_t* patch = (bf16_t*)smem;
-  bf16_t* wl = (bf16_t*)(smem + GE::PATCH_BYTES);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, g = lane >> 4;
-  const int tw_n = (a.Wo + TW - 1) / TW, th_n = (a.Ho + GE::TH - 1) / GE::TH, per = tw_n * th_n;
-  // the workgroup's output tiles t0 .. t0 + nt - 1 (image-major), one channel block n0: the
-  // (tile, 32-channel chunk) steps run as ONE pipelined sequence, so the next tile's first patch
-  // (and filter) loads are in flight under this tile's last MFMAs -- a workgroup of a single
-  // tile exposes its first fetch (a whole L2 / HBM round trip) in front of every tile
-  const int t0 = blockIdx.x * a.tpw, nt = min(a.tpw, a.N * per - t0), n0 = blockIdx.y * (NJ * 16);
-  const int cch = a.Cin >> 5;
-  const bool wres = cch == 1;  // one chunk: the filter taps are staged once and stay in LDS
-  int pbase[2];  // patch position of tap (0, 0) for this lane's pixel in pixel tiles 0, 1
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = wave * 32 + i * 16 + r16, ty = q / TW, tx = q % TW;
-    pbase[i] = ty * GE::PS * GE::PW + tx * GE::PS;
-  }
-  // chunk-0 element offsets of this thread's patch pieces for one tile (chunk ck adds 32 ck)
-  int poff[PM], woff[WM];
-  uint32_t okm = 0;  // bit k: patch piece k lies inside the image (else it stages as zero)
-  auto tile_geo = [&](int tile) __attribute__((always_inline)) {
-    const int b = tile / per, tix = tile - b * per, tyi = tix / tw_n;
-    const int ih0 = tyi * GE::TH * ST - a.pad, iw0 = (tix - tyi * tw_n) * TW * ST - a.pad;
-    okm = 0;
-#pragma unroll
-    for (int k = 0; k < PM; ++k) {
-      const int v = tid + k * CONV_TPB, vc = min(v, NP8 - 1);
-      const int pos = vc / QP, q4 = vc % QP, py = pos / GE::PW, px = pos % GE::PW;
-      const int ih = ih0 + py * GE::SS, iw = iw0 + px * GE::SS;
-      const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      const int ihc = min(max(ih, 0), a.H - 1), iwc = min(max(iw, 0), a.W - 1);
-      poff[k] = ((b * a.H + ihc) * a.W + iwc) * a.Cin + q4 * 8;
-      okm |= (ok && v < NP8) ? (1u << k) : 0u;
-    }
-  };
-#pragma unroll
-  for (int k = 0; k < WM; ++k) {
-    const int v = min(tid + k * CONV_TPB, NW - 1);  // clamped: every register is defined
-    const int q8 = v & 3, nt_ = v >> 2, n = nt_ / GE::TAPS, tap = nt_ % GE::TAPS;
-    woff[k] = ((n0 + n) * GE::TAPS + tap) * a.Cin + q8 * 8;
-  }
-  f32x4 acc[2][NJ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bf16_t* W = (const bf16_t*)a.w;
-  bf16x8 xr[PM], wr[WM];
-  uint32_t okm_cur = 0;
-  auto fetch = [&](int ck, bool wts) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < PM; ++k) xr[k] = *(const bf16x8*)(in + poff[k] + ck * 32);
-    if (wts) {
-#pragma unroll
-      for (int k = 0; k < WM; ++k) wr[k] = *(const bf16x8*)(W + woff[k] + ck * 32);
-    }
-  };
-  auto put = [&](bool wts) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < PM; ++k) {
-      const int v = tid + k * CONV_TPB;
-      if (v < NP8) {
-        const bf16x8 z = {};
-        *(bf16x8*)(patch + (v / QP) * CL_CS + (v % QP) * 8) = ((okm_cur >> k) & 1u) ? xr[k] : z;
-      }
-    }
-    if (wts) {
-#pragma unroll
-      for (int k = 0; k < WM; ++k) {
-        const int v = tid + k * CONV_TPB;
-        if (v < NW) *(bf16x8*)(wl + (v >> 2) * CL_CS + (v & 3) * 8) = wr[k];  // (n taps + tap) = v >> 2
-      }
-    }
-  };
-  tile_geo(t0);
-  fetch(0, true);
-  for (int it = 0; it < nt * cch; ++it) {
-    const int i = it / cch, ck = it - i * cch;
-    if (it > 0) __syncthreads();  // the previous step's MFMAs (and SE squeeze) are done with the LDS images
-    okm_cur = okm;
-    put(!wres || it == 0);
-    __syncthreads();
-    if (it + 1 < nt * cch) {
-      const int i2 = (it + 1) / cch, ck2 = it + 1 - i2 * cch;
-      if (ck2 == 0) tile_geo(t0 + i2);
-      fetch(ck2, !wres);
-    }
-#pragma unroll
-    for (int tap = 0; tap < GE::TAPS; ++tap) {
-      const int toff = (tap / KS) * GE::PW + tap % KS;
-      bf16x8 bv[2], av[NJ];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) bv[i] = *(const bf16x8*)(patch + (pbase[i] + toff) * CL_CS + g * 8);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) av[j] = *(const bf16x8*)(wl + ((j * 16 + r16) * GE::TAPS + tap) * CL_CS + g * 8);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[j], bv[i], acc[i][j], 0, 0, 0);
-    }
-    if (ck + 1 < cch) continue;
-    // epilogue of tile t0 + i: lane (pixel r16 of pixel tile ii, group g) holds output channels
-    // 16 j + 4 g .. + 3
-    const int tile = t0 + i, b = tile / per, tix = tile - b * per, tyi = tix / tw_n;
-    const int oh0 = tyi * GE::TH, ow0 = (tix - tyi * tw_n) * TW;
-    float cs[NJ][4];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int co = n0 + j * 16 + 4 * g;
-      const float4 bi = *(const float4*)(a.bias + co), sc = *(const float4*)(a.s + co), sh = *(const float4*)(a.t + co);
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii) {
-        const int q = wave * 32 + ii * 16 + r16, oh = oh0 + q / TW, ow = ow0 + q % TW;
-        const bool okp = oh < a.Ho && ow < a.Wo;
-        float v[4] = {acc[ii][j][0] + bi.x, acc[ii][j][1] + bi.y, acc[ii][j][2] + bi.z, acc[ii][j][3] + bi.w};
-        acc[ii][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (a.mode == CONV_RELU_BN) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-        }
-        v[0] = v[0] * sc.x + sh.x;
-        v[1] = v[1] * sc.y + sh.y;
-        v[2] = v[2] * sc.z + sh.z;
-        v[3] = v[3] * sc.w + sh.w;
-        if (okp) {
-          TO* dst = out + (((size_t)b * a.Ho + oh) * a.Wo + ow) * a.Cout_pad + co;
-          if constexpr (sizeof(TO) == 2) {
-            const uint32_t lo = pk_bf16(v[0], v[1]);
-            const uint32_t hi = pk_bf16(v[2], v[3]);
-            *(uint2*)dst = make_uint2(lo, hi);
-          } else {
-            *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cs[j][r] += okp ? v[r] : 0.f;
-      }
-    }
-    if (a.se_part) {
-      // SE squeeze of this tile (ResNetBlocks.py:81-96, the mean's first stage): per output channel
-      // the sum of the tile's valid f32 outputs in a fixed order (pixel tiles, 16 pixel lanes, waves)
-      // -> one [Cout_pad] row per (image, tile); enc_se_kernel adds the tiles in tile order
-      __syncthreads();  // every wave is past the MMA loop: the patch image is free (the filter stays)
-      float* red = (float*)smem;  // [4 waves][NJ * 16], inside the patch image
-      static_assert(4 * NJ * 16 * sizeof(float) <= GE::PATCH_BYTES, "squeeze rows overlay the patch only");
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float t = group_sum<16>(cs[j][r]);
-          if (r16 == 0) red[wave * NJ * 16 + j * 16 + 4 * g + r] = t;
-        }
-      __syncthreads();
-      if (tid < NJ * 16)
-        a.se_part[((size_t)b * per + tix) * a.Cout_pad + n0 + tid] =
-            (red[tid] + red[NJ * 16 + tid]) + (red[2 * NJ * 16 + tid] + red[3 * NJ * 16 + tid]);
-    }
-  }
-}
-
-// workgroups a multi-tile conv launch aims for; GGD_ENC_CONV_MT=0 keeps one tile per workgroup
-// (A/B switches of the tiling, read once)
-int conv_wg_target() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = std::getenv("GGD_ENC_CONV_WGS");
-    v = e ? std::max(1, std::atoi(e)) : 1024;
-  }
-  return v;
-}
-bool conv_mt_on() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = std::getenv("GGD_ENC_CONV_MT");
-    v = e ? std::atoi(e) != 0 : 1;
-  }
-  return v != 0;
-}
-
 template <int NJ, int TW, int KS, int ST, typename TO>
 hipError_t launch_conv_nhwc(const ConvArgs& a, hipStream_t s) {
   using GE = CGeo<TW, KS, ST>;
@@ -1107,26 +912,8 @@ hipError_t launch_conv_nhwc(const ConvArgs& a, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
     attr = true;
   }
-  // tiles per workgroup: enough workgroups for ~4 per CU (2 resident by LDS, 2 rounds), at most 8
-  // tiles each (the pipelined fetch hides one round trip per tile after the first)
-  const int tiles = a.N * ((a.Ho + GE::TH - 1) / GE::TH) * ((a.Wo + TW - 1) / TW), cb = a.Cout_pad / (NJ * 16);
-  ConvArgs b = a;
-  constexpr bool MT = KS == 3 && ST == 1;
-  b.tpw = MT && conv_mt_on() ? std::max(1, std::min(8, tiles * cb / conv_wg_target())) : 1;
-  const dim3 grid((tiles + b.tpw - 1) / b.tpw, cb);
-  if constexpr (MT) {
-    static bool attr_mt = false;
-    if (!attr_mt) {
-      (void)hipFuncSetAttribute((const void*)enc_conv_mt_kernel<NJ, TW, KS, ST, TO>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-      attr_mt = true;
-    }
-    if (conv_mt_on()) {
-      hipLaunchKernelGGL((enc_conv_mt_kernel<NJ, TW, KS, ST, TO>), grid, dim3(CONV_TPB), lds, s, b);
-      return hipGetLastError();
-    }
-  }
-  hipLaunchKernelGGL((enc_conv_nhwc_kernel<NJ, TW, KS, ST, TO>), grid, dim3(CONV_TPB), lds, s, b);
+  const dim3 grid(a.N * ((a.Ho + GE::TH - 1) / GE::TH) * ((a.Wo + TW - 1) / TW), a.Cout_pad / (NJ * 16));
+  hipLaunchKernelGGL((enc_conv_nhwc_kernel<NJ, TW, KS, ST, TO>), grid, dim3(CONV_TPB), lds, s, a);
   return hipGetLastError();
 }
 

@@ -202,7 +202,7 @@ __device__ __forceinline__ void lk_layernorm_mx(const float* hs, const float* gm
     const float4 b = *(const float4*)(bt + k);
     const float y0 = (x.x - mu) * rs * g.x + b.x, y1 = (x.y - mu) * rs * g.y + b.y;
     const float y2 = (x.z - mu) * rs * g.z + b.z, y3 = (x.w - mu) * rs * g.w + b.w;
-    const float m = mx_group_max<8>(fmaxf(fmaxf(fabsf(y0), fabsf(y1)), fmaxf(fabsf(y2), fabsf(y3))));
+    const float m = group_max<8>(fmaxf(fmaxf(fabsf(y0), fabsf(y1)), fmaxf(fabsf(y2), fabsf(y3))));
     const unsigned sb = mx_scale_byte(m);
     const float mul = mx_mul(sb);
     *(unsigned*)(xs8 + r * XS8_STR + k) = mx_pack4(y0 * mul, y1 * mul, y2 * mul, y3 * mul);
@@ -338,6 +338,8 @@ __device__ __forceinline__ void lk_iter(X& x) {
   if constexpr (mx) {
     if constexpr (kind == SK_F2)
       ch_mma_mx<TGB>(x.bb[IT % LK_DEPTH], hh8, HH8_STR, hh8 + LK_HSC, CH_FF / 32, c, x.lane, x.acc, tg);
+    else if constexpr (kind == SK_F1)  // transposed: the ReLU^2 epilogue quantises 4 columns of a row per lane
+      ch_mma_mx<TGB, true>(x.bb[IT % LK_DEPTH], xs8, XS8_STR, hh8 + LK_XSC, CH_D / 32, c, x.lane, x.acc, tg);
     else
       ch_mma_mx<TGB>(x.bb[IT % LK_DEPTH], xs8, XS8_STR, hh8 + LK_XSC, CH_D / 32, c, x.lane, x.acc, tg);
   } else if constexpr (kind == SK_F2) {
@@ -346,25 +348,33 @@ __device__ __forceinline__ void lk_iter(X& x) {
     ch_mma<W8, TGB>(x.bb[IT % LK_DEPTH], x.xs, XS_STR, c, x.lane, x.acc, tg);
   }
   if constexpr (c == nch - 1 && mx && kind == SK_F1) {  // ReLU^2 hidden rows -> e4m3 + block scales
+    // transposed accumulators: lane (c16, g4) holds row 16 i + c16, columns 16 (nt0 + j) + 4 g4 .. + 3;
+    // a 32-column block is the lane's two tiles x the 4 lane rows (permlane swaps), one 4-byte store
+    // per (row, tile)
     static_assert(tg == 2, "a lane's two column tiles are one 32-column block");
     constexpr int np = PL::s[si].ncols;
     const float* pp = x.prm + GE::prm(si);
-    const int n0 = nt0 * 16 + x.c16;
+    const int g4 = x.g4 >> 2;  // x.g4 = 4 (lane >> 4)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i) {
+      const int row = i * 16 + x.c16;
+      float y[2][4], m = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = i * 16 + x.g4 + r;
-        const float v0 = fmaxf(ch_val<W8>(pp, np, x.acc[i][0][r], n0), 0.f);
-        const float v1 = fmaxf(ch_val<W8>(pp, np, x.acc[i][1][r], n0 + 16), 0.f);
-        const float y0 = v0 * v0, y1 = v1 * v1;
-        const unsigned sb = mx_scale_byte(mx_group_max<16>(fmaxf(y0, y1)));
-        const float mul = mx_mul(sb);
-        const int w = __builtin_amdgcn_cvt_pk_fp8_f32(y0 * mul, y1 * mul, 0, false);
-        hh8[row * HH8_STR + n0] = (unsigned char)(w & 0xff);
-        hh8[row * HH8_STR + n0 + 16] = (unsigned char)((w >> 8) & 0xff);
-        if (x.c16 == 0) hh8[LK_HSC + row * (CH_FF / 32) + nt0 / 2] = (unsigned char)sb;
-      }
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = fmaxf(ch_val<W8>(pp, np, x.acc[i][j][r], (nt0 + j) * 16 + 4 * g4 + r), 0.f);
+          y[j][r] = v * v;
+          m = fmaxf(m, y[j][r]);
+        }
+      const unsigned sb = mx_scale_byte(lanerow_max4(m));
+      const float mul = mx_mul(sb);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        *(unsigned*)(hh8 + row * HH8_STR + (nt0 + j) * 16 + 4 * g4) =
+            mx_pack4(y[j][0] * mul, y[j][1] * mul, y[j][2] * mul, y[j][3] * mul);
+      if (g4 == 0) hh8[LK_HSC + row * (CH_FF / 32) + nt0 / 2] = (unsigned char)sb;
+    }
   } else if constexpr (c == nch - 1) {
     constexpr int np = PL::s[si].ncols;
     const float* pp = x.prm + GE::prm(si);
@@ -457,7 +467,7 @@ __device__ __forceinline__ void lk_chain(cla_T& a, cst_t sa, int b, int part, in
 #pragma unroll
         for (int q = 0; q < 4; ++q) mm = __builtin_elementwise_max(mm, __builtin_bit_cast(u16x2, w[q] & 0x7fff7fffu));
         const unsigned mb = (unsigned)max(mm.x, mm.y) << 16;
-        const unsigned sb = mx_scale_byte(mx_group_max<4>(__uint_as_float(mb)));
+        const unsigned sb = mx_scale_byte(group_max<4>(__uint_as_float(mb)));
         const float mul = mx_mul(sb);
         auto lo = [&](int q) { return __uint_as_float(w[q] << 16) * mul; };
         auto hi = [&](int q) { return __uint_as_float(w[q] & 0xffff0000u) * mul; };

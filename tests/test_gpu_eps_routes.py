@@ -208,14 +208,14 @@ def test_fp8_mfma_route_is_the_mx_oracle(pkg, beat_cfg, weights):
     2^(E - 7)) at the inputs of the Linears the loop runs on fp8 MFMA.  It must sit much closer to
     that oracle than to the plain dequantised-weight oracle (whose gap is the activation rounding):
     the loop quantises what, where and how it says.  (Layer 0's first-step QKV is computed in front
-    of the loop by the bf16 chain launch, so that Linear's input is not quantised on the GPU.)"""
+    of the loop by the bf16 chain launch, so the oracle leaves that Linear's input unquantised.)"""
     from oracle import fp8
     arch, sd = weights
     wav, out = run_route(pkg, beat_cfg, sd, "lk_fp8", (999, 402, 118))
     om = oracle_for("lk_fp8", arch, sd)
     for t, (x, eps, _) in out.items():
         e_plain, _ = reference_step(om, wav, x, t)
-        with fp8.mx_activations():
+        with fp8.mx_activations(first_qkv=False):   # one loop iteration: its layer-0 QKV is the bf16 launch's
             e_mx, _ = reference_step(om, wav, x, t)
         err_mx, err_plain = rel_rms(eps, e_mx), rel_rms(eps, e_plain)
         print(f"lk_fp8 t={t}: eps rel-RMS vs MX oracle {err_mx:.2e}, vs dequantised-weight oracle {err_plain:.2e}")
