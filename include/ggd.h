@@ -56,7 +56,9 @@ enum ggd_decoder_type { GGD_DEC_ONEWAY = 0, GGD_DEC_TWOWAY = 1 };
  * attention / FFN projections of every layer, out_layers.1) are stored as OCP fp8 e4m3fn with
  * one f32 scale per output channel (amax / 448), dequantized exactly into the bf16 MFMA tiles
  * and scaled in the GEMM epilogue -- BASELINE.json configs[3] (long clip, fp8 weights).  The
- * step-invariant projections (memory K/V, blend, step MLP) stay bf16.  Generic kernels only. */
+ * step-invariant projections (memory K/V, blend, step MLP) stay bf16.  Generic kernels and the
+ * long-clip loop; the loop runs its FFN and LayerNorm-projection GEMMs on block-scaled fp8 MFMA
+ * (e4m3 activations with one e8m0 scale per 32 values) unless GGD_ROUTE_FP8_MFMA = 1. */
 enum ggd_dtype { GGD_F32 = 0, GGD_BF16 = 1, GGD_FP8W = 2 };
 /* models/generator.py:34-45 -- sample_alg */
 enum ggd_alg { GGD_DDPM = 0, GGD_DDIM = 1 };
