@@ -73,7 +73,9 @@ __device__ __forceinline__ void pload(uint4 (&f)[N], const void* W, int kt_total
 // acc[rt][j] += A[rows of tile rt][k steps kc0 .. kc0 + KS) x f[j * KS + s] for j < nj (wave-
 // uniform).  The A fragments of step s + 1 are read from LDS before the MFMAs of step s issue,
 // so the LDS latency runs under the matrix work instead of between every MFMA.
-template <int RT, int NJ, int KS, int N>
+// TR: computed transposed (the weight fragments as the MFMA A operand), so lane (c16, g4) of tile
+// (rt, j) holds row 16 rt + c16, columns 16 j' + 4 g4 .. + 3 (four consecutive channels of one token)
+template <int RT, int NJ, int KS, int N, bool TR = false>
 __device__ __forceinline__ void pmma_n(f32x4 (&acc)[RT][NJ], const bf16_t* A, int SA, int kc0, const uint4 (&f)[N],
                                        int nj, int lane) {
   const int r16 = lane & 15, g = lane >> 4;
@@ -92,9 +94,14 @@ __device__ __forceinline__ void pmma_n(f32x4 (&acc)[RT][NJ], const bf16_t* A, in
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
-        if (j < nj)
-          acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[rt], __builtin_bit_cast(bf16x8, f[j * KS + s]),
-                                                               acc[rt][j], 0, 0, 0);
+        if (j < nj) {
+          if constexpr (TR)
+            acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, f[j * KS + s]), cur[rt],
+                                                                 acc[rt][j], 0, 0, 0);
+          else
+            acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[rt], __builtin_bit_cast(bf16x8, f[j * KS + s]),
+                                                                 acc[rt][j], 0, 0, 0);
+        }
     if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
     if (s + 1 < KS) {
 #pragma unroll
@@ -146,6 +153,12 @@ __device__ __forceinline__ void fattn_lds(unsigned char* att, int Lq, int Lk, fl
     if (a.stamps && k == 0 && li == 0 && hd == 1 && blockIdx.x == 0 && threadIdx.x == 0)         \
       a.stamps[i] = __builtin_amdgcn_s_memtime();                                               \
   } while (0)
+
+// A/B switch: the self-attention QKV of a head pair computed transposed with the 3-tap conv in
+// registers (1) or through a pre-conv bf16 image and a conv pass (0)
+#ifndef GGD_PSK_QKV_CONV
+#define GGD_PSK_QKV_CONV 1
+#endif
 
 constexpr int PK_THREADS = 512;  // 8 waves: two per SIMD, so one wave's LDS / L2 waits overlap the other's MFMAs
 
@@ -428,6 +441,62 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
       for (int hi = 0; hi < HP; ++hi) {
         LANE_IDS();
         const int hp = hp0 + hi;
+#if GGD_PSK_QKV_CONV
+        // the head pair's QKV computed transposed, the 3-tap conv over tokens in registers (DPP
+        // lane rotations, conv_tokens: the clip-group loop's KA epilogue) and the convolved rows
+        // written straight into the two attention images -- no pre-conv image, no conv pass, one
+        // LDS barrier fewer per head pair.  Local tile t (0 .. 11) = head t / 6, kind (Q, K, V)
+        // (t % 6) / 2, channels 16 (t % 2) .. of the head
+        {
+          f32x4 acc[RT][2];
+          zero_acc(acc);
+          pmma_n<RT, 2, 8, 16, true>(acc, Xn, SX, 0, fa, nq, lane);
+          if (hi < HP - 1) {  // refill: the next head pair, or the SA out-projection
+            const int tq[2] = {12 * (hp + 1) + tq0, 12 * (hp + 1) + tq1};
+            if (nq == 2) pload<2, 8>(fa, w.qkv, 8, tq, 0, lane);
+            else pload<1, 8>(fa, w.qkv, 8, tq, 0, lane);
+          } else {
+            const int to[2] = {2 * wave, 2 * wave + 1};
+            pload<2, 8>(fa, w.o_sa, 8, to, 0, lane);
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if (j >= nq) break;
+            const int t = j == 0 ? tq0 : tq1, hh = t / 6, kind = (t % 6) >> 1, c0 = (t & 1) * 16 + 4 * g4;
+            const float4 bq = ld_f4(w.qkv_b + hp * 192 + t * 16 + 4 * g4);
+            ConvW cw[4];
+            conv_w4(cw, kind == 0 ? w.sa_qw : kind == 1 ? w.sa_kw : w.sa_vw,
+                    kind == 0 ? w.sa_qb : kind == 1 ? w.sa_kb : w.sa_vb, c0);
+            f32x4 v[RT];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+              v[rt] = f32x4{acc[rt][j][0] + bq.x, acc[rt][j][1] + bq.y, acc[rt][j][2] + bq.z, acc[rt][j][3] + bq.w};
+            conv_tokens<RT>(v, cw, L, c16);
+            unsigned char* at = att_sa + hh * PL::ATT_B;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+              if (kind == 0) put_tok4<T, false>((T*)(at + AT::OQ), AT::SQ, rt * 16 + c16, c0, v[rt]);
+              else if (kind == 1) put_tok4<T, false>((T*)(at + AT::OK), AT::SQ, rt * 16 + c16, c0, v[rt]);
+              else put_tok4<T, true>((T*)(at + AT::OV), AT::SV, rt * 16 + c16, c0, v[rt]);
+            }
+          }
+          if constexpr (R < FLK) {  // keys past the row tiles: K rows finite, V^T columns zero
+            for (int e = tid; e < 2 * FDK * (FLK - R); e += NT) {
+              const int hh = e / (FDK * (FLK - R)), q = e % (FDK * (FLK - R)), c = q / (FLK - R), key = R + q % (FLK - R);
+              unsigned char* at = att_sa + hh * PL::ATT_B;
+              ((T*)(at + AT::OV))[c * AT::SV + key] = from_f32<T>(0.f);
+              ((T*)(at + AT::OK))[key * AT::SQ + c] = from_f32<T>(0.f);
+            }
+          }
+        }
+        bar_lds();
+        {  // both heads of the pair at once: threads 0-255 head 2hp, 256-511 head 2hp + 1
+          LANE_IDS();
+          const int hh = tid >> 8, t2 = tid & 255;
+          fattn_lds<R>(att_sa + hh * PL::ATT_B, L, L, a.scale, Ob + (2 * hp + hh) * FDK, SX, t2);
+          bar_lds();
+        }
+#else
         const float bq0 = w.qkv_b[hp * 192 + tq0 * 16 + c16], bq1 = w.qkv_b[hp * 192 + tq1 * 16 + c16];
         const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
                     cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
@@ -467,6 +536,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           fattn_lds<R>(at, L, L, a.scale, Ob + (2 * hp + hh) * FDK, SX, t2);
           bar_lds();
         }
+#endif
       }
       PSTAMP(2);
       if constexpr (PAIR)
