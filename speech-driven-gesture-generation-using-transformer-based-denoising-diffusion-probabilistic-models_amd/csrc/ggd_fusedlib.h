@@ -623,16 +623,20 @@ __device__ __forceinline__ float lanerow_sum4(float x) {
 // bf16 P values of key tile t are exactly the B operand (k = 4 g4 .. + 3, n = c16) of
 // O^T = V^T P^T on v_mfma_f32_16x16x16_bf16 -- no P tile through LDS, no per-element P stores.
 // Output lane map as fattn's: query c16, channels 4 g4 .. + 3 of each 16-channel tile.
+// qext (optional): the query rows come from another bf16 image (row stride sqe) instead of the
+// attention image's Q
 template <int LKT, int QR, bool TO_LDS, int CP>
 __device__ __forceinline__ void fattn_regp(unsigned char* att, int Lk, float scale, bf16_t* out, int ldo,
-                                           const OutRowsP<CP>& dst, int rt, int lane) {
+                                           const OutRowsP<CP>& dst, int rt, int lane, const bf16_t* qext = nullptr,
+                                           int sqe = 0) {
   using A = FAtt<bf16_t, QR>;
   typedef short s16x4 __attribute__((ext_vector_type(4)));
-  const bf16_t* Qm = (const bf16_t*)(att + A::OQ);
+  const bf16_t* Qm = qext ? qext : (const bf16_t*)(att + A::OQ);
+  const int sq = qext ? sqe : A::SQ;
   const bf16_t* Km = (const bf16_t*)(att + A::OK);
   const bf16_t* Vt = (const bf16_t*)(att + A::OV);
   const int c16 = lane & 15, g4 = lane >> 4;
-  const bf16x8 qf = *(const bf16x8*)(Qm + (rt * 16 + c16) * A::SQ + g4 * 8);
+  const bf16x8 qf = *(const bf16x8*)(Qm + (rt * 16 + c16) * sq + g4 * 8);
   f32x4 s[LKT];
 #pragma unroll
   for (int t = 0; t < LKT; ++t) {
@@ -690,7 +694,7 @@ __device__ __forceinline__ void fattn_regp(unsigned char* att, int Lk, float sca
 // bf16 runs fattn_regp (P in registers); f32 (the parity precision) keeps the P tile in LDS.
 template <typename T, int LKT, int QR = FR, bool TO_LDS = false, int CP = CP_KERNEL>
 __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float scale, T* out, int ldo,
-                                      int tid = ltid()) {
+                                      int tid = ltid(), const bf16_t* qext = nullptr, int sqe = 0) {
   using A = FAtt<T, QR>;
   const T* Qm = (const T*)(att + A::OQ);
   const T* Km = (const T*)(att + A::OK);
@@ -701,7 +705,7 @@ __device__ __forceinline__ void fattn(unsigned char* att, int Lq, int Lk, float 
   if (rt * 16 >= Lq) return;
   if constexpr (sizeof(T) == 2) {
     const OutRowsP<CP> dst(out, (uint32_t)(sizeof(T) * ((size_t)(Lq - 1) * ldo + FDK)));  // rows >= Lq dropped
-    fattn_regp<LKT, QR, TO_LDS, CP>(att, Lk, scale, out, ldo, dst, rt, lane);
+    fattn_regp<LKT, QR, TO_LDS, CP>(att, Lk, scale, out, ldo, dst, rt, lane, qext, sqe);
     return;
   }
   f32x4 s[LKT];

@@ -110,10 +110,29 @@ __device__ __forceinline__ void pmma_n(f32x4 (&acc)[RT][NJ], const bf16_t* A, in
   }
 }
 
-template <int RT, int NJ, int KS, int N>
+template <int RT, int NJ, int KS, int N, bool TR = false>
 __device__ __forceinline__ void pmma(f32x4 (&acc)[RT][NJ], const bf16_t* A, int SA, int kc0, const uint4 (&f)[N],
                                      int lane) {
-  pmma_n<RT, NJ, KS, N>(acc, A, SA, kc0, f, NJ, lane);
+  pmma_n<RT, NJ, KS, N, TR>(acc, A, SA, kc0, f, NJ, lane);
+}
+
+// residual epilogue of a transposed (TR) tile pair: lane (c16, g4) of tile (rt, j) holds row
+// 16 rt + c16, columns 16 (2 w + j) + 4 g4 .. + 3 -> one float4 read-modify-write of Hs per tile
+// (instead of four scalar ones); b: the bias of those 4 columns per j
+template <int RT>
+__device__ __forceinline__ void p_resid_tr(float* Hs, const f32x4 (&acc)[RT][2], const float4 (&b)[2], int wave,
+                                           int c16, int g4) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = (2 * wave + j) * 16 + 4 * g4;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float4* p = (float4*)(Hs + (rt * 16 + c16) * SH + col);
+      const float4 h = *p;
+      *p = make_float4(h.x + (acc[rt][j][0] + b[j].x), h.y + (acc[rt][j][1] + b[j].y), h.z + (acc[rt][j][2] + b[j].z),
+                       h.w + (acc[rt][j][3] + b[j].w));
+    }
+  }
 }
 
 template <int RT, int NJ>
@@ -126,11 +145,11 @@ __device__ __forceinline__ void zero_acc(f32x4 (&acc)[RT][NJ]) {
 
 template <int QR>
 __device__ __forceinline__ void fattn_lds(unsigned char* att, int Lq, int Lk, float scale, bf16_t* out, int ldo,
-                                          int tid) {
+                                          int tid, const bf16_t* qext = nullptr, int sqe = 0) {
   if (Lk <= 32)
-    fattn<bf16_t, 2, QR, true>(att, Lq, Lk, scale, out, ldo, tid);
+    fattn<bf16_t, 2, QR, true>(att, Lq, Lk, scale, out, ldo, tid, qext, sqe);
   else
-    fattn<bf16_t, 4, QR, true>(att, Lq, Lk, scale, out, ldo, tid);
+    fattn<bf16_t, 4, QR, true>(att, Lq, Lk, scale, out, ldo, tid, qext, sqe);
 }
 
 // Per-loop-body thread ids.  threadIdx.x is laundered through an empty asm so that every
@@ -158,6 +177,11 @@ __device__ __forceinline__ void fattn_lds(unsigned char* att, int Lq, int Lk, fl
 // registers (1) or through a pre-conv bf16 image and a conv pass (0)
 #ifndef GGD_PSK_QKV_CONV
 #define GGD_PSK_QKV_CONV 1
+#endif
+// A/B switch: the out-projections, the FFN-up chunk and the FFN-down residual computed transposed
+// (a lane holds 4 consecutive columns of one row: float4 / 8-byte LDS epilogues instead of scalar ones)
+#ifndef GGD_PSK_TR
+#define GGD_PSK_TR 1
 #endif
 
 constexpr int PK_THREADS = 512;  // 8 waves: two per SIMD, so one wave's LDS / L2 waits overlap the other's MFMAs
@@ -543,6 +567,20 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         if (!pp_swap_heads<R, SX>(Ob, part, xb, ep, flags, xl, a.status, &s_ok, L, tid)) return;
       // SA out-projection + residual
       {
+        #if GGD_PSK_TR
+        const float4 bo4[2] = {ld_f4(w.o_sa_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.o_sa_b + (2 * wave + 1) * 16 + 4 * g4)};
+        f32x4 acc[RT][2];
+        zero_acc(acc);
+        pmma<RT, 2, 8, 16, true>(acc, Ob, SX, 0, fa, lane);
+        if constexpr (PAIR) {  // fa <- cross-attn Q of this part's heads: wave w owns column tile 8 part + w
+          const int tq[1] = {8 * part + wave};
+          pload<1, 8>(fa, w.q_ca, 8, tq, 0, lane);
+        } else {  // fa <- cross-attn Q of every head: wave w owns head w's two column tiles
+          const int tq[2] = {2 * wave, 2 * wave + 1};
+          pload<2, 8>(fa, w.q_ca, 8, tq, 0, lane);
+        }
+        p_resid_tr<RT>(Hs, acc, bo4, wave, c16, g4);
+#else
         const float bo0 = w.o_sa_b[(2 * wave) * 16 + c16], bo1 = w.o_sa_b[(2 * wave + 1) * 16 + c16];
         f32x4 acc[RT][2];
         zero_acc(acc);
@@ -566,6 +604,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
               *p = *p + (acc[rt][j][r] + bo);
             }
         }
+#endif
         bar_lds();
       }
       // ---------------- cross-attention block (nn.py:163-167) ----------------
@@ -591,6 +630,33 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         // PAIR: the part's 4 heads, wave w one column tile (8 part + w)
         constexpr int NQJ = PAIR ? 1 : 2;
         const int qt0 = PAIR ? 8 * part + wave : 2 * wave;
+#if GGD_PSK_TR
+        // transposed, the 3-tap conv over tokens in registers: Yqb holds the CONVOLVED queries,
+        // which the attention reads in place (no conv pass per head pair)
+        f32x4 acc[RT][NQJ];
+        zero_acc(acc);
+        pmma<RT, NQJ, 8, 16, true>(acc, Xn, SX, 0, fa, lane);
+        {  // fa <- the CA out-projection
+          const int to[2] = {2 * wave, 2 * wave + 1};
+          pload<2, 8>(fa, w.o_ca, 8, to, 0, lane);
+        }
+        bar_lds();
+#pragma unroll
+        for (int j = 0; j < NQJ; ++j) {
+          const int c0 = ((qt0 + j) & 1) * 16 + 4 * g4;  // channel of the head
+          const float4 bq = ld_f4(w.q_ca_b + (qt0 + j) * 16 + 4 * g4);
+          ConvW cw[4];
+          conv_w4(cw, w.ca_qw, w.ca_qb, c0);
+          f32x4 v[RT];
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+            v[rt] = f32x4{acc[rt][j][0] + bq.x, acc[rt][j][1] + bq.y, acc[rt][j][2] + bq.z, acc[rt][j][3] + bq.w};
+          conv_tokens<RT>(v, cw, L, c16);
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt) put_tok4<T, false>(Yqb, SX, rt * 16 + c16, (qt0 + j) * 16 + 4 * g4, v[rt]);
+        }
+      }
+#else
         const float bq0 = w.q_ca_b[qt0 * 16 + c16], bq1 = w.q_ca_b[(qt0 + 1) * 16 + c16];
         f32x4 acc[RT][NQJ];
         zero_acc(acc);
@@ -610,6 +676,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
             for (int r = 0; r < 4; ++r) Yqb[(rt * 16 + 4 * g4 + r) * SX + col] = from_f32<T>(acc[rt][j][r] + bias);
         }
       }
+#endif
       // head pairs: both heads' conv and attention at once (threads 0-255 head 2hp, 256-511 head
       // 2hp + 1); the next pair's memory K|V loads fly under this pair's work
       for (int hi = 0; hi < HP; ++hi) {
@@ -622,13 +689,19 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         kvs.store(at, t2);
         if (hi < HP - 1) kvs.load(kvc_b + (size_t)(hd + 2) * KVC_ELEMS, t2);
         bar_lds();
+#if !GGD_PSK_TR
         conv_rows<T, false, R, NT / 2, T>((T*)(at + AT::OQ), AT::SQ, Yqb + hd * FDK, SX, L, dq, t2);
+#endif
         if (fixer) {
           fx.store<T, R>(at, dk, dv, Lk, lane);
           if (hi < HP - 1) fx.load(kvs_t, kvm_b, a.Ts, hd + 2, lane);
         }
         bar_lds();
+#if GGD_PSK_TR
+        fattn_lds<R>(at, L, Lk, a.scale, Ob + hd * FDK, SX, t2, Yqb + hd * FDK, SX);
+#else
         fattn_lds<R>(at, L, Lk, a.scale, Ob + hd * FDK, SX, t2);
+#endif
         bar_lds();
       }
       PSTAMP(3);
@@ -636,6 +709,17 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         if (!pp_swap_heads<R, SX>(Ob, part, xb, ep, flags, xl, a.status, &s_ok, L, tid)) return;
       // CA out-projection + residual
       {
+        #if GGD_PSK_TR
+        const float4 bo4[2] = {ld_f4(w.o_ca_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.o_ca_b + (2 * wave + 1) * 16 + 4 * g4)};
+        f32x4 acc[RT][2];
+        zero_acc(acc);
+        pmma<RT, 2, 8, 16, true>(acc, Ob, SX, 0, fa, lane);
+        {  // fa <- FFN-up chunk c0f (fb already holds FFN-down chunk c0f)
+          const int tf[1] = {8 * c0f + wave};
+          pload<1, 8>(fa, w.ff1, 8, tf, 0, lane);
+        }
+        p_resid_tr<RT>(Hs, acc, bo4, wave, c16, g4);
+#else
         const float bo0 = w.o_ca_b[(2 * wave) * 16 + c16], bo1 = w.o_ca_b[(2 * wave + 1) * 16 + c16];
         f32x4 acc[RT][2];
         zero_acc(acc);
@@ -656,6 +740,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
               *p = *p + (acc[rt][j][r] + bo);
             }
         }
+#endif
         bar_lds();
       }
       // ---------------- feed-forward block (nn.py:170-172) ----------------
@@ -671,10 +756,17 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         for (int ci = 0; ci < NC; ++ci) {
           LANE_IDS();
           const int c = c0f + ci;
+#if GGD_PSK_TR
+          const float4 bf4 = ld_f4(w.ff1_b + (8 * c + wave) * 16 + 4 * g4);
+          f32x4 acc[RT][1];
+          zero_acc(acc);
+          pmma<RT, 1, 8, 16, true>(acc, Xn, SX, 0, fa, lane);
+#else
           const float bf = w.ff1_b[(8 * c + wave) * 16 + c16];
           f32x4 acc[RT][1];
           zero_acc(acc);
           pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
+#endif
           if (ci < NC - 1) {
             const int tf[1] = {8 * (c + 1) + wave};
             pload<1, 8>(fa, w.ff1, 8, tf, 0, lane);
@@ -689,6 +781,18 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           // the chunk image is double-buffered: chunk c + 1 writes the other buffer, so no barrier
           // is needed behind the FFN-down MFMAs (the next chunk's barrier orders the reuse)
           T* Hc = Hd + (c & 1) * (PL::HID / sizeof(T));
+#if GGD_PSK_TR
+          {  // row 16 rt + c16, chunk columns 16 w + 4 g4 .. + 3: one 8-byte store per row tile
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+              const float v0 = fmaxf(acc[rt][0][0] + bf4.x, 0.f), v1 = fmaxf(acc[rt][0][1] + bf4.y, 0.f);
+              const float v2 = fmaxf(acc[rt][0][2] + bf4.z, 0.f), v3 = fmaxf(acc[rt][0][3] + bf4.w, 0.f);
+              put_tok4<T, false>(Hc, SHD, rt * 16 + c16, wave * 16 + 4 * g4, f32x4{v0 * v0, v1 * v1, v2 * v2, v3 * v3});
+            }
+          }
+          bar_lds();
+          pmma<RT, 2, 4, 8, true>(accd, Hc, SHD, 0, fb, lane);
+#else
           {
             const int col = (8 * c + wave) * 16 + c16 - 128 * c;  // column inside the chunk
 #pragma unroll
@@ -701,6 +805,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           }
           bar_lds();
           pmma<RT, 2, 4>(accd, Hc, SHD, 0, fb, lane);
+#endif
           {
             const int td[2] = {2 * wave, 2 * wave + 1};
             if (ci < NC - 1)
@@ -757,6 +862,10 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
                                   __uint_as_float(m.y & 0xffff0000u) + __uint_as_float(q.y & 0xffff0000u)};
             }
         }
+#if GGD_PSK_TR
+        const float4 b24[2] = {ld_f4(w.ff2_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.ff2_b + (2 * wave + 1) * 16 + 4 * g4)};
+        p_resid_tr<RT>(Hs, accd, b24, wave, c16, g4);
+#else
         const float b20 = w.ff2_b[(2 * wave) * 16 + c16], b21 = w.ff2_b[(2 * wave + 1) * 16 + c16];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -770,6 +879,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
               *p = *p + (accd[rt][j][r] + b2);
             }
         }
+#endif
         bar_lds();
       }
     }
