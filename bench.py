@@ -176,7 +176,8 @@ def parse():
     p.add_argument("--alg", default=None, choices=["ddpm", "ddim"])
     p.add_argument("--respacing", default=None)
     p.add_argument("--graph", action="store_true",
-                   help="replay each denoise step as a captured hipGraph (measured slower than eager launches)")
+                   help="the per-phase route with each denoise step replayed as a captured hipGraph (the persistent "
+                        "loops off: GGD_ROUTE_PER_CLIP = 1, GGD_ROUTE_PHASE_LAUNCHES = 1) -- for comparison")
     p.add_argument("--no-profile", action="store_true", help="skip the in-loop kernel events")
     p.add_argument("--overlap", default=None, choices=["on", "off"],
                    help="encode pass k+1's speech beside pass k's loop (default: per workload)")
@@ -452,6 +453,8 @@ def main():
     enc = __import__(ge.PKG_NAME + ".encoder", fromlist=["x"])
     ctx = model.context(L, enc.speech_len(arch["type"], wav_len), B)
     lib = ctx.lib
+    if args.graph:   # the hipGraph replay is a route of the per-phase launches: the persistent loops off
+        assert lib.ggd_set_route(ctx.h, 0, 1) == 0 and lib.ggd_set_route(ctx.h, 3, 1) == 0
     mx = args.dtype == "fp8" and not args.no_fp8_mfma   # block-scaled fp8 MFMA in the long loop (default)
     if args.dtype == "fp8":
         assert lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0 if mx else 1) == 0
