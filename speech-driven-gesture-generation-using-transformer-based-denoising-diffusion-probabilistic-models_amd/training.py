@@ -472,6 +472,7 @@ class TrainableModel:
         self._pe = {}
         self._enc_sd = {k: v.detach().cpu().clone() for k, v in sd.items() if k.startswith("speech_encoder.")}
         self._encoder = None
+        self._frontend = None
         self.training = True
         # BatchNorm running statistics of the trained encoder (buffers, updated in train mode)
         self.buffers = {k: v.detach().to(self.device).clone() for k, v in sd.items()
@@ -484,7 +485,8 @@ class TrainableModel:
         running statistics.  Eval mode (model.eval(), trainer.py:252): the encoder runs with the
         running statistics and updates nothing."""
         self.training = bool(mode)
-        self._encoder = None      # an eval-mode encoder is rebuilt from the current weights
+        if self.train_encoder:
+            self._encoder = None  # an eval-mode encoder is rebuilt from the current (trained) weights
         return self
 
     def eval(self):
@@ -510,6 +512,16 @@ class TrainableModel:
             self._encoder = SpeechEncoder(self._encoder_state(), self.device, dtype="f32", d_model=self.arch["d_model"])
         return self._encoder
 
+    def _frontend_encoder(self):
+        """A HIP encoder context kept only for its parameter-free front end (pre-emphasis, STFT, mel,
+        InstanceNorm: the wav2spec.* constants, which never train), built once: the trained
+        encoder's weights change every step, and rebuilding a context per step to reach the front
+        end cost a full weight upload per training step."""
+        if self._frontend is None:
+            from .encoder import SpeechEncoder
+            self._frontend = SpeechEncoder(self._enc_sd, self.device, dtype="f32", d_model=self.arch["d_model"])
+        return self._frontend
+
     # -- state ---------------------------------------------------------------------------------
     def load_state_dict(self, sd, strict=False):
         """Reference state_dict keys; with strict, every key of state_dict() must be present."""
@@ -528,6 +540,7 @@ class TrainableModel:
                 if k in sd and k not in self.params and k not in self.buffers:
                     self._enc_sd[k] = sd[k].detach().cpu().clone()
         self._encoder = None
+        self._frontend = None
         return missing
 
     def state_dict_keys(self):
@@ -614,7 +627,7 @@ class TrainableModel:
         front end's InstanceNorm'd mel image (N, 128, F) when already computed."""
         P = self.params
         if img is None:
-            img = self.speech_encoder().frontend(wav)                 # (N, 128, F), parameter-free
+            img = self._frontend_encoder().frontend(wav)              # (N, 128, F), parameter-free
         r = "speech_encoder.wav_encoder.feat_extractor."
         x = img[..., None]                                           # NHWC, C = 1
         x = self._bn(r + "bn1", relu(self._conv(r + "conv1", x, 1, 1)))
