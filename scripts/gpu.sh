@@ -13,7 +13,14 @@
 #   stamps            phase stamps of the clip-group loop           -> gpurun_out/$TAG_stamps.txt
 #   probe             L2 -> CU intake probe (scripts/build/l2probe) -> gpurun_out/$TAG_l2_intake.txt
 #   py:SCRIPT[:ARGS]  python3 scripts/SCRIPT ARGS                   -> gpurun_out/$TAG_SCRIPT.txt
-# Extra bench.py arguments: BENCH_ARGS.
+#   suite             the whole GPU suite without -x (every failure listed) -> gpurun_out/$TAG_pytest.txt
+#   train[:MODE]      training step, B = 64, MODE full|frozen        -> gpurun_out/$TAG_train_bench.txt (appended)
+#   trprof            rocprofv3 kernel stats of 5 training steps     -> gpurun_out/$TAG_train_kernel_stats.csv
+#   enctrace:B        encoder kernel trace at B clips               -> gpurun_out/$TAG_encoder_bB_trace.txt
+#   envab:WL:VAR      quick WL passes with VAR=0,1,0,1 on one box   -> gpurun_out/$TAG_WL_VAR_ab.txt
+# Extra bench.py arguments: BENCH_ARGS.  A round's evidence is two calls, e.g.
+#   TAG=r04t bash scripts/gpu.sh suite smoke prof:c2 prof:c4 prof:c5 bench:c2
+#   TAG=r04t bash scripts/gpu.sh pmc:c2 pmc:c4 pmc:c5 bench:c4 bench:c5
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -73,6 +80,41 @@ for step in "$@"; do
       out=gpurun_out/${T}_${s%.py}.txt
       timeout -k 10 600 python3 -u scripts/$s $a > $out 2>&1 || fail "$s" $out
       grep -v amdgpu.ids $out | tail -12 ;;
+    suite)
+      out=gpurun_out/${T}_pytest.txt
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v -s -p no:cacheprovider --timeout 300 --timeout-method thread \
+        > $out 2>&1 || fail suite $out
+      tail -1 $out ;;
+    train)
+      out=gpurun_out/${T}_train_bench.txt
+      timeout -k 10 300 python3 -u scripts/train_bench.py 64 10 ${arg:-full} >> $out 2>&1 || fail train $out
+      grep "train step" $out | tail -1 ;;
+    trprof)
+      d=gpurun_out/${T}_trprof
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d -o tr --output-format csv -- \
+        python3 -u scripts/train_bench.py 64 5 full > gpurun_out/${T}_trprof.log 2>&1 || fail trprof gpurun_out/${T}_trprof.log
+      f=$(find $d -name '*kernel_stats.csv' | head -1)
+      cp "$f" gpurun_out/${T}_train_kernel_stats.csv
+      rm -rf $d
+      head -6 gpurun_out/${T}_train_kernel_stats.csv | cut -c1-160 ;;
+    enctrace)
+      B=${arg:-32}
+      d=gpurun_out/${T}_enc_$B
+      timeout -k 10 300 rocprofv3 --kernel-trace -d $d -o run --output-format csv -- python3 scripts/enc_trace.py $B \
+        > gpurun_out/${T}_enc_$B.log 2>&1 || fail enctrace gpurun_out/${T}_enc_$B.log
+      python3 scripts/enc_trace.py --report $d > gpurun_out/${T}_encoder_b${B}_trace.txt && rm -rf $d
+      tail -1 gpurun_out/${T}_encoder_b${B}_trace.txt ;;
+    envab)
+      wl=${arg%%:*}
+      var=${arg#*:}
+      out=gpurun_out/${T}_${wl}_${var}_ab.txt
+      : > $out
+      for v in 0 1 0 1; do
+        env "$var=$v" timeout -k 10 300 python3 -u bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline \
+          --no-profile --no-f32-subrecord > gpurun_out/${T}_ab.json 2> gpurun_out/${T}_ab.err || fail envab gpurun_out/${T}_ab.err
+        python3 -c "import json; d=json.load(open('gpurun_out/${T}_ab.json')); print('$wl $var=$v', d['value'], d['ms_per_step'])" \
+          | tee -a $out
+      done ;;
     *)
       fail "unknown step $step" ;;
   esac
