@@ -64,6 +64,19 @@ def gemm(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, alpha=1.0, beta=0.0, bias=None
 # ------------------------------------------------------------------------------------------
 # autograd Functions over the HIP kernels
 # ------------------------------------------------------------------------------------------
+def _grad_slot(p):
+    """The .grad a weight-gradient kernel may accumulate into directly (beta = 1), sparing
+    AccumulateGrad's separate add: a leaf parameter whose .grad already exists as a contiguous f32
+    tensor (TrainableModel's views of the flat gradient buffer).  None: return the gradient to
+    autograd as usual."""
+    if p is None or not p.is_leaf or not p.requires_grad or th.is_grad_enabled():
+        return None
+    g = p.grad
+    if g is None or not g.is_contiguous() or g.dtype != th.float32 or g.shape != p.shape:
+        return None
+    return g
+
+
 class _Linear(th.autograd.Function):
     """nn.Linear (F.linear): y = x W^T + b; dX = dY W, dW = dY^T X, db = colsum dY."""
 
@@ -75,6 +88,7 @@ class _Linear(th.autograd.Function):
         gemm(0, 1, M, N, K, x, K, w, K, y, N, bias=b)
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
+        ctx.b = b
         return y
 
     @staticmethod
@@ -88,11 +102,20 @@ class _Linear(th.autograd.Function):
             dx = x.new_empty(M, K)
             gemm(0, 0, M, K, N, dy, N, w, K, dx, K)
         if ctx.needs_input_grad[1]:
-            dw = w.new_empty(N, K)
-            gemm(1, 0, N, K, M, dy, N, x, K, dw, K)
+            g = _grad_slot(w)
+            if g is not None:   # accumulate into the parameter's .grad (the flat gradient buffer)
+                gemm(1, 0, N, K, M, dy, N, x, K, g, K, beta=1.0)
+            else:
+                dw = w.new_empty(N, K)
+                gemm(1, 0, N, K, M, dy, N, x, K, dw, K)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = w.new_empty(N)
-            _ok(_lib().ggd_tr_colsum(M, N, _p(dy), N, _p(db), 0.0, _s(dy)), "colsum")
+            b = ctx.b
+            g = _grad_slot(b)
+            if g is not None:
+                _ok(_lib().ggd_tr_colsum(M, N, _p(dy), N, _p(g), 1.0, _s(dy)), "colsum")
+            else:
+                db = w.new_empty(N)
+                _ok(_lib().ggd_tr_colsum(M, N, _p(dy), N, _p(db), 0.0, _s(dy)), "colsum")
         return dx, dw, db
 
 
