@@ -62,8 +62,11 @@ class Generator:
     def generate_sample(self, shape: Tuple[int], wavs: th.Tensor, noise: th.Tensor = None,
                         inpaint_poses: th.Tensor = None, inpaint_masks: th.Tensor = None,
                         sample_alg: str = "ddim", trans_factor: float = None, pose_seed_len: int = None,
-                        return_dtype: str = "tensor", device: str = "cuda", progress: bool = True, **kw):
-        """generator.py:218-296 -> (N, L, C)."""
+                        return_dtype: str = "tensor", device: str = "cuda", progress: bool = True,
+                        check_status: bool = True, **kw):
+        """generator.py:218-296 -> (N, L, C).  The sampling loop is issued non-blocking; with
+        check_status (default) the model's contexts are synced before the result is returned, so
+        a persistent loop that failed on the device raises here instead of handing back x_T."""
         wavs = wavs.to(device)
         if inpaint_poses is not None:
             assert inpaint_masks is not None, "Provide inpaint_masks."
@@ -92,7 +95,16 @@ class Generator:
         out = sample_func(self.model, shape, noise=noise, denoise_fn=denoise_fn, model_kwargs=model_kwargs,
                           device=device, progress=progress, **kw)
         sample = out["sample"].transpose(1, 2)
+        if check_status:
+            self._check_status()
         return self.tensor2dtype(sample, return_dtype)
+
+    def _check_status(self):
+        """model.sync(): wait for the sampling contexts and raise the error of any loop that failed
+        after its non-blocking ggd_sample returned (status words, ggd_sync)."""
+        sync = getattr(self.model, "sync", None)
+        if sync is not None:
+            sync()
 
     @th.no_grad()
     def generate_batches(self, shape: Tuple[int], wav_batches, sample_alg: str = "ddim",
@@ -110,7 +122,8 @@ class Generator:
             nxt = wav_batches[k + 1] if k + 1 < len(wav_batches) else None
             shp = (wav.shape[0],) + tuple(shape[1:])
             outs.append(self.generate_sample(shp, wav, sample_alg=sample_alg, device=device, progress=False,
-                                             prefetch_wav=nxt, **kw))
+                                             prefetch_wav=nxt, check_status=False, **kw))
+        self._check_status()     # once, after every batch is issued (a failed loop raises here)
         return outs
 
     @th.no_grad()
@@ -159,7 +172,8 @@ class Generator:
                     wavs = th.cat([wavs, th.zeros((n, we - wav_seq_len), device=device)], dim=1)
                 sample = self.generate_sample((n, pose_dim, pose_window_len), wavs, inpaint_poses=inpaint_poses,
                                               inpaint_masks=masks, sample_alg=sample_alg, trans_factor=trans_factor,
-                                              pose_seed_len=pose_seed_len, device=device, progress=progress, **kw)
+                                              pose_seed_len=pose_seed_len, device=device, progress=progress,
+                                              check_status=False, **kw)
                 samples.append(sample)
                 ws = int(ps / pose_fps * wav_sr)
                 we = ws + wav_win
@@ -172,6 +186,7 @@ class Generator:
                     x = th.cat([tr, x[:, pose_seed_len:]], dim=1)
                 parts.append(x[:, :-pose_seed_len] if i < len(samples) - 1 else x)
             outs.append(th.cat(parts, dim=1)[:, :seq_len])
+        self._check_status()
         return self.tensor2dtype(th.cat(outs, dim=0), return_dtype)
 
     @staticmethod

@@ -31,3 +31,24 @@ def test_generate_batches_prefetches_next_batch():
     assert th.equal(diff.calls[0][1], wavs[1]) and th.equal(diff.calls[1][1], wavs[2])
     assert diff.calls[2][1] is None
     assert [c[2] for c in diff.calls] == [(3, 5, 7), (2, 5, 7), (4, 5, 7)]
+
+
+class _SyncModel(_FakeModel):
+    def __init__(self):
+        self.syncs = 0
+
+    def sync(self):
+        self.syncs += 1
+
+
+def test_generator_checks_loop_status_before_returning():
+    """ADVICE: the sampling loop is non-blocking, so the Generator entry points sync the model
+    (ggd_sync raises a failed loop's error) before handing results back: once per
+    generate_sample, once per generate_batches call."""
+    pkg = ge.load_package()
+    m = _SyncModel()
+    gen = pkg.Generator(m, _FakeDiffusion())
+    gen.generate_sample((2, 5, 7), th.randn(2, 320), sample_alg="ddim", device="cpu", progress=False)
+    assert m.syncs == 1
+    gen.generate_batches((0, 5, 7), [th.randn(n, 320) for n in (3, 2)], sample_alg="ddim", device="cpu")
+    assert m.syncs == 2
