@@ -285,3 +285,22 @@ def test_adamw_load_state_dict_restores_group_hyperparameters():
     ref.load_state_dict(st)
     g = ref.param_groups[0]
     assert tuple(g["betas"]) == opt.betas and g["eps"] == opt.eps and g["weight_decay"] == opt.weight_decay
+
+
+def test_grad_slot_only_for_existing_leaf_grads():
+    """training._grad_slot: a weight-gradient kernel accumulates (beta = 1) into .grad only for a
+    leaf parameter whose contiguous f32 .grad already exists (the flat gradient buffer's views),
+    and only outside create_graph backward; everything else goes back to autograd."""
+    tr = _training()
+    flat = th.zeros(12)
+    p = th.nn.Parameter(flat[:6].view(2, 3).clone())
+    with th.no_grad():
+        assert tr._grad_slot(p) is None                   # no .grad yet: autograd creates it
+        p.grad = flat[6:].view(2, 3)
+        assert tr._grad_slot(p).data_ptr() == flat[6:].data_ptr()
+        assert tr._grad_slot(p * 2) is None               # not a leaf
+        assert tr._grad_slot(None) is None
+        q = th.nn.Parameter(th.zeros(3, 2))
+        q.grad = th.zeros(2, 3).t()                       # non-contiguous .grad
+        assert tr._grad_slot(q) is None
+    assert tr._grad_slot(p) is None                        # grad mode on (create_graph backward)
