@@ -7,7 +7,8 @@ Workloads (BASELINE.json configs; beat-ours, 123 pose channels, random-init weig
      channels), ONE clip of L = 34 frames, 36,266-sample wav, respacing "50" DDPM, f32 (the
      reference computes in fp32) -- the CPU oracle's full 50-step loop is timed end to end beside it;
   c2 (default, the metric's config): 32 clips/GPU, L = 40, 32,000-sample wavs, DDPM T = 1000,
-     bf16 -- one launch of the clip-group persistent loop mk_kernel per pass; plus an f32
+     bf16 -- one launch of the clip-group persistent loop per pass (mr_kernel: the decoder split by
+     row blocks where its work is row-local; f32 runs mk_kernel); plus an f32
      sub-record (one pass of the same workload in f32, the parity precision);
   c4: 32 clips/GPU, L = 160, DDPM 1000, fp8-e4m3 step weights -- generic per-phase kernels;
   c5: 128 clips/GPU, L = 40, DDIM-50 -- one launch of the clip-pair loop (psk_kernel, two
@@ -47,6 +48,7 @@ sys.path.insert(0, ROOT)
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 FP8_PEAK_TFLOPS = 5000.0    # dense block-scaled fp8 MFMA (MI355X_MICROARCH.md:432; no sparsity)
 ROUTE_FP8_MFMA = 9          # include/ggd.h GGD_ROUTE_FP8_MFMA
+INFO_ROWS_LOOP = 9          # include/ggd.h GGD_INFO_ROWS_LOOP
 F32_PEAK_TFLOPS = 157.3
 
 
@@ -170,6 +172,7 @@ def parse():
     p.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
                    help="BASELINE.json config: c2 (default, the metric's config), c1 tedexp, c4 long clip, c5 DDIM-50")
     p.add_argument("--no-f32-subrecord", action="store_true", help="c2: skip the one-pass f32 sub-record")
+    p.add_argument("--no-subrecords", action="store_true", help="c2: skip the C4 / C5 sub-records")
     p.add_argument("--batch-per-gpu", type=int, default=None)
     p.add_argument("--dtype", default=None, choices=["bf16", "f32", "fp8"],
                    help="fp8: bf16 activations + e4m3 per-step decoder weights (default for c4)")
@@ -315,6 +318,67 @@ def f32_subrecord(pkg, cfg, sd, d_pose, L, B, wav, loop_name, diffusion, dev, T,
     return {"value": round(B * L / el, 2), "unit": "frames/s", "ms_per_step": round(el * 1e3, 3), "steps": 1,
             "warmup": 1, "dtype": "f32", "kernel_avg_launch_us": round(avg.value, 3), "launches": cnt.value,
             "roofline_frac_f32": round(ach / F32_PEAK_TFLOPS, 6) if ach else None, "peak_tflops": F32_PEAK_TFLOPS}
+
+
+def workload_subrecord(pkg, workload, dev, passes):
+    """One more BASELINE config under the same driver run: a warm-up pass, then ``passes`` timed
+    sampling passes (encoder + every denoise step, inputs resident in HBM) of WORKLOADS[workload] on
+    this GPU, the last one profiled: frames/s, ms per pass, the dominant loop's hipEvent time and
+    its fraction of the MFMA peak its arithmetic runs on (SURVEY.md 8d FLOPs).  No CPU leg."""
+    import ctypes
+    w = WORKLOADS[workload]
+    cfg = pkg.load_config(os.path.join(ROOT, "configs", "beat-ours.json"))
+    d_pose = int(cfg.Data.get("d_pose", 123))
+    L = int(cfg.Data.pose_window_len) * w["seq_mult"]
+    wav_len = int(cfg.Data.wav_sr * L / cfg.Data.pose_fps)
+    dtype, B = w.get("dtype", "bf16"), w["batch_per_gpu"]
+    model, diffusion, _, _, _ = pkg.create_model(d_pose, cfg.Model, dtype=dtype, device=dev)
+    if w["respacing"]:
+        diffusion = pkg.create_diffusion(dict(cfg.Model.Diffusion, timestep_respacing=w["respacing"]), False)
+    arch = model.arch
+    model.load_state_dict(pkg.init_state_dict(arch, seed=0))
+    T = diffusion.num_timesteps
+    loop = diffusion.p_sample_loop if w["alg"] == "ddpm" else diffusion.ddim_sample_loop
+    g = th.Generator(device=dev).manual_seed(4321)
+    wavs = [th.randn(B, wav_len, device=dev, generator=g) * 0.1 for _ in range(passes + 1)]
+    run = lambda wav, seed: loop(model, (B, d_pose, L), model_kwargs={"wav": wav}, seed=seed, extras=False)["sample"]
+    run(wavs[0], 1)
+    th.cuda.synchronize(dev)
+    ctx = next(iter(model._ctx.values()))
+    mx = dtype == "fp8"   # C4: the long loop's block-scaled fp8 MFMA route (the default)
+    if mx:
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0) == 0
+    t0 = time.perf_counter()
+    for k in range(passes):
+        if k == passes - 1:
+            ctx.lib.ggd_set_profiling(ctx.h, 1)
+        out = run(wavs[k + 1], 10 + k)
+    th.cuda.synchronize(dev)
+    model.sync()
+    el = time.perf_counter() - t0
+    ctx.lib.ggd_set_profiling(ctx.h, 0)
+    avg, cnt = ctypes.c_double(), ctypes.c_int64()
+    rc = ctx.lib.ggd_kernel_time(ctx.h, 0, ctypes.byref(avg), ctypes.byref(cnt))
+    kind = ctx.lib.ggd_profile_kind(ctx.h)
+    assert out.shape == (B, d_pose, L) and bool(th.isfinite(out).all())
+    Tm = 1 + int(ctx.desc.speech_len)
+    clip_step = clip_step_flops(L, Tm, arch["d_model"], d_pose, arch["n_layers"])
+    peak = FP8_PEAK_TFLOPS if mx else BF16_PEAK_TFLOPS
+    names = {1: "clip-group loop", 3: "psk_kernel (one workgroup per clip)", 4: "psk_kernel<pair> (clip-pair loop)",
+             5: "lk_kernel (long-clip loop)"}
+    rec = {"workload": f"{w['label']}: {B} clips x L={L}, wav {wav_len}, {w['alg'].upper()} T'={T}, "
+                       + ("fp8 MFMA (e4m3 step weights, block-scaled e4m3 activations)" if mx else "bf16"),
+           "value": round(passes * B * L / el, 2), "unit": "frames/s", "ms_per_step": round(el / passes * 1e3, 3),
+           "steps": passes, "warmup": 1, "dtype": "fp8" if mx else dtype}
+    if rc == 0 and cnt.value > 0 and avg.value > 0 and kind in names:
+        flop = clip_step * B * T / (cnt.value if kind in (1, 5) else 1)
+        ach = flop / (avg.value * 1e-6) / 1e12
+        rec.update({"kernel": names[kind], "kernel_avg_launch_us": round(avg.value, 3), "launches": cnt.value,
+                    "flop_per_launch": flop, "roofline_frac": round(ach / peak, 6), "peak_tflops": peak})
+    else:
+        rec.update({"kernel": None, "kernel_time_status": rc})
+    model._release()
+    return rec
 
 
 def rehearse(args, rank, world):
@@ -488,13 +552,21 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     prof_kind = 0
+    rows_loop = False
     if prof:  # the stamps of the profiled pass are read back after the clock stopped
         avg = ctypes.c_double()
         cnt = ctypes.c_int64()
-        lib.ggd_kernel_time(ctx.h, 0, ctypes.byref(avg), ctypes.byref(cnt))
+        rc = lib.ggd_kernel_time(ctx.h, 0, ctypes.byref(avg), ctypes.byref(cnt))
+        if rc != 0:   # e.g. the profiled loop fell back on the device: no kernel time to price
+            msg = lib.ggd_last_error(ctx.h)
+            raise SystemExit(f"ggd_kernel_time failed ({rc}): {msg.decode() if msg else ''}")
         prof_kind = lib.ggd_profile_kind(ctx.h)
         prof_us.append(avg.value * cnt.value)
         prof_n += cnt.value
+        if prof_kind == 1:   # which clip-group loop ran (GGD_INFO_ROWS_LOOP)
+            v = ctypes.c_double()
+            assert lib.ggd_route_info(ctx.h, INFO_ROWS_LOOP, ctypes.cast(ctypes.byref(v), ctypes.c_void_p)) == 0
+            rows_loop = v.value == 1.0
     dist_rec = None
     if dist is not None:
         t = th.tensor([elapsed], device=dev, dtype=th.float64)
@@ -530,7 +602,10 @@ def main():
         avg_us = sum(prof_us) / prof_n
         if prof_kind == 1:   # the persistent loop: one launch runs all T denoise steps of the batch
             flop = clip_step * B * T / prof_n   # one launch per chunk of <= 32 clips
-            kernel = f"mk_kernel<{args.dtype}> (persistent reverse loop: all {T} denoise steps, 17 phases each)"
+            kernel = (f"mr_kernel<{args.dtype}> (row-block clip-group loop: all {T} denoise steps in one launch, "
+                      "16 clip-group barriers each)" if rows_loop else
+                      f"mk_kernel<{args.dtype}> (head / chunk clip-group loop: all {T} denoise steps in one launch, "
+                      "16 clip-group barriers each)")
             timing = "hipEvent pair around the loop's single launch in the last timed pass"
         elif prof_kind == 3:  # one workgroup per clip: one launch runs all T steps of the batch
             flop = clip_step * B * T
@@ -556,7 +631,7 @@ def main():
             kernel = f"kb_kernel<{args.dtype}> (SA out-proj + LN2 + cross-attn Q + conv + cross-attention)"
             timing = "device realtime-clock span of every KB launch of the last timed pass"
         ach = flop / (avg_us * 1e-6) / 1e12
-        tr = pmc_traffic({1: "mk_kernel", 2: "attn_q_kernel", 3: "psk_kernel<3, false>",
+        tr = pmc_traffic({1: "mr_kernel" if rows_loop else "mk_kernel", 2: "attn_q_kernel", 3: "psk_kernel<3, false>",
                           4: "psk_kernel<3, true>", 5: "lk_kernel"}.get(
             prof_kind, "kb_kernel"),
                          args.workload)
@@ -599,6 +674,10 @@ def main():
             not args.no_f32_subrecord:
         res["f32_subrecord"] = f32_subrecord(pkg, cfg, sd, d_pose, L, B, wavs[-1][start:stop], loop_name=args.alg,
                                              diffusion=diffusion, dev=dev, T=T, clip_step=clip_step)
+    if rank == 0 and world == 1 and args.workload == "c2" and not args.no_subrecords:
+        # BASELINE configs 4 and 5 under the driver's clock too (one GPU each: their per-GPU legs)
+        res["c4_subrecord"] = workload_subrecord(pkg, "c4", dev, passes=1)
+        res["c5_subrecord"] = workload_subrecord(pkg, "c5", dev, passes=3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(pkg, cfg, sd, arch, B, L, wav_len, T,
                                            T if args.workload == "c1" else args.cpu_steps, args.alg,

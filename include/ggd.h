@@ -203,10 +203,14 @@ enum {
   GGD_ROUTE_SIMULATE_UNRESIDENT = 8, /* test hook, 1: the clip-group and clip-pair loops report status 2
                                         ("workgroups never all resident") without running, so the
                                         device-gated one-workgroup-per-clip fallback runs the clips */
-  GGD_ROUTE_FP8_MFMA = 9             /* GGD_FP8W long-clip loop: 0 the FFN and LayerNorm-projection GEMMs
+  GGD_ROUTE_FP8_MFMA = 9,            /* GGD_FP8W long-clip loop: 0 the FFN and LayerNorm-projection GEMMs
                                         on block-scaled fp8 MFMA (e4m3 activations, one e8m0 scale per
                                         32 values), 1 the e4m3 weights widened into bf16 MFMAs (the
                                         launch route's arithmetic, bit-equal to it) */
+  GGD_ROUTE_MEGA_ROWS = 10           /* clip-group loop, bf16: 0 the row-block decomposition (ggd_rows.hip:
+                                        the attention out-projections, LayerNorms and cross-attention on
+                                        each workgroup's own rows), 1 every phase split by head / FFN chunk
+                                        (ggd_mega.hip) */
 };
 int ggd_set_route(ggd_ctx* ctx, int32_t knob, int32_t value);
 enum {
@@ -219,7 +223,8 @@ enum {
   GGD_INFO_LONG_LAUNCHES = 6,        /* last ggd_sample: long-clip loop launches (0: another route) */
   GGD_INFO_CLIP_ATTN_LAUNCHES = 7,   /* running count of whole-clip attention launches (generic routes) */
   GGD_INFO_GATED_FALLBACKS = 8       /* last settled ggd_sample: chunks (clip-group loop) or batches
-                                        (clip pairs) the device-gated fallback loop ran instead */
+                                        (clip pairs) the device-gated fallback loop ran instead */,
+  GGD_INFO_ROWS_LOOP = 9             /* 1 when the last clip-group loop issued was the row-block loop */
 };
 int ggd_route_info(ggd_ctx* ctx, int32_t what, double* out);
 

@@ -47,7 +47,7 @@ for step in "$@"; do
       wl=${arg:-c2}
       out=gpurun_out/${T}_${wl}_bench.json
       extra=""
-      [ "$name" = quick ] && extra="--steps 3 --warmup 1 --no-cpu-baseline --no-f32-subrecord"
+      [ "$name" = quick ] && extra="--steps 3 --warmup 1 --no-cpu-baseline --no-f32-subrecord --no-subrecords"
       timeout -k 10 600 python -u bench.py --workload $wl $extra ${BENCH_ARGS} > $out 2> gpurun_out/${T}_${wl}_bench.err \
         || fail bench gpurun_out/${T}_${wl}_bench.err
       python3 -c "import json,sys; d=json.loads(open('$out').read().strip().splitlines()[-1]); r=d.get('roofline') or {}; print('$wl', d['value'], d['unit'], 'ms/pass', d['ms_per_step'], 'kernel_us', r.get('avg_launch_us'), 'frac', r.get('frac'))" ;;
@@ -55,7 +55,7 @@ for step in "$@"; do
       wl=${arg:-c2}
       d=gpurun_out/${T}_prof_$wl
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
-        python3 bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline --no-f32-subrecord ${BENCH_ARGS} \
+        python3 bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline --no-f32-subrecord --no-subrecords ${BENCH_ARGS} \
         > gpurun_out/${T}_prof_$wl.log 2>&1 || fail prof gpurun_out/${T}_prof_$wl.log
       f=$(find $d -name '*kernel_stats.csv' | head -1)
       cp "$f" gpurun_out/${T}_${wl}_kernel_stats.csv
@@ -111,7 +111,7 @@ for step in "$@"; do
       : > $out
       for v in 0 1 0 1; do
         env "$var=$v" timeout -k 10 300 python3 -u bench.py --workload $wl --steps 5 --warmup 2 --no-cpu-baseline \
-          --no-profile --no-f32-subrecord > gpurun_out/${T}_ab.json 2> gpurun_out/${T}_ab.err || fail envab gpurun_out/${T}_ab.err
+          --no-profile --no-f32-subrecord --no-subrecords > gpurun_out/${T}_ab.json 2> gpurun_out/${T}_ab.err || fail envab gpurun_out/${T}_ab.err
         python3 -c "import json; d=json.load(open('gpurun_out/${T}_ab.json')); print('$wl $var=$v', d['value'], d['ms_per_step'])" \
           | tee -a $out
       done ;;

@@ -1,4 +1,9 @@
-"""Per-phase time inside the persistent loop: body vs clip-group barrier (GPU box)."""
+"""Per-phase time inside the persistent clip-group loop: body vs clip-group barrier (GPU box).
+
+    python3 scripts/mega_stamps.py [heads] [layers=N]
+
+Default: the row-block loop (ggd_rows.hip mr_kernel); `heads`: the head / chunk loop (ggd_mega.hip
+mk_kernel, GGD_ROUTE_MEGA_ROWS = 1).  layers=N: a decoder of N layers (same weights' first N layers)."""
 import os as _os
 _os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
@@ -15,10 +20,16 @@ pkg = ge.load_package()
 native = __import__(ge.PKG_NAME + ".native", fromlist=["x"])
 cfg = pkg.load_config(os.path.join(ROOT, "configs", "beat-ours.json"))
 dev = th.device("cuda:0")
+HEADS = "heads" in sys.argv[1:]
+NL = int(next((a.split("=")[1] for a in sys.argv[1:] if a.startswith("layers=")), 4))
+if NL != 4:
+    cfg.Model.Decoder["n_layers"] = NL
 model, diffusion, _, _, _ = pkg.create_model(123, cfg.Model, dtype="bf16", device=dev)
 model.load_state_dict(pkg.init_state_dict(model.arch, seed=0))
 wav = th.randn(32, 32000, device=dev) * 0.1
 ctx, _ = model.prepare(wav, 40)
+assert ctx.lib.ggd_set_route(ctx.h, 10, 1 if HEADS else 0) == 0   # GGD_ROUTE_MEGA_ROWS
+print(f"{'head / chunk loop (mk_kernel)' if HEADS else 'row-block loop (mr_kernel)'}, {NL} layers", flush=True)
 
 
 def diag(what, p, n_out=1):
@@ -31,7 +42,7 @@ def diag(what, p, n_out=1):
 diffusion.p_sample_loop(model, (32, 123, 40), model_kwargs={"wav": wav}, seed=1, extras=False, n_steps=5)
 # bf16 loop: KA KB KC per layer (the FFN-down reduction runs inside the next phase) + KE
 # (round 4: the last layer's KD runs inside KE's rows phase -- 16 barriers per step)
-names = [f"L{li}{ph}" for li in range(4) for ph in ("ABCD" if li < 3 else "ABC")] + ["E"]
+names = [f"L{li}{ph}" for li in range(NL) for ph in ("ABCD" if li < NL - 1 else "ABC")] + ["E"]
 NB = len(names)
 for rep in range(3):
     diag(10, [1])
@@ -57,7 +68,9 @@ diag(11, [1])
 diffusion.p_sample_loop(model, (32, 123, 40), model_kwargs={"wav": wav}, seed=1, extras=False, n_steps=3)
 t = diag(11, [2], 80)
 labels = {0: "KA ln|qkv+conv|-|attn", 1: "KB load|oproj|ln2|q+conv|fix|attn", 2: "KC load|oproj|ln3|ffn1|ffn2",
-          3: "KD sum|-|store", 4: "KE ln+out|stage|upd"}
+          3: "KD sum|-|store", 4: "KE ln+out|stage|upd"} if HEADS else \
+    {0: "KA stage|qkv+conv|attn", 1: "KB stage|sa-oproj|ln2+fix|q+conv+ca|ca-oproj+ln3", 2: "KC stage|ffn1|ffn2",
+     3: "KD sum+ln1", 4: "KE kd+ln|eps|upd|emb+ln1"}
 for j in range(5):
     v = [round(x, 2) for x in t[16 * j + 1:16 * j + 8] if x >= 0]
     print(f"{labels[j]:40s} {v}", flush=True)

@@ -172,6 +172,9 @@ struct ggd_ctx {
   // persistent reverse loop (ggd_mega.hip)
   bool no_mega = false;                // ggd_diag what = 9: route sampling through per-phase launches
   int mega_place = 0;                  // ggd_diag what = 12: 0 XCD-local, 1 part per XCD, 2 group per XCD
+  bool mega_rows_off = false;          // GGD_ROUTE_MEGA_ROWS: 1 = the head / chunk loop (ggd_mega.hip) even
+                                       // where the row-block loop (ggd_rows.hip) runs the shape
+  bool mega_rows_last = false;         // the last clip-group loop issued was the row-block loop
   FusedArgs* mega_fa = nullptr;        // device [n_layers][4]
   unsigned long long* mega_phase_stamps = nullptr;  // ggd_diag what = 11: layer 1's phases + KE
   FinalArgs* mega_fe = nullptr;
@@ -1761,6 +1764,9 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
     case GGD_ROUTE_SIMULATE_UNRESIDENT:  // test hook: co-resident loops report status 2, run nothing
       c->sim_unresident = value != 0;
       return GGD_OK;
+    case GGD_ROUTE_MEGA_ROWS:       // 1: the clip-group loop split by head / chunk in every phase
+      c->mega_rows_off = value != 0;
+      return GGD_OK;
     default:
       break;
   }
@@ -1785,6 +1791,7 @@ int ggd_route_info(ggd_ctx* c, int32_t what, double* out) {
     case GGD_INFO_LONG_LAUNCHES: *out = c->long_launches; return GGD_OK;
     case GGD_INFO_CLIP_ATTN_LAUNCHES: *out = (double)c->clip_attn_launches; return GGD_OK;
     case GGD_INFO_GATED_FALLBACKS: *out = (double)c->gated_ran; return GGD_OK;
+    case GGD_INFO_ROWS_LOOP: *out = c->mega_rows_last ? 1.0 : 0.0; return GGD_OK;
     default: return fail(c, GGD_ERR_ARG, "unknown route info");
   }
 }
@@ -2367,14 +2374,20 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
     int r = prof_mark(c, s);
     if (r) return r;
   }
+  // bf16 shapes run the row-block decomposition (ggd_rows.hip) unless GGD_ROUTE_MEGA_ROWS = 1
+  const bool rows = !c->mega_rows_off && c->kvc && rows_supported(D.dtype, D.seq_len, D.speech_len);
+  c->mega_rows_last = rows;
+  auto launch = [&](const MegaArgs& m, int n, bool x) {
+    return rows ? launch_rows(D.dtype, D.seq_len, D.speech_len, m, n, x, s) : launch_mega(D.dtype, D.seq_len, m, n, x, s);
+  };
   for (int c0 = 0, ci = 0; c0 < a.n; c0 += cap, ++ci) {
     MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + ci,
                c0 == 0 ? c->mega_stamps : nullptr, c0, c->mega_place == 1 ? 1 : 0, nullptr, c->sim_unresident ? 1 : 0};
-    HIP_TRY(c, launch_mega(D.dtype, D.seq_len, m, std::min(cap, a.n - c0), xl, s));
+    HIP_TRY(c, launch(m, std::min(cap, a.n - c0), xl));
     if (xl) {  // the write-through re-run of this chunk, live only if the launch above reported 3
       MegaArgs g{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + MEGA_MAX_CHUNKS + ci,
                  nullptr, c0, 0, c->mega_status + ci, c->sim_unresident ? 1 : 0};
-      HIP_TRY(c, launch_mega(D.dtype, D.seq_len, g, std::min(cap, a.n - c0), false, s));
+      HIP_TRY(c, launch(g, std::min(cap, a.n - c0), false));
     }
   }
   if (c->profiling) {  // the loop's launches are the one timed span (read by ggd_kernel_time)

@@ -88,6 +88,19 @@ __device__ __forceinline__ float philox_normal(uint64_t seed, uint32_t clip, uin
 // ---------------------------------------------------------------------------
 struct UpdOut { float x0, raw, mean, xn; };
 
+// ---------------------------------------------------------------------------
+// bounded waits of the persistent loops (clip groups, clip pairs, long clips): a wait ends after
+// WAIT_TICKS of ELAPSED time on the chip-wide 100 MHz realtime counter, not after an iteration
+// count -- the exit cannot depend on what a poll observes or on how long one poll takes (round 4's
+// scalar-load poll variant hung: its polls never saw the partner flags).  No legitimate barrier or
+// residency wait comes near the bound; a loop that reaches it sets its status word and leaves.
+// ---------------------------------------------------------------------------
+constexpr unsigned long long WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
+__device__ __forceinline__ unsigned long long wait_t0() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ bool wait_expired(unsigned long long t0) {
+  return __builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS;
+}
+
 __device__ __forceinline__ UpdOut upd_math(const StepRec& r, int alg, float x, float e, bool have_x0,
                                            float x0_in, bool inp, float m, float p, float tf, float z) {
 #pragma clang fp contract(off)

@@ -329,6 +329,10 @@ bool persist_supported(int dtype, int d_model, int heads, int L, int Ts, int C);
 // xl: the XCD-local variant (CP_XL, grid padded to whole XCDs; placement 0 only)
 hipError_t launch_mega(int dtype, int L, const MegaArgs& a, int n, bool xl, hipStream_t s);
 int mega_capacity(int dtype, int L);   // clips one launch can hold (all workgroups co-resident)
+// the same loop with the decoder split by row blocks where its work is row-local (ggd_rows.hip, bf16;
+// Ts = memory tokens): one launch of 8 workgroups per clip, MegaArgs as launch_mega
+bool rows_supported(int dtype, int L, int Ts);
+hipError_t launch_rows(int dtype, int L, int Ts, const MegaArgs& a, int n, bool xl, hipStream_t s);
 hipError_t launch_mb(int mode, void* buf, size_t buf_bytes, int arg, int blocks, hipStream_t s);  // ggd_diag.hip
 hipError_t launch_gemm(int dtype, int pro, int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(int dtype, const AttnArgs& a, int n, hipStream_t s);

@@ -29,7 +29,6 @@ namespace {
 
 using namespace chainlib;
 
-constexpr int LK_SPIN_LIMIT = 1 << 21;
 constexpr int LK_DEPTH = 3;  // weight tile groups in flight per wave (4 measured no faster: 186.8 vs 184.7 us per step)
 constexpr int LK_ARRIVE = 128, LK_FLAGS = 256;  // ctl: tickets [x * 16], arrivals, group flag lines [g * 32]
 
@@ -47,9 +46,9 @@ __device__ int lk_role(unsigned* ctl, int* status, int nwg, int G) {
   xcc &= 7;
   const int t = (int)lk_add(ctl + xcc * 16, 1u);
   __hip_atomic_fetch_add(ctl + LK_ARRIVE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  for (int spin = 0; __hip_atomic_load(ctl + LK_ARRIVE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg;
-       ++spin) {
-    if (spin > LK_SPIN_LIMIT) {
+  const unsigned long long t_res = wait_t0();
+  while (__hip_atomic_load(ctl + LK_ARRIVE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg) {
+    if (wait_expired(t_res)) {
       atomicMax(status, 2);
       return -1;
     }
@@ -78,11 +77,12 @@ __device__ __forceinline__ bool lk_sync(unsigned* flags, int part, unsigned epoc
     const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
     const int off = (threadIdx.x & 7) * 4;
     int ok = 1;
+    const unsigned long long t0 = wait_t0();
     for (int spin = 0;; ++spin) {
       const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
       if (__ballot(v < epoch) == 0) break;
       if ((spin & 255) == 255 &&
-          (spin > LK_SPIN_LIMIT || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          (wait_expired(t0) || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
         if (threadIdx.x == 0) atomicMax(status, 1);
         ok = 0;
         break;

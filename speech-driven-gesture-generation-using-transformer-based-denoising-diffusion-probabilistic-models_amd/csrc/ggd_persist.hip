@@ -203,7 +203,6 @@ constexpr int PK_THREADS = 512;  // 8 waves: two per SIMD, so one wave's LDS / L
 // otherwise every workgroup takes pair blockIdx.x / 2 and hand-off stores write through (sc1).
 // All waits are bounded: a timed-out barrier sets `status` and its workgroups leave.
 // ------------------------------------------------------------------------------------------
-constexpr int PP_SPIN_LIMIT = 1 << 21;
 constexpr int PP_ARRIVE = 128, PP_FLAGS = 256;
 
 __device__ __forceinline__ int pp_slots(int x, int P) { return x < P ? 2 * ((P - 1 - x) / 8 + 1) : 0; }
@@ -216,9 +215,9 @@ __device__ int pp_role(const PersistArgs& a, int nwg, int P) {
   xcc &= 7;
   const int t = (int)__hip_atomic_fetch_add(ctl + xcc * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_add(ctl + PP_ARRIVE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  for (int spin = 0; __hip_atomic_load(ctl + PP_ARRIVE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg;
-       ++spin) {
-    if (spin > PP_SPIN_LIMIT) {
+  const unsigned long long t_res = wait_t0();
+  while (__hip_atomic_load(ctl + PP_ARRIVE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg) {
+    if (wait_expired(t_res)) {
       atomicMax(a.status, 2);
       return -1;
     }
@@ -249,12 +248,13 @@ __device__ __forceinline__ bool pp_sync(unsigned* flags, int part, unsigned epoc
   }
   if (threadIdx.x < 64) {
     int ok = 1;
+    const unsigned long long t0 = wait_t0();
     for (int spin = 0;; ++spin) {
       const unsigned v = xl ? __builtin_amdgcn_raw_buffer_load_b32(r, (part ^ 1) * 4, 0, CP_COH)
                             : __hip_atomic_load(flags + (part ^ 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (v >= epoch) break;
       if ((spin & 255) == 255 &&
-          (spin > PP_SPIN_LIMIT || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          (wait_expired(t0) || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
         if (threadIdx.x == 0) atomicMax(status, 1);
         ok = 0;
         break;

@@ -20,10 +20,10 @@ LIB_PATH = DIAG_LIB if os.environ.get("GGD_DIAG") == "1" else PRODUCT_LIB
 # A/B experiments (scripts/ab.sh): another build of the same library, same ABI
 if os.environ.get("GGD_LIB"):
     LIB_PATH = os.path.abspath(os.environ["GGD_LIB"])
-SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_persist.hip", "ggd_encoder.hip", "ggd_train.hip", "ggd_chain.hip", "ggd_attn.hip", "ggd_long.hip",
+SOURCES = ["ggd_kernels.hip", "ggd_fused.hip", "ggd_mega.hip", "ggd_rows.hip", "ggd_persist.hip", "ggd_encoder.hip", "ggd_train.hip", "ggd_chain.hip", "ggd_attn.hip", "ggd_long.hip",
            "ggd_api.hip"]
 DIAG_SOURCES = ["ggd_diag.hip"]   # + ggd_api.hip again with -DGGD_DIAG
-HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_chainlib.h", "ggd_fusedlib.h", "ggd_phases.h", os.path.join("..", "..", "include", "ggd.h"),
+HEADERS = ["ggd_kernels.h", "ggd_common.h", "ggd_chainlib.h", "ggd_fusedlib.h", "ggd_phases.h", "ggd_megasync.h", os.path.join("..", "..", "include", "ggd.h"),
            os.path.join("..", "..", "include", "ggd_train.h")]
 
 GGD_OK, GGD_IGNORED = 0, 1

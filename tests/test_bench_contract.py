@@ -98,3 +98,80 @@ def test_headline_pmc_summary_matches_the_kernel_sources():
     tr = bench.pmc_traffic("mk_kernel", "c2")
     assert tr is not None and not tr.get("stale"), tr
     assert tr["bytes_per_launch"] > 0
+
+
+class _FakeLib:
+    """The ggd_* calls workload_subrecord makes, answering like a loop that ran (kind, avg us)."""
+
+    def __init__(self, kind, avg_us, launches):
+        self.kind, self.avg_us, self.launches, self.prof = kind, avg_us, launches, []
+
+    def ggd_set_route(self, h, knob, value):
+        return 0
+
+    def ggd_set_profiling(self, h, on):
+        self.prof.append(on)
+        return 0
+
+    def ggd_kernel_time(self, h, which, avg, cnt):
+        avg._obj.value, cnt._obj.value = self.avg_us, self.launches
+        return 0
+
+    def ggd_profile_kind(self, h):
+        return self.kind
+
+
+@pytest.mark.parametrize("workload,kind,avg_us,launches", [("c4", 5, 159000.0, 1), ("c5", 4, 7500.0, 1)])
+def test_workload_subrecord_fields(monkeypatch, workload, kind, avg_us, launches):
+    """The C4 / C5 sub-records of the default C2 line: frames/s over the timed passes, ms per pass,
+    the loop's hipEvent time and its roofline fraction from SURVEY.md 8d's FLOPs (fp8 peak for C4's
+    block-scaled MFMA, bf16 for C5)."""
+    import types
+    import torch as th
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    monkeypatch.setattr(th.cuda, "synchronize", lambda *a, **k: None)
+    w = bench.WORKLOADS[workload]
+    L = 40 * w["seq_mult"]
+    lib = _FakeLib(kind, avg_us, launches)
+    calls = []
+
+    class FakeModel:
+        arch = {"d_model": 256, "n_layers": 4}
+        _ctx = {0: types.SimpleNamespace(lib=lib, h=None, desc=types.SimpleNamespace(speech_len=31 if L == 40 else 126))}
+
+        def load_state_dict(self, sd):
+            pass
+
+        def sync(self):
+            calls.append("sync")
+
+        def _release(self):
+            calls.append("release")
+
+    class FakeDiffusion:
+        num_timesteps = 50 if w["respacing"] else 1000
+
+        def _loop(self, model, shape, model_kwargs, seed, extras):
+            calls.append(shape)
+            return {"sample": th.zeros(shape)}
+        p_sample_loop = ddim_sample_loop = _loop
+
+    monkeypatch.setattr(pkg, "create_model", lambda *a, **k: (FakeModel(), FakeDiffusion(), None, None, None))
+    monkeypatch.setattr(pkg, "create_diffusion", lambda *a, **k: FakeDiffusion())
+    monkeypatch.setattr(pkg, "init_state_dict", lambda *a, **k: {})
+    passes = 3 if workload == "c5" else 1
+    rec = bench.workload_subrecord(pkg, workload, th.device("cpu"), passes=passes)
+    assert calls.count((w["batch_per_gpu"], 123, L)) == passes + 1 and calls[-1] == "release"
+    assert lib.prof == [1, 0]   # only the last timed pass is profiled
+    for k in ("workload", "value", "unit", "ms_per_step", "steps", "kernel", "kernel_avg_launch_us",
+              "roofline_frac", "peak_tflops", "flop_per_launch"):
+        assert k in rec, k
+    assert rec["unit"] == "frames/s" and rec["steps"] == passes and rec["value"] > 0
+    T = FakeDiffusion.num_timesteps
+    flop = bench.clip_step_flops(L, 1 + FakeModel._ctx[0].desc.speech_len, 256, 123, 4) * w["batch_per_gpu"] * T
+    assert rec["flop_per_launch"] == flop
+    peak = bench.FP8_PEAK_TFLOPS if workload == "c4" else bench.BF16_PEAK_TFLOPS
+    assert rec["peak_tflops"] == peak
+    assert abs(rec["roofline_frac"] - flop / (avg_us * 1e-6) / 1e12 / peak) < 1e-6
+    assert rec["dtype"] == ("fp8" if workload == "c4" else "bf16")
