@@ -156,7 +156,10 @@ typedef struct ggd_sample_args {
                              words are checked by a later call (ggd_sample, ggd_sync), and a failure is
                              returned by that call.  1: block until the loop has finished, check it,
                              and re-run a loop whose workgroups were never co-resident on a route
-                             that needs no co-residency (per-phase launches / one workgroup per clip) */
+                             that needs no co-residency (per-phase launches / one workgroup per clip).
+                             The clip-group loop is always blocking where the one-workgroup-per-clip
+                             loop cannot stand behind it as a device-gated fallback: f32, and bf16
+                             clips of 49..64 frames */
 } ggd_sample_args;
 
 /* Full reverse loop, i = T'-1 ... 0, one fused model+update per step.
@@ -224,7 +227,11 @@ enum {
   GGD_INFO_CLIP_ATTN_LAUNCHES = 7,   /* running count of whole-clip attention launches (generic routes) */
   GGD_INFO_GATED_FALLBACKS = 8       /* last settled ggd_sample: chunks (clip-group loop) or batches
                                         (clip pairs) the device-gated fallback loop ran instead */,
-  GGD_INFO_ROWS_LOOP = 9             /* 1 when the last clip-group loop issued was the row-block loop */
+  GGD_INFO_ROWS_LOOP = 9,            /* 1 when the last clip-group loop issued was the row-block loop */
+  GGD_INFO_BARRIER_TIMEOUTS = 10     /* running count of persistent-loop launches (clip-group chunks, clip-pair
+                                        batches, long-clip chunks) whose status word carried a barrier
+                                        timeout: such a launch is reported as an error, never covered by
+                                        a device-gated fallback */
 };
 int ggd_route_info(ggd_ctx* ctx, int32_t what, double* out);
 

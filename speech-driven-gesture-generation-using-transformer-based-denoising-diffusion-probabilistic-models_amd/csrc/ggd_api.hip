@@ -184,7 +184,8 @@ struct ggd_ctx {
   std::vector<FusedArgs> mega_fa_host;
   FinalArgs mega_fe_host{};
   int mega_status_host = 0;
-  int mega_xl_launches = 0, mega_fallbacks = 0;  // last ggd_sample: XCD-local launches, write-through re-runs
+  int mega_xl_launches = 0, mega_fallbacks = 0;  // last ggd_sample: XCD-local launches, chunks re-run elsewhere
+  int64_t barrier_timeouts = 0;        // running count of loop chunks / batches whose status word carried a timeout
   double wall_mhz = 100.0;             // realtime counter rate (hipDeviceAttributeWallClockRate)
 
   // Deferred status checks of the persistent loops: a ggd_sample that does not ask for `sync`
@@ -252,17 +253,20 @@ void settle(ggd_ctx* c, const ggd_ctx::Pending& p) {
     c->mega_fallbacks = 0;
     for (int ci = 0; ci < p.chunks; ++ci) {
       int st = p.host[ci];
-      if (p.xl && st == 3) {  // the gated write-through launch ran instead
-        ++c->mega_fallbacks;
+      bool fell_back = false;  // a chunk counts once in mega_fallbacks, however many re-runs it took
+      if (p.xl && st == 3) {   // the gated write-through launch ran instead
+        fell_back = true;
         st = p.host[MEGA_MAX_CHUNKS + ci];
       } else if (p.xl) {
         ++c->mega_xl_launches;
       }
       if (st == 2 && p.fb) {  // never all resident: the gated one-workgroup-per-clip loop ran the chunk
-        ++c->mega_fallbacks;
+        fell_back = true;
         ++c->gated_ran;
         st = 0;
       }
+      if (st & STATUS_TIMEOUT) ++c->barrier_timeouts;
+      c->mega_fallbacks += fell_back ? 1 : 0;
       worst = std::max(worst, st);
       unrun += st == 2 ? 1 : 0;
     }
@@ -271,10 +275,16 @@ void settle(ggd_ctx* c, const ggd_ctx::Pending& p) {
     if (worst && !c->sticky) {
       c->sticky = GGD_ERR_HIP;
       c->sticky_msg = worst == 2 ? "persistent loop (earlier ggd_sample): workgroups were not all resident"
-                                 : "persistent loop (earlier ggd_sample): a clip-group barrier timed out";
+                      : (worst & STATUS_TIMEOUT) || worst == 1 ? "persistent loop (earlier ggd_sample): a clip-group barrier timed out"
+                                                               : "persistent loop (earlier ggd_sample): failed (status " +
+                                                                     std::to_string(worst) + ")";
     }
   } else if (p.kind == 4) {
-    if (p.host[0] == 2 && p.fb) c->gated_ran = 1;
+    if (p.host[0] & STATUS_TIMEOUT) ++c->barrier_timeouts;
+    if (p.host[0] == 2 && p.fb) {
+      c->gated_ran = 1;
+      c->pair_launches = 0;   // the pair launches ran nothing: the gated fallback ran the batch
+    }
     if (p.host[0] && !(p.host[0] == 2 && p.fb) && !c->sticky) {
       c->sticky = GGD_ERR_HIP;
       c->sticky_msg = p.host[0] == 2 ? "clip-pair loop (earlier ggd_sample): workgroups were not all resident"
@@ -1792,6 +1802,7 @@ int ggd_route_info(ggd_ctx* c, int32_t what, double* out) {
     case GGD_INFO_CLIP_ATTN_LAUNCHES: *out = (double)c->clip_attn_launches; return GGD_OK;
     case GGD_INFO_GATED_FALLBACKS: *out = (double)c->gated_ran; return GGD_OK;
     case GGD_INFO_ROWS_LOOP: *out = c->mega_rows_last ? 1.0 : 0.0; return GGD_OK;
+    case GGD_INFO_BARRIER_TIMEOUTS: *out = (double)c->barrier_timeouts; return GGD_OK;
     default: return fail(c, GGD_ERR_ARG, "unknown route info");
   }
 }
@@ -2238,6 +2249,7 @@ int run_long(ggd_ctx* c, const ggd_sample_args& a, int nsteps) {
   HIP_TRY(c, hipStreamSynchronize(s));
   int worst = 0;
   for (int ci = 0; ci < chunks; ++ci) worst = std::max(worst, st[ci]);
+  if (worst & STATUS_TIMEOUT) ++c->barrier_timeouts;
   c->long_launches = chunks;
   if (worst == 3) {  // not placeable: nothing ran in the chunks that report 3; all chunks re-run on launches
     for (int ci = 0; ci < chunks; ++ci)
@@ -2364,9 +2376,11 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
   if (chunks > MEGA_MAX_CHUNKS) return fail(c, GGD_ERR_ARG, "batch too large for the persistent loop");
   HIP_TRY(c, hipMemsetAsync(c->mega_status, 0, sizeof(int) * 2 * MEGA_MAX_CHUNKS, s));
   const bool xl = c->mega_place == 0;
-  // bf16 clips the one-workgroup-per-clip loop can run get a device-gated fallback; otherwise (f32
-  // parity mode) the call checks the status itself before returning (blocking) and, when nothing
-  // ran, re-initialises x and hands the call to the launch route
+  // Shapes the one-workgroup-per-clip loop can run (bf16, L <= 48: persist_supported) get a
+  // device-gated fallback and the call returns once issued.  Every other shape is blocking: f32
+  // (the parity mode) AND bf16 clips of 49..64 frames (the clip-group loops run them, the
+  // one-workgroup loop does not) -- the call checks the status itself before returning and, when
+  // nothing ran, re-initialises x and hands the call to the launch route (include/ggd.h ggd_sample)
   const bool fb = c->persist;
   if (!fb) sync = true;
   if (c->profiling) {

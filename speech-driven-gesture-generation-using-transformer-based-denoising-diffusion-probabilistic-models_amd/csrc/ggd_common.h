@@ -96,6 +96,11 @@ struct UpdOut { float x0, raw, mean, xn; };
 // residency wait comes near the bound; a loop that reaches it sets its status word and leaves.
 // ---------------------------------------------------------------------------
 constexpr unsigned long long WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
+// a timed-out barrier: code 1 and the STATUS_TIMEOUT bit (ggd_kernels.h)
+__device__ __forceinline__ void status_timeout(int* status) {
+  atomicMax(status, 1);
+  atomicOr(status, STATUS_TIMEOUT);
+}
 __device__ __forceinline__ unsigned long long wait_t0() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ bool wait_expired(unsigned long long t0) {
   return __builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS;

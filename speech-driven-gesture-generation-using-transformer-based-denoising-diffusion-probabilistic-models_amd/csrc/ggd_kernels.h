@@ -222,6 +222,11 @@ struct MegaArgs {
                          // the device so the host never waits for the first launch's status
   int sim_unresident;    // test hook (GGD_ROUTE_SIMULATE_UNRESIDENT): report status 2 and run nothing
 };
+// A persistent loop's barrier that timed out ORs this bit into the loop's status word beside its
+// code 1: codes of other workgroups (2 not resident, 3 not placeable) are merged by atomicMax and
+// cannot hide it, and a word carrying it never equals 2 / 3, so no device-gated fallback runs in
+// its place -- the host reports the timeout (ggd_api.hip settle) instead of a fallback's success.
+constexpr int STATUS_TIMEOUT = 1 << 16;
 constexpr int MEGA_STAMP_STEPS = 2;
 constexpr int MEGA_MAX_CHUNKS = 16;  // status words: one per launch of up to mega_capacity() clips
 // PersistArgs::gate: open when the stood-in loop reported status 2 (nothing of it may be trusted)

@@ -131,7 +131,7 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
         if (__ballot(v < epoch) == 0) break;
         if ((spin & 255) == 255 && (wait_expired(t0) || __hip_atomic_load(status, __ATOMIC_RELAXED,
                                                                          __HIP_MEMORY_SCOPE_AGENT))) {
-          if (threadIdx.x == 0) atomicMax(status, 1);
+          if (threadIdx.x == 0) status_timeout(status);
           ok = 0;
           break;
         }
@@ -147,7 +147,7 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
       for (int spin = 0; mk_load(ctr) < target; ++spin) {
         if ((spin & 255) == 255 && (wait_expired(t0) || __hip_atomic_load(status, __ATOMIC_RELAXED,
                                                                          __HIP_MEMORY_SCOPE_AGENT))) {
-          atomicMax(status, 1);
+          status_timeout(status);
           ok = 0;
           break;
         }

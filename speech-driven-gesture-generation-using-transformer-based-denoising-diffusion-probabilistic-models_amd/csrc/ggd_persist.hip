@@ -255,7 +255,7 @@ __device__ __forceinline__ bool pp_sync(unsigned* flags, int part, unsigned epoc
       if (v >= epoch) break;
       if ((spin & 255) == 255 &&
           (wait_expired(t0) || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        if (threadIdx.x == 0) atomicMax(status, 1);
+        if (threadIdx.x == 0) status_timeout(status);
         ok = 0;
         break;
       }

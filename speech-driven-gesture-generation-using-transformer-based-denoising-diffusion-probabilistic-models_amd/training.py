@@ -64,12 +64,30 @@ def gemm(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, alpha=1.0, beta=0.0, bias=None
 # ------------------------------------------------------------------------------------------
 # autograd Functions over the HIP kernels
 # ------------------------------------------------------------------------------------------
+_DIRECT_GRAD = [0]   # > 0 inside direct_grad_accumulation()
+
+
+class direct_grad_accumulation:
+    """Context manager: inside it the Linear weight / bias gradients of leaf parameters whose .grad
+    exists (TrainableModel's views of the flat gradient buffer) are accumulated straight into that
+    .grad (beta = 1) and returned to autograd as None.  Only Trainer.step's own loss.backward() runs
+    inside it: there every such gradient is meant for .grad.  Outside it (torch.autograd.grad,
+    backward(inputs=...), parameter hooks) the gradients go through autograd as usual."""
+
+    def __enter__(self):
+        _DIRECT_GRAD[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _DIRECT_GRAD[0] -= 1
+        return False
+
+
 def _grad_slot(p):
     """The .grad a weight-gradient kernel may accumulate into directly (beta = 1), sparing
-    AccumulateGrad's separate add: a leaf parameter whose .grad already exists as a contiguous f32
-    tensor (TrainableModel's views of the flat gradient buffer).  None: return the gradient to
-    autograd as usual."""
-    if p is None or not p.is_leaf or not p.requires_grad or th.is_grad_enabled():
+    AccumulateGrad's separate add: inside direct_grad_accumulation() only, a leaf parameter whose
+    .grad already exists as a contiguous f32 tensor.  None: return the gradient to autograd as usual."""
+    if not _DIRECT_GRAD[0] or p is None or not p.is_leaf or not p.requires_grad or th.is_grad_enabled():
         return None
     g = p.grad
     if g is None or not g.is_contiguous() or g.dtype != th.float32 or g.shape != p.shape:
@@ -1066,7 +1084,8 @@ class Trainer:
         self.optimizer.zero_grad()
         broadcast_buffers(self.model)
         terms = self._compute_loss(batch, noise=noise, t=t)
-        terms["loss"].backward()
+        with direct_grad_accumulation():
+            terms["loss"].backward()
         allreduce_gradients(self.model.flat_grad)
         gn = grad_norm(self.model)
         scale = 1.0

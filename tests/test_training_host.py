@@ -297,10 +297,14 @@ def test_grad_slot_only_for_existing_leaf_grads():
     with th.no_grad():
         assert tr._grad_slot(p) is None                   # no .grad yet: autograd creates it
         p.grad = flat[6:].view(2, 3)
-        assert tr._grad_slot(p).data_ptr() == flat[6:].data_ptr()
-        assert tr._grad_slot(p * 2) is None               # not a leaf
-        assert tr._grad_slot(None) is None
-        q = th.nn.Parameter(th.zeros(3, 2))
-        q.grad = th.zeros(2, 3).t()                       # non-contiguous .grad
-        assert tr._grad_slot(q) is None
-    assert tr._grad_slot(p) is None                        # grad mode on (create_graph backward)
+        assert tr._grad_slot(p) is None                   # outside Trainer.step's backward: autograd
+        with tr.direct_grad_accumulation():
+            assert tr._grad_slot(p).data_ptr() == flat[6:].data_ptr()
+            assert tr._grad_slot(p * 2) is None           # not a leaf
+            assert tr._grad_slot(None) is None
+            q = th.nn.Parameter(th.zeros(3, 2))
+            q.grad = th.zeros(2, 3).t()                   # non-contiguous .grad
+            assert tr._grad_slot(q) is None
+        assert tr._grad_slot(p) is None
+    with tr.direct_grad_accumulation():
+        assert tr._grad_slot(p) is None                    # grad mode on (create_graph backward)
