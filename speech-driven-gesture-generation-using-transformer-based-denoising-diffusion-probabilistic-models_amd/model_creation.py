@@ -24,7 +24,8 @@ def create_model(d_pose, model_params, lr=1e-2, weight_decay=None, scheduler_par
     Inference (is_training False): the HIP sampler model; optimizer, schedule_sampler and
     lr_scheduler are None.  Training: a training.TrainableModel (reference init, seed 0; the HA2G
     encoder trained in train mode unless train_encoder=False) with AdamW, the uniform schedule
-    sampler and the configured lr schedule (s2g_v2 + one-way decoder).  Legacy {"type","args"} model params
+    sampler and the configured lr schedule (the one-way decoder under s2g_v2, default or
+    inpaint).  Legacy {"type","args"} model params
     (tedexp) are adapted to the flat schema first.
     """
     if is_training:
@@ -35,7 +36,11 @@ def create_model(d_pose, model_params, lr=1e-2, weight_decay=None, scheduler_par
         if is_legacy_schema(model_params):
             model_params = adapt_legacy({"Model": model_params.to_dict()}).Model
         arch = arch_from_config(model_params, d_pose)
-        model = training.TrainableModel(arch, init_state_dict(arch, seed=0), device=device, train_encoder=train_encoder)
+        seed_len = None
+        if arch["type"] == "inpaint":   # model_creation.py:134-142
+            seed_len = int(model_params["Generate"]["pose_seed_len"])
+        model = training.TrainableModel(arch, init_state_dict(arch, seed=0), device=device, train_encoder=train_encoder,
+                                        pose_seed_len=seed_len)
         diffusion = create_diffusion(model_params["Diffusion"], True)
         optimizer = training.AdamW(model, lr=lr, weight_decay=weight_decay)
         sp = scheduler_params.to_dict() if isinstance(scheduler_params, JsonConfig) else scheduler_params

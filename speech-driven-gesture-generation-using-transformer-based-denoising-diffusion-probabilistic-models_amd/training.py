@@ -19,8 +19,11 @@ ops) and a few copies (transposes, concatenations, padding).  Parameters live in
 second flat buffer (each parameter's .grad a view; autograd accumulates into it in place), so
 the all-reduce is one RCCL call per bucket and AdamW is one HIP launch over the whole model.
 
-Scope: the s2g_v2 model with the one-way decoder (the beat-ours configuration): step encoder,
-blend layer, decoder and -- by default (train_encoder=True, as the reference) -- the HA2G speech
+Scope: the one-way decoder under the s2g_v2 model (the beat-ours configuration: step encoder,
+blend layer, decoder), the default model (memory = the step token and the three speech levels
+concatenated, model.py:41-73) and the inpaint model (the default model plus the seed-pose
+projection MLP, model.py:120-166, trained with the trainer's seed poses and masks,
+trainer.py:139-146), and -- by default (train_encoder=True, as the reference) -- the HA2G speech
 encoder, whose SE-ResNet trains with BatchNorm in train mode (batch statistics, running-stat
 updates).  train_encoder=False freezes the encoder: it then runs as the HIP inference encoder
 (eval mode) and its weights pass through state_dict() unchanged.  TrainableModel.eval() switches
@@ -490,10 +493,15 @@ class TrainableModel:
     """The s2g_v2 + one-way-decoder denoiser (models/model.py:76-117, nn.py:177-228) with its
     trainable parameters in one flat f32 device buffer under the reference's state_dict names."""
 
-    def __init__(self, arch, sd, device="cuda", train_encoder=False):
-        if arch["type"] != "s2g_v2" or arch["decoder"] != "oneway_cross_attention":
-            raise ValueError("the training path covers s2g_v2 with the one-way decoder (beat-ours)")
+    def __init__(self, arch, sd, device="cuda", train_encoder=False, pose_seed_len=None):
+        if arch["type"] not in ("s2g_v2", "default", "inpaint") or arch["decoder"] != "oneway_cross_attention":
+            raise ValueError("the training path covers the one-way decoder under the s2g_v2, default and inpaint "
+                             "models")
+        if arch["type"] == "inpaint" and pose_seed_len is None:
+            raise ValueError("the inpaint model trains with its pose_seed_len (Model.Generate.pose_seed_len, "
+                             "model_creation.py:141)")
         self.arch = arch
+        self.pose_seed_len = pose_seed_len   # Speech2GestureModelInpaint.pose_seed_len (model.py:134)
         self.device = th.device(device)
         if self.device.type != "cuda":
             raise ValueError("the training path runs on a GPU device only (no CPU fallback)")
@@ -687,29 +695,47 @@ class TrainableModel:
             out.append(linear(h, proj_w, proj_b))
         return tuple(out)
 
-    def __call__(self, x_t, t, z=None, wav=None):
+    def __call__(self, x_t, t, z=None, wav=None, inpaint_pose=None, inpaint_mask=None):
         """x_t (N, C, L), t (N,) int64 original timesteps -> eps (N, C, L).  Speech: z = (z_low, z_mid,
         z_high) tokens (N, T_i, d) from the frozen encoder, or wav (N, T_wav) encoded here (through the
         trained encoder in train mode when train_encoder, else the HIP eval-mode encoder on the
-        current weights -- no gradient reaches the encoder in eval mode)."""
+        current weights -- no gradient reaches the encoder in eval mode).  The inpaint model also
+        takes inpaint_pose (L, N, C) and inpaint_mask (L, N, 1), the reference's model kwargs."""
         if z is None:
             z = self.encode(wav) if (self.train_encoder and self.training) else self.speech_encoder()(wav)
         P, a = self.params, self.arch
         d = a["d_model"]
         N, C, L = x_t.shape
-        # memory: [step token; blend(left-padded levels)] (model.py:91-106)
         e = step_embedding(t.to(self.device), d)
         s = linear(silu(linear(e, P["diffusion_step_encoder.proj.0.weight"], P["diffusion_step_encoder.proj.0.bias"])),
                    P["diffusion_step_encoder.proj.2.weight"], P["diffusion_step_encoder.proj.2.bias"])
-        longest = max(zi.shape[1] for zi in z)
-        zz = th.cat([F.pad(zi, (0, 0, longest - zi.shape[1], 0)) for zi in z], dim=-1)
-        sp = linear(zz, P["blend_layer.weight"], P["blend_layer.bias"])
-        mem = th.cat([s[:, None], sp], dim=1)
+        if a["type"] == "s2g_v2":
+            # memory: [step token; blend(left-padded levels)] (model.py:91-106)
+            longest = max(zi.shape[1] for zi in z)
+            zz = th.cat([F.pad(zi, (0, 0, longest - zi.shape[1], 0)) for zi in z], dim=-1)
+            sp = linear(zz, P["blend_layer.weight"], P["blend_layer.bias"])
+            mem = th.cat([s[:, None], sp], dim=1)
+        else:
+            # default / inpaint: memory = [step token; z_low; z_mid; z_high] along time (model.py:44-67)
+            mem = th.cat([s[:, None]] + [zi for zi in z], dim=1)
         Tm = mem.shape[1]
         pre = "pose_decoder."
         m = add(linear(mem, P[pre + "emb_mem.weight"], P[pre + "emb_mem.bias"]), self._pe_rows(N, Tm))
-        h = add(linear(x_t.transpose(1, 2).contiguous(), P[pre + "emb_x.weight"], P[pre + "emb_x.bias"]),
-                self._pe_rows(N, L))
+        x_in = x_t.transpose(1, 2).contiguous()                                      # (N, L, C)
+        if a["type"] == "inpaint":
+            # Speech2GestureModelInpaint.myforward (model.py:152-166): x + proj([pose * mask, mask]); the
+            # batch's seed poses and mask are data (no parameters): their product and concatenation are
+            # plain device tensor ops, the proj MLP runs on the HIP kernels with its gradients
+            if inpaint_pose is None or inpaint_mask is None:
+                raise TypeError("Speech2GestureModelInpaint.myforward() needs inpaint_pose and inpaint_mask")
+            assert tuple(inpaint_pose.shape) == (L, N, C) and tuple(inpaint_mask.shape) == (L, N, 1)
+            pose = inpaint_pose.to(self.device, th.float32).transpose(0, 1)
+            mask = inpaint_mask.to(self.device, th.float32).transpose(0, 1)
+            xi = th.cat([pose * mask, mask], dim=-1).contiguous()                    # (N, L, C + 1)
+            u = silu(linear(xi, P["proj.0.weight"], P["proj.0.bias"]))
+            u = silu(linear(u, P["proj.2.weight"], P["proj.2.bias"]))
+            x_in = add(x_in, linear(u, P["proj.4.weight"], P["proj.4.bias"]))       # Dropout p = 0 (configs)
+        h = add(linear(x_in, P[pre + "emb_x.weight"], P[pre + "emb_x.bias"]), self._pe_rows(N, L))
         for i in range(a["n_layers"]):
             q = pre + f"layers.{i}."
             u = layer_norm(h, P[q + "norm_self_attn.weight"], P[q + "norm_self_attn.bias"])
@@ -771,7 +797,8 @@ def training_losses(diffusion, model, x_start, t, model_kwargs, noise=None):
         noise = th.randn_like(x_start)
     noise = noise.contiguous().float()
     x_t = q_sample(diffusion, x_start, t, noise)
-    eps = model(x_t, t, z=model_kwargs.get("speech_tokens"), wav=model_kwargs.get("wav"))
+    eps = model(x_t, t, z=model_kwargs.get("speech_tokens"), wav=model_kwargs.get("wav"),
+                inpaint_pose=model_kwargs.get("inpaint_pose"), inpaint_mask=model_kwargs.get("inpaint_mask"))
     assert eps.shape == noise.shape == x_start.shape
     mse = _DiffusionMSE.apply(eps, noise)
     idx = t.cpu().numpy()
@@ -1067,6 +1094,13 @@ class Trainer:
             kw = {"wav": batch["wav"]}                       # encoded with grad (train-mode SE-ResNet)
         elif z is None:
             kw = {"speech_tokens": self.encoder(batch["wav"])}   # frozen HA2G encoder (eval mode)
+        if self.model.arch["type"] == "inpaint":
+            # trainer.py:139-146: the seed poses (the clip's first pose_seed_len frames) and their mask
+            inpaint_poses = poses.clone()
+            inpaint_masks = th.ones_like(inpaint_poses)[:, :, 0:1]          # (N, T, 1)
+            inpaint_masks[:, self.model.pose_seed_len:] = 0
+            kw["inpaint_pose"] = inpaint_poses.transpose(0, 1)              # (T, N, C)
+            kw["inpaint_mask"] = inpaint_masks.transpose(0, 1)              # (T, N, 1)
         x_start = poses.transpose(1, 2)
         if noise is None:
             noise = th.randn_like(x_start)

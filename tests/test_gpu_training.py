@@ -542,3 +542,76 @@ def test_optimizer_state_is_torch_adamw_layout(pkg, beat_cfg, tr):
     assert opt2.step_count == 3
     close(opt2.exp_avg, opt.exp_avg, 1e-6)
     close(opt2.exp_avg_sq, opt.exp_avg_sq, 1e-6)
+
+
+# ------------------------------------------------------------------------------------------
+# the inpaint model's training inputs (trainer.py:139-146, model.py:120-166)
+# ------------------------------------------------------------------------------------------
+def test_inpaint_training_gradients_match_oracle_and_checkpoint_samples(pkg, beat_cfg, tr):
+    """Speech2GestureModelInpaint trained the reference's way: the trainer builds inpaint_pose = the
+    clip's poses and inpaint_mask = 1 on the first pose_seed_len frames (trainer.py:139-146); the
+    model adds proj([pose * mask, mask]) to x (model.py:152-166).  Loss and every gradient (the proj
+    MLP's included) against torch autograd through the oracle; then a Trainer step's checkpoint loads
+    strictly into the inpaint sampler and its eps matches the oracle on the trained weights."""
+    cfg = dict(beat_cfg.Model.to_dict(), type="inpaint")   # beat-ours with Model.type "inpaint"
+    arch = pkg.arch_from_config(cfg, D_POSE)
+    assert arch["type"] == "inpaint"
+    seed_len = int(cfg["Generate"]["pose_seed_len"])
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    g = th.Generator().manual_seed(53)
+    for k in [k for k in sd if k.startswith("proj.")]:   # GLIDE zero init would give proj.0 / proj.2 zero gradients
+        sd[k] = th.randn(sd[k].shape, generator=g) * 0.05
+    sampler, _, _, _, _ = pkg.create_model(D_POSE, cfg, dtype="f32", device="cuda:0")
+    sampler.load_state_dict(sd)
+    n = 3
+    wav = th.randn(n, WAV, generator=g) * 0.1
+    z = sampler.encoder()(wav.cuda())
+    diffusion = pkg.create_diffusion(beat_cfg.Model.Diffusion.to_dict(), True)
+    model = tr.TrainableModel(arch, sd, "cuda", pose_seed_len=seed_len)
+    assert "proj.0.weight" in model.params and "blend_layer.weight" not in model.params
+    trainer = tr.Trainer(model, diffusion, None, lr=1e-3, weight_decay=0.0)
+    poses = th.randn(n, L, D_POSE, generator=g)
+    t = th.tensor([901, 333, 12])
+    noise = th.randn(n, D_POSE, L, generator=g)
+    model.zero_grad()
+    terms = trainer._compute_loss({"pose": poses.cuda(), "speech_tokens": z}, noise=noise.cuda(), t=t.cuda())
+    terms["loss"].backward()
+    names = list(model.params)
+    sd_ref = {k: v.detach().float().clone() for k, v in sd.items()}
+    for k in names:
+        sd_ref[k].requires_grad_(True)
+    x0 = poses.transpose(1, 2)
+    idx = t.numpy()
+    ext = lambda a: th.from_numpy(a[idx]).float().reshape(-1, 1, 1)
+    x_t = ext(diffusion.sqrt_alphas_cumprod) * x0 + ext(diffusion.sqrt_one_minus_alphas_cumprod) * noise
+    ocfg = oracle_cfg(arch)
+    mask = th.zeros(L, n, 1)
+    mask[:seed_len] = 1.0
+    speech = ref_denoiser.speech_memory(sd_ref, ocfg, tuple(a.cpu() for a in z))
+    eps = ref_denoiser.denoise(sd_ref, ocfg, x_t, t, speech=speech, inpaint_pose=poses.transpose(0, 1),
+                               inpaint_mask=mask)
+    want = ((eps - noise) ** 2).mean(dim=(1, 2)).mean()
+    want.backward()
+    loss = terms["loss"].item()
+    assert abs(loss - want.item()) <= 1e-5 * want.item(), (loss, want.item())
+    floor = 1e-4 * max(sd_ref[k].grad.abs().max().item() for k in names)
+    worst = max(((model.params[k].grad.cpu() - sd_ref[k].grad).abs().max().item()
+                 / max(sd_ref[k].grad.abs().max().item(), floor), k) for k in names)
+    print("\ninpaint: worst gradient error", worst,
+          "| proj.0.weight max|grad|", sd_ref["proj.0.weight"].grad.abs().max().item())
+    assert sd_ref["proj.0.weight"].grad.abs().max().item() > 0
+    assert worst[0] <= 2e-3, worst
+    # one full Trainer step, then the checkpoint into the inpaint sampler (main.py:113-115)
+    res = trainer.step({"pose": poses.cuda(), "speech_tokens": z}, noise=noise.cuda(), t=t.cuda())
+    assert np.isfinite(res["loss"])
+    trained = {k: v.cpu() for k, v in model.state_dict().items()}
+    assert set(trained) == set(sd)
+    assert not th.equal(trained["proj.0.weight"], sd["proj.0.weight"])
+    sampler.load_state_dict(trained, strict=True)
+    xs = th.randn(n, D_POSE, L, generator=g)
+    ts = th.tensor([999, 500, 0])
+    got = sampler(xs.cuda(), ts.cuda(), wav=wav.cuda(), inpaint_pose=poses.transpose(0, 1).cuda(),
+                  inpaint_mask=mask.cuda()).cpu()
+    ref = ref_denoiser.OracleModel(trained, ocfg, cache_speech=True)(xs, ts, wav=wav, inpaint_pose=poses.transpose(0, 1),
+                                                                       inpaint_mask=mask)
+    assert (got - ref).abs().max().item() <= 1e-4
