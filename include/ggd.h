@@ -210,10 +210,10 @@ enum {
                                         on block-scaled fp8 MFMA (e4m3 activations, one e8m0 scale per
                                         32 values), 1 the e4m3 weights widened into bf16 MFMAs (the
                                         launch route's arithmetic, bit-equal to it) */
-  GGD_ROUTE_MEGA_ROWS = 10           /* clip-group loop, bf16: 0 the row-block decomposition (ggd_rows.hip:
+  GGD_ROUTE_MEGA_ROWS = 10           /* clip-group loop, bf16: 0 (default) every phase split by head / FFN
+                                        chunk (ggd_mega.hip), 1 the row-block decomposition (ggd_rows.hip:
                                         the attention out-projections, LayerNorms and cross-attention on
-                                        each workgroup's own rows), 1 every phase split by head / FFN chunk
-                                        (ggd_mega.hip) */
+                                        each workgroup's own rows; measured ~1 % slower at C2) */
 };
 int ggd_set_route(ggd_ctx* ctx, int32_t knob, int32_t value);
 enum {

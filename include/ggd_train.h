@@ -92,8 +92,23 @@ int ggd_tr_scale_clamp(int64_t n, float* x, float s, float clip_value, void* str
 /* ---- speech-encoder training (HA2G SE-ResNet34, ha2g/model/ResNetSE34V2.py:118-188,
  * ResNetBlocks.py:7-96) on NHWC activations: rows = pixels (n, h, w), channels innermost ---- */
 
-/* nn.Conv2d as im2col + ggd_tr_gemm: col[(n, oh, ow)][(ky, kx, c)] (zeros outside the image);
- * col2im is its adjoint (a gather: each input pixel sums the entries copied from it). */
+/* nn.Conv2d (ha2g/model/ResNetBlocks.py:21-37, ResNetSE34V2.py:127-188) as implicit GEMMs on NHWC
+ * images (no im2col copy; the conv operand is gathered while the GEMM stages it):
+ *   fwd:   y[(n, oh, ow)][co] = sum_(ky, kx, c) x[n][oh s - pad + ky][ow s - pad + kx][c] wp[co][(ky, kx, c)] + bias
+ *   dgrad: dx[(n, ih, iw)][c] = sum_(ky, kx, co) dy[n][(ih + pad - ky) / s][(iw + pad - kx) / s][co] wt[(ky, kx, co)][c]
+ *          (exact divisions in range only)
+ *   wgrad: dwp[co][(ky, kx, c)] = sum_(n, oh, ow) dy[(n, oh, ow)][co] x[...] + beta dwp
+ * wp = the filter as [Co][KH][KW][C], wt = as [KH][KW][Co][C].  C (fwd, wgrad) / Co (dgrad) must be
+ * a multiple of 4 (-2 otherwise: conv1's single input channel runs im2col + ggd_tr_gemm). */
+int ggd_tr_conv_fwd(int N, int H, int W, int C, int Co, int KH, int KW, int stride, int pad, const float* x,
+                    const float* wp, const float* bias, float* y, void* stream);
+int ggd_tr_conv_dgrad(int N, int H, int W, int C, int Co, int KH, int KW, int stride, int pad, const float* dy,
+                      const float* wt, float* dx, void* stream);
+int ggd_tr_conv_wgrad(int N, int H, int W, int C, int Co, int KH, int KW, int stride, int pad, const float* dy,
+                      const float* x, float beta, float* dwp, void* stream);
+/* nn.Conv2d as im2col + ggd_tr_gemm (shapes the implicit GEMMs do not take): col[(n, oh, ow)][(ky, kx, c)]
+ * (zeros outside the image); col2im is its adjoint (a gather: each input pixel sums the entries copied
+ * from it). */
 int ggd_tr_im2col(int N, int H, int W, int C, int KH, int KW, int stride, int pad, const float* x, float* col,
                   void* stream);
 int ggd_tr_col2im(int N, int H, int W, int C, int KH, int KW, int stride, int pad, const float* dcol, float* dx,

@@ -172,8 +172,8 @@ struct ggd_ctx {
   // persistent reverse loop (ggd_mega.hip)
   bool no_mega = false;                // ggd_diag what = 9: route sampling through per-phase launches
   int mega_place = 0;                  // ggd_diag what = 12: 0 XCD-local, 1 part per XCD, 2 group per XCD
-  bool mega_rows_off = false;          // GGD_ROUTE_MEGA_ROWS: 1 = the head / chunk loop (ggd_mega.hip) even
-                                       // where the row-block loop (ggd_rows.hip) runs the shape
+  bool mega_rows = false;              // GGD_ROUTE_MEGA_ROWS: 1 = the row-block loop (ggd_rows.hip) where it
+                                       // runs the shape, instead of the head / chunk loop (ggd_mega.hip)
   bool mega_rows_last = false;         // the last clip-group loop issued was the row-block loop
   FusedArgs* mega_fa = nullptr;        // device [n_layers][4]
   unsigned long long* mega_phase_stamps = nullptr;  // ggd_diag what = 11: layer 1's phases + KE
@@ -1774,8 +1774,8 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
     case GGD_ROUTE_SIMULATE_UNRESIDENT:  // test hook: co-resident loops report status 2, run nothing
       c->sim_unresident = value != 0;
       return GGD_OK;
-    case GGD_ROUTE_MEGA_ROWS:       // 1: the clip-group loop split by head / chunk in every phase
-      c->mega_rows_off = value != 0;
+    case GGD_ROUTE_MEGA_ROWS:       // 1: the row-block clip-group loop (bf16)
+      c->mega_rows = value != 0;
       return GGD_OK;
     default:
       break;
@@ -2388,8 +2388,8 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
     int r = prof_mark(c, s);
     if (r) return r;
   }
-  // bf16 shapes run the row-block decomposition (ggd_rows.hip) unless GGD_ROUTE_MEGA_ROWS = 1
-  const bool rows = !c->mega_rows_off && c->kvc && rows_supported(D.dtype, D.seq_len, D.speech_len);
+  // GGD_ROUTE_MEGA_ROWS = 1: bf16 shapes on the row-block decomposition (ggd_rows.hip)
+  const bool rows = c->mega_rows && c->kvc && rows_supported(D.dtype, D.seq_len, D.speech_len);
   c->mega_rows_last = rows;
   auto launch = [&](const MegaArgs& m, int n, bool x) {
     return rows ? launch_rows(D.dtype, D.seq_len, D.speech_len, m, n, x, s) : launch_mega(D.dtype, D.seq_len, m, n, x, s);

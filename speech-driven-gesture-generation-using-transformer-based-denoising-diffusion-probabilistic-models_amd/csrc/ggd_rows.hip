@@ -215,24 +215,7 @@ __device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int it, unsig
   bo[0] = ld_f4(w.o_sa_b + (2 * wave) * 16 + 4 * g4);
   bo[1] = ld_f4(w.o_sa_b + (2 * wave + 1) * 16 + 4 * g4);
   __builtin_amdgcn_sched_barrier(0);  // the staging loads first: loads retire in issue order
-  // memory K / V^T fragments of head w (kvc block: K [64][32] | V^T [32][64], keys 0 / 1 zero): the
-  // lane's query dims are {4 g4 .. + 3} u {16 + 4 g4 .. + 3} (the transposed query GEMM's lane map),
-  // so its K fragment holds those dims of key 16 t + c16 -- the contraction runs in that order
-  const T* kvh = (const T*)w.kvc + ((size_t)b * (FD / FDK) + wave) * KVC_ELEMS;
-  uint2 kf[LKT][2], vf[2][LKT];
-#pragma unroll
-  for (int t = 0; t < LKT; ++t) {
-    kf[t][0] = ld_g8(kvh + (t * 16 + c16) * FDK + 4 * g4);
-    kf[t][1] = ld_g8(kvh + (t * 16 + c16) * FDK + 16 + 4 * g4);
-  }
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-    for (int t = 0; t < LKT; ++t) vf[ct][t] = ld_g8(kvh + FLK * FDK + (ct * 16 + c16) * FLK + t * 16 + 4 * g4);
-  const ConvW ckv = conv_w(lane < 32 ? w.ca_kw : w.ca_vw, lane < 32 ? w.ca_kb : w.ca_vb, lane & 31);
-  const ConvW cqv = conv_w(w.ca_qw, w.ca_qb, tid & 31);  // (stored by threads 0-31)
   so.store(Oi);
-  if (tid < FDK) cqs[tid] = make_float4(cqv.w0, cqv.w1, cqv.w2, cqv.b);
   if (tid < 128) *(uint4*)(Hr + (hs ? R + 1 : 0) * SH + hc) = hv;
   bar_lds();
   STAMP(1);
@@ -253,9 +236,26 @@ __device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int it, unsig
   const int t_orig = a.t_clip ? G(a.t_clip)[b] : G(a.steps)[it].t_orig;
   KvFix fx;
   fx.load(w.kv_step + (size_t)t_orig * 2 * FD, w.kv_mem + (size_t)b * Ts * 2 * FD, Ts, wave, lane);
+  // memory K / V^T fragments of head w (kvc block: K [64][32] | V^T [32][64], keys 0 / 1 zero): the
+  // lane's query dims are {4 g4 .. + 3} u {16 + 4 g4 .. + 3} (the transposed query GEMM's lane map),
+  // so its K fragment holds those dims of key 16 t + c16 -- the contraction runs in that order
+  const T* kvh = (const T*)w.kvc + ((size_t)b * (FD / FDK) + wave) * KVC_ELEMS;
+  uint2 kf[LKT][2], vf[2][LKT];
+#pragma unroll
+  for (int t = 0; t < LKT; ++t) {
+    kf[t][0] = ld_g8(kvh + (t * 16 + c16) * FDK + 4 * g4);
+    kf[t][1] = ld_g8(kvh + (t * 16 + c16) * FDK + 16 + 4 * g4);
+  }
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int t = 0; t < LKT; ++t) vf[ct][t] = ld_g8(kvh + FLK * FDK + (ct * 16 + c16) * FLK + t * 16 + 4 * g4);
+  const ConvW ckv = conv_w(lane < 32 ? w.ca_kw : w.ca_vw, lane < 32 ? w.ca_kb : w.ca_vb, lane & 31);
+  const ConvW cqv = conv_w(w.ca_qw, w.ca_qb, tid & 31);  // (stored by threads 0-31)
   float4 bq[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bq[j] = ld_f4(w.q_ca_b + wave * FDK + j * 16 + 4 * g4);
+  if (tid < FDK) cqs[tid] = make_float4(cqv.w0, cqv.w1, cqv.w2, cqv.b);
   bar_lds();
   STAMP(2);
   // ---- LN2 of rows 0 .. R + 1; the step-token rows of head w's memory K / V (wave-local LDS)

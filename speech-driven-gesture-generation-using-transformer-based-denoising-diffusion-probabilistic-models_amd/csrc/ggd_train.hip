@@ -7,9 +7,11 @@
 // hand-written forward and backward kernel; the host (…_amd/training.py) chains them through
 // torch.autograd.Function and owns the buffers.  Layout: token-major rows [clip][frame][feature].
 //
-//   tgemm_kernel<TA, TB>  C = alpha op(A) op(B) + beta C (+ bias): Linear forward (NT), dX (NN),
+//   tgemm_kernel<TA, TB, GM>  C = alpha op(A) op(B) + beta C (+ bias): Linear forward (NT), dX (NN),
 //                         dW (TN) on v_mfma_f32_16x16x4_f32 (exact f32 products), 64 x 64 tiles
-//                         (split-K with a fixed-order slice reduction when few tiles cover a long K)
+//                         (split-K with a fixed-order slice reduction when few tiles cover a long K);
+//                         GM != 0: the encoder's convolutions as implicit GEMMs (forward, dgrad,
+//                         wgrad), the conv operand gathered from the NHWC image while it is staged
 //   colsum_partial / _final  bias and LayerNorm affine gradients: two-stage column sums
 //   ln_fwd / ln_bwd       LayerNorm (eps 1e-5) with saved mean / rstd
 //   seqconv_fwd / _bwd / _param_grad  SpatialDepthWiseConv (3 taps along frames, per d_k channel,
@@ -40,12 +42,26 @@ constexpr int TT = 256;  // threads per block of the element / row kernels
 // ------------------------------------------------------------------------------------------
 constexpr int GT = 64, GK = 16, GS = GK + 1;
 
+// Implicit-GEMM convolutions (NHWC activations, nn.Conv2d, ha2g/model/ResNetBlocks.py:21-37): the
+// conv operand is gathered from the image while it is staged, instead of through an im2col copy.
+//   G_CONV_A   forward:  A[m = (n, oh, ow)][k = (ky, kx, c)] = x[n][oh s - pad + ky][ow s - pad + kx][c]
+//   G_DCONV_A  dgrad:    A[m = (n, ih, iw)][k = (ky, kx, co)] = dy[n][(ih + pad - ky) / s][(iw + pad - kx) / s][co]
+//                        where the division is exact and in range (the adjoint of the forward gather)
+//   G_CONV_B   wgrad:    B[k = (n, oh, ow)][j = (ky, kx, c)] = the forward gather, K = output pixels
+// (0 outside the image).  The gathered axis (c / co) must be a multiple of 4: a thread stages 4
+// consecutive k (A) or j (B) of one tap -- one 16-byte load.
+struct ConvGeo { int H, W, C, KH, KW, st, pad, Ho, Wo, Co; };
+constexpr int G_PLAIN = 0, G_CONV_A = 1, G_DCONV_A = 2, G_CONV_B = 3;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p; }
+
 // Split-K (part != null): slice blockIdx.z covers k in [z kchunk, (z + 1) kchunk) and stores its
 // raw f32 accumulators to part[z][M][N]; splitk_reduce_kernel adds the slices in a fixed order.
-template <bool TA, bool TB>
+template <bool TA, bool TB, int GM = G_PLAIN>
 __global__ void __launch_bounds__(256) tgemm_kernel(int M, int N, int K, float alpha, const float* __restrict__ A, int lda,
                                                     const float* __restrict__ B, int ldb, float beta, float* C, int ldc,
-                                                    const float* __restrict__ bias, int kchunk, float* part) {
+                                                    const float* __restrict__ bias, int kchunk, float* part,
+                                                    ConvGeo cg = ConvGeo{}) {
   __shared__ float As[GT * GS], Bs[GT * GS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
@@ -55,18 +71,73 @@ __global__ void __launch_bounds__(256) tgemm_kernel(int M, int N, int K, float a
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the thread's fixed gather coordinates: the pixel of its A row (G_CONV_A / G_DCONV_A) or the tap
+  // and channel of its 4 B columns (G_CONV_B)
+  int gp_n = 0, gp_y = 0, gp_x = 0, gt_ky = 0, gt_kx = 0, gt_c = 0;
+  if constexpr (GM == G_CONV_A || GM == G_DCONV_A) {
+    const int gm = m0 + (tid >> 2);
+    const int ww = GM == G_CONV_A ? cg.Wo : cg.W, hh = GM == G_CONV_A ? cg.Ho : cg.H;
+    gp_x = gm % ww;
+    gp_y = (gm / ww) % hh;
+    gp_n = gm / (ww * hh);
+  } else if constexpr (GM == G_CONV_B) {
+    const int gn = n0 + (tid & 15) * 4, t = gn / cg.C;
+    gt_c = gn - t * cg.C;
+    gt_ky = t / cg.KW;
+    gt_kx = t - gt_ky * cg.KW;
+  }
   for (int k0 = kbeg; k0 < kend; k0 += GK) {
     // stage: 1024 elements of each operand, 4 per thread along the operand's contiguous axis
+    if constexpr (GM == G_CONV_A || GM == G_DCONV_A) {
+      const int r = tid >> 2, kq = (tid & 3) * 4, gm = m0 + r, gk = k0 + kq;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gm < M && gk < kend) {
+        const int cc = GM == G_CONV_A ? cg.C : cg.Co, t = gk / cc, c = gk - t * cc, ky = t / cg.KW, kx = t - ky * cg.KW;
+        if constexpr (GM == G_CONV_A) {
+          const int ih = gp_y * cg.st - cg.pad + ky, iw = gp_x * cg.st - cg.pad + kx;
+          if (ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W) v = ld4(A + (((size_t)gp_n * cg.H + ih) * cg.W + iw) * cg.C + c);
+        } else {
+          const int ty = gp_y + cg.pad - ky, tx = gp_x + cg.pad - kx;
+          if (ty >= 0 && tx >= 0 && ty % cg.st == 0 && tx % cg.st == 0) {
+            const int oh = ty / cg.st, ow = tx / cg.st;
+            if (oh < cg.Ho && ow < cg.Wo) v = ld4(A + (((size_t)gp_n * cg.Ho + oh) * cg.Wo + ow) * cg.Co + c);
+          }
+        }
+      }
+      As[r * GS + kq + 0] = v.x;
+      As[r * GS + kq + 1] = v.y;
+      As[r * GS + kq + 2] = v.z;
+      As[r * GS + kq + 3] = v.w;
+    } else {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      int r, k;
-      if (!TA) { r = tid >> 2; k = (tid & 3) * 4 + u; } else { k = tid >> 4; r = (tid & 15) * 4 + u; }
-      const int gm = m0 + r, gk = k0 + k;
-      As[r * GS + k] = (gm < M && gk < kend) ? (TA ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk]) : 0.f;
-      int c, kb;
-      if (TB) { c = tid >> 2; kb = (tid & 3) * 4 + u; } else { kb = tid >> 4; c = (tid & 15) * 4 + u; }
-      const int gn = n0 + c, gkb = k0 + kb;
-      Bs[c * GS + kb] = (gn < N && gkb < kend) ? (TB ? B[(size_t)gn * ldb + gkb] : B[(size_t)gkb * ldb + gn]) : 0.f;
+      for (int u = 0; u < 4; ++u) {
+        int r, k;
+        if (!TA) { r = tid >> 2; k = (tid & 3) * 4 + u; } else { k = tid >> 4; r = (tid & 15) * 4 + u; }
+        const int gm = m0 + r, gk = k0 + k;
+        As[r * GS + k] = (gm < M && gk < kend) ? (TA ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk]) : 0.f;
+      }
+    }
+    if constexpr (GM == G_CONV_B) {
+      static_assert(!TB, "the wgrad gather stages B as [k][j]");
+      const int kb = tid >> 4, cq = (tid & 15) * 4, gn = n0 + cq, gkb = k0 + kb;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gn < N && gkb < kend) {
+        const int ow = gkb % cg.Wo, oh = (gkb / cg.Wo) % cg.Ho, n = gkb / (cg.Wo * cg.Ho);
+        const int ih = oh * cg.st - cg.pad + gt_ky, iw = ow * cg.st - cg.pad + gt_kx;
+        if (ih >= 0 && ih < cg.H && iw >= 0 && iw < cg.W) v = ld4(B + (((size_t)n * cg.H + ih) * cg.W + iw) * cg.C + gt_c);
+      }
+      Bs[(cq + 0) * GS + kb] = v.x;
+      Bs[(cq + 1) * GS + kb] = v.y;
+      Bs[(cq + 2) * GS + kb] = v.z;
+      Bs[(cq + 3) * GS + kb] = v.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        int c, kb;
+        if (TB) { c = tid >> 2; kb = (tid & 3) * 4 + u; } else { kb = tid >> 4; c = (tid & 15) * 4 + u; }
+        const int gn = n0 + c, gkb = k0 + kb;
+        Bs[c * GS + kb] = (gn < N && gkb < kend) ? (TB ? B[(size_t)gn * ldb + gkb] : B[(size_t)gkb * ldb + gn]) : 0.f;
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -733,6 +804,9 @@ inline int rc(hipError_t e) { return e == hipSuccess ? 0 : -3; }  // GGD_ERR_HIP
 
 bool att_lds_ready = false;
 
+int tgemm_launch(int ta, int tb, int gm, int M, int N, int K, float alpha, const float* A, int lda, const float* B,
+                 int ldb, float beta, float* C, int ldc, const float* bias, ConvGeo cg, hipStream_t s);
+
 }  // namespace
 
 extern "C" {
@@ -741,7 +815,14 @@ int ggd_tr_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A
                 float beta, float* C, int ldc, const float* bias, void* stream) {
   if (M < 0 || N < 0 || K < 0 || !A || !B || !C) return -1;
   if (M == 0 || N == 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
+  return tgemm_launch(ta, tb, G_PLAIN, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, ConvGeo{}, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+namespace {
+int tgemm_launch(int ta, int tb, int gm, int M, int N, int K, float alpha, const float* A, int lda, const float* B,
+                 int ldb, float beta, float* C, int ldc, const float* bias, ConvGeo cg, hipStream_t s) {
   // few output tiles over a long K (the weight gradients dW = dY^T X, K = clips x frames): split
   // K so that the launch covers the chip, then add the slices in a fixed order
   const int tiles = ((N + GT - 1) / GT) * ((M + GT - 1) / GT);
@@ -755,18 +836,64 @@ int ggd_tr_gemm(int ta, int tb, int M, int N, int K, float alpha, const float* A
     if (!part) return -3;
   }
   const dim3 grid((N + GT - 1) / GT, (M + GT - 1) / GT, S), blk(256);
-#define GGD_TGEMM(a_, b_)                                                                                  \
-  hipLaunchKernelGGL((tgemm_kernel<a_, b_>), grid, blk, 0, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, kchunk, \
-                     part)
-  if (!ta && tb) GGD_TGEMM(false, true);
-  else if (!ta && !tb) GGD_TGEMM(false, false);
-  else if (ta && !tb) GGD_TGEMM(true, false);
-  else GGD_TGEMM(true, true);
+#define GGD_TGEMM(a_, b_, g_)                                                                              \
+  hipLaunchKernelGGL((tgemm_kernel<a_, b_, g_>), grid, blk, 0, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, \
+                     kchunk, part, cg)
+  if (gm == G_CONV_A) GGD_TGEMM(false, true, G_CONV_A);          // x (gathered) . W^T
+  else if (gm == G_DCONV_A) GGD_TGEMM(false, false, G_DCONV_A);  // dy (gathered) . W'
+  else if (gm == G_CONV_B) GGD_TGEMM(true, false, G_CONV_B);     // dy^T . x (gathered)
+  else if (!ta && tb) GGD_TGEMM(false, true, G_PLAIN);
+  else if (!ta && !tb) GGD_TGEMM(false, false, G_PLAIN);
+  else if (ta && !tb) GGD_TGEMM(true, false, G_PLAIN);
+  else GGD_TGEMM(true, true, G_PLAIN);
 #undef GGD_TGEMM
   if (S > 1)
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks_for((int64_t)M * N)), dim3(TT), 0, s, M, N, S, part, alpha, beta,
                        C, ldc, bias);
   return rc(hipGetLastError());
+}
+
+// output size of a conv, or -2 (unsupported shape)
+int conv_geo(int N, int H, int W, int C, int Co, int KH, int KW, int stride, int pad, ConvGeo& g) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Co <= 0 || KH <= 0 || KW <= 0 || stride <= 0 || pad < 0) return -1;
+  g = ConvGeo{H, W, C, KH, KW, stride, pad, (H + 2 * pad - KH) / stride + 1, (W + 2 * pad - KW) / stride + 1, Co};
+  return g.Ho > 0 && g.Wo > 0 ? 0 : -2;
+}
+}  // namespace
+
+extern "C" {
+
+int ggd_tr_conv_fwd(int N, int H, int W, int C, int Co, int KH, int KW, int stride, int pad, const float* x,
+                    const float* wp, const float* bias, float* y, void* stream) {
+  ConvGeo g;
+  const int e = conv_geo(N, H, W, C, Co, KH, KW, stride, pad, g);
+  if (e) return e;
+  if (!x || !wp || !y) return -1;
+  if (C % 4) return -2;
+  const int P = N * g.Ho * g.Wo, K = KH * KW * C;
+  return tgemm_launch(0, 1, G_CONV_A, P, Co, K, 1.f, x, 0, wp, K, 0.f, y, Co, bias, g, (hipStream_t)stream);
+}
+
+int ggd_tr_conv_dgrad(int N, int H, int W, int C, int Co, int KH, int KW, int stride, int pad, const float* dy,
+                      const float* wt, float* dx, void* stream) {
+  ConvGeo g;
+  const int e = conv_geo(N, H, W, C, Co, KH, KW, stride, pad, g);
+  if (e) return e;
+  if (!dy || !wt || !dx) return -1;
+  if (Co % 4) return -2;
+  return tgemm_launch(0, 0, G_DCONV_A, N * H * W, C, KH * KW * Co, 1.f, dy, 0, wt, C, 0.f, dx, C, nullptr, g,
+                      (hipStream_t)stream);
+}
+
+int ggd_tr_conv_wgrad(int N, int H, int W, int C, int Co, int KH, int KW, int stride, int pad, const float* dy,
+                      const float* x, float beta, float* dwp, void* stream) {
+  ConvGeo g;
+  const int e = conv_geo(N, H, W, C, Co, KH, KW, stride, pad, g);
+  if (e) return e;
+  if (!dy || !x || !dwp) return -1;
+  if (C % 4) return -2;
+  const int P = N * g.Ho * g.Wo, K = KH * KW * C;
+  return tgemm_launch(1, 0, G_CONV_B, Co, K, P, 1.f, dy, Co, x, 0, beta, dwp, K, nullptr, g, (hipStream_t)stream);
 }
 
 int ggd_tr_colsum(int M, int N, const float* X, int ldx, float* out, float beta, void* stream) {

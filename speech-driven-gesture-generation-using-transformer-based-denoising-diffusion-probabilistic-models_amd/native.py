@@ -44,7 +44,7 @@ EXPORTS = [
     "ggd_tr_gemm", "ggd_tr_colsum", "ggd_tr_layernorm_fwd", "ggd_tr_layernorm_bwd", "ggd_tr_seqconv_fwd",
     "ggd_tr_seqconv_bwd", "ggd_tr_attention_fwd", "ggd_tr_attention_bwd", "ggd_tr_elementwise", "ggd_tr_q_sample",
     "ggd_tr_mse", "ggd_tr_sumsq", "ggd_tr_sumsq_blocks", "ggd_tr_adamw", "ggd_tr_scale", "ggd_tr_scale_clamp",
-    "ggd_tr_im2col", "ggd_tr_col2im", "ggd_tr_batchnorm_fwd", "ggd_tr_batchnorm_bwd", "ggd_tr_image_channel_sum",
+    "ggd_tr_conv_fwd", "ggd_tr_conv_dgrad", "ggd_tr_conv_wgrad", "ggd_tr_im2col", "ggd_tr_col2im", "ggd_tr_batchnorm_fwd", "ggd_tr_batchnorm_bwd", "ggd_tr_image_channel_sum",
     "ggd_tr_channel_scale", "ggd_tr_pixel_shuffle", "ggd_tr_head_flatten", "ggd_enc_frontend",
 ]
 
@@ -185,6 +185,9 @@ def load():
         "ggd_tr_adamw": (ctypes.c_int, [I64, VP, VP, VP, VP, F, F, F, F, F, I64, F, VP]),
         "ggd_tr_scale": (ctypes.c_int, [I64, VP, F, VP]),
         "ggd_tr_scale_clamp": (ctypes.c_int, [I64, VP, F, F, VP]),
+        "ggd_tr_conv_fwd": (ctypes.c_int, [I32] * 9 + [VP, VP, VP, VP, VP]),
+        "ggd_tr_conv_dgrad": (ctypes.c_int, [I32] * 9 + [VP, VP, VP, VP]),
+        "ggd_tr_conv_wgrad": (ctypes.c_int, [I32] * 9 + [VP, VP, F, VP, VP]),
         "ggd_tr_im2col": (ctypes.c_int, [I32, I32, I32, I32, I32, I32, I32, I32, VP, VP, VP]),
         "ggd_tr_col2im": (ctypes.c_int, [I32, I32, I32, I32, I32, I32, I32, I32, VP, VP, VP]),
         "ggd_tr_batchnorm_fwd": (ctypes.c_int, [I32, I32, VP, VP, VP, F, VP, VP, VP, VP, VP]),

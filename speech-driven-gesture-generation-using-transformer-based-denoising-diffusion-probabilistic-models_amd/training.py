@@ -294,8 +294,10 @@ class _Sigmoid(th.autograd.Function):
 # speech-encoder ops on NHWC activations (N, H, W, C): H = mel axis, W = frames
 # ------------------------------------------------------------------------------------------
 class _Conv2d(th.autograd.Function):
-    """nn.Conv2d = im2col + GEMM against the [Cout][(ky, kx, c)] filter matrix; backward: dW = dY^T col,
-    db = colsum dY, dcol = dY W, dX = col2im(dcol).  col is recomputed in backward (memory)."""
+    """nn.Conv2d on NHWC images.  Input channels a multiple of 4 (every tower / head conv): implicit GEMMs
+    (ggd_tr_conv_fwd / _dgrad / _wgrad) gather the conv operand from the image while staging it -- no
+    im2col copy; db = colsum dY.  conv1 (one input channel): im2col + GEMM, dW = dY^T col, dcol = dY W,
+    dX = col2im(dcol), col recomputed in backward (memory)."""
 
     @staticmethod
     def forward(ctx, x, w, b, stride, pad):
@@ -306,37 +308,51 @@ class _Conv2d(th.autograd.Function):
         Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
         K, P = KH * KW * C, N * Ho * Wo
         wp = w.permute(0, 2, 3, 1).contiguous().reshape(Co, K)
-        col = x.new_empty(P, K)
         lib = _lib()
-        _ok(lib.ggd_tr_im2col(N, H, W, C, KH, KW, stride, pad, _p(x), _p(col), _s(x)), "im2col")
         y = x.new_empty(P, Co)
-        gemm(0, 1, P, Co, K, col, K, wp, K, y, Co, bias=b)
-        ctx.save_for_backward(x, wp)
-        ctx.geo = (N, H, W, C, Co, KH, KW, stride, pad, Ho, Wo, b is not None)
+        implicit = C % 4 == 0 and Co % 4 == 0
+        if implicit:
+            _ok(lib.ggd_tr_conv_fwd(N, H, W, C, Co, KH, KW, stride, pad, _p(x), _p(wp), _p(b), _p(y), _s(x)),
+                "conv fwd")
+        else:
+            col = x.new_empty(P, K)
+            _ok(lib.ggd_tr_im2col(N, H, W, C, KH, KW, stride, pad, _p(x), _p(col), _s(x)), "im2col")
+            gemm(0, 1, P, Co, K, col, K, wp, K, y, Co, bias=b)
+        ctx.save_for_backward(x, w if implicit else wp)
+        ctx.geo = (N, H, W, C, Co, KH, KW, stride, pad, Ho, Wo, b is not None, implicit)
         return y.view(N, Ho, Wo, Co)
 
     @staticmethod
     def backward(ctx, dy):
-        x, wp = ctx.saved_tensors
-        N, H, W, C, Co, KH, KW, stride, pad, Ho, Wo, has_b = ctx.geo
+        x, wq = ctx.saved_tensors
+        N, H, W, C, Co, KH, KW, stride, pad, Ho, Wo, has_b, implicit = ctx.geo
         K, P = KH * KW * C, N * Ho * Wo
         dy = dy.contiguous().view(P, Co)
         lib = _lib()
-        col = x.new_empty(P, K)
-        _ok(lib.ggd_tr_im2col(N, H, W, C, KH, KW, stride, pad, _p(x), _p(col), _s(x)), "im2col")
-        dwp = wp.new_empty(Co, K)
-        gemm(1, 0, Co, K, P, dy, Co, col, K, dwp, K)
+        dwp = x.new_empty(Co, K)
+        dx = None
+        if implicit:
+            _ok(lib.ggd_tr_conv_wgrad(N, H, W, C, Co, KH, KW, stride, pad, _p(dy), _p(x), 0.0, _p(dwp), _s(dy)),
+                "conv wgrad")
+            if ctx.needs_input_grad[0]:
+                wt = wq.permute(2, 3, 0, 1).contiguous()            # [KH][KW][Co][C]
+                dx = th.empty_like(x)
+                _ok(lib.ggd_tr_conv_dgrad(N, H, W, C, Co, KH, KW, stride, pad, _p(dy), _p(wt), _p(dx), _s(dy)),
+                    "conv dgrad")
+        else:
+            col = x.new_empty(P, K)
+            _ok(lib.ggd_tr_im2col(N, H, W, C, KH, KW, stride, pad, _p(x), _p(col), _s(x)), "im2col")
+            gemm(1, 0, Co, K, P, dy, Co, col, K, dwp, K)
+            if ctx.needs_input_grad[0]:
+                dcol = col  # reuse the buffer
+                gemm(0, 0, P, K, Co, dy, Co, wq, K, dcol, K)
+                dx = th.empty_like(x)
+                _ok(lib.ggd_tr_col2im(N, H, W, C, KH, KW, stride, pad, _p(dcol), _p(dx), _s(x)), "col2im")
         dw = dwp.view(Co, KH, KW, C).permute(0, 3, 1, 2).contiguous()
         db = None
         if has_b:
-            db = wp.new_empty(Co)
+            db = x.new_empty(Co)
             _ok(lib.ggd_tr_colsum(P, Co, _p(dy), Co, _p(db), 0.0, _s(dy)), "colsum")
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dcol = col  # reuse the buffer
-            gemm(0, 0, P, K, Co, dy, Co, wp, K, dcol, K)
-            dx = th.empty_like(x)
-            _ok(lib.ggd_tr_col2im(N, H, W, C, KH, KW, stride, pad, _p(dcol), _p(dx), _s(x)), "col2im")
         return dx, dw, db, None, None
 
 

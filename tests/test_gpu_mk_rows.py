@@ -48,7 +48,7 @@ def test_frame_block_update_matches_oracle(pkg, beat_cfg, weights, dtype, L, n, 
     ctx, _ = model.prepare(wav.cuda(), L)
     try:
         assert ctx.lib.ggd_set_route(ctx.h, ROUTE_PER_CLIP, 1) == 0   # never the per-clip loops
-        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_MEGA_ROWS, 0 if rows else 1) == 0
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_MEGA_ROWS, rows) == 0
         out = diffusion.p_sample_loop(model, (n, D_POSE, L), {"wav": wav.cuda()}, seed=seed, clip_offset=off,
                                       n_steps=steps, sync=True)["sample"].cpu()
         v = ctypes.c_double()

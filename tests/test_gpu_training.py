@@ -311,8 +311,12 @@ def test_checkpoint_roundtrip_resumes_identically(pkg, beat_cfg, tr, train_setup
 # ------------------------------------------------------------------------------------------
 # speech-encoder training (train-mode SE-ResNet34 on NHWC activations)
 # ------------------------------------------------------------------------------------------
+# (1, 32): im2col route (conv1); the others: the implicit GEMMs, incl. a 64-column tile spanning taps
+# (16 input channels) and stride-2 dgrad parity cases
 @pytest.mark.parametrize("cin,cout,k,stride,pad,bias", [(1, 32, 3, 1, 1, True), (32, 64, 3, 2, 1, False),
-                                                         (32, 64, 1, 2, 0, False), (64, 64, 2, 1, 0, True)])
+                                                         (32, 64, 1, 2, 0, False), (64, 64, 2, 1, 0, True),
+                                                         (16, 32, 3, 1, 1, True), (64, 128, 3, 2, 1, False),
+                                                         (128, 16, 1, 1, 0, True)])
 def test_conv2d_nhwc_matches_torch(tr, cin, cout, k, stride, pad, bias):
     g = th.Generator().manual_seed(cin + cout + k)
     x = th.randn(3, 17, 13, cin, generator=g)                         # NHWC
