@@ -294,10 +294,27 @@ int ggd_enc_lengths(const ggd_enc* enc, int32_t* t_low, int32_t* t_mid, int32_t*
 int ggd_enc_run(ggd_enc* enc, const float* wav, int32_t n, float* z_low, float* z_mid, float* z_high,
                 void* stream);
 
+/* The same encoder run, its tokens written straight into the decoder's speech memory (the input of
+ * ggd_set_memory) instead of three tensors.  layout GGD_MEM_BLEND (s2g_v2): mem (N, Ts, 3 d) with
+ * Ts = max(T_low, T_mid, T_high), level l in columns [l d, l d + d), left-zero-padded to Ts -- the
+ * F.pad + th.cat of models/model.py:97-104.  GGD_MEM_CONCAT (default / inpaint): mem
+ * (N, T_low + T_mid + T_high, d), the levels concatenated on time (models/model.py:55-68). */
+enum { GGD_MEM_BLEND = 0, GGD_MEM_CONCAT = 1 };
+int ggd_enc_run_memory(ggd_enc* enc, const float* wav, int32_t n, int32_t layout, float* mem, void* stream);
+
 /* The encoder's front end only: wav (N, wav_len) -> the InstanceNorm'd mel image img (N, 128, F)
  * f32 (pre-emphasis, STFT power, mel, +1e-6, InstanceNorm1d: speech_encoder.py:18-34,53-58), the
  * parameter-free input of the SE-ResNet that the training path differentiates through. */
 int ggd_enc_frontend(ggd_enc* enc, const float* wav, int32_t n, float* img, void* stream);
+
+/* Verification entry (not part of the reference surface): ONE Linear on block-scaled fp8 MFMA exactly
+ * as the long-clip loop's fp8-MFMA stages run it (GGD_ROUTE_FP8_MFMA = 0) -- a (M, K) device f32 rows
+ * quantised to e4m3 with one e8m0 scale per 32 consecutive values (2^(E - 7) for the block max
+ * 1.f 2^E), w_e4m3 (N, K) device e4m3fn codes with per-output-channel scales wscale (N), then
+ * out (M, N) = (a_q . w^T) * wscale + bias.  K % 256 == 0, K <= 1024, N % 64 == 0; blocking.  The
+ * tests pin the stages' arithmetic against a numpy restatement of the same quantisation. */
+int ggd_mx_linear(int32_t M, int32_t N, int32_t K, const float* a, const uint8_t* w_e4m3, const float* wscale,
+                  const float* bias, float* out, void* stream);
 
 /* Library version string. */
 const char* ggd_version(void);

@@ -345,4 +345,87 @@ hipError_t launch_chain(int w8, const ChainArgs& a, hipStream_t s) {
   return w8 ? chain_stages<true>(a, s) : chain_stages<false>(a, s);
 }
 
+// ------------------------------------------------------------------------------------------
+// One block-scaled fp8 MFMA Linear, exactly as the long-clip loop's MX stages compute it
+// (ggd_long.hip: LayerNorm projections and FFN; ggd_chainlib.h ch_mma_mx): the f32 input rows
+// quantised to e4m3 with one e8m0 scale per 32 consecutive values (mx_scale_byte / mx_mul /
+// mx_pack4), the e4m3 weights in the MX B order (chain_pack_kernel<true, true>), 256-k chunks of two
+// v_mfma_scale_f32_16x16x128_f8f6f4 per (row tile, column tile), and the epilogue
+// out = acc * wscale[col] + bias[col] (ch_val).  A verification entry (ggd_mx_linear): it pins the
+// arithmetic of those stages value by value against a numpy restatement (tests/test_gpu_mx_linear.py).
+// One wave per 32 rows x 32 columns; K % 256 == 0, K <= 1024.
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr int MXL_KMAX = 1024, MXL_STR = MXL_KMAX + 16;
+__global__ void __launch_bounds__(64) mx_linear_kernel(int M, int N, int K, const float* __restrict__ a,
+                                                       const unsigned char* __restrict__ wpk, const float* __restrict__ wscale,
+                                                       const float* __restrict__ bias, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) unsigned char xs8[32 * MXL_STR];
+  __shared__ unsigned char sc8[32 * (MXL_KMAX / 32)];
+  const int lane = threadIdx.x, m0 = blockIdx.y * 32, t0 = blockIdx.x * 2, nb = K / 32;
+  // quantise: lane takes (row, 32-block) pairs; the block max, its scale byte, 8 packed quads
+  for (int pr = lane; pr < 32 * nb; pr += 64) {
+    const int r = pr / nb, blk = pr - r * nb;
+    const float* src = a + (size_t)min(m0 + r, M - 1) * K + blk * 32;
+    float v[32];
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      v[i] = src[i];
+      m = fmaxf(m, fabsf(v[i]));
+    }
+    const unsigned sb = mx_scale_byte(m);
+    const float mul = mx_mul(sb);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      *(unsigned*)(xs8 + r * MXL_STR + blk * 32 + 4 * q) =
+          mx_pack4(v[4 * q] * mul, v[4 * q + 1] * mul, v[4 * q + 2] * mul, v[4 * q + 3] * mul);
+    sc8[r * nb + blk] = (unsigned char)sb;
+  }
+  __syncthreads();
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int upt = K / 64;
+  for (int c = 0; c < K / 256; ++c) {
+    BBuf<true, 2> B;
+    ch_load<true, 2>(B, wpk, (unsigned)lane * 16, t0, c, upt, 2);
+    ch_mma_mx<2>(B, xs8, MXL_STR, sc8, nb, c, lane, acc, 2);
+  }
+  // C layout: row 16 i + 4 (lane >> 4) + r, column 16 (t0 + j) + (lane & 15)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = (t0 + j) * 16 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + 16 * i + 4 * (lane >> 4) + r;
+        if (row < M && col < N) out[(size_t)row * N + col] = acc[i][j][r] * wscale[col] + bias[col];
+      }
+  }
+}
+}  // namespace
+
 }  // namespace ggd
+
+extern "C" int ggd_mx_linear(int32_t M, int32_t N, int32_t K, const float* a, const uint8_t* w_e4m3, const float* wscale,
+                             const float* bias, float* out, void* stream) {
+  using namespace ggd;
+  if (M <= 0 || N <= 0 || K <= 0 || K % 256 || K > MXL_KMAX || N % 64 || !a || !w_e4m3 || !wscale || !bias || !out)
+    return -1;   // GGD_ERR_ARG
+  hipStream_t s = (hipStream_t)stream;
+  void* pk = nullptr;
+  if (hipMalloc(&pk, (size_t)N * K) != hipSuccess) return -3;
+  hipError_t e = launch_chain_pack(2, w_e4m3, pk, N, K, s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(mx_linear_kernel, dim3(N / 32, (M + 31) / 32), dim3(64), 0, s, M, N, K, a,
+                       (const unsigned char*)pk, wscale, bias, out);
+    e = hipGetLastError();
+  }
+  const hipError_t e2 = hipStreamSynchronize(s);
+  (void)hipFree(pk);
+  return e == hipSuccess && e2 == hipSuccess ? 0 : -3;
+}

@@ -466,7 +466,8 @@ __global__ void __launch_bounds__(64 * HFC_WAVES) enc_head_fc_kernel(const float
                                                                      const float* __restrict__ b1,
                                                                      const float* __restrict__ wp,
                                                                      const float* __restrict__ bp,
-                                                                     float* __restrict__ z, int d) {
+                                                                     float* __restrict__ z, int d, int zrows,
+                                                                     int zld, int zoff) {
   __shared__ float red[HFC_WAVES][16][33], h1[16][33];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, g = lane >> 4;
   const int row0 = blockIdx.x * 16;
@@ -536,9 +537,19 @@ __global__ void __launch_bounds__(64 * HFC_WAVES) enc_head_fc_kernel(const float
       float v = bo;
 #pragma unroll
       for (int j = 0; j < 32; ++j) v += wr[j] * h1[r][j];
-      z[(size_t)(row0 + r) * d + o] = v;
+      // row (clip c, token t) of the level -> z row c zrows + zoff + t, zld floats apart: the
+      // separate (N, T, d) tensor, or its place in the decoder's speech memory (see MemMap)
+      const int gr = row0 + r, c = gr / Wo;
+      z[((size_t)c * zrows + zoff + (gr - c * Wo)) * zld + o] = v;
     }
   }
+}
+
+// the left padding of a level in the s2g_v2 speech memory (model.py:97-104: F.pad on time before the
+// feature concat): rows [0, npad) of columns [0, d) of every clip's (zrows x zld) block
+__global__ void enc_zpad_kernel(float* __restrict__ z, int npad, int d, int zrows, int zld) {
+  const int c = blockIdx.x;
+  for (int e = threadIdx.x; e < npad * d; e += blockDim.x) z[((size_t)c * zrows + e / d) * zld + e % d] = 0.f;
 }
 
 inline unsigned blocks_for(size_t n, int tpb) { return (unsigned)((n + tpb - 1) / tpb); }
@@ -1426,12 +1437,64 @@ int ggd_enc_frontend(ggd_enc* e, const float* wav, int32_t n, float* img, void* 
   return GGD_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Where the heads write token t of clip c of level l: z[l] + ((c rows + off[l] + t) ld + col)
+// floats (col folded into z[l]); pad[l] rows in front of the level are zeroed (s2g_v2 memory)
+struct MemMap {
+  float* z[3];
+  int rows, ld, off[3], pad[3];
+};
+
+int enc_run(ggd_enc* e, const float* wav, int32_t n, const MemMap& mm, hipStream_t s);
+}  // namespace
+
+extern "C" {
+
 int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_mid, float* z_high, void* stream) {
   if (!e || !wav || !z_low || !z_mid || !z_high) return efail(e, GGD_ERR_ARG, "null argument");
   if (!e->finalized) return efail(e, GGD_ERR_STATE, "encoder weights not finalized");
+  MemMap mm{};  // three separate (N, T_l, d) tensors: rows = 0 -> each level's own T_l
+  float* z[3] = {z_low, z_mid, z_high};
+  for (int l = 0; l < 3; ++l) mm.z[l] = z[l];
+  mm.ld = e->d_model;
+  return enc_run(e, wav, n, mm, (hipStream_t)stream);
+}
+
+int ggd_enc_run_memory(ggd_enc* e, const float* wav, int32_t n, int32_t layout, float* mem, void* stream) {
+  if (!e || !wav || !mem) return efail(e, GGD_ERR_ARG, "null argument");
+  if (!e->finalized) return efail(e, GGD_ERR_STATE, "encoder weights not finalized");
+  const int d = e->d_model, t[3] = {e->t_low, e->t_mid, e->t_high};
+  MemMap mm{};
+  if (layout == GGD_MEM_BLEND) {  // (N, Tmax, 3d): level l in columns [l d, l d + d), left-zero-padded
+    const int tm = std::max(t[0], std::max(t[1], t[2]));
+    mm.rows = tm;
+    mm.ld = 3 * d;
+    for (int l = 0; l < 3; ++l) {
+      mm.z[l] = mem + (size_t)l * d;
+      mm.pad[l] = mm.off[l] = tm - t[l];
+    }
+  } else if (layout == GGD_MEM_CONCAT) {  // (N, T_low + T_mid + T_high, d): levels one after another
+    mm.rows = t[0] + t[1] + t[2];
+    mm.ld = d;
+    for (int l = 0, o = 0; l < 3; o += t[l], ++l) {
+      mm.z[l] = mem;
+      mm.off[l] = o;
+      mm.pad[l] = 0;
+    }
+  } else {
+    return efail(e, GGD_ERR_ARG, "unknown memory layout");
+  }
+  return enc_run(e, wav, n, mm, (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+namespace {
+int enc_run(ggd_enc* e, const float* wav, int32_t n, const MemMap& mm, hipStream_t s) {
   if (n <= 0 || n > e->max_batch) return efail(e, GGD_ERR_ARG, "batch outside [1, max_batch]");
   ENC_TRY(e, hipSetDevice(e->device));
-  hipStream_t s = (hipStream_t)stream;
   const int F = e->F, d = e->d_model;
   for (int c0 = 0; c0 < n; c0 += e->chunk) {
     const int m = std::min(e->chunk, n - c0);
@@ -1513,9 +1576,7 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
         H = Ho;
         W = Wo;
       }
-    // heads
-    float* zs[3] = {z_low + (size_t)c0 * e->t_low * d, z_mid + (size_t)c0 * e->t_mid * d,
-                    z_high + (size_t)c0 * e->t_high * d};
+    // heads: each level's tokens straight into their place (MemMap)
     const int tl[3] = {e->t_low, e->t_mid, e->t_high};
     for (int i = 0; i < 3; ++i) {
       const EHead& h = e->head[i];
@@ -1541,12 +1602,18 @@ int ggd_enc_run(ggd_enc* e, const float* wav, int32_t n, float* z_low, float* z_
       if (Wo != tl[i]) return efail(e, GGD_ERR_STATE, "head length mismatch");
       const int Ho = conv_out(Hh, h.conv.kh, 1, 0), C = h.conv.cout;
       if (h.K % 16 || h.K != C * Ho || (C & (C - 1)) || C % 4) return efail(e, GGD_ERR_STATE, "head feature shape");
+      const int zrows = mm.rows ? mm.rows : tl[i];
+      float* zc = mm.z[i] + (size_t)c0 * zrows * mm.ld;
       hipLaunchKernelGGL(enc_head_fc_kernel, dim3((m * Wo + 15) / 16), dim3(64 * HFC_WAVES), 0, s, e->hbuf, m * Wo, h.K, Ho, Wo,
-                         h.conv.cout_pad, __builtin_ctz(C), h.fc_w, h.fc_b, e->proj_w, e->proj_b, zs[i], d);
+                         h.conv.cout_pad, __builtin_ctz(C), h.fc_w, h.fc_b, e->proj_w, e->proj_b, zc, d, zrows, mm.ld,
+                         mm.off[i]);
       ENC_TRY(e, hipGetLastError());
+      if (mm.pad[i] > 0) {
+        hipLaunchKernelGGL(enc_zpad_kernel, dim3(m), dim3(256), 0, s, zc, mm.pad[i], d, zrows, mm.ld);
+        ENC_TRY(e, hipGetLastError());
+      }
     }
   }
   return GGD_OK;
 }
-
-}  // extern "C"
+}  // namespace

@@ -36,7 +36,7 @@
 // bit-identical, both on: scripts/ab.sh on one box, profiles/r04m_c2_ab.txt, C2 mk_kernel 75.07 ->
 // 74.21 ms (FUSE_KD) and 74.85 ms (CMAP))
 //   GGD_MK_FUSE_KD  the last layer's FFN-down reduction runs inside KE, for each block's rows (one
-//                   clip-group barrier and the KD phase fewer per step: 15 instead of 16)
+//                   clip-group barrier and the KD phase fewer per step: 16 instead of 17)
 //   GGD_MK_CMAP     KE update threads take channel t % 128 (coalesced x access) instead of t / 3
 #ifndef GGD_MK_FUSE_KD
 #define GGD_MK_FUSE_KD 1

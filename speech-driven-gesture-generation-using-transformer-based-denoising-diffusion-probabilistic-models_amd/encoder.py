@@ -86,6 +86,32 @@ class SpeechEncoder:
         return tuple(z)
 
     @th.no_grad()
+    def memory(self, wav, model_type):
+        """wav (N, T) f32 -> the decoder's step-invariant speech memory, written by the encoder's head
+        kernels in place (ggd_enc_run_memory): s2g_v2 (N, Ts, 3 d) left-zero-padded levels side by
+        side (models/model.py:97-104), default / inpaint (N, T_low + T_mid + T_high, d) (model.py:55-68).
+        Equals speech_tokens(model_type, self(wav)) without the pad / concat copies."""
+        if model_type == "s2g_v2":
+            layout = native.MEM_BLEND
+        elif model_type in ("default", "inpaint"):
+            layout = native.MEM_CONCAT
+        else:
+            raise ValueError(f"Unsupported model_type {model_type}")
+        wav = wav.to(self.device, th.float32).contiguous()
+        n, tw = wav.shape
+        if n > self.max_batch:
+            return th.cat([self.memory(wav[i:i + self.max_batch], model_type) for i in range(0, n, self.max_batch)])
+        h = self._context(tw)
+        tl = self.lengths(tw)
+        shape = (n, max(tl), 3 * self.d_model) if layout == native.MEM_BLEND else (n, sum(tl), self.d_model)
+        mem = th.empty(shape, device=self.device)
+        stream = ctypes.c_void_p(th.cuda.current_stream(self.device).cuda_stream)
+        native.check(h, self.lib.ggd_enc_run_memory(h, ctypes.c_void_p(wav.data_ptr()), n, layout,
+                                                    ctypes.c_void_p(mem.data_ptr()), stream),
+                     "encode", "ggd_enc_last_error")
+        return mem
+
+    @th.no_grad()
     def frontend(self, wav):
         """wav (N, T) f32 -> the InstanceNorm'd mel image (N, 128, F) (ggd_enc_frontend): the input of
         the SE-ResNet, parameter-free, for the training path."""

@@ -17,7 +17,7 @@ import numpy as np
 import torch as th
 
 from . import native
-from .encoder import SpeechEncoder, speech_len, speech_tokens
+from .encoder import SpeechEncoder, speech_len
 from .weights import arch_from_config, parameter_shapes
 
 # "fp8": bf16 activations, OCP e4m3 per-step decoder weights with per-channel scales (GGD_FP8W)
@@ -215,7 +215,7 @@ class Speech2GestureModel:
         cur = th.cuda.current_stream(self.device)
         self._side.wait_stream(cur)
         with th.cuda.stream(self._side):
-            tok = speech_tokens(self.arch["type"], self.encoder()(wav))
+            tok = self.encoder().memory(wav, self.arch["type"])
             ev = th.cuda.Event()
             ev.record(self._side)
         wav.record_stream(self._side)
@@ -250,7 +250,7 @@ class Speech2GestureModel:
         else:
             if self._side is not None:  # the encoder's buffers may still be in use by a prefetch
                 th.cuda.current_stream(self.device).wait_stream(self._side)
-            tok = speech_tokens(self.arch["type"], self.encoder()(wav))
+            tok = self.encoder().memory(wav, self.arch["type"])
         assert tok.shape[1] == Ts, (tok.shape, Ts)
         native.check(ctx.h, ctx.lib.ggd_set_memory(ctx.h, ctypes.c_void_p(tok.data_ptr()), n, Ts, tok.shape[2],
                                                    _stream_ptr(self.device)), "set memory")

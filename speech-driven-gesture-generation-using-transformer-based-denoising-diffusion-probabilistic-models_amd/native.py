@@ -32,14 +32,16 @@ MODEL_S2G_V2, MODEL_DEFAULT, MODEL_INPAINT = 0, 1, 2
 DEC_ONEWAY, DEC_TWOWAY = 0, 1
 F32, BF16, FP8W = 0, 1, 2   # ggd_dtype (include/ggd.h)
 DDPM, DDIM = 0, 1
+MEM_BLEND, MEM_CONCAT = 0, 1   # ggd_enc_run_memory layouts
 
 EXPORTS = [
     "ggd_create", "ggd_destroy", "ggd_last_error", "ggd_load_weight", "ggd_finalize_weights",
     "ggd_set_schedule", "ggd_set_memory", "ggd_set_inpaint", "ggd_denoise", "ggd_posterior_step", "ggd_sample",
     "ggd_sync",
     "ggd_set_profiling", "ggd_kernel_time", "ggd_profile_kind", "ggd_set_route", "ggd_route_info", "ggd_version",
+    "ggd_mx_linear",
     "ggd_enc_create", "ggd_enc_destroy", "ggd_enc_last_error", "ggd_enc_load_weight", "ggd_enc_finalize",
-    "ggd_enc_lengths", "ggd_enc_run",
+    "ggd_enc_lengths", "ggd_enc_run", "ggd_enc_run_memory",
     # training path (include/ggd_train.h)
     "ggd_tr_gemm", "ggd_tr_colsum", "ggd_tr_layernorm_fwd", "ggd_tr_layernorm_bwd", "ggd_tr_seqconv_fwd",
     "ggd_tr_seqconv_bwd", "ggd_tr_attention_fwd", "ggd_tr_attention_bwd", "ggd_tr_elementwise", "ggd_tr_q_sample",
@@ -161,6 +163,7 @@ def load():
         "ggd_set_route": (ctypes.c_int, [CTX, I32, I32]),
         "ggd_route_info": (ctypes.c_int, [CTX, I32, VP]),
         "ggd_version": (ctypes.c_char_p, []),
+        "ggd_mx_linear": (ctypes.c_int, [I32, I32, I32, VP, VP, VP, VP, VP, VP]),
         "ggd_enc_create": (ctypes.c_int, [ctypes.c_int, I32, I32, I32, I32, P(CTX)]),
         "ggd_enc_destroy": (ctypes.c_int, [CTX]),
         "ggd_enc_last_error": (ctypes.c_char_p, [CTX]),
@@ -168,6 +171,7 @@ def load():
         "ggd_enc_finalize": (ctypes.c_int, [CTX]),
         "ggd_enc_lengths": (ctypes.c_int, [CTX, P(I32), P(I32), P(I32)]),
         "ggd_enc_run": (ctypes.c_int, [CTX, VP, I32, VP, VP, VP, VP]),
+        "ggd_enc_run_memory": (ctypes.c_int, [CTX, VP, I32, I32, VP, VP]),
         "ggd_tr_gemm": (ctypes.c_int, [I32, I32, I32, I32, I32, F, VP, I32, VP, I32, F, VP, I32, VP, VP]),
         "ggd_tr_colsum": (ctypes.c_int, [I32, I32, VP, I32, VP, F, VP]),
         "ggd_tr_layernorm_fwd": (ctypes.c_int, [I32, I32, VP, VP, VP, F, VP, VP, VP, VP]),

@@ -90,3 +90,19 @@ def test_encoder_frontend_matches_scipy_mel(pkg, sd, wav_len):
         err = np.abs(got[i] - want).max()
         print(f"frontend {wav_len}: max|diff| {err:.3e}")
         assert err <= 1e-3, err
+
+
+@pytest.mark.parametrize("wav_len", [32000, 128000])
+@pytest.mark.parametrize("model_type", ["s2g_v2", "default"])
+def test_encoder_writes_the_memory_layout(pkg, sd, wav_len, model_type):
+    """ggd_enc_run_memory: the head kernels write the decoder's speech memory in place -- s2g_v2's
+    left-zero-padded levels side by side (model.py:97-104, unequal lengths 31/30/30 and 125/124/126)
+    and the default / inpaint time concat (model.py:55-68) -- bit-equal to the three tensors padded
+    and concatenated by torch (encoder.speech_tokens)."""
+    enc_mod = __import__(pkg.__name__ + ".encoder", fromlist=["x"])
+    enc = encoder(pkg, sd, "bf16")
+    wav = wavs(3, wav_len).cuda()
+    want = enc_mod.speech_tokens(model_type, enc(wav))
+    got = enc.memory(wav, model_type)
+    assert got.shape == want.shape, (got.shape, want.shape)
+    assert th.equal(got, want)

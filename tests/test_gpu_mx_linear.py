@@ -1,0 +1,89 @@
+"""Block-scaled fp8 (MX) MFMA arithmetic pinned value by value (ggd_mx_linear, include/ggd.h).
+
+The long-clip loop's GGD_ROUTE_FP8_MFMA stages (csrc/ggd_long.hip over ggd_chainlib.h mx_scale_byte /
+mx_mul / mx_pack4 / ch_mma_mx) quantise activations to e4m3 with one e8m0 scale per 32 values and
+multiply them with per-channel e4m3 weights.  Model-level tests (test_gpu_fullsize.py) can only bound
+that route's drift from the f32 oracle; this one runs the same device functions on one Linear and
+compares with the numpy restatement (oracle/fp8.py mx_e4m3, e4m3_decode) in float64.
+  * The quantisation itself is pinned bit for bit (identity weights: out = the quantised values).
+  * The Linear: products of two e4m3 values scaled by powers of two are exact, so what is left is the
+    block-scaled MFMA's own accumulation.  Measured on MI355X (gpurun_out r05k, 9 cases): max error
+    3e-6 .. 6.5e-6 relative to sum |a_q| |w_q| when the row's blocks share a magnitude, up to 3.3e-5
+    when they span 2^32 -- the instruction's internal sum is narrower than an f32 chain.  Tolerance
+    2e-5 (same-magnitude blocks) / 1e-4 (2^32 spread), still 600x below one e4m3 code step (2^-4).
+"""
+import numpy as np
+import pytest
+import torch as th
+
+from oracle import fp8
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib(pkg):
+    from importlib import import_module
+    native = import_module(pkg.__name__ + ".native")
+    return native.load()
+
+
+def run(lib, a, codes, scale, bias):
+    M, K = a.shape
+    N = codes.shape[0]
+    ad, cd, sd, bd = a.cuda(), th.from_numpy(codes).cuda(), th.from_numpy(scale).cuda(), bias.cuda()
+    out = th.full((M, N), float("nan"), device="cuda")
+    rc = lib.ggd_mx_linear(M, N, K, ad.data_ptr(), cd.data_ptr(), sd.data_ptr(), bd.data_ptr(), out.data_ptr(), None)
+    assert rc == 0, rc
+    return out.cpu()
+
+
+@pytest.mark.parametrize("spread", [0, 4, 32])
+@pytest.mark.parametrize("M,N,K", [(32, 64, 256), (45, 128, 1024), (96, 192, 512)])
+def test_mx_linear_matches_the_restated_quantisation(lib, M, N, K, spread):
+    g = th.Generator().manual_seed(M + N + K)
+    # rows whose 32-value blocks differ in magnitude by up to 2^spread (MX scales across the row),
+    # zero blocks, tiny values that land in e4m3's subnormal range inside a block with a large max
+    lo = -(spread * 5) // 8
+    e = th.randint(lo, lo + spread + 1, (M, K // 32, 1), generator=g).float()
+    a = th.randn(M, K, generator=g) * th.exp2(e).expand(M, K // 32, 32).reshape(M, K)
+    a[0, :32] = 0.0
+    a[1, 32:64] *= th.exp2(-th.arange(32).float())
+    w = (th.randn(N, K, generator=g) * 0.05).numpy()
+    codes, scale, _ = fp8.quantize_rows(w)
+    bias = th.randn(N, generator=g)
+    got = run(lib, a, codes, scale, bias).double()
+    aq = fp8.mx_e4m3(a).double()
+    wq = th.from_numpy(fp8.e4m3_decode(codes)).double()
+    acc = aq @ wq.t()
+    want = acc * th.from_numpy(scale).double() + bias.double()
+    mag = aq.abs() @ wq.abs().t() * th.from_numpy(scale).double() + bias.double().abs()
+    err = ((got - want).abs() / mag.clamp_min(1e-30)).max().item()
+    print(f"mx_linear {M}x{N}x{K} spread {spread}: max rel err {err:.2e}")
+    assert err <= (1e-4 if spread > 4 else 2e-5), err
+
+
+def test_mx_quantisation_is_bit_exact(lib):
+    """Identity e4m3 weights (code 0x38 = 1.0, scale 1, bias 0): out = the quantised activations
+    themselves, so every value of mx_e4m3 is compared bit for bit -- subnormal e4m3 codes, zero
+    blocks, round-to-nearest-even ties, and blocks whose max sits on a power of two."""
+    K = 256
+    g = th.Generator().manual_seed(11)
+    rows = [th.randn(K, generator=g) * th.exp2(th.randint(-20, 12, (K // 32, 1), generator=g).float()).expand(
+        K // 32, 32).reshape(K) for _ in range(24)]
+    ramp = th.exp2(-th.arange(K).float() / 16.0) * 3.0           # every exponent a block spans, subnormals
+    ties = (th.arange(K).float() % 32 + 0.5) / 4.0 * 2.0 ** -3     # exact e4m3 midpoints
+    pow2 = th.where(th.arange(K) % 32 == 0, 256.0, 1.0 + th.arange(K).float() % 32 / 64.0)
+    a = th.stack(rows + [ramp, -ramp, ties, -ties, pow2, th.zeros(K), ramp * 2.0 ** -100, ties * 2.0 ** 60])
+    codes = np.where(np.eye(K, dtype=bool), 0x38, 0).astype(np.uint8)
+    got = run(lib, a, codes, np.ones(K, np.float32), th.zeros(K))
+    want = fp8.mx_e4m3(a)
+    bad = (got != want).nonzero()
+    for r, k in bad[:12].tolist():
+        print(f"row {r} k {k}: in {a[r, k].item():.9g} gpu {got[r, k].item():.9g} oracle {want[r, k].item():.9g}")
+    assert bad.shape[0] == 0, bad.shape[0]
+
+
+def test_mx_linear_rejects_bad_shapes(lib):
+    for M, N, K in ((32, 64, 128), (32, 60, 256), (0, 64, 256), (32, 64, 2048)):
+        assert lib.ggd_mx_linear(M, N, K, 1, 1, 1, 1, 1, None) == -1
