@@ -196,6 +196,7 @@ enum { LAYOUT_NHWC = 0, LAYOUT_NWCH = 1 };
 struct ConvArgs {
   const void* in;           // NHWC [N][H][W][Cin] (Cin a multiple of 32), f32 or bf16 (in_bf16)
   const void* w;            // T [Cout_pad][KH * KW][Cin]
+  const void* wp;           // bf16 plane-major copy for enc_conv_nhwc_kernel: [Cin / 32][4][Cout_pad][TAPSP][8]
   const float *bias, *s, *t;  // [Cout_pad]: BN folded to y = x * s + t
   void* out;                // f32 or bf16 (out_bf16)
   int N, H, W, Cin, Ho, Wo, Cout_pad, Cvalid, KH, KW, stride, pad, mode, layout, in_bf16, out_bf16;
@@ -746,7 +747,7 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int 
 // The residual tower's convolutions (NHWC bf16 in / out; 3x3 stride 1 and 2, the 1x1 stride-2
 // downsample), with the tile geometry fixed at compile time.  Same tiling as enc_conv_lds_kernel
 // (128 output pixels x NJ 16 output channels per 256-thread workgroup, per 32-channel chunk the
-// patch and the filter taps staged in LDS, the next chunk in registers), three differences:
+// patch and the filter taps staged in LDS, the next chunk in registers), and:
 //   * the geometry is constexpr: every index split is a shift / multiply (the runtime version
 //     spent ~2x its MFMA time on integer division in the staging and the epilogue), and the
 //     per-piece source offsets are computed once, each chunk adding 32 channels;
@@ -754,87 +755,138 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_lds_kernel(ConvArgs a, int 
 //   * the product is computed transposed (A = filter taps, B = patch), so a lane holds 4
 //     consecutive output channels of one pixel: one 8-byte store per (pixel tile, channel tile)
 //     instead of four 2-byte stores, and the SE squeeze reduces over the 16 pixel lanes by DPP.
+//   * round 5: the LDS images are PLANE-major -- 16-byte piece q (channels 8q..8q+7) of every patch
+//     position / filter row in plane q, 64 B per position instead of 80 -- so that every ds_read_b128
+//     lane group (16 lanes, 16 distinct pixels or filter rows) and every ds_write_b128 group (8
+//     consecutive positions of one plane) covers 64 distinct banks: conflict-free.  The 80-byte rows
+//     cost 2x on the tap reads (PMC r05e: SQ_LDS_BANK_CONFLICT = 49 % of SQ_LDS_IDX_ACTIVE) and
+//     25 % more LDS per workgroup (2 instead of 3 workgroups per CU on the 64-channel convs, 1
+//     instead of 2 on the stride-2 ones).  For that: a stride-2 3x3 patch stores its columns by
+//     parity (even | odd), so a row of output pixels reads consecutive positions at every tap; an
+//     8-wide tile pads the patch row so its two pixel rows sit 8 positions (32 banks) apart; the
+//     filter rows of one output channel are padded to an odd count (TAPSP) and come from a
+//     plane-major copy of the weights (EConv::wp, made at finalize).  The MFMA sequence and its
+//     operands are unchanged.  scripts/conv_lds_sim.py checks the addressing and the bank cycles
+//     of every compiled shape on the CPU.
 // ------------------------------------------------------------------------------------------
 template <int TW, int KS, int ST> struct CGeo {
   static constexpr int TH = CL_PX / TW;
   static constexpr int PH = KS == 1 ? TH : (TH - 1) * ST + KS;  // 1x1: only the pixels read
   static constexpr int PW = KS == 1 ? TW : (TW - 1) * ST + KS;
-  static constexpr int PS = KS == 1 ? 1 : ST;                   // patch step per output pixel
+  static constexpr int PS = KS == 1 ? 1 : ST;                   // patch rows / columns per output pixel
   static constexpr int SS = KS == 1 ? ST : 1;                   // source step per patch position
-  static constexpr int TAPS = KS * KS, NPOS = PH * PW;
-  static constexpr size_t PATCH_BYTES = (size_t)NPOS * CL_CS * 2;
+  static constexpr bool DI = KS > 1 && ST == 2;                 // columns stored by parity
+  static constexpr int HALF = (PW + 1) / 2;
+  static constexpr int PWC = DI ? 2 * HALF : PW;                // stored columns
+  static constexpr int pws() {  // row stride (positions): TW = 8 puts a wave's 2 pixel rows 8 slots apart
+    int w = PWC;
+    if (TW == 8)
+      while ((PS * w) % 16 != 8) ++w;
+    return w;
+  }
+  static constexpr int PWS = pws();
+  static constexpr int NPOS = (PH * PWS + 15) / 16 * 16;        // positions per plane (256-byte planes)
+  static constexpr int TAPS = KS * KS, TAPSP = TAPS | 1;        // filter rows per output channel (odd)
+  static constexpr size_t PATCH_BYTES = (size_t)4 * NPOS * 16;
+  // stored column of patch column px
+  static __host__ __device__ constexpr int col(int px) { return DI ? (px & 1) * HALF + (px >> 1) : px; }
 };
 
-template <int NJ, int TW, int KS, int ST, typename TO>
-__global__ void __launch_bounds__(CONV_TPB) enc_conv_nhwc_kernel(ConvArgs a) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t conv_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// workgroups per CU the LDS image allows (5 at most; 4 for the f32-output head convs, whose
+// epilogue does not fit 96 VGPRs): the kernel's register budget is set to match
+template <int NJ, int TW, int KS, int ST, typename TO> constexpr int conv_occ() {
   using GE = CGeo<TW, KS, ST>;
-  constexpr int QP = 4;                                        // 16-byte pieces (8 bf16) per 32 channels
-  constexpr int NP8 = GE::NPOS * QP, PM = (NP8 + CONV_TPB - 1) / CONV_TPB;
-  constexpr int NW = NJ * 16 * GE::TAPS * 4, WM = (NW + CONV_TPB - 1) / CONV_TPB;
+  const size_t lds = GE::PATCH_BYTES + (size_t)4 * NJ * 16 * GE::TAPSP * 16;
+  const int n = (int)((160 * 1024) / lds), cap = sizeof(TO) == 4 ? 4 : 5;
+  return n > cap ? cap : n;
+}
+
+template <int NJ, int TW, int KS, int ST, typename TO>
+__global__ void __launch_bounds__(CONV_TPB, (conv_occ<NJ, TW, KS, ST, TO>())) enc_conv_nhwc_kernel(ConvArgs a) {
+  using GE = CGeo<TW, KS, ST>;
+  constexpr int NP = GE::NPOS * 4, PM = (NP + CONV_TPB - 1) / CONV_TPB;     // patch pieces
+  constexpr int NWQ = NJ * 16 * GE::TAPSP, NW = 4 * NWQ, WM = (NW + CONV_TPB - 1) / CONV_TPB;  // filter pieces
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const bf16_t* in = (const bf16_t*)a.in;
   TO* out = (TO*)a.out;
-  bf16_t* patch = (bf16_t*)smem;
-  bf16_t* wl = (bf16_t*)(smem + GE::PATCH_BYTES);
+  bf16_t* patch = (bf16_t*)smem;                       // [4][NPOS][8]
+  bf16_t* wl = (bf16_t*)(smem + GE::PATCH_BYTES);      // [4][NJ 16][TAPSP][8]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, g = lane >> 4;
   const int tw_n = (a.Wo + TW - 1) / TW, th_n = (a.Ho + GE::TH - 1) / GE::TH, per = tw_n * th_n;
   const int b = blockIdx.x / per, tix = blockIdx.x - b * per, tyi = tix / tw_n;
   const int oh0 = tyi * GE::TH, ow0 = (tix - tyi * tw_n) * TW, n0 = blockIdx.y * (NJ * 16);
   const int ih0 = oh0 * ST - a.pad, iw0 = ow0 * ST - a.pad;
-  int pbase[2];  // patch position of tap (0, 0) for this lane's pixel in pixel tiles 0, 1
+  int pbase[2];  // stored position of tap (0, 0) for this lane's pixel in pixel tiles 0, 1
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = wave * 32 + i * 16 + r16, ty = q / TW, tx = q % TW;
-    pbase[i] = ty * GE::PS * GE::PW + tx * GE::PS;
+    pbase[i] = ty * GE::PS * GE::PWS + tx;
   }
-  // chunk-0 element offsets of this thread's patch / filter pieces (chunk ck adds 32 ck)
-  int poff[PM], woff[WM];
+  // chunk-0 element offsets of this thread's pieces (chunk ck adds 32 ck / 4 Cout_pad TAPSP 8 ck).
+  // Patch piece v: position p = 8 (v >> 5) + (v & 7) of plane q = (v >> 3) & 3 -- 8 consecutive lanes
+  // write 8 consecutive positions of one plane; a wave's 64 lanes read 16 whole pixels.
+  uint32_t poff[PM], woff[WM];  // BYTE offsets from the chunk's uniform base (saddr + voffset loads)
+  int pdst[PM];
   uint32_t okm = 0;  // bit k: patch piece k lies inside the image (else it stages as zero)
 #pragma unroll
   for (int k = 0; k < PM; ++k) {
-    const int v = tid + k * CONV_TPB, vc = min(v, NP8 - 1);
-    const int pos = vc / QP, q4 = vc % QP, py = pos / GE::PW, px = pos % GE::PW;
+    const int v = tid + k * CONV_TPB, vc = min(v, NP - 1);
+    const int p = (vc >> 5) * 8 + (vc & 7), q = (vc >> 3) & 3, py = p / GE::PWS, pc = p % GE::PWS;
+    const int px = GE::DI ? (pc < GE::HALF ? 2 * pc : 2 * (pc - GE::HALF) + 1) : pc;
     const int ih = ih0 + py * GE::SS, iw = iw0 + px * GE::SS;
-    const bool ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+    const bool ok = py < GE::PH && px < GE::PW && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
     const int ihc = min(max(ih, 0), a.H - 1), iwc = min(max(iw, 0), a.W - 1);
-    poff[k] = ((b * a.H + ihc) * a.W + iwc) * a.Cin + q4 * 8;
-    okm |= (ok && v < NP8) ? (1u << k) : 0u;
+    poff[k] = (uint32_t)(((b * a.H + ihc) * a.W + iwc) * a.Cin + q * 8) * 2u;
+    pdst[k] = (q * GE::NPOS + p) * 8;
+    okm |= (ok && v < NP) ? (1u << k) : 0u;
   }
+  const bf16_t* W = (const bf16_t*)a.wp;
+  const int wstep = 4 * a.Cout_pad * GE::TAPSP * 8;  // elements per 32-channel chunk of the plane-major copy
 #pragma unroll
   for (int k = 0; k < WM; ++k) {
     const int v = min(tid + k * CONV_TPB, NW - 1);  // clamped: every register is defined
-    const int q8 = v & 3, nt = v >> 2, n = nt / GE::TAPS, tap = nt % GE::TAPS;
-    woff[k] = ((n0 + n) * GE::TAPS + tap) * a.Cin + q8 * 8;
+    const int q = v / NWQ, r = v - q * NWQ;
+    woff[k] = (uint32_t)(((q * a.Cout_pad + n0) * GE::TAPSP + r) * 8) * 2u;
   }
   f32x4 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bf16_t* W = (const bf16_t*)a.w;
   const int cch = a.Cin >> 5;
+  // buffer loads: uniform base + 32-bit lane offset + the chunk's scalar offset (no 64-bit address math)
+  const __amdgpu_buffer_rsrc_t rin = conv_rsrc(in), rw = conv_rsrc(W);
   bf16x8 xr[PM], wr[WM];
   auto fetch = [&](int ck) __attribute__((always_inline)) {
 #pragma unroll
-    for (int k = 0; k < PM; ++k) xr[k] = *(const bf16x8*)(in + poff[k] + ck * 32);
+    for (int k = 0; k < PM; ++k)
+      xr[k] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rin, (int)poff[k], ck * 64, 0));
 #pragma unroll
-    for (int k = 0; k < WM; ++k) wr[k] = *(const bf16x8*)(W + woff[k] + ck * 32);
+    for (int k = 0; k < WM; ++k)
+      wr[k] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, (int)woff[k], ck * wstep * 2, 0));
   };
   auto put = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < PM; ++k) {
       const int v = tid + k * CONV_TPB;
-      if (v < NP8) {
+      if (v < NP) {
         const bf16x8 z = {};
-        *(bf16x8*)(patch + (v / QP) * CL_CS + (v % QP) * 8) = ((okm >> k) & 1u) ? xr[k] : z;
+        *(bf16x8*)(patch + pdst[k]) = ((okm >> k) & 1u) ? xr[k] : z;
       }
     }
 #pragma unroll
     for (int k = 0; k < WM; ++k) {
       const int v = tid + k * CONV_TPB;
-      if (v < NW) *(bf16x8*)(wl + (v >> 2) * CL_CS + (v & 3) * 8) = wr[k];  // (n taps + tap) = v >> 2
+      if (v < NW) *(bf16x8*)(wl + v * 8) = wr[k];
     }
   };
+  // this lane's LDS read bases (plane g): its two pixels' tap-(0, 0) positions, its filter row
+  const bf16_t* pl[2] = {patch + (g * GE::NPOS + pbase[0]) * 8, patch + (g * GE::NPOS + pbase[1]) * 8};
+  const bf16_t* wlb = wl + (g * NWQ + r16 * GE::TAPSP) * 8;
   fetch(0);
   for (int ck = 0; ck < cch; ++ck) {
     if (ck > 0) __syncthreads();  // the previous chunk's MFMAs are done with the LDS images
@@ -843,12 +895,12 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_nhwc_kernel(ConvArgs a) {
     if (ck + 1 < cch) fetch(ck + 1);
 #pragma unroll
     for (int tap = 0; tap < GE::TAPS; ++tap) {
-      const int toff = (tap / KS) * GE::PW + tap % KS;
+      const int toff = (tap / KS) * GE::PWS + GE::col(tap % KS);  // compile-time: the ds_read offset field
       bf16x8 bv[2], av[NJ];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) bv[i] = *(const bf16x8*)(patch + (pbase[i] + toff) * CL_CS + g * 8);
+      for (int i = 0; i < 2; ++i) bv[i] = *(const bf16x8*)(pl[i] + toff * 8);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) av[j] = *(const bf16x8*)(wl + ((j * 16 + r16) * GE::TAPS + tap) * CL_CS + g * 8);
+      for (int j = 0; j < NJ; ++j) av[j] = *(const bf16x8*)(wlb + (j * 16 * GE::TAPSP + tap) * 8);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -915,7 +967,7 @@ __global__ void __launch_bounds__(CONV_TPB) enc_conv_nhwc_kernel(ConvArgs a) {
 template <int NJ, int TW, int KS, int ST, typename TO>
 hipError_t launch_conv_nhwc(const ConvArgs& a, hipStream_t s) {
   using GE = CGeo<TW, KS, ST>;
-  constexpr size_t lds = GE::PATCH_BYTES + (size_t)NJ * 16 * GE::TAPS * CL_CS * 2;
+  constexpr size_t lds = GE::PATCH_BYTES + (size_t)4 * NJ * 16 * GE::TAPSP * 16;
   static_assert(lds <= 96 * 1024, "conv tile LDS");
   static bool attr = false;
   if (!attr) {
@@ -933,7 +985,7 @@ hipError_t launch_conv_nhwc(const ConvArgs& a, hipStream_t s) {
 // pixel shuffles)
 typedef hipError_t (*ConvLaunch)(const ConvArgs&, hipStream_t);
 ConvLaunch conv_nhwc_for(const ConvArgs& a) {
-  if (!a.in_bf16 || a.layout != LAYOUT_NHWC || conv_no_lds || a.KH != a.KW) return nullptr;
+  if (!a.in_bf16 || !a.wp || a.layout != LAYOUT_NHWC || conv_no_lds || a.KH != a.KW) return nullptr;
   const int nj = a.Cout_pad % 64 == 0 ? 4 : 2, TW = a.Wo >= 16 ? 16 : a.Wo >= 8 ? 8 : 0;
   const int shape = a.KH * 10 + a.stride;
 #define GGD_CONV_CASE(NJ_, TW_, KS_, ST_, TO_)                                             \
@@ -1023,6 +1075,7 @@ hipError_t launch_conv(int dtype, const ConvArgs& a, hipStream_t s) {
 struct EConv {            // one convolution + its folded BN epilogue
   int cin = 0, cin_pad = 0, cout = 0, cout_pad = 0, kh = 0, kw = 0, stride = 1, pad = 0;
   void* w = nullptr;      // T [cout_pad][kh*kw][cin_pad]
+  void* wp = nullptr;     // bf16 contexts: plane-major copy [cin_pad / 32][4][cout_pad][taps | 1][8] (ConvArgs::wp)
   float *bias = nullptr, *s = nullptr, *t = nullptr;
 };
 
@@ -1232,6 +1285,17 @@ int make_conv(ggd_enc* e, EConv& cv, const std::string& conv, const std::string&
     }
     ENC_TRY(e, ealloc(e, &cv.w, h.size() * 2));
     ENC_TRY(e, hipMemcpy(cv.w, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    const int tp = taps | 1, cch = cv.cin_pad / 32;
+    std::vector<uint16_t> hp((size_t)cch * 4 * cv.cout_pad * tp * 8, 0);
+    for (int ck = 0; ck < cch; ++ck)
+      for (int q = 0; q < 4; ++q)
+        for (int o = 0; o < cv.cout_pad; ++o)
+          for (int tap = 0; tap < taps; ++tap)
+            for (int el = 0; el < 8; ++el)
+              hp[((((size_t)ck * 4 + q) * cv.cout_pad + o) * tp + tap) * 8 + el] =
+                  h[((size_t)o * taps + tap) * cv.cin_pad + ck * 32 + q * 8 + el];
+    ENC_TRY(e, ealloc(e, &cv.wp, hp.size() * 2));
+    ENC_TRY(e, hipMemcpy(cv.wp, hp.data(), hp.size() * 2, hipMemcpyHostToDevice));
   } else {
     ENC_TRY(e, ealloc(e, &cv.w, p.size() * 4));
     ENC_TRY(e, hipMemcpy(cv.w, p.data(), p.size() * 4, hipMemcpyHostToDevice));
@@ -1251,15 +1315,14 @@ int make_lin(ggd_enc* e, const std::string& name, int out, int in, float** w, fl
   return GGD_OK;
 }
 
-// se_S non-null: squeeze into e->se_part in the epilogue when the shape takes the LDS path, and
-// return its rows per image there (0: not squeezed, the caller runs enc_se_sum_kernel)
-int run_conv(ggd_enc* e, const EConv& cv, const void* in, int n, int H, int W, void* out, int mode, int layout,
-             hipStream_t s, bool out_act = true, int* se_S = nullptr) {
+ConvArgs conv_args(ggd_enc* e, const EConv& cv, const void* in, int n, int H, int W, void* out, int mode, int layout,
+                   bool out_act) {
   ConvArgs a{};
   a.in = in;
   a.in_bf16 = e->asz == 2;
   a.out_bf16 = out_act && e->asz == 2;   // the heads' outputs feed f32 Linear layers
   a.w = cv.w;
+  a.wp = cv.wp;
   a.bias = cv.bias;
   a.s = cv.s;
   a.t = cv.t;
@@ -1278,6 +1341,14 @@ int run_conv(ggd_enc* e, const EConv& cv, const void* in, int n, int H, int W, v
   a.pad = cv.pad;
   a.mode = mode;
   a.layout = layout;
+  return a;
+}
+
+// se_S non-null: squeeze into e->se_part in the epilogue when the shape takes the LDS path, and
+// return its rows per image there (0: not squeezed, the caller runs enc_se_sum_kernel)
+int run_conv(ggd_enc* e, const EConv& cv, const void* in, int n, int H, int W, void* out, int mode, int layout,
+             hipStream_t s, bool out_act = true, int* se_S = nullptr) {
+  ConvArgs a = conv_args(e, cv, in, n, H, W, out, mode, layout, out_act);
   if (se_S) {
     *se_S = 0;
     if (conv_lds_tw(e->dtype, a) && layout == LAYOUT_NHWC) {
