@@ -10,7 +10,7 @@ mkdir -p ab /tmp/ggd_variant
 hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -fno-slp-vectorize -Wno-unused-value -Wno-unused-result $2 \
   -c $P/csrc/$U.hip -o /tmp/ggd_variant/${U}_$1.o || exit 1
 objs=""
-for s in ggd_kernels ggd_fused ggd_mega ggd_persist ggd_encoder ggd_train ggd_chain ggd_attn ggd_long ggd_api; do
+for s in ggd_kernels ggd_fused ggd_mega ggd_rows ggd_persist ggd_encoder ggd_train ggd_chain ggd_attn ggd_long ggd_api; do
   [ "$s" = "$U" ] || objs="$objs $P/build/$s.o"
 done
 hipcc --offload-arch=gfx950 -shared -fPIC $objs /tmp/ggd_variant/${U}_$1.o -o ab/libggd_$1.so && echo "ab/libggd_$1.so"

@@ -32,6 +32,10 @@ def diag(what, vals, n_out=17):
 
 
 names = ["emb", "L3 SA", "L3 CA", "layers", "step"]
+# slots 6 .. 16 inside the last layer (ggd_persist.hip LSTAMP): after LN1, the SA out-projection's
+# MFMAs and its partial exchange, LN2, the CA query GEMM, the CA out-projection + residual, LN3,
+# the FFN chunks, the FFN partial exchange, the CA out-projection's MFMAs and its exchange
+lnames = ["ln1", "sa-oproj", "sa-sum", "ln2", "caq", "ca-res", "ln3", "ffn", "ffsum", "ca-oproj", "ca-sum"]
 for label, pair in (("one workgroup per clip", 1), ("clip pair", 2)):
     diag(7, [0])            # the per-clip loops
     diag(14, [pair, 0])
@@ -40,5 +44,6 @@ for label, pair in (("one workgroup per clip", 1), ("clip pair", 2)):
         diffusion.ddim_sample_loop(model, (B, 123, 40), model_kwargs={"wav": wav}, seed=1, n_steps=3, extras=False)
         t = diag(8, [2])
         print(f"{label:24s} rep {rep}: " + "  ".join(f"{n} {t[i]:7.2f}" for i, n in enumerate(names)), flush=True)
+        print(" " * 24 + "    last layer: " + "  ".join(f"{n} {t[5 + i]:7.2f}" for i, n in enumerate(lnames)), flush=True)
 diag(14, [0, 0])
 diag(7, [2])

@@ -167,6 +167,11 @@ __device__ __forceinline__ void fattn_lds(unsigned char* att, int Lq, int Lk, fl
   do {                                                                                          \
     if (a.stamps && k == 0 && blockIdx.x == 0 && threadIdx.x == 0) a.stamps[i] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// stamps inside the last layer (scripts/pair_stamps.py: slots 6 .. 15)
+#define LSTAMP(i)                                                                               \
+  do {                                                                                          \
+    if (li + 1 == a.n_layers) PSTAMP(i);                                                        \
+  } while (0)
 #define FSTAMP(i)                                                                               \
   do {                                                                                          \
     if (a.stamps && k == 0 && li == 0 && hd == 1 && blockIdx.x == 0 && threadIdx.x == 0)         \
@@ -182,6 +187,13 @@ __device__ __forceinline__ void fattn_lds(unsigned char* att, int Lq, int Lk, fl
 // (a lane holds 4 consecutive columns of one row: float4 / 8-byte LDS epilogues instead of scalar ones)
 #ifndef GGD_PSK_TR
 #define GGD_PSK_TR 1
+#endif
+// A/B switch (clip pairs, transposed route): each part runs the attention out-projections on its
+// OWN four heads only (K = 128 of 256: half the MFMAs and half the 128 KiB weight stream) and the
+// partners exchange bf16 partial sums, as after the FFN (1), instead of swapping their heads'
+// attention outputs and both running the full out-projection (0)
+#ifndef GGD_PSK_SPLITO
+#define GGD_PSK_SPLITO 1
 #endif
 
 constexpr int PK_THREADS = 512;  // 8 waves: two per SIMD, so one wave's LDS / L2 waits overlap the other's MFMAs
@@ -317,8 +329,60 @@ __device__ __forceinline__ bool pp_swap_heads(bf16_t* Ob, int part, unsigned cha
   return true;
 }
 
+// partial sums of the two halves of a K split (FFN-down; with GGD_PSK_SPLITO the attention
+// out-projections): wave w's accumulators of column tiles 2w, 2w + 1, rounded to bf16 and handed
+// over in lane order; both parts add part 0's + part 1's -- each rounds its OWN partial too, so both
+// add the same two bf16 values and hold the same bits
+template <int RT>
+__device__ __forceinline__ bool pp_sum_partials(f32x4 (&acc)[RT][2], int part, unsigned char* xb, unsigned& ep,
+                                                unsigned* flags, bool xl, int* status, int* s_ok, int wave, int lane) {
+  ++ep;
+  const size_t sl = (size_t)(ep & 1) * PAIR_SLOT_BYTES;
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  u32x2 mine[RT][2];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const f32x4 v = acc[rt][j];
+      mine[rt][j] = u32x2{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])};
+    }
+  {
+    const __amdgpu_buffer_rsrc_t r = uni_rsrc(xb + (size_t)part * 2 * PAIR_SLOT_BYTES + sl, (uint32_t)PAIR_SLOT_BYTES);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int off = (((wave * RT + rt) * 2 + j) * 64 + lane) * 8;
+        if (xl) __builtin_amdgcn_raw_buffer_store_b64(mine[rt][j], r, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b64(mine[rt][j], r, off, 0, CP_COH);
+      }
+  }
+  if (!pp_sync(flags, part, ep, xl, status, s_ok)) return false;
+  const __amdgpu_buffer_rsrc_t r = uni_rsrc(xb + (size_t)(part ^ 1) * 2 * PAIR_SLOT_BYTES + sl, (uint32_t)PAIR_SLOT_BYTES);
+  u32x2 o[RT][2];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      o[rt][j] = __builtin_amdgcn_raw_buffer_load_b64(r, (((wave * RT + rt) * 2 + j) * 64 + lane) * 8, 0, CP_COH);
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const u32x2 m = mine[rt][j], q = o[rt][j];
+      acc[rt][j] = f32x4{__uint_as_float(m.x << 16) + __uint_as_float(q.x << 16),              // commutative:
+                         __uint_as_float(m.x & 0xffff0000u) + __uint_as_float(q.x & 0xffff0000u),  // same bits
+                         __uint_as_float(m.y << 16) + __uint_as_float(q.y << 16),              // in both parts
+                         __uint_as_float(m.y & 0xffff0000u) + __uint_as_float(q.y & 0xffff0000u)};
+    }
+  return true;
+}
+
 template <int RT, bool PAIR>
 __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
+  // the split out-projections: pairs on the transposed route
+  constexpr bool SPLITO = PAIR && GGD_PSK_SPLITO && GGD_PSK_TR;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_role, s_ok;
   if (a.gate && !gate_open(a.gate, a.gate_xl)) return;  // the loop this launch stands in for ran
@@ -462,6 +526,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         ln_rows<T, NT, R, SX>(Hs, L, Xn, tid);  // LN1 affine folded into the next Linear
         bar_lds();
       }
+      LSTAMP(6);
       for (int hi = 0; hi < HP; ++hi) {
         LANE_IDS();
         const int hp = hp0 + hi;
@@ -481,7 +546,8 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
             else pload<1, 8>(fa, w.qkv, 8, tq, 0, lane);
           } else {
             const int to[2] = {2 * wave, 2 * wave + 1};
-            pload<2, 8>(fa, w.o_sa, 8, to, 0, lane);
+            if constexpr (SPLITO) pload<2, 4>(fa, w.o_sa, 8, to, 4 * part, lane);  // K rows of its own heads
+            else pload<2, 8>(fa, w.o_sa, 8, to, 0, lane);
           }
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
@@ -534,7 +600,8 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
             else pload<1, 8>(fa, w.qkv, 8, tq, 0, lane);
           } else {
             const int to[2] = {2 * wave, 2 * wave + 1};
-            pload<2, 8>(fa, w.o_sa, 8, to, 0, lane);
+            if constexpr (SPLITO) pload<2, 4>(fa, w.o_sa, 8, to, 4 * part, lane);  // K rows of its own heads
+            else pload<2, 8>(fa, w.o_sa, 8, to, 0, lane);
           }
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
@@ -563,7 +630,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
 #endif
       }
       PSTAMP(2);
-      if constexpr (PAIR)
+      if constexpr (PAIR && !SPLITO)
         if (!pp_swap_heads<R, SX>(Ob, part, xb, ep, flags, xl, a.status, &s_ok, L, tid)) return;
       // SA out-projection + residual
       {
@@ -571,7 +638,8 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         const float4 bo4[2] = {ld_f4(w.o_sa_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.o_sa_b + (2 * wave + 1) * 16 + 4 * g4)};
         f32x4 acc[RT][2];
         zero_acc(acc);
-        pmma<RT, 2, 8, 16, true>(acc, Ob, SX, 0, fa, lane);
+        if constexpr (SPLITO) pmma<RT, 2, 4, 16, true>(acc, Ob, SX, 4 * part, fa, lane);  // its own heads' columns
+        else pmma<RT, 2, 8, 16, true>(acc, Ob, SX, 0, fa, lane);
         if constexpr (PAIR) {  // fa <- cross-attn Q of this part's heads: wave w owns column tile 8 part + w
           const int tq[1] = {8 * part + wave};
           pload<1, 8>(fa, w.q_ca, 8, tq, 0, lane);
@@ -579,6 +647,10 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           const int tq[2] = {2 * wave, 2 * wave + 1};
           pload<2, 8>(fa, w.q_ca, 8, tq, 0, lane);
         }
+        LSTAMP(7);
+        if constexpr (SPLITO)
+          if (!pp_sum_partials<RT>(acc, part, xb, ep, flags, xl, a.status, &s_ok, wave, lane)) return;
+        LSTAMP(8);
         p_resid_tr<RT>(Hs, acc, bo4, wave, c16, g4);
 #else
         const float bo0 = w.o_sa_b[(2 * wave) * 16 + c16], bo1 = w.o_sa_b[(2 * wave + 1) * 16 + c16];
@@ -612,6 +684,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         ln_rows<T, NT, R, SX>(Hs, L, Xn, tid);  // LN2 affine folded into the next Linear
         bar_lds();
       }
+      LSTAMP(9);
       // memory K / V of a head pair: the step-invariant rows come convolved and in image order
       // from the kvc block (set_memory); rows 0 / 1 (the step token's conv reach) are computed by
       // the last wave of each half.  Threads 0-255 stage head 2hp, 256-511 head 2hp + 1.
@@ -638,7 +711,8 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         pmma<RT, NQJ, 8, 16, true>(acc, Xn, SX, 0, fa, lane);
         {  // fa <- the CA out-projection
           const int to[2] = {2 * wave, 2 * wave + 1};
-          pload<2, 8>(fa, w.o_ca, 8, to, 0, lane);
+          if constexpr (SPLITO) pload<2, 4>(fa, w.o_ca, 8, to, 4 * part, lane);
+          else pload<2, 8>(fa, w.o_ca, 8, to, 0, lane);
         }
         bar_lds();
 #pragma unroll
@@ -663,7 +737,8 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         pmma<RT, NQJ, 8>(acc, Xn, SX, 0, fa, lane);
         {  // fa <- the CA out-projection
           const int to[2] = {2 * wave, 2 * wave + 1};
-          pload<2, 8>(fa, w.o_ca, 8, to, 0, lane);
+          if constexpr (SPLITO) pload<2, 4>(fa, w.o_ca, 8, to, 4 * part, lane);
+          else pload<2, 8>(fa, w.o_ca, 8, to, 0, lane);
         }
         bar_lds();
 #pragma unroll
@@ -677,6 +752,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         }
       }
 #endif
+      LSTAMP(10);
       // head pairs: both heads' conv and attention at once (threads 0-255 head 2hp, 256-511 head
       // 2hp + 1); the next pair's memory K|V loads fly under this pair's work
       for (int hi = 0; hi < HP; ++hi) {
@@ -705,7 +781,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         bar_lds();
       }
       PSTAMP(3);
-      if constexpr (PAIR)
+      if constexpr (PAIR && !SPLITO)
         if (!pp_swap_heads<R, SX>(Ob, part, xb, ep, flags, xl, a.status, &s_ok, L, tid)) return;
       // CA out-projection + residual
       {
@@ -713,11 +789,16 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         const float4 bo4[2] = {ld_f4(w.o_ca_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.o_ca_b + (2 * wave + 1) * 16 + 4 * g4)};
         f32x4 acc[RT][2];
         zero_acc(acc);
-        pmma<RT, 2, 8, 16, true>(acc, Ob, SX, 0, fa, lane);
+        if constexpr (SPLITO) pmma<RT, 2, 4, 16, true>(acc, Ob, SX, 4 * part, fa, lane);
+        else pmma<RT, 2, 8, 16, true>(acc, Ob, SX, 0, fa, lane);
         {  // fa <- FFN-up chunk c0f (fb already holds FFN-down chunk c0f)
           const int tf[1] = {8 * c0f + wave};
           pload<1, 8>(fa, w.ff1, 8, tf, 0, lane);
         }
+        LSTAMP(15);
+        if constexpr (SPLITO)
+          if (!pp_sum_partials<RT>(acc, part, xb, ep, flags, xl, a.status, &s_ok, wave, lane)) return;
+        LSTAMP(16);
         p_resid_tr<RT>(Hs, acc, bo4, wave, c16, g4);
 #else
         const float bo0 = w.o_ca_b[(2 * wave) * 16 + c16], bo1 = w.o_ca_b[(2 * wave + 1) * 16 + c16];
@@ -744,10 +825,12 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         bar_lds();
       }
       // ---------------- feed-forward block (nn.py:170-172) ----------------
+      LSTAMP(11);
       {
         ln_rows<T, NT, R, SX>(Hs, L, Xn, tid);  // LN3 affine folded into the next Linear
         bar_lds();
       }
+      LSTAMP(12);
       {
         const bool last = li + 1 == a.n_layers;
         const FusedLayer& wn = a.layers[last ? li : li + 1];
@@ -817,51 +900,10 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           }
         }
         static_assert(2 * PL::HID <= PL::SCR, "double-buffered FFN chunk image");
-        if constexpr (PAIR) {  // FFN-down partials of the two halves of K: both add part 0's + part 1's
-          // as bf16 (half the hand-off bytes of f32); each part rounds its OWN partial too, so both
-          // add the same two bf16 values and hold the same bits
-          ++ep;
-          const size_t sl = (size_t)(ep & 1) * PAIR_SLOT_BYTES;
-          typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
-          u32x2 mine[RT][2];
-#pragma unroll
-          for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const f32x4 v = accd[rt][j];
-              mine[rt][j] = u32x2{pk_bf16(v[0], v[1]),
-                                  pk_bf16(v[2], v[3])};
-            }
-          {
-            const __amdgpu_buffer_rsrc_t r = uni_rsrc(xb + (size_t)part * 2 * PAIR_SLOT_BYTES + sl, (uint32_t)PAIR_SLOT_BYTES);
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                const int off = (((wave * RT + rt) * 2 + j) * 64 + lane) * 8;
-                if (xl) __builtin_amdgcn_raw_buffer_store_b64(mine[rt][j], r, off, 0, 0);
-                else __builtin_amdgcn_raw_buffer_store_b64(mine[rt][j], r, off, 0, CP_COH);
-              }
-          }
-          if (!pp_sync(flags, part, ep, xl, a.status, &s_ok)) return;
-          const __amdgpu_buffer_rsrc_t r = uni_rsrc(xb + (size_t)(part ^ 1) * 2 * PAIR_SLOT_BYTES + sl, (uint32_t)PAIR_SLOT_BYTES);
-          u32x2 o[RT][2];
-#pragma unroll
-          for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              o[rt][j] = __builtin_amdgcn_raw_buffer_load_b64(r, (((wave * RT + rt) * 2 + j) * 64 + lane) * 8, 0, CP_COH);
-#pragma unroll
-          for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const u32x2 m = mine[rt][j], q = o[rt][j];
-              accd[rt][j] = f32x4{__uint_as_float(m.x << 16) + __uint_as_float(q.x << 16),      // commutative:
-                                  __uint_as_float(m.x & 0xffff0000u) + __uint_as_float(q.x & 0xffff0000u),  // same bits
-                                  __uint_as_float(m.y << 16) + __uint_as_float(q.y << 16),      // in both parts
-                                  __uint_as_float(m.y & 0xffff0000u) + __uint_as_float(q.y & 0xffff0000u)};
-            }
-        }
+        LSTAMP(13);
+        if constexpr (PAIR)  // FFN-down partials of the two halves of K
+          if (!pp_sum_partials<RT>(accd, part, xb, ep, flags, xl, a.status, &s_ok, wave, lane)) return;
+        LSTAMP(14);
 #if GGD_PSK_TR
         const float4 b24[2] = {ld_f4(w.ff2_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.ff2_b + (2 * wave + 1) * 16 + 4 * g4)};
         p_resid_tr<RT>(Hs, accd, b24, wave, c16, g4);
