@@ -16,10 +16,13 @@ import __graft_entry__ as ge  # noqa: E402
 pkg = ge.load_package()
 native = __import__(ge.PKG_NAME + ".native", fromlist=["x"])
 cfg = pkg.load_config(os.path.join(ROOT, "configs", "beat-ours.json"))
+NL = int(next((a.split("=")[1] for a in sys.argv[1:] if a.startswith("layers=")), 4))  # layers=N
+if NL != 4:
+    cfg.Model.Decoder["n_layers"] = NL
 model, _, _, _, _ = pkg.create_model(123, cfg.Model, dtype="bf16", device="cuda:0")
 model.load_state_dict(pkg.init_state_dict(model.arch, seed=0))
 diffusion = pkg.create_diffusion(dict(cfg.Model.Diffusion.to_dict(), timestep_respacing="ddim50"), False)
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
+B = int(next((a for a in sys.argv[1:] if a.isdigit()), 128))
 wav = th.randn(B, 32000, device="cuda") * 0.1
 ctx, _ = model.prepare(wav, 40)
 
@@ -36,7 +39,7 @@ names = ["emb", "L3 SA", "L3 CA", "layers", "step"]
 # MFMAs and its partial exchange, LN2, the CA query GEMM, the CA out-projection + residual, LN3,
 # the FFN chunks, the FFN partial exchange, the CA out-projection's MFMAs and its exchange
 lnames = ["ln1", "sa-oproj", "sa-sum", "ln2", "caq", "ca-res", "ln3", "ffn", "ffsum", "ca-oproj", "ca-sum"]
-for label, pair in (("one workgroup per clip", 1), ("clip pair", 2)):
+for label, pair in (("clip pair", 2),) if NL != 4 else (("one workgroup per clip", 1), ("clip pair", 2)):
     diag(7, [0])            # the per-clip loops
     diag(14, [pair, 0])
     for rep in range(3):

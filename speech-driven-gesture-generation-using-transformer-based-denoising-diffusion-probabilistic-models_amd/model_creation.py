@@ -24,8 +24,8 @@ def create_model(d_pose, model_params, lr=1e-2, weight_decay=None, scheduler_par
     Inference (is_training False): the HIP sampler model; optimizer, schedule_sampler and
     lr_scheduler are None.  Training: a training.TrainableModel (reference init, seed 0; the HA2G
     encoder trained in train mode unless train_encoder=False) with AdamW, the uniform schedule
-    sampler and the configured lr schedule (the one-way decoder under s2g_v2, default or
-    inpaint).  Legacy {"type","args"} model params
+    sampler and the configured lr schedule (the one-way or two-way decoder under
+    s2g_v2, default or inpaint).  Legacy {"type","args"} model params
     (tedexp) are adapted to the flat schema first.
     """
     if is_training:

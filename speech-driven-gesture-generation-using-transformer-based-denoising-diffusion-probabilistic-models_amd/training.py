@@ -506,13 +506,15 @@ def _trainable(arch, train_encoder=False):
 
 
 class TrainableModel:
-    """The s2g_v2 + one-way-decoder denoiser (models/model.py:76-117, nn.py:177-228) with its
-    trainable parameters in one flat f32 device buffer under the reference's state_dict names."""
+    """The denoiser (models/model.py:41-166) -- s2g_v2, default or inpaint model, one-way
+    (nn.py:177-228) or two-way (nn.py:381-447) decoder -- with its trainable parameters in one flat
+    f32 device buffer under the reference's state_dict names."""
 
     def __init__(self, arch, sd, device="cuda", train_encoder=False, pose_seed_len=None):
-        if arch["type"] not in ("s2g_v2", "default", "inpaint") or arch["decoder"] != "oneway_cross_attention":
-            raise ValueError("the training path covers the one-way decoder under the s2g_v2, default and inpaint "
-                             "models")
+        if arch["type"] not in ("s2g_v2", "default", "inpaint") or \
+                arch["decoder"] not in ("oneway_cross_attention", "cross_attention"):
+            raise ValueError("the training path covers the one-way and two-way decoders under the s2g_v2, default "
+                             "and inpaint models")
         if arch["type"] == "inpaint" and pose_seed_len is None:
             raise ValueError("the inpaint model trains with its pose_seed_len (Model.Generate.pose_seed_len, "
                              "model_creation.py:141)")
@@ -711,6 +713,41 @@ class TrainableModel:
             out.append(linear(h, proj_w, proj_b))
         return tuple(out)
 
+    def _ffn(self, q, sfx, h):
+        """h + FeedForward(LayerNorm(h)) with SquaredReLU (transformer.py:129-154); sfx "" or "_mem"."""
+        P = self.params
+        u = layer_norm(h, P[q + f"norm_ff{sfx}.weight"], P[q + f"norm_ff{sfx}.bias"])
+        f = squared_relu(linear(u, P[q + f"feed_forward{sfx}.layer1.weight"], P[q + f"feed_forward{sfx}.layer1.bias"]))
+        return add(h, linear(f, P[q + f"feed_forward{sfx}.layer2.weight"], P[q + f"feed_forward{sfx}.layer2.bias"]))
+
+    def _twoway(self, x, m):
+        """CrossAttention.forward (nn.py:428-447) over embedded poses x (N, L, d) and memory m (N, Tm, d):
+        one positional encoding over the joint sequence [x; m] (nn.py:438-442); per layer
+        (CrossAttentionLayer, nn.py:381-418) self-attention of x and of m, attention over the joint
+        sequence, then the feed-forward of x -- and of m except in the last layer.  The joint
+        sequence is a concatenation of the two streams' token rows (data movement); every op on it
+        runs on the HIP kernels with its backward."""
+        P, a = self.params, self.arch
+        N, L, _ = x.shape
+        Tm = m.shape[1]
+        pe = self._pe_rows(N, L + Tm)
+        x = add(x, pe[:, :L].contiguous())
+        m = add(m, pe[:, L:].contiguous())
+        for i in range(a["n_layers"]):
+            q = f"pose_decoder.layers.{i}."
+            u = layer_norm(x, P[q + "norm_self_attn.weight"], P[q + "norm_self_attn.bias"])
+            x = add(x, self._mdha(q + "self_attn", u, u))
+            u = layer_norm(m, P[q + "norm_self_attn_mem.weight"], P[q + "norm_self_attn_mem.bias"])
+            m = add(m, self._mdha(q + "self_attn_mem", u, u))
+            h = th.cat([x, m], dim=1)
+            u = layer_norm(h, P[q + "norm_cross_attn.weight"], P[q + "norm_cross_attn.bias"])
+            h = add(h, self._mdha(q + "cross_attn", u, u))
+            x, m = h[:, :L].contiguous(), h[:, L:].contiguous()
+            x = self._ffn(q, "", x)
+            if (q + "feed_forward_mem.layer1.weight") in P:
+                m = self._ffn(q, "_mem", m)
+        return x
+
     def __call__(self, x_t, t, z=None, wav=None, inpaint_pose=None, inpaint_mask=None):
         """x_t (N, C, L), t (N,) int64 original timesteps -> eps (N, C, L).  Speech: z = (z_low, z_mid,
         z_high) tokens (N, T_i, d) from the frozen encoder, or wav (N, T_wav) encoded here (through the
@@ -736,7 +773,8 @@ class TrainableModel:
             mem = th.cat([s[:, None]] + [zi for zi in z], dim=1)
         Tm = mem.shape[1]
         pre = "pose_decoder."
-        m = add(linear(mem, P[pre + "emb_mem.weight"], P[pre + "emb_mem.bias"]), self._pe_rows(N, Tm))
+        if a["decoder"] == "oneway_cross_attention":   # positions restart at 0 for the memory (nn.py:222-223)
+            m = add(linear(mem, P[pre + "emb_mem.weight"], P[pre + "emb_mem.bias"]), self._pe_rows(N, Tm))
         x_in = x_t.transpose(1, 2).contiguous()                                      # (N, L, C)
         if a["type"] == "inpaint":
             # Speech2GestureModelInpaint.myforward (model.py:152-166): x + proj([pose * mask, mask]); the
@@ -751,16 +789,18 @@ class TrainableModel:
             u = silu(linear(xi, P["proj.0.weight"], P["proj.0.bias"]))
             u = silu(linear(u, P["proj.2.weight"], P["proj.2.bias"]))
             x_in = add(x_in, linear(u, P["proj.4.weight"], P["proj.4.bias"]))       # Dropout p = 0 (configs)
-        h = add(linear(x_in, P[pre + "emb_x.weight"], P[pre + "emb_x.bias"]), self._pe_rows(N, L))
-        for i in range(a["n_layers"]):
-            q = pre + f"layers.{i}."
-            u = layer_norm(h, P[q + "norm_self_attn.weight"], P[q + "norm_self_attn.bias"])
-            h = add(h, self._mdha(q + "self_attn", u, u))
-            u = layer_norm(h, P[q + "norm_cross_attn.weight"], P[q + "norm_cross_attn.bias"])
-            h = add(h, self._mdha(q + "cross_attn", u, m))
-            u = layer_norm(h, P[q + "norm_ff.weight"], P[q + "norm_ff.bias"])
-            f = squared_relu(linear(u, P[q + "feed_forward.layer1.weight"], P[q + "feed_forward.layer1.bias"]))
-            h = add(h, linear(f, P[q + "feed_forward.layer2.weight"], P[q + "feed_forward.layer2.bias"]))
+        if a["decoder"] == "cross_attention":
+            h = self._twoway(linear(x_in, P[pre + "emb_x.weight"], P[pre + "emb_x.bias"]),
+                             linear(mem, P[pre + "emb_mem.weight"], P[pre + "emb_mem.bias"]))
+        else:
+            h = add(linear(x_in, P[pre + "emb_x.weight"], P[pre + "emb_x.bias"]), self._pe_rows(N, L))
+            for i in range(a["n_layers"]):
+                q = pre + f"layers.{i}."
+                u = layer_norm(h, P[q + "norm_self_attn.weight"], P[q + "norm_self_attn.bias"])
+                h = add(h, self._mdha(q + "self_attn", u, u))
+                u = layer_norm(h, P[q + "norm_cross_attn.weight"], P[q + "norm_cross_attn.bias"])
+                h = add(h, self._mdha(q + "cross_attn", u, m))
+                h = self._ffn(q, "", h)
         u = layer_norm(h, P[pre + "out_layers.0.weight"], P[pre + "out_layers.0.bias"])
         y = linear(u, P[pre + "out_layers.1.weight"], P[pre + "out_layers.1.bias"])
         return y.transpose(1, 2)

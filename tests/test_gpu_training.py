@@ -619,3 +619,59 @@ def test_inpaint_training_gradients_match_oracle_and_checkpoint_samples(pkg, bea
     ref = ref_denoiser.OracleModel(trained, ocfg, cache_speech=True)(xs, ts, wav=wav, inpaint_pose=poses.transpose(0, 1),
                                                                        inpaint_mask=mask)
     assert (got - ref).abs().max().item() <= 1e-4
+
+
+def test_twoway_decoder_training_gradients_match_oracle_and_checkpoint_samples(pkg, beat_cfg, tr):
+    """The two-way CrossAttention decoder (nn.py:381-447, the tedexp configuration's decoder) trained
+    under the default model (memory concat on time, model.py:41-73): one step's loss and every
+    gradient -- the memory stream's self-attention / feed-forward, the joint attention, the last
+    layer without feed_forward_mem -- against torch autograd through the oracle's twoway_decoder;
+    then a Trainer step's checkpoint loads strictly into the two-way sampler and its eps matches the
+    oracle on the trained weights."""
+    cfg = beat_cfg.Model.to_dict()
+    cfg = dict(cfg, type="default", Decoder=dict(cfg["Decoder"], type="cross_attention", n_layers=2))
+    arch = pkg.arch_from_config(cfg, D_POSE)
+    assert arch["decoder"] == "cross_attention" and arch["type"] == "default"
+    sd = pkg.init_state_dict(arch, seed=0, perturb=True)
+    assert "pose_decoder.layers.0.feed_forward_mem.layer1.weight" in sd
+    assert "pose_decoder.layers.1.feed_forward_mem.layer1.weight" not in sd   # last layer (nn.py:408-418)
+    g = th.Generator().manual_seed(61)
+    sampler, _, _, _, _ = pkg.create_model(D_POSE, cfg, dtype="f32", device="cuda:0")
+    sampler.load_state_dict(sd)
+    n = 2
+    wav = th.randn(n, WAV, generator=g) * 0.1
+    z = sampler.encoder()(wav.cuda())
+    diffusion = pkg.create_diffusion(beat_cfg.Model.Diffusion.to_dict(), True)
+    model = tr.TrainableModel(arch, sd, "cuda")
+    assert "pose_decoder.layers.0.self_attn_mem.output.weight" in model.params
+    trainer = tr.Trainer(model, diffusion, None, lr=1e-3, weight_decay=0.0)
+    x0 = th.randn(n, D_POSE, L, generator=g)
+    t = th.tensor([811, 40])
+    noise = th.randn(n, D_POSE, L, generator=g)
+    model.zero_grad()
+    out = tr.training_losses(diffusion, model, x0.cuda(), t.cuda(), {"speech_tokens": z}, noise=noise.cuda())
+    loss = out["mse"].mean()
+    loss.backward()
+    names = list(model.params)
+    sd_ref = {k: v.detach().float().clone() for k, v in sd.items()}
+    for k in names:
+        sd_ref[k].requires_grad_(True)
+    want = _oracle_loss(arch, sd_ref, diffusion, x0, t, noise, tuple(a.cpu() for a in z))
+    want.backward()
+    assert abs(loss.item() - want.item()) <= 1e-5 * want.item(), (loss.item(), want.item())
+    floor = 1e-4 * max(sd_ref[k].grad.abs().max().item() for k in names)
+    worst = sorted(((model.params[k].grad.cpu() - sd_ref[k].grad).abs().max().item()
+                    / max(sd_ref[k].grad.abs().max().item(), floor), k) for k in names)[::-1]
+    print("\ntwo-way: worst gradient errors", worst[:4])
+    assert sd_ref["pose_decoder.layers.0.feed_forward_mem.layer2.weight"].grad.abs().max().item() > 0
+    assert worst[0][0] <= 2e-3, worst[:4]
+    res = trainer.step({"pose": x0.transpose(1, 2).cuda(), "speech_tokens": z}, noise=noise.cuda(), t=t.cuda())
+    assert np.isfinite(res["loss"])
+    trained = {k: v.cpu() for k, v in model.state_dict().items()}
+    assert set(trained) == set(sd)
+    sampler.load_state_dict(trained, strict=True)
+    xs = th.randn(n, D_POSE, L, generator=g)
+    ts = th.tensor([999, 0])
+    got = sampler(xs.cuda(), ts.cuda(), wav=wav.cuda()).cpu()
+    ref = ref_denoiser.OracleModel(trained, oracle_cfg(arch), cache_speech=True)(xs, ts, wav=wav)
+    assert (got - ref).abs().max().item() <= 1e-4
