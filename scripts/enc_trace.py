@@ -12,7 +12,7 @@ if sys.argv[1] == "--report":
                  r.get("Grid_Size_X", r.get("Grid_Size", "?")), r.get("Workgroup_Size_X", "?"),
                  r.get("LDS_Block_Size", r.get("Lds_Size", "?")))
                 for r in csv.DictReader(open(f)))
-    st = [i for i, e in enumerate(ev) if "enc_stft_power" in e[2]]
+    st = [i for i, e in enumerate(ev) if "enc_stft_power" in e[2] or "enc_stft_mel" in e[2]]
     a = st[-1]
     t0 = ev[a][0]
     tot = 0.0

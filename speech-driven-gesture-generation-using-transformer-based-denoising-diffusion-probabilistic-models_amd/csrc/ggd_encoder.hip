@@ -55,7 +55,67 @@ constexpr int SE_SLICES = 64;   // pixel slices of the SE squeeze's first stage
 // ------------------------------------------------------------------------------------------
 // front end
 // ------------------------------------------------------------------------------------------
-// Power spectrum of frame (clip b, frame f): torch.stft(n_fft 1024, hop 512, Hann window,
+// Mel power spectrum of frame (clip b, frame f): torch.stft(n_fft 1024, hop 512, Hann window,
+// center=True, pad_mode='reflect', onesided) |X_k|^2 (speech_encoder.py:18-26), then the HTK mel
+// filterbank.  The frame is loaded in bit-reversed order, then 10 radix-2 decimation-in-time stages
+// run in LDS (512 butterflies per stage over 256 threads); tw[t] = exp(-2 pi i t / 1024), t < 512,
+// rounded once from f64.  LDS index i + i / 32 (one float2 of padding per 32): the bit-reversed
+// stores and the short-stride butterflies of the first stages hit distinct banks (2-dword pairs of
+// 32 lanes; 32-way conflicts on the unpadded stores).
+// Round 5: the filterbank product is done here instead of by a GEMM over the written-out power
+// rows: each triangular filter is nonzero on a short band of bins (fb_lo[m] .. + fb_n[m], the
+// band's values packed at fb_off[m], made at finalize from the loaded matrix), so mel bin m is a
+// short f32 sum over that band in ascending bin order -- 1-2 % of the dense GEMM's work and no
+// power rows in HBM.
+__device__ __forceinline__ int fft_ix(int i) { return i + (i >> 5); }
+__global__ void __launch_bounds__(256) enc_stft_mel_kernel(const float* __restrict__ wav, const float* __restrict__ window,
+                                                           const float2* __restrict__ tw, const int* __restrict__ fb_lo,
+                                                           const int* __restrict__ fb_n, const int* __restrict__ fb_off,
+                                                           const float* __restrict__ fb_val, float* __restrict__ mel,
+                                                           int Tw, int F, float coef) {
+  __shared__ float2 a[NFFT + NFFT / 32];
+  __shared__ float pwr[POW_LD];
+  const int fr = blockIdx.x, b = fr / F, f = fr - b * F;
+  const float* x = wav + (size_t)b * Tw;
+  for (int k = threadIdx.x; k < NFFT; k += blockDim.x) {
+    // centre reflect padding of n_fft / 2 (torch.stft center=True, pad_mode='reflect')
+    int src = f * HOP + k - NFFT / 2;
+    if (src < 0) src = -src;
+    if (src >= Tw) src = 2 * (Tw - 1) - src;
+    // pre-emphasis y[j] = x[j] - c x[j - 1], reflect-padded on the left: y[0] = x[0] - c x[1]
+    const int prev = src == 0 ? 1 : src - 1;
+    a[fft_ix(__brev((unsigned)k) >> 22)] = make_float2((x[src] - coef * x[prev]) * window[k], 0.f);
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int st = 1; st <= 10; ++st) {
+    const int half = 1 << (st - 1), stride = NFFT >> st;
+    for (int j = threadIdx.x; j < NFFT / 2; j += blockDim.x) {
+      const int pos = j & (half - 1), i1 = ((j >> (st - 1)) << st) + pos, i2 = i1 + half;
+      const float2 w = tw[pos * stride], u = a[fft_ix(i1)], v = a[fft_ix(i2)];
+      const float2 t = make_float2(v.x * w.x - v.y * w.y, v.x * w.y + v.y * w.x);
+      a[fft_ix(i1)] = make_float2(u.x + t.x, u.y + t.y);
+      a[fft_ix(i2)] = make_float2(u.x - t.x, u.y - t.y);
+    }
+    __syncthreads();
+  }
+  for (int k = threadIdx.x; k < NBIN; k += blockDim.x) {
+    const float2 v = a[fft_ix(k)];
+    pwr[k] = v.x * v.x + v.y * v.y;
+  }
+  __syncthreads();
+  if (threadIdx.x < NMEL) {
+    const int m = threadIdx.x, lo = fb_lo[m], n = fb_n[m];
+    const float* wv = fb_val + fb_off[m];
+    float acc = 0.f;
+    for (int j = 0; j < n; ++j) acc += pwr[lo + j] * wv[j];
+    mel[(size_t)fr * NMEL + m] = acc;
+  }
+}
+
+// Power spectrum rows for the dense mel GEMM (the training front end, ggd_enc_frontend: its image
+// feeds the train-mode encoder and is kept as it was measured against the oracle).  Frame (clip b,
+// frame f): torch.stft(n_fft 1024, hop 512, Hann window,
 // center=True, pad_mode='reflect', onesided) |X_k|^2 (speech_encoder.py:18-26).  The frame is loaded
 // in bit-reversed order, then 10 radix-2 decimation-in-time stages run in LDS (512 butterflies
 // per stage over 256 threads); tw[t] = exp(-2 pi i t / 1024), t < 512, rounded once from f64.
@@ -1104,7 +1164,8 @@ struct ggd_enc {
   std::vector<void*> allocs;
   bool finalized = false;
   // weights
-  float *window = nullptr, *twiddle = nullptr, *fbT = nullptr, *zeros = nullptr;
+  float *window = nullptr, *twiddle = nullptr, *fb_val = nullptr, *fbT = nullptr, *zeros = nullptr;
+  int *fb_lo = nullptr, *fb_n = nullptr, *fb_off = nullptr;  // the filterbank's nonzero band per mel bin
   float coef = 0.97f;
   float *c1_w = nullptr, *c1_b = nullptr, *c1_s = nullptr, *c1_t = nullptr;
   std::vector<EBlock> blocks;
@@ -1381,7 +1442,32 @@ int ggd_enc_finalize(ggd_enc* e) {
   }
   ENC_TRY(e, upload(e, &e->twiddle, tw));
   ENC_TRY(e, upload(e, &e->window, *win));
-  std::vector<float> fbT((size_t)NMEL * 768, 0.f);
+  {  // each mel filter's band of nonzero bins [lo, lo + n) and its values (any matrix works: a dense
+     // column is a band of all 513 bins)
+    std::vector<int> lo(NMEL), cnt(NMEL), off(NMEL);
+    std::vector<float> val;
+    for (int m = 0; m < NMEL; ++m) {
+      int first = -1, last = -1;
+      for (int f = 0; f < NBIN; ++f)
+        if ((*fb)[(size_t)f * NMEL + m] != 0.f) {
+          if (first < 0) first = f;
+          last = f;
+        }
+      lo[m] = first < 0 ? 0 : first;
+      cnt[m] = first < 0 ? 0 : last - first + 1;
+      off[m] = (int)val.size();
+      for (int f = lo[m]; f < lo[m] + cnt[m]; ++f) val.push_back((*fb)[(size_t)f * NMEL + m]);
+    }
+    val.push_back(0.f);
+    ENC_TRY(e, upload(e, &e->fb_val, val));
+    ENC_TRY(e, ealloc(e, &e->fb_lo, sizeof(int) * NMEL));
+    ENC_TRY(e, ealloc(e, &e->fb_n, sizeof(int) * NMEL));
+    ENC_TRY(e, ealloc(e, &e->fb_off, sizeof(int) * NMEL));
+    ENC_TRY(e, hipMemcpy(e->fb_lo, lo.data(), sizeof(int) * NMEL, hipMemcpyHostToDevice));
+    ENC_TRY(e, hipMemcpy(e->fb_n, cnt.data(), sizeof(int) * NMEL, hipMemcpyHostToDevice));
+    ENC_TRY(e, hipMemcpy(e->fb_off, off.data(), sizeof(int) * NMEL, hipMemcpyHostToDevice));
+  }
+  std::vector<float> fbT((size_t)NMEL * 768, 0.f);  // the dense matrix of the training front end's GEMM
   for (int m = 0; m < NMEL; ++m)
     for (int f = 0; f < NBIN; ++f) fbT[(size_t)m * 768 + f] = (*fb)[(size_t)f * NMEL + m];
   ENC_TRY(e, upload(e, &e->fbT, fbT));
@@ -1571,22 +1657,9 @@ int enc_run(ggd_enc* e, const float* wav, int32_t n, const MemMap& mm, hipStream
     const int m = std::min(e->chunk, n - c0);
     const float* w = wav + (size_t)c0 * e->wav_len;
     // front end: STFT power, then the mel GEMM
-    hipLaunchKernelGGL(enc_stft_power_kernel, dim3(m * F), dim3(256), 0, s, w, e->window, (const float2*)e->twiddle,
-                       e->pw, e->wav_len, F, e->coef);
+    hipLaunchKernelGGL(enc_stft_mel_kernel, dim3(m * F), dim3(256), 0, s, w, e->window, (const float2*)e->twiddle,
+                       e->fb_lo, e->fb_n, e->fb_off, e->fb_val, e->mel, e->wav_len, F, e->coef);
     ENC_TRY(e, hipGetLastError());
-    GemmArgs g{};
-    g.M = m * F;
-    g.bias = e->zeros;
-    g.N = NMEL;
-    g.K = 768;
-    g.k_valid = NBIN;
-    g.A = e->pw;
-    g.lda = POW_LD;
-    g.W = e->fbT;
-    g.out = e->mel;
-    g.ldo = NMEL;
-    g.n_valid = NMEL;
-    ENC_TRY(e, launch_gemm(GGD_F32, PRO_F32, EPI_F32, g, s));
     hipLaunchKernelGGL(enc_inorm_kernel, dim3(m), dim3(4 * NMEL), 0, s, e->mel, e->img, F);
     ENC_TRY(e, hipGetLastError());
     const size_t n1 = (size_t)m * e->H[1] * e->W[1] * 4;
