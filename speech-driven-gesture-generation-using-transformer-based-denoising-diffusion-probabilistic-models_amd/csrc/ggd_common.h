@@ -98,12 +98,16 @@ struct UpdOut { float x0, raw, mean, xn; };
 constexpr unsigned long long WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
 // a timed-out barrier: code 1 and the STATUS_TIMEOUT bit (ggd_kernels.h)
 __device__ __forceinline__ void status_timeout(int* status) {
-  atomicMax(status, 1);
-  atomicOr(status, STATUS_TIMEOUT);
+  // one atomic: the bit dominates any code (every gate tests for an exact code, so a timed-out
+  // launch opens none; the host counts the bit and reports the timeout).  A second atomic here cost
+  // the long-clip loop a register spill (it sits at 256 VGPRs).
+  atomicMax(status, 1 | STATUS_TIMEOUT);
 }
-__device__ __forceinline__ unsigned long long wait_t0() { return __builtin_amdgcn_s_memrealtime(); }
-__device__ __forceinline__ bool wait_expired(unsigned long long t0) {
-  return __builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS;
+// 32-bit: the low word of the 100 MHz counter wraps every 43 s, far above WAIT_TICKS; one register
+// fewer than the 64-bit value in the persistent loops' poll code (the long loop sits at 256 VGPRs)
+__device__ __forceinline__ unsigned wait_t0() { return (unsigned)__builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ bool wait_expired(unsigned t0) {
+  return (unsigned)__builtin_amdgcn_s_memrealtime() - t0 > (unsigned)WAIT_TICKS;
 }
 
 __device__ __forceinline__ UpdOut upd_math(const StepRec& r, int alg, float x, float e, bool have_x0,

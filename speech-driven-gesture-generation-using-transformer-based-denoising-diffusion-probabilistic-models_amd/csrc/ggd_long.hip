@@ -46,7 +46,7 @@ __device__ int lk_role(unsigned* ctl, int* status, int nwg, int G) {
   xcc &= 7;
   const int t = (int)lk_add(ctl + xcc * 16, 1u);
   __hip_atomic_fetch_add(ctl + LK_ARRIVE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long t_res = wait_t0();
+  const unsigned t_res = wait_t0();
   while (__hip_atomic_load(ctl + LK_ARRIVE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg) {
     if (wait_expired(t_res)) {
       atomicMax(status, 2);
@@ -77,7 +77,7 @@ __device__ __forceinline__ bool lk_sync(unsigned* flags, int part, unsigned epoc
     const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
     const int off = (threadIdx.x & 7) * 4;
     int ok = 1;
-    const unsigned long long t0 = wait_t0();
+    const unsigned t0 = wait_t0();
     for (int spin = 0;; ++spin) {
       const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
       if (__ballot(v < epoch) == 0) break;

@@ -31,7 +31,7 @@ static __device__ int mk_role(const MegaArgs& m, int nwg) {
   xcc &= 7;
   const int t = (int)mk_add(ctl + xcc * 16, 1u);
   mk_add(ctl + MK_ARRIVE, 1u);
-  const unsigned long long t0 = wait_t0();
+  const unsigned t0 = wait_t0();
   while (mk_load(ctl + MK_ARRIVE) < (unsigned)nwg) {  // every workgroup is resident
     if (wait_expired(t0)) {
       atomicMax(m.status, 2);
@@ -72,7 +72,7 @@ static __device__ int mk_role_xl(const MegaArgs& m, int nwg, int G) {
   xcc &= 7;
   const int t = (int)mk_add(ctl + xcc * 16, 1u);
   __hip_atomic_fetch_add(ctl + MK_ARRIVE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long t0 = wait_t0();
+  const unsigned t0 = wait_t0();
   while (__hip_atomic_load(ctl + MK_ARRIVE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg) {
     if (wait_expired(t0)) {
       atomicMax(m.status, 2);
@@ -125,7 +125,7 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
       const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
       const int off = (threadIdx.x & 7) * 4;
       int ok = 1;
-      const unsigned long long t0 = wait_t0();
+      const unsigned t0 = wait_t0();
       for (int spin = 0;; ++spin) {
         const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
         if (__ballot(v < epoch) == 0) break;
@@ -143,7 +143,7 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
     if (threadIdx.x == 0) {
       const unsigned target = 8u * epoch;
       int ok = 1;
-      const unsigned long long t0 = wait_t0();
+      const unsigned t0 = wait_t0();
       for (int spin = 0; mk_load(ctr) < target; ++spin) {
         if ((spin & 255) == 255 && (wait_expired(t0) || __hip_atomic_load(status, __ATOMIC_RELAXED,
                                                                          __HIP_MEMORY_SCOPE_AGENT))) {

@@ -227,7 +227,7 @@ __device__ int pp_role(const PersistArgs& a, int nwg, int P) {
   xcc &= 7;
   const int t = (int)__hip_atomic_fetch_add(ctl + xcc * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_add(ctl + PP_ARRIVE, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  const unsigned long long t_res = wait_t0();
+  const unsigned t_res = wait_t0();
   while (__hip_atomic_load(ctl + PP_ARRIVE, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg) {
     if (wait_expired(t_res)) {
       atomicMax(a.status, 2);
@@ -260,7 +260,7 @@ __device__ __forceinline__ bool pp_sync(unsigned* flags, int part, unsigned epoc
   }
   if (threadIdx.x < 64) {
     int ok = 1;
-    const unsigned long long t0 = wait_t0();
+    const unsigned t0 = wait_t0();
     for (int spin = 0;; ++spin) {
       const unsigned v = xl ? __builtin_amdgcn_raw_buffer_load_b32(r, (part ^ 1) * 4, 0, CP_COH)
                             : __hip_atomic_load(flags + (part ^ 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
