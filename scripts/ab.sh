@@ -12,7 +12,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   for lib in "$@"; do
     out=gpurun_out/${T}_${wl}_$(basename $lib .so)_$r.json
     GGD_LIB=$lib timeout -k 10 300 python -u bench.py --workload $wl --steps 3 --warmup 1 --no-cpu-baseline \
-      --no-f32-subrecord --no-subrecords > $out 2> ${out%.json}.err || { echo "FAILED $lib"; tail -5 ${out%.json}.err; exit 1; }
+      --no-f32-subrecord --no-subrecords ${BENCH_ARGS} > $out 2> ${out%.json}.err || { echo "FAILED $lib"; tail -5 ${out%.json}.err; exit 1; }
     python3 -c "import json; d=json.loads(open('$out').read().strip().splitlines()[-1]); r=d['roofline']; print('$wl', '$(basename $lib)', 'round $r', d['value'], 'frames/s', 'kernel_us', r['avg_launch_us'])"
   done
 done

@@ -29,7 +29,14 @@ namespace {
 
 using namespace chainlib;
 
-constexpr int LK_DEPTH = 3;  // weight tile groups in flight per wave (4 measured no faster: 186.8 vs 184.7 us per step)
+// weight tile groups in flight per wave.  Round 5, A/B on one box (profiles/r05y4_c4_depth_ab.txt,
+// r05y6_c4w_depth_ab.txt): 2 -> 156.1-157.0 ms per C4 launch, 3 -> 159.0-159.5, 4 -> 163.0 (fp8 MFMA
+// route; widened route 163.5-164.4 vs 164.7-165.7 at 3): the loop sits at the 256-VGPR limit, and
+// the 32 registers of the third group cost more than its prefetch distance buys (4 spills).
+#ifndef GGD_LK_DEPTH
+#define GGD_LK_DEPTH 2
+#endif
+constexpr int LK_DEPTH = GGD_LK_DEPTH;
 constexpr int LK_ARRIVE = 128, LK_FLAGS = 256;  // ctl: tickets [x * 16], arrivals, group flag lines [g * 32]
 
 __device__ __forceinline__ unsigned lk_add(unsigned* p, unsigned v) {
@@ -428,9 +435,9 @@ __device__ __forceinline__ void lk_chain(cla_T& a, cst_t sa, int b, int part, in
   x.part = part;
   x.it = it;
   lk_issue<W8, KIND, 0>(x);
-  if constexpr (GE::TOTAL > 1) lk_issue<W8, KIND, 1>(x);
+  if constexpr (LK_DEPTH > 2 && GE::TOTAL > 1) lk_issue<W8, KIND, 1>(x);
   if constexpr (LK_DEPTH > 3 && GE::TOTAL > 2) lk_issue<W8, KIND, 2>(x);
-  static_assert(LK_DEPTH <= 4, "the prologue issues LK_DEPTH - 1 iterations");
+  static_assert(LK_DEPTH >= 2 && LK_DEPTH <= 4, "the prologue issues LK_DEPTH - 1 iterations");
   // parameters (bias | scale per stage, LayerNorm vectors), the first stage's A rows
 #pragma unroll
   for (int si = 0; si < PL::NS; ++si) {
