@@ -49,8 +49,8 @@ def test_create_model_surface(pkg, beat_cfg, tedexp_cfg):
         pkg.create_model(123, dict(beat_cfg.Model.to_dict(), type="unet"))
     with pytest.raises(ValueError):   # the training path runs on the GPU only (no CPU fallback)
         pkg.create_model(123, beat_cfg.Model, is_training=True, device="cpu")
-    with pytest.raises(ValueError):   # and covers s2g_v2 + the one-way decoder
-        pkg.create_model(126, tedexp_cfg.Model, is_training=True, device="cuda")
+    with pytest.raises(ValueError):   # and rejects model types the reference does not have
+        pkg.create_model(123, dict(beat_cfg.Model.to_dict(), type="unet"), is_training=True, device="cuda")
 
 
 def test_load_state_dict_checks_names_and_shapes(pkg, beat_cfg):
