@@ -315,6 +315,12 @@ int ggd_enc_frontend(ggd_enc* enc, const float* wav, int32_t n, float* img, void
  * tests pin the stages' arithmetic against a numpy restatement of the same quantisation. */
 int ggd_mx_linear(int32_t M, int32_t N, int32_t K, const float* a, const uint8_t* w_e4m3, const float* wscale,
                   const float* bias, float* out, void* stream);
+/* Verification entry (not part of the reference surface): the long-clip loop's LayerNorm into the
+ * block-scaled fp8 A image of its MX stages (the same device function), on one block of 32 rows:
+ * rows (32, 256) device f32, gamma / beta (256) -> codes (32, 256) e4m3 bytes and scales (32, 8) e8m0
+ * bytes, one per 32 consecutive columns (2^(E - 7) for the block max 1.f 2^E).  Blocking. */
+int ggd_mx_layernorm(const float* rows, const float* gamma, const float* beta, uint8_t* codes, uint8_t* scales,
+                     void* stream);
 
 /* Library version string. */
 const char* ggd_version(void);

@@ -757,6 +757,30 @@ size_t lk_lds(int L, int Lk) {
   return std::max(m, LK_HS + lk_attn_lds(L, Lk));
 }
 
+// Verification kernel (ggd_mx_layernorm): lk_layernorm_mx -- the long loop's LayerNorm into the
+// block-scaled fp8 A image of its MX stages (LN2 / LN3 / LN1 before the Q, FFN-up and QKV
+// projections) -- on one 32-row block given as f32 rows, the fp8 rows and e8m0 scale bytes copied out
+// as the stage's MFMAs read them.  One workgroup of the loop's shape (8 waves).
+__global__ void __launch_bounds__(CH_NT) lk_ln_mx_probe_kernel(const float* __restrict__ rows, const float* __restrict__ gm,
+                                                            const float* __restrict__ bt, unsigned char* __restrict__ codes,
+                                                            unsigned char* __restrict__ scales) {
+  __shared__ __attribute__((aligned(16))) float hs[CH_MT * HS_STR];
+  __shared__ __attribute__((aligned(16))) unsigned char xs8[CH_MT * XS8_STR];
+  __shared__ unsigned char sc[CH_MT * (CH_D / 32)];
+  __shared__ float st[2 * CH_MT];
+  __shared__ __attribute__((aligned(16))) float prm[2 * CH_D];
+  for (int e = threadIdx.x; e < CH_MT * CH_D; e += CH_NT) hs[(e / CH_D) * HS_STR + e % CH_D] = rows[e];
+  for (int e = threadIdx.x; e < CH_D; e += CH_NT) {
+    prm[e] = gm[e];
+    prm[CH_D + e] = bt[e];
+  }
+  __syncthreads();
+  lk_layernorm_mx(hs, prm, prm + CH_D, xs8, sc, st);
+  __syncthreads();
+  for (int e = threadIdx.x; e < CH_MT * CH_D; e += CH_NT) codes[e] = xs8[(e / CH_D) * XS8_STR + e % CH_D];
+  for (int e = threadIdx.x; e < CH_MT * (CH_D / 32); e += CH_NT) scales[e] = sc[e];
+}
+
 }  // namespace
 
 bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C, int out_npad) {
@@ -810,3 +834,13 @@ hipError_t launch_long_loop(int w8, const LongArgs& a, int G, hipStream_t s) {
 }
 
 }  // namespace ggd
+
+extern "C" int ggd_mx_layernorm(const float* rows, const float* gamma, const float* beta, uint8_t* codes, uint8_t* scales,
+                                void* stream) {
+  if (!rows || !gamma || !beta || !codes || !scales) return -1;  // GGD_ERR_ARG
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(ggd::lk_ln_mx_probe_kernel, dim3(1), dim3(ggd::chainlib::CH_NT), 0, s, rows, gamma, beta, codes, scales);
+  hipError_t e = hipGetLastError();
+  const hipError_t e2 = hipStreamSynchronize(s);
+  return e == hipSuccess && e2 == hipSuccess ? 0 : -3;
+}

@@ -1,4 +1,7 @@
-"""Block-scaled fp8 (MX) MFMA arithmetic pinned value by value (ggd_mx_linear, include/ggd.h).
+"""Block-scaled fp8 (MX) MFMA arithmetic pinned value by value (ggd_mx_linear, ggd_mx_layernorm,
+include/ggd.h).  ggd_mx_layernorm runs the long loop's own LayerNorm-into-MX device function
+(lk_layernorm_mx: the block -> lane map, the 8-lane block max, the scale byte, the packing order);
+ggd_mx_linear the quantiser and the MFMA chunk of its MX stages.
 
 The long-clip loop's GGD_ROUTE_FP8_MFMA stages (csrc/ggd_long.hip over ggd_chainlib.h mx_scale_byte /
 mx_mul / mx_pack4 / ch_mma_mx) quantise activations to e4m3 with one e8m0 scale per 32 values and
@@ -87,3 +90,49 @@ def test_mx_quantisation_is_bit_exact(lib):
 def test_mx_linear_rejects_bad_shapes(lib):
     for M, N, K in ((32, 64, 128), (32, 60, 256), (0, 64, 256), (32, 64, 2048)):
         assert lib.ggd_mx_linear(M, N, K, 1, 1, 1, 1, 1, None) == -1
+
+
+def test_mx_layernorm_scales_exact_and_codes_within_rounding(lib):
+    """The long loop's LayerNorm into its MX A image (lk_layernorm_mx, ggd_mx_layernorm) against a
+    float64 restatement: LN (two-pass statistics, eps 1e-5, nn.py:141-147) then per (row, 32
+    columns) the block max -> e8m0 scale 2^(E - 7) and e4m3 codes of y / scale.  The kernel's f32
+    statistics differ from float64 in the last bits, so: every scale byte equal unless the block max
+    sits within 1e-5 of a power of two; every code equal unless y / scale sits within 1e-5 relative of
+    an e4m3 rounding boundary (then one code step apart) -- which pins the block -> lane map, the
+    scale choice and the packing order of the stage."""
+    g = th.Generator().manual_seed(5)
+    rows = th.randn(32, 256, generator=g) * th.exp2(th.randint(-6, 6, (32, 1), generator=g).float()) + \
+        th.randn(32, 1, generator=g) * 3.0
+    gamma = th.randn(256, generator=g) * th.exp2(th.randint(-3, 3, (256,), generator=g).float())
+    beta = th.randn(256, generator=g) * 0.5
+    codes = th.zeros(32, 256, dtype=th.uint8, device="cuda")
+    scales = th.zeros(32, 8, dtype=th.uint8, device="cuda")
+    rd, gd, bd = rows.cuda(), gamma.cuda(), beta.cuda()
+    assert lib.ggd_mx_layernorm(rd.data_ptr(), gd.data_ptr(), bd.data_ptr(), codes.data_ptr(), scales.data_ptr(),
+                                None) == 0
+    codes, scales = codes.cpu().numpy(), scales.cpu().numpy()
+    x = rows.double().numpy()
+    mu = x.mean(1, keepdims=True)
+    var = ((x - mu) ** 2).mean(1, keepdims=True)
+    y = (x - mu) / np.sqrt(var + 1e-5) * gamma.double().numpy() + beta.double().numpy()
+    yb = y.reshape(32, 8, 32)
+    m = np.abs(yb).max(-1)
+    e = np.floor(np.log2(m))
+    want_sb = np.clip(e + 127 - 7, 2, 253).astype(np.int64)
+    near_pow2 = np.abs(m / np.exp2(e) - 1.0) < 1e-5
+    bad_sb = (scales.astype(np.int64) != want_sb) & ~near_pow2
+    assert not bad_sb.any(), np.argwhere(bad_sb)[:5]
+    mul = np.exp2(127.0 - scales.astype(np.float64))[:, :, None]
+    v = (yb * mul).reshape(32, 256).astype(np.float32)
+    want = fp8.e4m3_encode(v)
+    got_val = fp8.e4m3_decode(codes).astype(np.float64)
+    want_val = fp8.e4m3_decode(want).astype(np.float64)
+    diff = codes != want
+    # a mismatch must be a rounding-boundary case: one e4m3 step apart and y / scale within 1e-5 of the midpoint
+    if diff.any():
+        step = np.abs(got_val - want_val)[diff]
+        mid = (np.abs(got_val) + np.abs(want_val))[diff] / 2
+        assert np.all(np.abs(np.abs(v.astype(np.float64)[diff]) - mid) <= 1e-5 * mid + 1e-12), \
+            (np.argwhere(diff)[:5], step[:5])
+    print(f"mx layernorm: {int(diff.sum())} of 8192 codes at a rounding boundary, scales exact")
+    assert diff.sum() <= 16
