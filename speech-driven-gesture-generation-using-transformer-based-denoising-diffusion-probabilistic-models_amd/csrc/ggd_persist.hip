@@ -18,6 +18,14 @@
 //           rows [step token(t); speech]) , attention -> O ; Hs += O Wo^T + b ; Xn = LN3(Hs);
 //           per 128-wide chunk: H = relu(Xn W1^T + b)^2, acc += H W2^T ; Hs += acc + b2
 //   out:    E = LN_out(Hs) W_out^T + b ; x = posterior update (Philox noise)  (nn.py:211-228)
+// No scheduling fence between a GEMM's k steps in this unit (ggd_fusedlib.h GGD_SCHED_FENCE; the
+// clip-group loop keeps it): the per-clip loops sit at 256 VGPRs, and letting the scheduler move the
+// next step's LDS reads across the MFMAs measured 7.15-7.17 ms per C5 launch against 7.46-7.60 with
+// the fence (profiles/r05w3_c5_fence_ab.txt; the clip-group loop is 1.6 % slower without it,
+// r05w3_c2_fence_ab.txt).  Same instructions, same results.
+#ifndef GGD_SCHED_FENCE
+#define GGD_SCHED_FENCE 0
+#endif
 #include "ggd_fusedlib.h"
 
 namespace ggd {
