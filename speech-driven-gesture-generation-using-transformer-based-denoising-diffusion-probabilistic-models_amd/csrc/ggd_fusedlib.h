@@ -292,9 +292,11 @@ struct WGemm {
   // fragments of k step k + 1 are read from LDS before the MFMAs of step k issue, so the LDS
   // latency overlaps the matrix work (one wave per SIMD hides nothing on its own).
   // zero = false: accumulate onto the caller's acc (e.g. residual + bias preloaded)
-  template <bool TR = false>
+  // FENCE: -1 the unit's SCHED_FENCE, 0 / 1 this call site's own choice
+  template <bool TR = false, int FENCE = -1>
   __device__ __forceinline__ void run(f32x4 (&acc)[RT][NJ], const T* A, int SA, int lane, int nj_on = NJ,
                                       bool zero = true) {
+    constexpr bool FEN = FENCE < 0 ? SCHED_FENCE : FENCE != 0;
     if (zero) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
@@ -315,7 +317,7 @@ struct WGemm {
         }
         // keep step k + 1's LDS reads ahead of step k's MFMAs: left alone, the scheduler (under
         // register pressure) sinks each read next to its MFMA and exposes the LDS latency per step
-        if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (FEN) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -328,7 +330,7 @@ struct WGemm {
                 acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[rt], __builtin_bit_cast(bf16x8, wb[j][k]),
                                                                      acc[rt][j], 0, 0, 0);
             }
-        if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (FEN) __builtin_amdgcn_sched_barrier(0);
         if (k + 1 < KT) {
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) cur[rt] = nxt[rt];

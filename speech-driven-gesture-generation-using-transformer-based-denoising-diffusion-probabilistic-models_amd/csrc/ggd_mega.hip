@@ -19,6 +19,14 @@
 // sizes the grid from the occupancy query, and all waits are bounded -- a barrier that times
 // out sets `status` and its workgroups leave, so a wrong assumption ends the launch instead
 // of hanging the GPU.
+//
+// GEMM k-step fences (ggd_phases.h GGD_MK_FENCE_*): kept everywhere except in KA's QKV tile, where
+// letting the scheduler move the next k step's LDS reads gives 73.5-73.7 ms per C2 launch against
+// 73.9-74.0 (one box, three alternations: profiles/r05w10_c2_fence_qkv_ab.txt); dropping it at the
+// cross-attention query costs 1 ms, at the out-projections / FFN 0.1-0.3 ms (r05w9_c2_fence_sites_ab.txt)
+#ifndef GGD_MK_FENCE_QKV
+#define GGD_MK_FENCE_QKV 0
+#endif
 #include "ggd_megasync.h"
 
 namespace ggd {

@@ -44,6 +44,26 @@
 #ifndef GGD_MK_CMAP
 #define GGD_MK_CMAP 1
 #endif
+// per-GEMM k-step fence (WGemm::run FENCE; -1: the unit's GGD_SCHED_FENCE): out-projections,
+// QKV, cross-attention query, FFN-up, FFN-down, output projection
+#ifndef GGD_MK_FENCE_OUT
+#define GGD_MK_FENCE_OUT -1
+#endif
+#ifndef GGD_MK_FENCE_QKV
+#define GGD_MK_FENCE_QKV -1
+#endif
+#ifndef GGD_MK_FENCE_Q
+#define GGD_MK_FENCE_Q -1
+#endif
+#ifndef GGD_MK_FENCE_FF1
+#define GGD_MK_FENCE_FF1 -1
+#endif
+#ifndef GGD_MK_FENCE_FF2
+#define GGD_MK_FENCE_FF2 -1
+#endif
+#ifndef GGD_MK_FENCE_EPS
+#define GGD_MK_FENCE_EPS -1
+#endif
 
 namespace ggd {
 
@@ -89,7 +109,7 @@ __device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGe
       acc[rt][j] = f32x4{h.x + bias[j].x, h.y + bias[j].y, h.z + bias[j].z, h.w + bias[j].w};
     }
   }
-  g.template run<true>(acc, A, SA, lane, NJ, false);
+  g.template run<true, GGD_MK_FENCE_OUT>(acc, A, SA, lane, NJ, false);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = (NJ * wave + j) * 16 + 4 * g4;
@@ -254,7 +274,7 @@ __device__ __forceinline__ void ka_phase(const FA& a, int h, int b, unsigned cha
   using AT = FAtt<T>;
   {
     f32x4 acc[RT][1];
-    gm.template run<true>(acc, Xn, Frag<T>::SX, lane, nq);
+    gm.template run<true, GGD_MK_FENCE_QKV>(acc, Xn, Frag<T>::SX, lane, nq);
     if (nq) {
       f32x4 v[RT];
 #pragma unroll
@@ -352,7 +372,7 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   if constexpr (!R::ON) kvs.store(att, tid);
   if (wave < 2) {  // the head's query, convolved over tokens in registers, into the Q image
     f32x4 acc[RT][1];
-    gq.template run<true>(acc, Ax, Frag<T>::SX, lane);
+    gq.template run<true, GGD_MK_FENCE_Q>(acc, Ax, Frag<T>::SX, lane);
     f32x4 v[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
@@ -428,7 +448,7 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   T* Hc = (T*)(pv + PL::IMG + PL::ST);
   {
     f32x4 acc[RT][1];
-    gf.template run<true>(acc, Ax, Frag<T>::SX, lane);
+    gf.template run<true, GGD_MK_FENCE_FF1>(acc, Ax, Frag<T>::SX, lane);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const float v0 = fmaxf(acc[rt][0][0] + bf.x, 0.f), v1 = fmaxf(acc[rt][0][1] + bf.y, 0.f);
@@ -440,7 +460,7 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   STAMP(4);
   {
     f32x4 acc[RT][2];
-    gd.template run<true>(acc, Hc, SHC, lane);
+    gd.template run<true, GGD_MK_FENCE_FF2>(acc, Hc, SHC, lane);
     const OutRowsP<CP> out((T*)a.ffp + ((size_t)b * 8 + c) * L * FD, (uint32_t)(sizeof(T) * L * FD));
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -840,7 +860,7 @@ __device__ __forceinline__ void ker_phase(const FA& a, int p, int b, int k, unsi
   STAMP(1);
   if (16 * wave < C) {
     f32x4 acc[1][1];
-    go.template run<true>(acc, Xn, Frag<T>::SX, lane);
+    go.template run<true, GGD_MK_FENCE_EPS>(acc, Xn, Frag<T>::SX, lane);
     *(float4*)(E + c16 * SE + 16 * wave + 4 * g4) =
         make_float4(acc[0][0][0] + bo.x, acc[0][0][1] + bo.y, acc[0][0][2] + bo.z, acc[0][0][3] + bo.w);
   }
