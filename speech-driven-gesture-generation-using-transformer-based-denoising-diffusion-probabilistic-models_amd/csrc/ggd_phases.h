@@ -45,7 +45,7 @@
 #define GGD_MK_CMAP 1
 #endif
 // per-GEMM k-step fence (WGemm::run FENCE; -1: the unit's GGD_SCHED_FENCE): out-projections,
-// QKV, cross-attention query, FFN-up, FFN-down, output projection
+// QKV, cross-attention query, FFN-up, FFN-down, output projection, emb_x of the updated rows
 #ifndef GGD_MK_FENCE_OUT
 #define GGD_MK_FENCE_OUT -1
 #endif
@@ -63,6 +63,9 @@
 #endif
 #ifndef GGD_MK_FENCE_EPS
 #define GGD_MK_FENCE_EPS -1
+#endif
+#ifndef GGD_MK_FENCE_EMB
+#define GGD_MK_FENCE_EMB -1
 #endif
 
 namespace ggd {
@@ -670,7 +673,7 @@ __device__ __forceinline__ void emb_rows_store(const FA& a, int b, int r0, int R
   f32x4 acc[1][2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) acc[0][j] = f32x4{pe[j].x, pe[j].y, pe[j].z, pe[j].w};
-  ge.template run<true>(acc, Xb, KerPlan<T>::SB, lane, 2, false);
+  ge.template run<true, GGD_MK_FENCE_EMB>(acc, Xb, KerPlan<T>::SB, lane, 2, false);
   const OutRowsP<CP> ho(a.h + ((size_t)b * a.L + r0) * FD, (uint32_t)(sizeof(float) * R * FD));  // rows >= R dropped
 #pragma unroll
   for (int j = 0; j < 2; ++j)
