@@ -83,9 +83,10 @@ __device__ __forceinline__ void pload(uint4 (&f)[N], const void* W, int kt_total
 // so the LDS latency runs under the matrix work instead of between every MFMA.
 // TR: computed transposed (the weight fragments as the MFMA A operand), so lane (c16, g4) of tile
 // (rt, j) holds row 16 rt + c16, columns 16 j' + 4 g4 .. + 3 (four consecutive channels of one token)
-template <int RT, int NJ, int KS, int N, bool TR = false>
+template <int RT, int NJ, int KS, int N, bool TR = false, int FENCE = -1>  // FENCE -1: the unit's SCHED_FENCE
 __device__ __forceinline__ void pmma_n(f32x4 (&acc)[RT][NJ], const bf16_t* A, int SA, int kc0, const uint4 (&f)[N],
                                        int nj, int lane) {
+  constexpr bool FEN = FENCE < 0 ? SCHED_FENCE : FENCE != 0;
   const int r16 = lane & 15, g = lane >> 4;
   const bf16_t* a0 = A + r16 * SA + kc0 * 32 + g * 8;
   bf16x8 cur[RT], nxt[RT];
@@ -97,7 +98,7 @@ __device__ __forceinline__ void pmma_n(f32x4 (&acc)[RT][NJ], const bf16_t* A, in
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) nxt[rt] = *(const bf16x8*)(a0 + rt * 16 * SA + (s + 1) * 32);
     }
-    if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);  // reads of s + 1 stay ahead (WGemm::run)
+    if constexpr (FEN) __builtin_amdgcn_sched_barrier(0);  // reads of s + 1 stay ahead (WGemm::run)
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -110,7 +111,7 @@ __device__ __forceinline__ void pmma_n(f32x4 (&acc)[RT][NJ], const bf16_t* A, in
             acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[rt], __builtin_bit_cast(bf16x8, f[j * KS + s]),
                                                                  acc[rt][j], 0, 0, 0);
         }
-    if constexpr (SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (FEN) __builtin_amdgcn_sched_barrier(0);
     if (s + 1 < KS) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) cur[rt] = nxt[rt];
@@ -118,10 +119,10 @@ __device__ __forceinline__ void pmma_n(f32x4 (&acc)[RT][NJ], const bf16_t* A, in
   }
 }
 
-template <int RT, int NJ, int KS, int N, bool TR = false>
+template <int RT, int NJ, int KS, int N, bool TR = false, int FENCE = -1>
 __device__ __forceinline__ void pmma(f32x4 (&acc)[RT][NJ], const bf16_t* A, int SA, int kc0, const uint4 (&f)[N],
                                      int lane) {
-  pmma_n<RT, NJ, KS, N, TR>(acc, A, SA, kc0, f, NJ, lane);
+  pmma_n<RT, NJ, KS, N, TR, FENCE>(acc, A, SA, kc0, f, NJ, lane);
 }
 
 // residual epilogue of a transposed (TR) tile pair: lane (c16, g4) of tile (rt, j) holds row
@@ -202,6 +203,33 @@ __device__ __forceinline__ void fattn_lds(unsigned char* att, int Lq, int Lk, fl
 // attention outputs and both running the full out-projection (0)
 #ifndef GGD_PSK_SPLITO
 #define GGD_PSK_SPLITO 1
+#endif
+// per-GEMM k-step fence of the transposed pair / clip route (pmma FENCE; -1: the unit's
+// GGD_SCHED_FENCE): emb_x, QKV, SA out-projection, CA query, CA out-projection, FFN-up, FFN-down,
+// output projection
+#ifndef GGD_PSK_FENCE_EMB
+#define GGD_PSK_FENCE_EMB -1
+#endif
+#ifndef GGD_PSK_FENCE_QKV
+#define GGD_PSK_FENCE_QKV -1
+#endif
+#ifndef GGD_PSK_FENCE_OSA
+#define GGD_PSK_FENCE_OSA -1
+#endif
+#ifndef GGD_PSK_FENCE_Q
+#define GGD_PSK_FENCE_Q -1
+#endif
+#ifndef GGD_PSK_FENCE_OCA
+#define GGD_PSK_FENCE_OCA -1
+#endif
+#ifndef GGD_PSK_FENCE_FF1
+#define GGD_PSK_FENCE_FF1 -1
+#endif
+#ifndef GGD_PSK_FENCE_FF2
+#define GGD_PSK_FENCE_FF2 -1
+#endif
+#ifndef GGD_PSK_FENCE_OUT  // fenced: 7.14 vs 7.20 ms per C5 launch, mean of five alternations on two
+#define GGD_PSK_FENCE_OUT 1  // boxes (profiles/r05w14_c5_fence_sites_ab.txt, r05w15_c5_fence_out_ab.txt)
 #endif
 
 constexpr int PK_THREADS = 512;  // 8 waves: two per SIMD, so one wave's LDS / L2 waits overlap the other's MFMAs
@@ -509,7 +537,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
       bar_lds();
       f32x4 acc[RT][2];
       zero_acc(acc);
-      pmma<RT, 2, 4>(acc, Xb, SHD, 0, fb, lane);
+      pmma<RT, 2, 4, 8, false, GGD_PSK_FENCE_EMB>(acc, Xb, SHD, 0, fb, lane);
       {  // fb <- layer 0's first FFN-down chunk
         const int td[2] = {2 * wave, 2 * wave + 1};
         pload<2, 4>(fb, a.layers[0].ff2, 32, td, 4 * c0f, lane);
@@ -547,7 +575,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         {
           f32x4 acc[RT][2];
           zero_acc(acc);
-          pmma_n<RT, 2, 8, 16, true>(acc, Xn, SX, 0, fa, nq, lane);
+          pmma_n<RT, 2, 8, 16, true, GGD_PSK_FENCE_QKV>(acc, Xn, SX, 0, fa, nq, lane);
           if (hi < HP - 1) {  // refill: the next head pair, or the SA out-projection
             const int tq[2] = {12 * (hp + 1) + tq0, 12 * (hp + 1) + tq1};
             if (nq == 2) pload<2, 8>(fa, w.qkv, 8, tq, 0, lane);
@@ -646,7 +674,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         const float4 bo4[2] = {ld_f4(w.o_sa_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.o_sa_b + (2 * wave + 1) * 16 + 4 * g4)};
         f32x4 acc[RT][2];
         zero_acc(acc);
-        if constexpr (SPLITO) pmma<RT, 2, 4, 16, true>(acc, Ob, SX, 4 * part, fa, lane);  // its own heads' columns
+        if constexpr (SPLITO) pmma<RT, 2, 4, 16, true, GGD_PSK_FENCE_OSA>(acc, Ob, SX, 4 * part, fa, lane);  // its own heads' columns
         else pmma<RT, 2, 8, 16, true>(acc, Ob, SX, 0, fa, lane);
         if constexpr (PAIR) {  // fa <- cross-attn Q of this part's heads: wave w owns column tile 8 part + w
           const int tq[1] = {8 * part + wave};
@@ -716,7 +744,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         // which the attention reads in place (no conv pass per head pair)
         f32x4 acc[RT][NQJ];
         zero_acc(acc);
-        pmma<RT, NQJ, 8, 16, true>(acc, Xn, SX, 0, fa, lane);
+        pmma<RT, NQJ, 8, 16, true, GGD_PSK_FENCE_Q>(acc, Xn, SX, 0, fa, lane);
         {  // fa <- the CA out-projection
           const int to[2] = {2 * wave, 2 * wave + 1};
           if constexpr (SPLITO) pload<2, 4>(fa, w.o_ca, 8, to, 4 * part, lane);
@@ -797,7 +825,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         const float4 bo4[2] = {ld_f4(w.o_ca_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.o_ca_b + (2 * wave + 1) * 16 + 4 * g4)};
         f32x4 acc[RT][2];
         zero_acc(acc);
-        if constexpr (SPLITO) pmma<RT, 2, 4, 16, true>(acc, Ob, SX, 4 * part, fa, lane);
+        if constexpr (SPLITO) pmma<RT, 2, 4, 16, true, GGD_PSK_FENCE_OCA>(acc, Ob, SX, 4 * part, fa, lane);
         else pmma<RT, 2, 8, 16, true>(acc, Ob, SX, 0, fa, lane);
         {  // fa <- FFN-up chunk c0f (fb already holds FFN-down chunk c0f)
           const int tf[1] = {8 * c0f + wave};
@@ -851,7 +879,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           const float4 bf4 = ld_f4(w.ff1_b + (8 * c + wave) * 16 + 4 * g4);
           f32x4 acc[RT][1];
           zero_acc(acc);
-          pmma<RT, 1, 8, 16, true>(acc, Xn, SX, 0, fa, lane);
+          pmma<RT, 1, 8, 16, true, GGD_PSK_FENCE_FF1>(acc, Xn, SX, 0, fa, lane);
 #else
           const float bf = w.ff1_b[(8 * c + wave) * 16 + c16];
           f32x4 acc[RT][1];
@@ -882,7 +910,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
             }
           }
           bar_lds();
-          pmma<RT, 2, 4, 8, true>(accd, Hc, SHD, 0, fb, lane);
+          pmma<RT, 2, 4, 8, true, GGD_PSK_FENCE_FF2>(accd, Hc, SHD, 0, fb, lane);
 #else
           {
             const int col = (8 * c + wave) * 16 + c16 - 128 * c;  // column inside the chunk
@@ -943,7 +971,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
       const float bo = a.b_out[wave * 16 + c16];
       f32x4 acc[RT][1];
       zero_acc(acc);
-      pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
+      pmma<RT, 1, 8, 16, false, GGD_PSK_FENCE_OUT>(acc, Xn, SX, 0, fa, lane);
       {  // fa <- layer 0's first QKV pair (next step)
         const int tq[2] = {qoff + tq0, qoff + tq1};
         if (nq == 2) pload<2, 8>(fa, a.layers[0].qkv, 8, tq, 0, lane);
