@@ -324,8 +324,9 @@ def f32_subrecord(pkg, cfg, sd, d_pose, L, B, wav, loop_name, diffusion, dev, T,
 def workload_subrecord(pkg, workload, dev, passes):
     """One more BASELINE config under the same driver run: a warm-up pass, then ``passes`` timed
     sampling passes (encoder + every denoise step, inputs resident in HBM) of WORKLOADS[workload] on
-    this GPU, the last one profiled: frames/s, ms per pass, the dominant loop's hipEvent time and
-    its fraction of the MFMA peak its arithmetic runs on (SURVEY.md 8d FLOPs).  No CPU leg."""
+    this GPU, none of them profiled, then one profiled pass outside the timed window: frames/s and
+    ms per pass from the unprofiled passes, the dominant loop's hipEvent time from the profiled one
+    and its fraction of the MFMA peak its arithmetic runs on (SURVEY.md 8d FLOPs).  No CPU leg."""
     import ctypes
     w = WORKLOADS[workload]
     cfg = pkg.load_config(os.path.join(ROOT, "configs", "beat-ours.json"))
@@ -341,7 +342,7 @@ def workload_subrecord(pkg, workload, dev, passes):
     T = diffusion.num_timesteps
     loop = diffusion.p_sample_loop if w["alg"] == "ddpm" else diffusion.ddim_sample_loop
     g = th.Generator(device=dev).manual_seed(4321)
-    wavs = [th.randn(B, wav_len, device=dev, generator=g) * 0.1 for _ in range(passes + 1)]
+    wavs = [th.randn(B, wav_len, device=dev, generator=g) * 0.1 for _ in range(passes + 2)]
     run = lambda wav, seed: loop(model, (B, d_pose, L), model_kwargs={"wav": wav}, seed=seed, extras=False)["sample"]
     run(wavs[0], 1)
     th.cuda.synchronize(dev)
@@ -351,12 +352,15 @@ def workload_subrecord(pkg, workload, dev, passes):
         assert ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0) == 0
     t0 = time.perf_counter()
     for k in range(passes):
-        if k == passes - 1:
-            ctx.lib.ggd_set_profiling(ctx.h, 1)
         out = run(wavs[k + 1], 10 + k)
     th.cuda.synchronize(dev)
     model.sync()
     el = time.perf_counter() - t0
+    assert out.shape == (B, d_pose, L) and bool(th.isfinite(out).all())
+    ctx.lib.ggd_set_profiling(ctx.h, 1)   # the profiled pass: after the clock stopped
+    out = run(wavs[passes + 1], 10 + passes)
+    th.cuda.synchronize(dev)
+    model.sync()
     ctx.lib.ggd_set_profiling(ctx.h, 0)
     avg, cnt = ctypes.c_double(), ctypes.c_int64()
     rc = ctx.lib.ggd_kernel_time(ctx.h, 0, ctypes.byref(avg), ctypes.byref(cnt))
@@ -370,7 +374,8 @@ def workload_subrecord(pkg, workload, dev, passes):
     rec = {"workload": f"{w['label']}: {B} clips x L={L}, wav {wav_len}, {w['alg'].upper()} T'={T}, "
                        + ("fp8 MFMA (e4m3 step weights, block-scaled e4m3 activations)" if mx else "bf16"),
            "value": round(passes * B * L / el, 2), "unit": "frames/s", "ms_per_step": round(el / passes * 1e3, 3),
-           "steps": passes, "warmup": 1, "dtype": "fp8" if mx else dtype}
+           "steps": passes, "warmup": 1, "dtype": "fp8" if mx else dtype,
+           "timing": f"{passes} unprofiled timed passes; the kernel time from one more, profiled pass outside them"}
     if rc == 0 and cnt.value > 0 and avg.value > 0 and kind in names:
         flop = clip_step * B * T / (cnt.value if kind in (1, 5) else 1)
         ach = flop / (avg.value * 1e-6) / 1e12
@@ -387,6 +392,9 @@ def rehearse(args, rank, world):
 
     Same launch, barrier + max-over-ranks timing and all-gather as a GPU run; 2 clips per rank,
     2 DDPM steps of the beat-ours architecture (bounded weight init), noise keyed by global clip id.
+    ``--workload c5``: the C5 shape (``--batch-per-gpu`` clips per rank, 128 by default: B = 1024 at
+    8 ranks) through the same shard / all-gather path, the sampler replaced by each clip's x_T draw
+    (keyed by global clip id) plus its wav's mean -- the plumbing at full payload, no model.
     """
     import numpy as np
     import torch.distributed as dist
@@ -403,11 +411,16 @@ def rehearse(args, rank, world):
     om = ref_denoiser.OracleModel(sd, {k: arch[k] for k in ("type", "d_model", "decoder", "heads", "n_layers")},
                                   cache_speech=True)
     sch = ref_diffusion.make_schedule("linear", 1000, "")
-    B, L, n_steps = 2, 40, 2
+    full = args.workload == "c5"
+    B, L, n_steps = (args.batch_per_gpu if full else 2), 40, 2
     n_total = B * world
     wav_all = th.randn(n_total, 32000, generator=th.Generator().manual_seed(1234)) * 0.1
 
     def fn(wav_local, offset):  # one clip at a time: a clip's result does not depend on its shard
+        if full:
+            ids = np.arange(offset, offset + wav_local.shape[0])
+            x_T = ref_diffusion.PhiloxNoise(7, ids).initial((len(ids), 123, L))
+            return x_T + wav_local.mean(dim=1)[:, None, None]
         outs = []
         for j in range(wav_local.shape[0]):
             noise = ref_diffusion.PhiloxNoise(7, np.array([offset + j]))
@@ -448,6 +461,7 @@ def distributed_record(dist, args, stats, gather_ms, kernel_us, device):
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return {"backend": dist.get_backend() + (" (RCCL)" if dist.get_backend() == "nccl" else ""),
             "world_size": world, "all_gather_bytes": stats.get("gather_bytes"),
+            "all_gather_bytes_per_rank": stats.get("gather_bytes_per_rank"),
             "all_gather_ms_max_over_ranks": round(float(t[0]), 4),
             "kernel_avg_launch_us_max_over_ranks": round(float(t[1]), 3) if kernel_us else None,
             "timing": "hipEvent pair on the sampling stream around all_gather_into_tensor (includes the wait "

@@ -205,7 +205,9 @@ enum {
                                         step on launches (chains + whole-clip attention) */
   GGD_ROUTE_SIMULATE_UNRESIDENT = 8, /* test hook, 1: the clip-group and clip-pair loops report status 2
                                         ("workgroups never all resident") without running, so the
-                                        device-gated one-workgroup-per-clip fallback runs the clips */
+                                        device-gated one-workgroup-per-clip fallback runs the clips;
+                                        2: only the odd parts report 2, the others wait in their first
+                                        barrier and must drain without hiding that 2 */
   GGD_ROUTE_FP8_MFMA = 9,            /* GGD_FP8W long-clip loop: 0 the FFN and LayerNorm-projection GEMMs
                                         on block-scaled fp8 MFMA (e4m3 activations, one e8m0 scale per
                                         32 values), 1 the e4m3 weights widened into bf16 MFMAs (the
@@ -321,6 +323,16 @@ int ggd_mx_linear(int32_t M, int32_t N, int32_t K, const float* a, const uint8_t
  * bytes, one per 32 consecutive columns (2^(E - 7) for the block max 1.f 2^E).  Blocking. */
 int ggd_mx_layernorm(const float* rows, const float* gamma, const float* beta, uint8_t* codes, uint8_t* scales,
                      void* stream);
+/* Verification entry (not part of the reference surface): the long-clip loop's FFN-up stage on
+ * block-scaled fp8 MFMA (the same device functions: the transposed MFMA chunk and the ReLU^2 epilogue
+ * that quantises the hidden rows), on one block of 32 rows: a_codes (32, 256) e4m3 bytes with
+ * a_scales (32, 8) e8m0 bytes (one per 32 consecutive k), w_e4m3 (1024, 256) e4m3fn codes with
+ * per-output-channel wscale (1024) and bias (1024), all device memory -> h_codes (32, 1024) e4m3
+ * bytes of relu(a . w^T * wscale + bias)^2 / scale and h_scales (32, 32) e8m0 bytes, one per 32
+ * consecutive hidden columns (2^(E - 7) for the block max 1.f 2^E).  Blocking.
+ * Reference: models/modules/transformer.py:8-16 (SquaredReLU), :151-154 (FFN). */
+int ggd_mx_ffn_up(const uint8_t* a_codes, const uint8_t* a_scales, const uint8_t* w_e4m3, const float* wscale,
+                  const float* bias, uint8_t* h_codes, uint8_t* h_scales, void* stream);
 
 /* Library version string. */
 const char* ggd_version(void);

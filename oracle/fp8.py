@@ -147,3 +147,39 @@ class mx_activations:
         from oracle import ref_denoiser
         ref_denoiser.ACT_QUANT = self._prev
         return False
+
+
+def mx_scale_bytes(m):
+    """e8m0 scale bytes of blocks whose max |v| is ``m`` (float32 array): the biased exponent of m
+    minus 7, clamped to [2, 253] (csrc/ggd_chainlib.h mx_scale_byte)."""
+    be = (np.asarray(m, np.float32).view(np.int32) >> 23) & 0xFF
+    return np.clip(be - 7, 2, 253).astype(np.uint8)
+
+
+def mx_quantise_blocks(y, block_cols=32):
+    """float32 rows (R, N) -> (e4m3 codes (R, N), e8m0 scale bytes (R, N / block_cols)), one scale per
+    ``block_cols`` consecutive columns of a row (32: the MX block), values divided by the exact power
+    of two 2^(sb - 127) in float32 and rounded to nearest even."""
+    y = np.asarray(y, np.float32)
+    R, N = y.shape
+    yb = y.reshape(R, N // block_cols, block_cols)
+    sb = mx_scale_bytes(np.abs(yb).max(-1))
+    mul = ((254 - sb.astype(np.int32)) << 23).view(np.float32)[:, :, None]
+    return e4m3_encode((yb * mul).reshape(R, N)), sb
+
+
+def mx_ffn_up(a_codes, a_scales, w_codes, wscale, bias, square=True, block_cols=32):
+    """The long loop's FFN-up stage on block-scaled fp8 (csrc/ggd_long.hip lk_relu2_mx after
+    ch_mma_mx<2, true>): h = relu(a . w^T * wscale + bias)^2 (models/modules/transformer.py:8-16
+    SquaredReLU, :151-154 FFN.layer1) from the MX A image (codes (R, K) with one e8m0 scale per 32 k)
+    and per-output-channel e4m3 weights, then re-quantised per 32 hidden columns.  The product is
+    summed in float64 (the tests pick operands whose sums are exact); the epilogue in float32, as the
+    kernel.  Returns (codes (R, N), scales (R, N / 32)).  ``square`` / ``block_cols``: deliberately
+    wrong variants for the tests' sensitivity checks."""
+    a = e4m3_decode(a_codes).astype(np.float64)
+    R, K = a.shape
+    a = (a.reshape(R, K // 32, 32) * np.exp2(np.asarray(a_scales, np.float64) - 127.0)[:, :, None]).reshape(R, K)
+    acc = (a @ e4m3_decode(w_codes).astype(np.float64).T).astype(np.float32)
+    v = np.maximum(acc * np.asarray(wscale, np.float32) + np.asarray(bias, np.float32), np.float32(0.0))
+    y = (v * v if square else v).astype(np.float32)
+    return mx_quantise_blocks(y, block_cols)

@@ -206,7 +206,7 @@ struct ggd_ctx {
   std::string sticky_msg;
   bool mega_none_ran = false;          // settled clip-group check: every chunk reported 2 (nothing ran)
   int gated_ran = 0;                   // settled check: chunks the device-gated fallback loop ran instead
-  bool sim_unresident = false;         // GGD_ROUTE_SIMULATE_UNRESIDENT
+  int sim_unresident = 0;              // GGD_ROUTE_SIMULATE_UNRESIDENT
 
   // Per-call uploads (step records, the loop's argument blocks): from pageable memory a small
   // hipMemcpyAsync is staged by the runtime in pieces (several blit kernels and host waits per
@@ -1771,8 +1771,9 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
     case GGD_ROUTE_FP8_MFMA:        // 1: the long loop's e4m3 weights widened into bf16 MFMAs
       c->fp8_mfma_off = value != 0;
       return GGD_OK;
-    case GGD_ROUTE_SIMULATE_UNRESIDENT:  // test hook: co-resident loops report status 2, run nothing
-      c->sim_unresident = value != 0;
+    case GGD_ROUTE_SIMULATE_UNRESIDENT:  // test hook: 1 co-resident loops report status 2, run nothing;
+      if (value < 0 || value > 2) break;  // 2 only odd parts do, the rest wait in a barrier
+      c->sim_unresident = value;
       return GGD_OK;
     case GGD_ROUTE_MEGA_ROWS:       // 1: the row-block clip-group loop (bf16)
       c->mega_rows = value != 0;
@@ -2396,11 +2397,11 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
   };
   for (int c0 = 0, ci = 0; c0 < a.n; c0 += cap, ++ci) {
     MegaArgs m{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + ci,
-               c0 == 0 ? c->mega_stamps : nullptr, c0, c->mega_place == 1 ? 1 : 0, nullptr, c->sim_unresident ? 1 : 0};
+               c0 == 0 ? c->mega_stamps : nullptr, c0, c->mega_place == 1 ? 1 : 0, nullptr, c->sim_unresident};
     HIP_TRY(c, launch(m, std::min(cap, a.n - c0), xl));
     if (xl) {  // the write-through re-run of this chunk, live only if the launch above reported 3
       MegaArgs g{c->mega_fa, c->mega_fe, NL, 0, nsteps, c->mega_ctl, c->mega_status + MEGA_MAX_CHUNKS + ci,
-                 nullptr, c0, 0, c->mega_status + ci, c->sim_unresident ? 1 : 0};
+                 nullptr, c0, 0, c->mega_status + ci, c->sim_unresident};
       HIP_TRY(c, launch(g, std::min(cap, a.n - c0), false));
     }
   }
@@ -2500,7 +2501,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
       p.status = c->pair_status;
       p.xbuf = c->pair_xbuf;
       p.force_coh = c->pair_force_coh;
-      p.sim_unresident = c->sim_unresident ? 1 : 0;
+      p.sim_unresident = c->sim_unresident;
       HIP_TRY(c, hipMemsetAsync(c->pair_status, 0, sizeof(int), s));
     }
     if (c->profiling) {

@@ -96,12 +96,14 @@ struct UpdOut { float x0, raw, mean, xn; };
 // residency wait comes near the bound; a loop that reaches it sets its status word and leaves.
 // ---------------------------------------------------------------------------
 constexpr unsigned long long WAIT_TICKS = 200000000ull;  // 2 s at 100 MHz
-// a timed-out barrier: code 1 and the STATUS_TIMEOUT bit (ggd_kernels.h)
-__device__ __forceinline__ void status_timeout(int* status) {
-  // one atomic: the bit dominates any code (every gate tests for an exact code, so a timed-out
-  // launch opens none; the host counts the bit and reports the timeout).  A second atomic here cost
-  // the long-clip loop a register spill (it sits at 256 VGPRs).
-  atomicMax(status, 1 | STATUS_TIMEOUT);
+// a wave leaving a barrier wait early.  `expired`: its OWN wait ran out -- code 1 and the
+// STATUS_TIMEOUT bit (ggd_kernels.h; the bit dominates any code, so a timed-out launch opens no
+// gate and the host reports the timeout).  Otherwise it only saw another workgroup's code (e.g. 2:
+// a workgroup whose residency wait expired) and drains with code 1, which keeps that 2 / 3 intact
+// so the device-gated fallback still opens.  One atomic either way (a second one cost the long-clip
+// loop a register spill: it sits at 256 VGPRs).
+__device__ __forceinline__ void status_leave(int* status, bool expired) {
+  atomicMax(status, expired ? (1 | STATUS_TIMEOUT) : 1);
 }
 // 32-bit: the low word of the 100 MHz counter wraps every 43 s, far above WAIT_TICKS; one register
 // fewer than the 64-bit value in the persistent loops' poll code (the long loop sits at 256 VGPRs)

@@ -196,7 +196,7 @@ struct PersistArgs {
   // and gate[MEGA_MAX_CHUNKS] its gated write-through re-run's (used when gate[0] == 3)
   const int* gate;
   int gate_xl;
-  int sim_unresident;          // test hook (GGD_ROUTE_SIMULATE_UNRESIDENT): the clip-pair loop reports 2, runs nothing
+  int sim_unresident;          // test hook (GGD_ROUTE_SIMULATE_UNRESIDENT): 1 the clip-pair loop reports 2, runs nothing; 2 part 1 reports 2
 };
 constexpr int PAIR_MAX = 128;                              // clip pairs per launch (ctl words)
 constexpr int PAIR_CTL_WORDS = 256 + PAIR_MAX * 32;        // tickets / arrival, one flag line per pair
@@ -220,7 +220,7 @@ struct MegaArgs {
   const int* gate;       // non-null: the launch runs only if *gate == 3 (the XCD-local launch of the same
                          // chunk could not place its clip groups) -- the write-through re-run, decided on
                          // the device so the host never waits for the first launch's status
-  int sim_unresident;    // test hook (GGD_ROUTE_SIMULATE_UNRESIDENT): report status 2 and run nothing
+  int sim_unresident;    // test hook (GGD_ROUTE_SIMULATE_UNRESIDENT): 1 report status 2 and run nothing; 2 odd parts do
 };
 // A persistent loop's barrier that timed out ORs this bit into the loop's status word beside its
 // code 1: codes of other workgroups (2 not resident, 3 not placeable) are merged by atomicMax and

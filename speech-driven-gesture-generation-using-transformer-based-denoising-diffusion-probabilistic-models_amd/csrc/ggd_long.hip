@@ -88,11 +88,13 @@ __device__ __forceinline__ bool lk_sync(unsigned* flags, int part, unsigned epoc
     for (int spin = 0;; ++spin) {
       const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
       if (__ballot(v < epoch) == 0) break;
-      if ((spin & 255) == 255 &&
-          (wait_expired(t0) || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        if (threadIdx.x == 0) status_timeout(status);
-        ok = 0;
-        break;
+      if ((spin & 255) == 255) {
+        const bool expired = wait_expired(t0);
+        if (expired || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          if (threadIdx.x == 0) status_leave(status, expired);
+          ok = 0;
+          break;
+        }
       }
       __builtin_amdgcn_s_sleep(1);
     }
@@ -303,6 +305,37 @@ static_assert(LK_XSC >= sizeof(float) * CH_MT * EPS_STR, "eps rows (out_layers) 
 #ifndef GGD_LK_MX_R
 #define GGD_LK_MX_R 0
 #endif
+// The FFN-up stage's epilogue on the MX route: ReLU^2 of the transposed accumulators into the
+// block-scaled fp8 hidden image.  Lane (c16, g4) holds row 16 i + c16, columns 16 (nt0 + j) + 4 g4
+// .. + 3; a 32-column block is the lane's two tiles x the 4 lane rows of its row (permlane swaps,
+// lanerow_max4), one 4-byte store per (row, tile), the block's scale byte by the g4 = 0 lane.
+// pp: the stage's LDS parameters [bias[NP] | scale[NP]]; hh8: [32][HH8_STR] e4m3 rows, their e8m0
+// scales [32][CH_FF / 32] at LK_HSC.  Also run on its own by ggd_mx_ffn_up (the verification entry).
+template <int NP>
+__device__ __forceinline__ void lk_relu2_mx(const f32x4 (&acc)[2][2], const float* pp, int nt0, int c16, int g4,
+                                            unsigned char* hh8) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = i * 16 + c16;
+    float y[2][4], m = 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = fmaxf(ch_val<true>(pp, NP, acc[i][j][r], (nt0 + j) * 16 + 4 * g4 + r), 0.f);
+        y[j][r] = v * v;
+        m = fmaxf(m, y[j][r]);
+      }
+    const unsigned sb = mx_scale_byte(lanerow_max4(m));
+    const float mul = mx_mul(sb);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      *(unsigned*)(hh8 + row * HH8_STR + (nt0 + j) * 16 + 4 * g4) =
+          mx_pack4(y[j][0] * mul, y[j][1] * mul, y[j][2] * mul, y[j][3] * mul);
+    if (g4 == 0) hh8[LK_HSC + row * (CH_FF / 32) + nt0 / 2] = (unsigned char)sb;
+  }
+}
+
 template <int KIND, int si, bool MX>
 constexpr bool lk_mx() {
   constexpr int k = LkPlan<KIND>::s[si].kind;
@@ -355,33 +388,8 @@ __device__ __forceinline__ void lk_iter(X& x) {
     ch_mma<W8, TGB>(x.bb[IT % LK_DEPTH], x.xs, XS_STR, c, x.lane, x.acc, tg);
   }
   if constexpr (c == nch - 1 && mx && kind == SK_F1) {  // ReLU^2 hidden rows -> e4m3 + block scales
-    // transposed accumulators: lane (c16, g4) holds row 16 i + c16, columns 16 (nt0 + j) + 4 g4 .. + 3;
-    // a 32-column block is the lane's two tiles x the 4 lane rows (permlane swaps), one 4-byte store
-    // per (row, tile)
-    static_assert(tg == 2, "a lane's two column tiles are one 32-column block");
-    constexpr int np = PL::s[si].ncols;
-    const float* pp = x.prm + GE::prm(si);
-    const int g4 = x.g4 >> 2;  // x.g4 = 4 (lane >> 4)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = i * 16 + x.c16;
-      float y[2][4], m = 0.f;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = fmaxf(ch_val<W8>(pp, np, x.acc[i][j][r], (nt0 + j) * 16 + 4 * g4 + r), 0.f);
-          y[j][r] = v * v;
-          m = fmaxf(m, y[j][r]);
-        }
-      const unsigned sb = mx_scale_byte(lanerow_max4(m));
-      const float mul = mx_mul(sb);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        *(unsigned*)(hh8 + row * HH8_STR + (nt0 + j) * 16 + 4 * g4) =
-            mx_pack4(y[j][0] * mul, y[j][1] * mul, y[j][2] * mul, y[j][3] * mul);
-      if (g4 == 0) hh8[LK_HSC + row * (CH_FF / 32) + nt0 / 2] = (unsigned char)sb;
-    }
+    static_assert(tg == 2 && TGB == 2, "a lane's two column tiles are one 32-column block");
+    lk_relu2_mx<PL::s[si].ncols>(x.acc, x.prm + GE::prm(si), nt0, x.c16, x.g4 >> 2, hh8);  // x.g4 = 4 (lane >> 4)
   } else if constexpr (c == nch - 1) {
     constexpr int np = PL::s[si].ncols;
     const float* pp = x.prm + GE::prm(si);
@@ -781,6 +789,48 @@ __global__ void __launch_bounds__(CH_NT) lk_ln_mx_probe_kernel(const float* __re
   for (int e = threadIdx.x; e < CH_MT * (CH_D / 32); e += CH_NT) scales[e] = sc[e];
 }
 
+// Verification kernel (ggd_mx_ffn_up): the long loop's FFN-up stage on the MX route -- the
+// transposed block-scaled MFMA (ch_mma_mx<2, true>) over one 32-row block of an e4m3 A image with
+// its e8m0 scales, then lk_relu2_mx -- with the loop's wave -> column-tile map (iteration l: tiles
+// 16 l + 2 wave, + 1) and weight fragment addressing (lk_issue).  The hidden codes and scale bytes
+// are copied out as the FFN-down stage reads them.  One workgroup of the loop's shape (8 waves).
+__global__ void __launch_bounds__(CH_NT) lk_ffn_up_mx_probe_kernel(const unsigned char* __restrict__ a_codes,
+                                                                const unsigned char* __restrict__ a_scales,
+                                                                const unsigned char* __restrict__ wpk,
+                                                                const float* __restrict__ wscale,
+                                                                const float* __restrict__ bias,
+                                                                unsigned char* __restrict__ h_codes,
+                                                                unsigned char* __restrict__ h_scales) {
+  __shared__ __attribute__((aligned(16))) unsigned char xs8[CH_MT * XS8_STR];
+  __shared__ unsigned char sc[CH_MT * (CH_D / 32)];
+  __shared__ __attribute__((aligned(16))) unsigned char hh8[LK_HSC + CH_MT * (CH_FF / 32)];
+  __shared__ __attribute__((aligned(16))) float prm[2 * CH_FF];
+  for (int e = threadIdx.x; e < CH_MT * CH_D; e += CH_NT) xs8[(e / CH_D) * XS8_STR + e % CH_D] = a_codes[e];
+  for (int e = threadIdx.x; e < CH_MT * (CH_D / 32); e += CH_NT) sc[e] = a_scales[e];
+  for (int e = threadIdx.x; e < CH_FF; e += CH_NT) {
+    prm[e] = bias[e];
+    prm[CH_FF + e] = wscale[e];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int TG = 2, UPT = Units<true>::U;  // one 256-k chunk: 4 units per tile
+  const unsigned char* wb = wpk + (size_t)wave * TG * UPT * 1024;
+  for (int l = 0; l < CH_FF / (16 * CH_WAVES * TG); ++l) {
+    BBuf<true, TG> B;
+    ch_load<true, TG>(B, wb, (unsigned)lane * 16, l * CH_WAVES * TG, 0, UPT, TG);
+    f32x4 acc[2][TG];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TG; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ch_mma_mx<TG, true>(B, xs8, XS8_STR, sc, CH_D / 32, 0, lane, acc, TG);
+    lk_relu2_mx<CH_FF>(acc, prm, (l * CH_WAVES + wave) * TG, lane & 15, lane >> 4, hh8);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < CH_MT * CH_FF; e += CH_NT) h_codes[e] = hh8[(e / CH_FF) * HH8_STR + e % CH_FF];
+  for (int e = threadIdx.x; e < CH_MT * (CH_FF / 32); e += CH_NT) h_scales[e] = hh8[LK_HSC + e];
+}
+
 }  // namespace
 
 bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C, int out_npad) {
@@ -842,5 +892,24 @@ extern "C" int ggd_mx_layernorm(const float* rows, const float* gamma, const flo
   hipLaunchKernelGGL(ggd::lk_ln_mx_probe_kernel, dim3(1), dim3(ggd::chainlib::CH_NT), 0, s, rows, gamma, beta, codes, scales);
   hipError_t e = hipGetLastError();
   const hipError_t e2 = hipStreamSynchronize(s);
+  return e == hipSuccess && e2 == hipSuccess ? 0 : -3;
+}
+
+extern "C" int ggd_mx_ffn_up(const uint8_t* a_codes, const uint8_t* a_scales, const uint8_t* w_e4m3, const float* wscale,
+                             const float* bias, uint8_t* h_codes, uint8_t* h_scales, void* stream) {
+  using namespace ggd;
+  using namespace ggd::chainlib;
+  if (!a_codes || !a_scales || !w_e4m3 || !wscale || !bias || !h_codes || !h_scales) return -1;  // GGD_ERR_ARG
+  hipStream_t s = (hipStream_t)stream;
+  void* pk = nullptr;
+  if (hipMalloc(&pk, (size_t)CH_FF * CH_D) != hipSuccess) return -3;
+  hipError_t e = launch_chain_pack(2, w_e4m3, pk, CH_FF, CH_D, s);  // the MX B order, as the context packs wmx
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(lk_ffn_up_mx_probe_kernel, dim3(1), dim3(CH_NT), 0, s, a_codes, a_scales,
+                       (const unsigned char*)pk, wscale, bias, h_codes, h_scales);
+    e = hipGetLastError();
+  }
+  const hipError_t e2 = hipStreamSynchronize(s);
+  (void)hipFree(pk);
   return e == hipSuccess && e2 == hipSuccess ? 0 : -3;
 }

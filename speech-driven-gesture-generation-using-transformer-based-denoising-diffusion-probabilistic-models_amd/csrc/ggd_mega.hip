@@ -36,7 +36,7 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_role, s_ok;
   if (m.gate && ggd::G(m.gate)[0] != 3) return;  // gated re-run: the XCD-local launch placed (or failed otherwise)
-  if (m.sim_unresident) {  // test hook: as if the workgroups were never all resident
+  if (m.sim_unresident == 1) {  // test hook: as if the workgroups were never all resident
     if (threadIdx.x == 0) atomicMax(m.status, 2);
     return;
   }
@@ -44,6 +44,10 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
   __syncthreads();
   const int role = s_role;
   if (role < 0) return;
+  if (m.sim_unresident == 2 && (role & 1)) {  // test hook: odd parts report 2, the rest wait in a barrier
+    if (threadIdx.x == 0) atomicMax(m.status, 2);
+    return;
+  }
   const int grp = role >> 3, b = m.clip0 + grp, part = role & 7, lane = ltid() & 63, wave = ltid() >> 6;
   unsigned* ctr = m.ctl + MK_GROUP + grp * 16;
   unsigned* flags = m.ctl + MK_FLAGS + grp * 32;

@@ -129,11 +129,13 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
       for (int spin = 0;; ++spin) {
         const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
         if (__ballot(v < epoch) == 0) break;
-        if ((spin & 255) == 255 && (wait_expired(t0) || __hip_atomic_load(status, __ATOMIC_RELAXED,
-                                                                         __HIP_MEMORY_SCOPE_AGENT))) {
-          if (threadIdx.x == 0) status_timeout(status);
-          ok = 0;
-          break;
+        if ((spin & 255) == 255) {
+          const bool expired = wait_expired(t0);
+          if (expired || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            if (threadIdx.x == 0) status_leave(status, expired);
+            ok = 0;
+            break;
+          }
         }
         __builtin_amdgcn_s_sleep(1);
       }
@@ -145,11 +147,13 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
       int ok = 1;
       const unsigned t0 = wait_t0();
       for (int spin = 0; mk_load(ctr) < target; ++spin) {
-        if ((spin & 255) == 255 && (wait_expired(t0) || __hip_atomic_load(status, __ATOMIC_RELAXED,
-                                                                         __HIP_MEMORY_SCOPE_AGENT))) {
-          status_timeout(status);
-          ok = 0;
-          break;
+        if ((spin & 255) == 255) {
+          const bool expired = wait_expired(t0);
+          if (expired || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            status_leave(status, expired);
+            ok = 0;
+            break;
+          }
         }
         __builtin_amdgcn_s_sleep(1);
       }

@@ -301,11 +301,13 @@ __device__ __forceinline__ bool pp_sync(unsigned* flags, int part, unsigned epoc
       const unsigned v = xl ? __builtin_amdgcn_raw_buffer_load_b32(r, (part ^ 1) * 4, 0, CP_COH)
                             : __hip_atomic_load(flags + (part ^ 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (v >= epoch) break;
-      if ((spin & 255) == 255 &&
-          (wait_expired(t0) || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        if (threadIdx.x == 0) status_timeout(status);
-        ok = 0;
-        break;
+      if ((spin & 255) == 255) {
+        const bool expired = wait_expired(t0);
+        if (expired || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          if (threadIdx.x == 0) status_leave(status, expired);
+          ok = 0;
+          break;
+        }
       }
       __builtin_amdgcn_s_sleep(1);
     }
@@ -448,7 +450,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
   unsigned char* xb = nullptr;
   unsigned ep = 0;
   if constexpr (PAIR) {
-    if (a.sim_unresident) {  // test hook: as if the pairs were never all resident
+    if (a.sim_unresident == 1) {  // test hook: as if the pairs were never all resident
       if (threadIdx.x == 0) atomicMax(a.status, 2);
       return;
     }
@@ -461,6 +463,10 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
     xl = (role & 2) != 0;
     flags = a.ctl + PP_FLAGS + (role >> 2) * 32;
     xb = a.xbuf + (size_t)(role >> 2) * 4 * PAIR_SLOT_BYTES;
+    if (a.sim_unresident == 2 && part == 1) {  // test hook: part 1 reports 2, part 0 waits in its first hand-off
+      if (threadIdx.x == 0) atomicMax(a.status, 2);
+      return;
+    }
   }
   constexpr int HP = PAIR ? 2 : 4, NC = PAIR ? 4 : 8;  // head pairs, FFN chunks of this workgroup
   const int hp0 = PAIR ? 2 * part : 0, c0f = PAIR ? 4 * part : 0, qoff = 12 * hp0;

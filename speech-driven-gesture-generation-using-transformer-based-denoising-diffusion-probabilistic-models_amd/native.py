@@ -39,7 +39,7 @@ EXPORTS = [
     "ggd_set_schedule", "ggd_set_memory", "ggd_set_inpaint", "ggd_denoise", "ggd_posterior_step", "ggd_sample",
     "ggd_sync",
     "ggd_set_profiling", "ggd_kernel_time", "ggd_profile_kind", "ggd_set_route", "ggd_route_info", "ggd_version",
-    "ggd_mx_linear", "ggd_mx_layernorm",
+    "ggd_mx_linear", "ggd_mx_layernorm", "ggd_mx_ffn_up",
     "ggd_enc_create", "ggd_enc_destroy", "ggd_enc_last_error", "ggd_enc_load_weight", "ggd_enc_finalize",
     "ggd_enc_lengths", "ggd_enc_run", "ggd_enc_run_memory",
     # training path (include/ggd_train.h)
@@ -165,6 +165,7 @@ def load():
         "ggd_version": (ctypes.c_char_p, []),
         "ggd_mx_linear": (ctypes.c_int, [I32, I32, I32, VP, VP, VP, VP, VP, VP]),
         "ggd_mx_layernorm": (ctypes.c_int, [VP, VP, VP, VP, VP, VP]),
+        "ggd_mx_ffn_up": (ctypes.c_int, [VP, VP, VP, VP, VP, VP, VP, VP]),
         "ggd_enc_create": (ctypes.c_int, [ctypes.c_int, I32, I32, I32, I32, P(CTX)]),
         "ggd_enc_destroy": (ctypes.c_int, [CTX]),
         "ggd_enc_last_error": (ctypes.c_char_p, [CTX]),

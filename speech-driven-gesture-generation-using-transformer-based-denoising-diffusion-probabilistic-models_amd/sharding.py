@@ -51,5 +51,6 @@ def sample_sharded(sample_fn, wavs, n_total, rank, world, device, stats=None):
         stats["gather_ms"] = (time.perf_counter() - t0) * 1e3
     if stats is not None:
         stats["gather_bytes"] = gathered.numel() * gathered.element_size()
+        stats["gather_bytes_per_rank"] = pad.numel() * pad.element_size()
     parts = [gathered[r * maxn: r * maxn + sizes[r]] for r in range(world)]
     return th.cat(parts, dim=0)

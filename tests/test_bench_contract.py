@@ -64,11 +64,11 @@ def test_launch_command_one_rank_per_gpu():
     assert cmd[i + 1:] == ["--gpus", "4", "--steps", "3"]
 
 
-def _rehearse(n):
+def _rehearse(n, *extra):
     import subprocess
     env = dict(os.environ, OMP_NUM_THREADS="1")
     env.pop("RANK", None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--rehearse"],
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--rehearse", *extra],
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -92,6 +92,20 @@ def test_self_launch_rehearsal_matches_single_rank():
     assert one["distributed"] is None
 
 
+def test_rehearsal_at_the_c5_eight_gpu_shape():
+    """C5's 8-GPU leg (BASELINE.json configs[4]: B = 1024 over 8 ranks, 128 clips each) through the
+    same launch / shard / all-gather path over gloo: the gathered payload is SURVEY.md 8e's 2.52 MB
+    per rank, 20.2 MB in all, and the clips come back in global order (equal to one rank's)."""
+    one = _rehearse(1, "--workload", "c5", "--batch-per-gpu", "1024")
+    eight = _rehearse(8, "--workload", "c5")
+    assert eight["global_batch"] == one["global_batch"] == 1024 and eight["shape"] == [1024, 123, 40]
+    d = eight["distributed"]
+    assert d["world_size"] == 8 and d["backend"] == "gloo"
+    assert d["all_gather_bytes_per_rank"] == 128 * 123 * 40 * 4 == 2_519_040
+    assert d["all_gather_bytes"] == 8 * 2_519_040 == 20_152_320
+    assert eight["first"] == one["first"] and eight["checksum"] == one["checksum"]
+
+
 def test_headline_pmc_summary_matches_the_kernel_sources():
     """The default (driver-run) C2 line prices its roofline traffic from a PMC summary taken on THIS
     csrc/ tree: a kernel change has to come with a fresh summary (scripts/pmc_all.sh)."""
@@ -104,13 +118,15 @@ class _FakeLib:
     """The ggd_* calls workload_subrecord makes, answering like a loop that ran (kind, avg us)."""
 
     def __init__(self, kind, avg_us, launches):
-        self.kind, self.avg_us, self.launches, self.prof = kind, avg_us, launches, []
+        self.kind, self.avg_us, self.launches, self.prof, self.calls = kind, avg_us, launches, [], None
 
     def ggd_set_route(self, h, knob, value):
         return 0
 
     def ggd_set_profiling(self, h, on):
         self.prof.append(on)
+        if self.calls is not None:
+            self.calls.append(("prof", on))
         return 0
 
     def ggd_kernel_time(self, h, which, avg, cnt):
@@ -135,6 +151,7 @@ def test_workload_subrecord_fields(monkeypatch, workload, kind, avg_us, launches
     L = 40 * w["seq_mult"]
     lib = _FakeLib(kind, avg_us, launches)
     calls = []
+    lib.calls = calls
 
     class FakeModel:
         arch = {"d_model": 256, "n_layers": 4}
@@ -162,8 +179,11 @@ def test_workload_subrecord_fields(monkeypatch, workload, kind, avg_us, launches
     monkeypatch.setattr(pkg, "init_state_dict", lambda *a, **k: {})
     passes = 3 if workload == "c5" else 1
     rec = bench.workload_subrecord(pkg, workload, th.device("cpu"), passes=passes)
-    assert calls.count((w["batch_per_gpu"], 123, L)) == passes + 1 and calls[-1] == "release"
-    assert lib.prof == [1, 0]   # only the last timed pass is profiled
+    assert calls.count((w["batch_per_gpu"], 123, L)) == passes + 2 and calls[-1] == "release"
+    assert lib.prof == [1, 0]   # one profiled pass, after the timed ones
+    shape = (w["batch_per_gpu"], 123, L)
+    # warm-up, the timed passes, their sync; then the profiled pass alone between the profiling calls
+    assert calls == [shape] * (1 + passes) + ["sync", ("prof", 1), shape, "sync", ("prof", 0), "release"]
     for k in ("workload", "value", "unit", "ms_per_step", "steps", "kernel", "kernel_avg_launch_us",
               "roofline_frac", "peak_tflops", "flop_per_launch"):
         assert k in rec, k

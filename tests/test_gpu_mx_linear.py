@@ -136,3 +136,61 @@ def test_mx_layernorm_scales_exact_and_codes_within_rounding(lib):
             (np.argwhere(diff)[:5], step[:5])
     print(f"mx layernorm: {int(diff.sum())} of 8192 codes at a rounding boundary, scales exact")
     assert diff.sum() <= 16
+
+
+def _ffn_up_inputs(seed):
+    """Operands whose FFN-up sums are exact in f32 (integers below 2^15 before the power-of-two
+    channel scale), so that the kernel's result is fully determined and every byte can be compared:
+    A = e4m3 integers in [-8, 8] with block scales 2^-1 .. 2^2, W = e4m3 integers in [-4, 4], per-channel
+    scales 2^-6 .. 2^-2, bias multiples of 1/16; about half the pre-activations negative (ReLU zeros),
+    one row and one 32-column block of weights all zero (zero blocks: scale byte 2)."""
+    rng = np.random.default_rng(seed)
+    a_codes = fp8.e4m3_encode(rng.integers(-8, 9, (32, 256)).astype(np.float32))
+    a_scales = rng.integers(126, 130, (32, 8)).astype(np.uint8)
+    a_codes[7] = 0
+    w_codes = fp8.e4m3_encode(rng.integers(-4, 5, (1024, 256)).astype(np.float32))
+    w_codes[64:96] = 0
+    wscale = np.exp2(rng.integers(-6, -1, 1024)).astype(np.float32)
+    bias = (rng.integers(-256, 257, 1024) / 16.0).astype(np.float32)
+    bias[64:96] = 0.0
+    return a_codes, a_scales, w_codes, wscale, bias
+
+
+def _run_ffn_up(lib, a_codes, a_scales, w_codes, wscale, bias):
+    dev = [th.from_numpy(np.ascontiguousarray(v)).cuda() for v in (a_codes, a_scales, w_codes, wscale, bias)]
+    h_codes = th.full((32, 1024), 0x7f, dtype=th.uint8, device="cuda")
+    h_scales = th.full((32, 32), 0xff, dtype=th.uint8, device="cuda")
+    rc = lib.ggd_mx_ffn_up(*[t.data_ptr() for t in dev], h_codes.data_ptr(), h_scales.data_ptr(), None)
+    assert rc == 0, rc
+    return h_codes.cpu().numpy(), h_scales.cpu().numpy()
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_mx_ffn_up_epilogue_bit_exact(lib, seed):
+    """The long loop's FFN-up stage on block-scaled fp8 MFMA -- the transposed MFMA chunk and the
+    ReLU^2 epilogue that quantises the hidden rows (lk_relu2_mx: the lane's two column tiles x its 4
+    lane rows as one 32-column block via lanerow_max4, the e8m0 byte, mx_pack4's byte order, the
+    scale placement) -- run by ggd_mx_ffn_up on one 32-row block: every one of the 32,768 e4m3 codes
+    and 1,024 scale bytes equals oracle/fp8.py mx_ffn_up.  A deliberately wrong block -> lane map
+    (blocks of 16 or 64 columns), a plain ReLU, or the blocks shifted by 16 columns each disagree."""
+    a_codes, a_scales, w_codes, wscale, bias = _ffn_up_inputs(seed)
+    got_c, got_s = _run_ffn_up(lib, a_codes, a_scales, w_codes, wscale, bias)
+    want_c, want_s = fp8.mx_ffn_up(a_codes, a_scales, w_codes, wscale, bias)
+    bad_s = np.argwhere(got_s != want_s)
+    bad_c = np.argwhere(got_c != want_c)
+    for r, k in bad_c[:8].tolist():
+        print(f"code row {r} col {k}: gpu {got_c[r, k]:#04x} oracle {want_c[r, k]:#04x}")
+    assert len(bad_s) == 0, bad_s[:8]
+    assert len(bad_c) == 0, len(bad_c)
+    assert (want_s == 2).any() and (want_c == 0).mean() > 0.3 and (want_s > 2).mean() > 0.5  # cases covered
+    # sensitivity: the wrong maps / activation are told apart
+    for kw in (dict(block_cols=16), dict(block_cols=64), dict(square=False)):
+        wc, ws = fp8.mx_ffn_up(a_codes, a_scales, w_codes, wscale, bias, **kw)
+        assert (wc != got_c).any() or ws.shape != got_s.shape or (ws != got_s).any(), kw
+    shifted = np.roll(fp8.mx_ffn_up(np.roll(a_codes, 0, 1), a_scales, np.roll(w_codes, 16, 0), np.roll(wscale, 16),
+                                    np.roll(bias, 16))[0], -16, 1)
+    assert (shifted != got_c).any()
+
+
+def test_mx_ffn_up_rejects_null_pointers(lib):
+    assert lib.ggd_mx_ffn_up(0, 0, 0, 0, 0, 0, 0, None) == -1

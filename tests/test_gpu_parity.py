@@ -547,11 +547,16 @@ def test_clip_pair_batches_ddim_bf16(pkg, beat_cfg, setup, n):
 # The persistent loops that need every workgroup resident at once (clip groups, clip pairs) stand
 # behind a device-gated fallback: when a loop reports status 2 (never all resident, nothing trusted)
 # the clips are re-initialised and run on the one-workgroup-per-clip loop, decided on the device, so
-# a non-blocking ggd_sample never hands back an unrun x.  GGD_ROUTE_SIMULATE_UNRESIDENT makes the
-# loops report 2 without running.
+# a non-blocking ggd_sample never hands back an unrun x.  GGD_ROUTE_SIMULATE_UNRESIDENT = 1 makes the
+# loops report 2 without running; = 2 makes only the odd parts report 2 while the others go on into
+# their first barrier, whose poll sees the 2 and must drain without turning it into a timeout code
+# (which no gate opens on: round-5 review).
 # ------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("sync", [False, True])
-def test_unresident_loops_fall_back_on_device_bf16(pkg, beat_cfg, setup, sync):
+INFO_BARRIER_TIMEOUTS = 10
+
+
+@pytest.mark.parametrize("sync,sim", [(False, 1), (True, 1), (False, 2)])
+def test_unresident_loops_fall_back_on_device_bf16(pkg, beat_cfg, setup, sync, sim):
     _, sd, om = setup
     model, diffusion = make_model(pkg, beat_cfg, sd, "bf16")
     n, steps = 4, 6
@@ -565,7 +570,9 @@ def test_unresident_loops_fall_back_on_device_bf16(pkg, beat_cfg, setup, sync):
         _route(ctx, 0)
         _pair(ctx, 1)
         outs["psk"] = run()                                   # the fallback loop itself
-        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_SIM_UNRESIDENT, 1) == 0
+        model.sync()
+        timeouts0 = _info(ctx, INFO_BARRIER_TIMEOUTS)
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_SIM_UNRESIDENT, sim) == 0
         _route(ctx, 1)                                        # clip-group loop (mk_kernel), never resident
         outs["mk_sim"] = run()
         model.sync()                                          # no error: the fallback ran the clips
@@ -575,6 +582,7 @@ def test_unresident_loops_fall_back_on_device_bf16(pkg, beat_cfg, setup, sync):
         outs["pair_sim"] = run()
         model.sync()
         assert _info(ctx, INFO_GATED_FALLBACKS) == 1
+        assert _info(ctx, INFO_BARRIER_TIMEOUTS) == timeouts0  # a drained wait is no timeout
         assert ctx.lib.ggd_set_route(ctx.h, ROUTE_SIM_UNRESIDENT, 0) == 0
         _route(ctx, 1)
         outs["mk"] = run()                                    # the loop itself again: fallback idle
