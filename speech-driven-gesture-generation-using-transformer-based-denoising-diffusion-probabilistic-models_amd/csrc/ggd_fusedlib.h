@@ -288,14 +288,30 @@ struct WGemm {
       wb[j][k] = make_uint4(v.x, v.y, v.z, v.w);
     }
   }
+  // k step k of every tile (bf16: group 0 holds the whole K)
+  __device__ __forceinline__ void load_step(int k, int lane) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+      const u32x4 v = ggd::G((const u32x4*)W)[((size_t)tiles[j] * kt_total + k0 + k) * 64 + lane];
+      wb[j][k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  }
   // group 0 must have been loaded; tiles j >= nj_on are skipped (wave-uniform).  bf16: the A
   // fragments of k step k + 1 are read from LDS before the MFMAs of step k issue, so the LDS
   // latency overlaps the matrix work (one wave per SIMD hides nothing on its own).
   // zero = false: accumulate onto the caller's acc (e.g. residual + bias preloaded)
   // FENCE: -1 the unit's SCHED_FENCE, 0 / 1 this call site's own choice
+  // after(k) runs once step k's MFMAs have issued (bf16): e.g. the next GEMM's step k loaded into
+  // the registers step k has just freed (WGemm::load_step), a weight stream without a second set
   template <bool TR = false, int FENCE = -1>
   __device__ __forceinline__ void run(f32x4 (&acc)[RT][NJ], const T* A, int SA, int lane, int nj_on = NJ,
                                       bool zero = true) {
+    run_then<TR, FENCE>(acc, A, SA, lane, [](int) {}, nj_on, zero);
+  }
+  template <bool TR = false, int FENCE = -1, typename AF>
+  __device__ __forceinline__ void run_then(f32x4 (&acc)[RT][NJ], const T* A, int SA, int lane, AF&& after,
+                                           int nj_on = NJ, bool zero = true) {
     constexpr bool FEN = FENCE < 0 ? SCHED_FENCE : FENCE != 0;
     if (zero) {
 #pragma unroll
@@ -331,6 +347,7 @@ struct WGemm {
                                                                      acc[rt][j], 0, 0, 0);
             }
         if constexpr (FEN) __builtin_amdgcn_sched_barrier(0);
+        after(k);
         if (k + 1 < KT) {
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) cur[rt] = nxt[rt];

@@ -98,9 +98,18 @@ template <typename T, int CP> struct Res {
 // NJ w .. NJ w + NJ - 1.  Computed transposed (WGemm TR): lane (c16, g4) of tile (rt, j) holds
 // row rt 16 + c16, columns 16 (NJ w + j) + 4 g4 .. + 3, so the accumulators start from one
 // float4 of Hs + bias and the epilogue is one float4 store (no dependent read-modify-write).
+template <typename T, int KT, int NJ, int RT, typename AF>
+__device__ __forceinline__ void residual_gemm_then(float* Hs, const T* A, int SA, WGemm<T, NJ, KT, RT>& g,
+                                                   const float4 (&bias)[NJ], int lane, int wave, AF&& after);
 template <typename T, int KT, int NJ, int RT>
 __device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGemm<T, NJ, KT, RT>& g,
                                               const float4 (&bias)[NJ], int lane, int wave) {
+  residual_gemm_then<T, KT, NJ, RT>(Hs, A, SA, g, bias, lane, wave, [](int) {});
+}
+// residual_gemm with WGemm::run_then's per-k-step hook
+template <typename T, int KT, int NJ, int RT, typename AF>
+__device__ __forceinline__ void residual_gemm_then(float* Hs, const T* A, int SA, WGemm<T, NJ, KT, RT>& g,
+                                                   const float4 (&bias)[NJ], int lane, int wave, AF&& after) {
   const int c16 = lane & 15, g4 = lane >> 4;
   f32x4 acc[RT][NJ];
 #pragma unroll
@@ -112,7 +121,7 @@ __device__ __forceinline__ void residual_gemm(float* Hs, const T* A, int SA, WGe
       acc[rt][j] = f32x4{h.x + bias[j].x, h.y + bias[j].y, h.z + bias[j].z, h.w + bias[j].w};
     }
   }
-  g.template run<true, GGD_MK_FENCE_OUT>(acc, A, SA, lane, NJ, false);
+  g.template run_then<true, GGD_MK_FENCE_OUT>(acc, A, SA, lane, after, NJ, false);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = (NJ * wave + j) * 16 + 4 * g4;

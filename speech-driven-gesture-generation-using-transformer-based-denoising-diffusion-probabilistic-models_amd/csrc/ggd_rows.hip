@@ -48,9 +48,40 @@ template <int RT> struct RowPlan {
   static constexpr size_t HC = al16(sizeof(T) * RT * 16 * (128 + Frag<T>::PT));
   static constexpr size_t KC = HR + XN + HC;
   static constexpr size_t KE = HR + KerPlan<T>::BYTES;
+  // KB's CA out-projection fragments, k steps 0 .. GCK - 1 of every wave's two tiles, copied into
+  // LDS by LDS-DMA in the KA in front (no registers: the loop is at ~240 VGPRs), clear of KA's and
+  // KB's own regions
+  static constexpr int GCK = 4;
+  static constexpr size_t GC = al16(KA > KB ? KA : KB);
+  static constexpr size_t GC_BYTES = 8 * 2 * GCK * 1024;
   static_assert(KA <= 160 * 1024 - 256 && KB <= 160 * 1024 - 256 && KC <= 160 * 1024 - 256 &&
-                    KE <= 160 * 1024 - 256, "row-block loop LDS");
+                    KE <= 160 * 1024 - 256 && GC + GC_BYTES <= 160 * 1024 - 256, "row-block loop LDS");
 };
+
+// LDS-DMA of this wave's CA out-projection tiles 2 wave, 2 wave + 1, k steps 0 .. GCK - 1 (fragment
+// [tile][k step][lane][16 B]) into the GC region: [wave][tile j][k step] x 1 KiB, lane l at 16 l.
+// Written as asm: the compiler treats a builtin LDS-DMA as a store that may alias every later LDS
+// access and drains it (vmcnt(0)) at the next one -- measured: KA's staging waited for the whole
+// copy (+0.7 us).  hipcc does not count asm loads either, so nothing waits for these until the
+// KA -> KB barrier's vmcnt drain (every load issued after them is drained there too).
+__device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+template <int RT>
+__device__ __forceinline__ void gc_dma(const void* w_oca, unsigned char* smem, int wave, int lane) {
+  using RP = RowPlan<RT>;
+  typedef __attribute__((address_space(3))) unsigned char lds_u8;
+  const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_u8*)(smem + RP::GC + wave * 2 * RP::GCK * 1024));
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int k = 0; k < RP::GCK; ++k)
+      glds16_asm((const char*)w_oca + ((size_t)((2 * wave + j) * KT + k) * 64 + lane) * 16, base + (j * RP::GCK + k) * 1024);
+}
 
 // 8 bytes through the global view
 __device__ __forceinline__ uint2 ld_g8(const T* p) {
@@ -139,6 +170,9 @@ __device__ __forceinline__ void ka_rows(const FA& a, int h, int b, unsigned char
   so.store(Xn);
   bar_lds();
   STAMP(1);
+  // half of KB's CA out-projection weights into LDS while the QKV GEMM runs (KB's operand intake is
+  // its bound: round 6)
+  gc_dma<RT>(a.w.o_ca, smem, wave, lane);
   using AT = FAtt<T>;
   {
     f32x4 acc[RT][1];
@@ -193,7 +227,7 @@ struct KBRPre {
 // every row that reaches a valid output is finite: staged rows are clamped copies).
 // ------------------------------------------------------------------------------------------
 template <int RT, int LKT, int CP, typename FA>
-__device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int it, unsigned char* smem, KBRPre& pre) {
+__device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int t_orig, unsigned char* smem, KBRPre& pre) {
   using RP = RowPlan<RT>;
   const int tid = ltid(), lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), c16 = lane & 15, g4 = lane >> 4;
   const int L = a.L, Ts = a.Ts, Lk = 1 + Ts;
@@ -206,7 +240,11 @@ __device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int it, unsig
   const auto& w = a.w;
   const size_t row0 = (size_t)b * L;
   STAMP(0);
-  // ---- loads, in the order they are needed: staging first (its waits leave the rest in flight)
+  // ---- loads, in the order they are needed (vector loads retire in issue order, so a load issued
+  // behind a weight stream is not usable before the whole stream has landed): the staging, then the
+  // small operands of LN2 / the step-token fix / the query epilogue, then the query weights, the
+  // memory K / V fragments and last the CA out-projection weights (round 6: issued behind the
+  // query stream, the conv taps made the SA out-projection segment wait for it, 3.3 us)
   RowsStage<16, CP> so;
   so.load((const T*)a.o_sa + row0 * FD, r0 - 1, L);
   const int hs = (tid >> 6) & 1, hc = 4 * (tid & 63);  // halo residual rows: tokens r0 - 1 / r1 (tid < 128)
@@ -214,28 +252,27 @@ __device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int it, unsig
   float4 bo[2];
   bo[0] = ld_f4(w.o_sa_b + (2 * wave) * 16 + 4 * g4);
   bo[1] = ld_f4(w.o_sa_b + (2 * wave + 1) * 16 + 4 * g4);
-  __builtin_amdgcn_sched_barrier(0);  // the staging loads first: loads retire in issue order
+  // memory rows 0 / 1 of head w see the step token through the conv: lane l fixes K (l < 32) or V
+  // (l >= 32) channel l & 31 (KvFix's arithmetic); t_orig comes from the step loop (one load per step)
+  KvFix fx;
+  fx.load(w.kv_step + (size_t)t_orig * 2 * FD, w.kv_mem + (size_t)b * Ts * 2 * FD, Ts, wave, lane);
+  const ConvW ckv = conv_w(lane < 32 ? w.ca_kw : w.ca_vw, lane < 32 ? w.ca_kb : w.ca_vb, lane & 31);
+  const ConvW cqv = conv_w(w.ca_qw, w.ca_qb, tid & 31);  // (stored by threads 0-31)
+  float4 bq[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bq[j] = ld_f4(w.q_ca_b + wave * FDK + j * 16 + 4 * g4);
+  __builtin_amdgcn_sched_barrier(0);  // the staging and the small operands first: loads retire in issue order
   so.store(Oi);
   if (tid < 128) *(uint4*)(Hr + (hs ? R + 1 : 0) * SH + hc) = hv;
   bar_lds();
   STAMP(1);
-  // ---- SA out-projection + residual (rows 0 .. 15)
-  residual_gemm<T, KT, 2, 1>(Hr, Oi, SX, pre.go, bo, lane, wave);
-  // the CA out-projection tiles (in the registers the SA tiles held), in flight across LN2, the
-  // query GEMM and the attention; the query's bias and conv taps
-  // the query tiles of head w (q_ca tiles 2w, 2w + 1) in the registers the SA tiles held, in flight
-  // across LN2 (issued here, not earlier: a wave's weight stream issued in front of its own critical
-  // work delays that work by the stream's intake time, ~115 GB/s per CU)
+  // ---- SA out-projection + residual (rows 0 .. 15).  The query tiles of head w (q_ca tiles 2w,
+  // 2w + 1) stream into the registers the SA tiles held, k step by k step as the out-projection
+  // frees them, in flight across LN2
   WGemm<T, 2, KT, 1> gq(w.q_ca, KT, 0);
   gq.tiles[0] = 2 * wave;
   gq.tiles[1] = 2 * wave + 1;
-  gq.load(0, lane);
-  // memory rows 0 / 1 of head w see the step token through the conv: lane l fixes K (l < 32) or V
-  // (l >= 32) channel l & 31 (KvFix's arithmetic).  Its loads need t (a two-load dependent chain):
-  // issued here, behind the out-projection, so that the chain does not stall the staging above
-  const int t_orig = a.t_clip ? G(a.t_clip)[b] : G(a.steps)[it].t_orig;
-  KvFix fx;
-  fx.load(w.kv_step + (size_t)t_orig * 2 * FD, w.kv_mem + (size_t)b * Ts * 2 * FD, Ts, wave, lane);
+  residual_gemm_then<T, KT, 2, 1>(Hr, Oi, SX, pre.go, bo, lane, wave, [&](int k) { gq.load_step(k, lane); });
   // memory K / V^T fragments of head w (kvc block: K [64][32] | V^T [32][64], keys 0 / 1 zero): the
   // lane's query dims are {4 g4 .. + 3} u {16 + 4 g4 .. + 3} (the transposed query GEMM's lane map),
   // so its K fragment holds those dims of key 16 t + c16 -- the contraction runs in that order
@@ -250,11 +287,6 @@ __device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int it, unsig
   for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
     for (int t = 0; t < LKT; ++t) vf[ct][t] = ld_g8(kvh + FLK * FDK + (ct * 16 + c16) * FLK + t * 16 + 4 * g4);
-  const ConvW ckv = conv_w(lane < 32 ? w.ca_kw : w.ca_vw, lane < 32 ? w.ca_kb : w.ca_vb, lane & 31);
-  const ConvW cqv = conv_w(w.ca_qw, w.ca_qb, tid & 31);  // (stored by threads 0-31)
-  float4 bq[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) bq[j] = ld_f4(w.q_ca_b + wave * FDK + j * 16 + 4 * g4);
   if (tid < FDK) cqs[tid] = make_float4(cqv.w0, cqv.w1, cqv.w2, cqv.b);
   bar_lds();
   STAMP(2);
@@ -272,13 +304,21 @@ __device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int it, unsig
   bar_lds();
   STAMP(3);
   // ---- query of head w (transposed: lane = image row c16, channels 16 j + 4 g4 ..) + conv over tokens
+  // the CA out-projection tiles go into the query's registers as the query GEMM frees them: k steps
+  // < GCK from the LDS copy KA made, the rest streamed from L2, in flight across the conv and the attention
   f32x4 q[1][2];
-  gq.template run<true>(q, Xi, SX, lane);
-  // the CA out-projection tiles in the query's registers, in flight across the conv and the attention
   WGemm<T, 2, KT, 1> gc(w.o_ca, KT, 0);
   gc.tiles[0] = 2 * wave;
   gc.tiles[1] = 2 * wave + 1;
-  gc.load(0, lane);
+  const unsigned char* gcl = smem + RP::GC + wave * 2 * RP::GCK * 1024 + lane * 16;
+  gq.template run_then<true>(q, Xi, SX, lane, [&](int k) {
+    if (k < RP::GCK) {  // DMA'd in KA (drained by the KA -> KB barrier's vmcnt wait)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) gc.wb[j][k] = *(const uint4*)(gcl + (j * RP::GCK + k) * 1024);
+    } else {
+      gc.load_step(k, lane);
+    }
+  });
   {
     constexpr int ROR1 = 0x121, ROR15 = 0x12F;  // lanes c16 - 1 / c16 + 1 of the 16-lane row
     const int tk = r0 - 1 + c16;
@@ -685,6 +725,8 @@ __global__ void __launch_bounds__(FT) mr_kernel(MegaArgs m, int G) {
     const int it = m.k0 + k;
     unsigned long long* st = (m.stamps && role == 0 && k < MEGA_STAMP_STEPS) ? m.stamps : nullptr;
     unsigned long long* ar = (m.stamps && grp == 0 && k < MEGA_STAMP_STEPS) ? m.stamps + 2 * 17 * MEGA_STAMP_STEPS + 1 : nullptr;
+    // the step token's original t (KB's memory-row fix): one load per step
+    const int t_orig = __builtin_amdgcn_readfirstlane(fa0[0].t_clip ? ggd::G(fa0[0].t_clip)[b] : ggd::G(fa0[0].steps)[it].t_orig);
     for (int li = 0; li < NL; ++li) {
       cfa_t f = fa0 + 4 * li;
       asm volatile("" : "+s"(f));  // per-layer arguments are re-read, not held across the loop
@@ -693,7 +735,7 @@ __global__ void __launch_bounds__(FT) mr_kernel(MegaArgs m, int G) {
       if (!mk_sync<CPV, KBRPre::TILE_LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
       // (the four per-layer argument blocks differ only in h / h_out, which these phases read as f[1] /
       // f[3] hold them: h; and in the phase-stamp pointer of the diagnostics)
-      kb_rows<RT, LKT, CPV>(f[1], part, b, it, smem, pb);
+      kb_rows<RT, LKT, CPV>(f[1], part, b, t_orig, smem, pb);
       KCRPre<RT> pc(f[0], part, wave);
       if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pc.load(lane); }, ar)) return;
       kc_rows<RT, CPV>(f[2], part, b, smem, pc);
