@@ -43,7 +43,7 @@ template <int RT> struct RowPlan {
   static constexpr size_t IMG16 = al16(sizeof(T) * 16 * SX);         // a 16-row operand image (KB)
   static constexpr size_t FIX = sizeof(float) * 8 * 128;             // KB: per head K rows 0-1 [2][32], V [32][2]
   static constexpr size_t CQ = sizeof(float4) * FDK;                 // KB: the query conv taps (w0, w1, w2, b) per channel
-  static constexpr size_t KA = HR + XN + FAtt<T>::BYTES;
+  static constexpr size_t KA = HR + XN + FAtt<T, RT * 16>::BYTES;  // Q image: the clip's RT row tiles only
   static constexpr size_t KB = HR + 2 * IMG16 + FIX + CQ;
   static constexpr size_t HC = al16(sizeof(T) * RT * 16 * (128 + Frag<T>::PT));
   static constexpr size_t KC = HR + XN + HC;
@@ -51,11 +51,16 @@ template <int RT> struct RowPlan {
   // KB's CA out-projection fragments, k steps 0 .. GCK - 1 of every wave's two tiles, copied into
   // LDS by LDS-DMA in the KA in front (no registers: the loop is at ~240 VGPRs), clear of KA's and
   // KB's own regions
-  static constexpr int GCK = 4;
+  // GCK: 5 of the 8 k steps at L <= 48 (80 KiB), as many as fit at RT = 4.  Measured (C2 mr_kernel,
+  // one box, two rounds each, profiles/r06g_c2_rows_dma_ab.txt, r06h_c2_rows_dma_ab.txt): 4 / 5 / 6
+  // k steps 68.17 / 67.68-67.82 / 68.21-68.26 ms per launch (KA's own intake starts to show at 6);
+  // moving query k steps into LDS instead (0-4 of them, the rest of the budget CA) 67.7-68.6 ms
   static constexpr size_t GC = al16(KA > KB ? KA : KB);
+  static constexpr int FREE_K = (int)((160 * 1024 - 256 - GC) / (8 * 2 * 1024));  // k steps of 16 KiB that fit
+  static constexpr int GCK = 5 < FREE_K ? 5 : FREE_K;
   static constexpr size_t GC_BYTES = 8 * 2 * GCK * 1024;
   static_assert(KA <= 160 * 1024 - 256 && KB <= 160 * 1024 - 256 && KC <= 160 * 1024 - 256 &&
-                    KE <= 160 * 1024 - 256 && GC + GC_BYTES <= 160 * 1024 - 256, "row-block loop LDS");
+                    KE <= 160 * 1024 - 256 && GC + GC_BYTES <= 160 * 1024 - 256 && GCK >= 1, "row-block loop LDS");
 };
 
 // LDS-DMA of this wave's CA out-projection tiles 2 wave, 2 wave + 1, k steps 0 .. GCK - 1 (fragment
@@ -71,16 +76,21 @@ __device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_dst) {
                : "v"(gsrc), "s"(lds_dst)
                : "memory");
 }
-template <int RT>
-__device__ __forceinline__ void gc_dma(const void* w_oca, unsigned char* smem, int wave, int lane) {
-  using RP = RowPlan<RT>;
+template <int NK>
+__device__ __forceinline__ void w2_dma(const void* w, unsigned char* dst, int wave, int lane) {
   typedef __attribute__((address_space(3))) unsigned char lds_u8;
-  const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_u8*)(smem + RP::GC + wave * 2 * RP::GCK * 1024));
+  const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_u8*)(dst + wave * 2 * NK * 1024));
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int k = 0; k < RP::GCK; ++k)
-      glds16_asm((const char*)w_oca + ((size_t)((2 * wave + j) * KT + k) * 64 + lane) * 16, base + (j * RP::GCK + k) * 1024);
+    for (int k = 0; k < NK; ++k)
+      glds16_asm((const char*)w + ((size_t)((2 * wave + j) * KT + k) * 64 + lane) * 16, base + (j * NK + k) * 1024);
+}
+// this wave's two tiles' k step k from such a copy
+template <int NK, int J>
+__device__ __forceinline__ void w2_lds_step(WGemm<T, J, KT, 1>& g, const unsigned char* src, int wave, int lane, int k) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) g.wb[j][k] = *(const uint4*)(src + ((wave * 2 + j) * NK + k) * 1024 + lane * 16);
 }
 
 // 8 bytes through the global view
@@ -172,8 +182,8 @@ __device__ __forceinline__ void ka_rows(const FA& a, int h, int b, unsigned char
   STAMP(1);
   // half of KB's CA out-projection weights into LDS while the QKV GEMM runs (KB's operand intake is
   // its bound: round 6)
-  gc_dma<RT>(a.w.o_ca, smem, wave, lane);
-  using AT = FAtt<T>;
+  w2_dma<RowPlan<RT>::GCK>(a.w.o_ca, smem + RowPlan<RT>::GC, wave, lane);
+  using AT = FAtt<T, RT * 16>;
   {
     f32x4 acc[RT][1];
     gm.template run<true>(acc, Xn, SX, lane, nq);
@@ -198,7 +208,10 @@ __device__ __forceinline__ void ka_rows(const FA& a, int h, int b, unsigned char
   bar_lds();
   STAMP(2);
   hook0();
-  fattn_any<T, CP>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
+  if (L <= 32)
+    fattn<T, 2, RT * 16, false, CP>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
+  else
+    fattn<T, 4, RT * 16, false, CP>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
   asm volatile("" ::: "memory");  // the hook's loads stay behind every store above (mk_sync counts them)
   hook();
   STAMP_END(3);
@@ -310,14 +323,9 @@ __device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int t_orig, u
   WGemm<T, 2, KT, 1> gc(w.o_ca, KT, 0);
   gc.tiles[0] = 2 * wave;
   gc.tiles[1] = 2 * wave + 1;
-  const unsigned char* gcl = smem + RP::GC + wave * 2 * RP::GCK * 1024 + lane * 16;
   gq.template run_then<true>(q, Xi, SX, lane, [&](int k) {
-    if (k < RP::GCK) {  // DMA'd in KA (drained by the KA -> KB barrier's vmcnt wait)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) gc.wb[j][k] = *(const uint4*)(gcl + (j * RP::GCK + k) * 1024);
-    } else {
-      gc.load_step(k, lane);
-    }
+    if (k < RP::GCK) w2_lds_step<RP::GCK>(gc, smem + RP::GC, wave, lane, k);  // DMA'd in KA (drained by the KA -> KB barrier)
+    else gc.load_step(k, lane);
   });
   {
     constexpr int ROR1 = 0x121, ROR15 = 0x12F;  // lanes c16 - 1 / c16 + 1 of the 16-lane row
