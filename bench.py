@@ -7,8 +7,8 @@ Workloads (BASELINE.json configs; beat-ours, 123 pose channels, random-init weig
      channels), ONE clip of L = 34 frames, 36,266-sample wav, respacing "50" DDPM, f32 (the
      reference computes in fp32) -- the CPU oracle's full 50-step loop is timed end to end beside it;
   c2 (default, the metric's config): 32 clips/GPU, L = 40, 32,000-sample wavs, DDPM T = 1000,
-     bf16 -- one launch of the clip-group persistent loop mk_kernel per pass (GGD_MEGA_ROWS=1: the
-     row-block decomposition mr_kernel instead, for A/B); plus an f32
+     bf16 -- one launch of the clip-group persistent loop mr_kernel (row-block decomposition) per
+     pass; plus an f32
      sub-record (one pass of the same workload in f32, the parity precision);
   c4: 32 clips/GPU, L = 160, DDPM 1000, fp8-e4m3 step weights -- generic per-phase kernels;
   c5: 128 clips/GPU, L = 40, DDIM-50 -- one launch of the clip-pair loop (psk_kernel, two
@@ -49,7 +49,6 @@ BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 FP8_PEAK_TFLOPS = 5000.0    # dense block-scaled fp8 MFMA (MI355X_MICROARCH.md:432; no sparsity)
 ROUTE_FP8_MFMA = 9          # include/ggd.h GGD_ROUTE_FP8_MFMA
 INFO_ROWS_LOOP = 9          # include/ggd.h GGD_INFO_ROWS_LOOP
-ROUTE_MEGA_ROWS = 10        # include/ggd.h GGD_ROUTE_MEGA_ROWS
 F32_PEAK_TFLOPS = 157.3
 
 
@@ -534,8 +533,6 @@ def main():
     lib = ctx.lib
     if args.graph:   # the hipGraph replay is a route of the per-phase launches: the persistent loops off
         assert lib.ggd_set_route(ctx.h, 0, 1) == 0 and lib.ggd_set_route(ctx.h, 3, 1) == 0
-    if os.environ.get("GGD_MEGA_ROWS") in ("0", "1"):   # A/B of the clip-group loop's decompositions
-        assert lib.ggd_set_route(ctx.h, ROUTE_MEGA_ROWS, int(os.environ["GGD_MEGA_ROWS"])) == 0
     mx = args.dtype == "fp8" and not args.no_fp8_mfma   # block-scaled fp8 MFMA in the long loop (default)
     if args.dtype == "fp8":
         assert lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0 if mx else 1) == 0

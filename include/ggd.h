@@ -195,7 +195,8 @@ enum {
                                         (one workgroup or a clip pair per clip, ggd_persist.hip) */
   GGD_ROUTE_PAIR = 1,                /* per-clip loops: 0 auto, 1 never, 2 always two workgroups per clip */
   GGD_ROUTE_PAIR_WRITE_THROUGH = 2,  /* 1: clip-pair hand-offs written through on any placement */
-  GGD_ROUTE_PHASE_LAUNCHES = 3,      /* 1: per-phase launches instead of the clip-group loop (ggd_mega.hip) */
+  GGD_ROUTE_PHASE_LAUNCHES = 3,      /* 1: per-phase launches instead of the clip-group loop (ggd_rows.hip
+                                        bf16, ggd_mega.hip f32) */
   GGD_ROUTE_PLACEMENT = 4,           /* clip-group loop: 0 XCD-local, 1 part p on XCD p, 2 group per XCD */
   GGD_ROUTE_GEMM_LAUNCHES = 5,       /* generic one-way route: 1 = one launch per GEMM instead of the
                                         row-block chains (ggd_chain.hip) */
@@ -208,14 +209,10 @@ enum {
                                         device-gated one-workgroup-per-clip fallback runs the clips;
                                         2: only the odd parts report 2, the others wait in their first
                                         barrier and must drain without hiding that 2 */
-  GGD_ROUTE_FP8_MFMA = 9,            /* GGD_FP8W long-clip loop: 0 the FFN and LayerNorm-projection GEMMs
+  GGD_ROUTE_FP8_MFMA = 9             /* GGD_FP8W long-clip loop: 0 the FFN and LayerNorm-projection GEMMs
                                         on block-scaled fp8 MFMA (e4m3 activations, one e8m0 scale per
                                         32 values), 1 the e4m3 weights widened into bf16 MFMAs (the
                                         launch route's arithmetic, bit-equal to it) */
-  GGD_ROUTE_MEGA_ROWS = 10           /* clip-group loop, bf16: 0 (default) every phase split by head / FFN
-                                        chunk (ggd_mega.hip), 1 the row-block decomposition (ggd_rows.hip:
-                                        the attention out-projections, LayerNorms and cross-attention on
-                                        each workgroup's own rows; measured ~1 % slower at C2) */
 };
 int ggd_set_route(ggd_ctx* ctx, int32_t knob, int32_t value);
 enum {
@@ -229,7 +226,8 @@ enum {
   GGD_INFO_CLIP_ATTN_LAUNCHES = 7,   /* running count of whole-clip attention launches (generic routes) */
   GGD_INFO_GATED_FALLBACKS = 8       /* last settled ggd_sample: chunks (clip-group loop) or batches
                                         (clip pairs) the device-gated fallback loop ran instead */,
-  GGD_INFO_ROWS_LOOP = 9,            /* 1 when the last clip-group loop issued was the row-block loop */
+  GGD_INFO_ROWS_LOOP = 9,            /* 1 when the last clip-group loop issued was the row-block loop
+                                        (bf16; f32 contexts run the head / chunk loop) */
   GGD_INFO_BARRIER_TIMEOUTS = 10     /* running count of persistent-loop launches (clip-group chunks, clip-pair
                                         batches, long-clip chunks) whose status word carried a barrier
                                         timeout: such a launch is reported as an error, never covered by

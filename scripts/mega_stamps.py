@@ -1,9 +1,9 @@
 """Per-phase time inside the persistent clip-group loop: body vs clip-group barrier (GPU box).
 
-    python3 scripts/mega_stamps.py [rows] [layers=N]
+    python3 scripts/mega_stamps.py [layers=N]
 
-Default: the head / chunk loop (ggd_mega.hip mk_kernel); `rows`: the row-block loop (ggd_rows.hip
-mr_kernel, GGD_ROUTE_MEGA_ROWS = 1).  layers=N: a decoder of N layers (same weights' first N layers)."""
+The bf16 clip-group loop, the row-block decomposition (ggd_rows.hip mr_kernel; round 6 removed the
+bf16 head / chunk loop).  layers=N: a decoder of N layers (same weights' first N layers)."""
 import os as _os
 _os.environ["GGD_DIAG"] = "1"  # ggd_diag lives in libggd_diag.so only (native.py)
 import ctypes
@@ -20,7 +20,7 @@ pkg = ge.load_package()
 native = __import__(ge.PKG_NAME + ".native", fromlist=["x"])
 cfg = pkg.load_config(os.path.join(ROOT, "configs", "beat-ours.json"))
 dev = th.device("cuda:0")
-HEADS = "rows" not in sys.argv[1:]
+HEADS = False
 NL = int(next((a.split("=")[1] for a in sys.argv[1:] if a.startswith("layers=")), 4))
 if NL != 4:
     cfg.Model.Decoder["n_layers"] = NL
@@ -28,7 +28,6 @@ model, diffusion, _, _, _ = pkg.create_model(123, cfg.Model, dtype="bf16", devic
 model.load_state_dict(pkg.init_state_dict(model.arch, seed=0))
 wav = th.randn(32, 32000, device=dev) * 0.1
 ctx, _ = model.prepare(wav, 40)
-assert ctx.lib.ggd_set_route(ctx.h, 10, 0 if HEADS else 1) == 0   # GGD_ROUTE_MEGA_ROWS
 print(f"{'head / chunk loop (mk_kernel)' if HEADS else 'row-block loop (mr_kernel)'}, {NL} layers", flush=True)
 
 

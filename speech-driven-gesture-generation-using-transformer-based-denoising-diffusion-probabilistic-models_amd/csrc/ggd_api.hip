@@ -172,9 +172,7 @@ struct ggd_ctx {
   // persistent reverse loop (ggd_mega.hip)
   bool no_mega = false;                // ggd_diag what = 9: route sampling through per-phase launches
   int mega_place = 0;                  // ggd_diag what = 12: 0 XCD-local, 1 part per XCD, 2 group per XCD
-  bool mega_rows = false;              // GGD_ROUTE_MEGA_ROWS: 1 = the row-block loop (ggd_rows.hip) where it
-                                       // runs the shape, instead of the head / chunk loop (ggd_mega.hip)
-  bool mega_rows_last = false;         // the last clip-group loop issued was the row-block loop
+  bool mega_rows_last = false;         // the last clip-group loop issued was the row-block loop (bf16)
   FusedArgs* mega_fa = nullptr;        // device [n_layers][4]
   unsigned long long* mega_phase_stamps = nullptr;  // ggd_diag what = 11: layer 1's phases + KE
   FinalArgs* mega_fe = nullptr;
@@ -1499,7 +1497,7 @@ int ggd_finalize_weights(ggd_ctx* c) {
       TRY(pack(c->emb_x));
       if (D.dtype == GGD_FP8W)  // the FFN / LN-projection weights the block-scaled stages read
         for (Layer& Ly : c->layers)
-          for (Lin* L : {&Ly.qkv, &Ly.q_ca, &Ly.ff1, &Ly.ff2, &Ly.o_sa, &Ly.o_ca}) {
+          for (Lin* L : {&Ly.qkv, &Ly.q_ca, &Ly.ff1, &Ly.ff2}) {
             HIP_TRY(c, dalloc(c, &L->wmx, chain_pack_bytes(1, L->npad, L->kpad)));
             HIP_TRY(c, launch_chain_pack(2, L->w, L->wmx, L->npad, L->kpad, c->stream));
           }
@@ -1738,6 +1736,17 @@ int ggd_kernel_time(ggd_ctx* c, int32_t which, double* avg_us, int64_t* launches
   return GGD_OK;
 }
 
+// Clips one clip-group launch holds on this context's shape (0: no clip-group loop runs it): f32 (the
+// parity mode) the head / chunk loop (ggd_mega.hip mk_kernel), bf16 the row-block loop (ggd_rows.hip
+// mr_kernel; round 6: 69.2 vs 75.1 ms per C2 pass, so the bf16 head / chunk loop was removed) where
+// its shape limits hold.  sampling: also honour the per-phase-launch switch (ggd_diag what = 9).
+static int group_capacity(const ggd_ctx* c, bool sampling) {
+  const ggd_desc& D = c->desc;
+  if (!c->fused || (sampling && c->no_mega)) return 0;
+  if (D.dtype != 0 && !(c->kvc && rows_supported(D.dtype, D.seq_len, D.speech_len))) return 0;
+  return mega_capacity(D.dtype, D.seq_len);
+}
+
 int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
   if (!c) return GGD_ERR_ARG;
   switch (knob) {
@@ -1775,9 +1784,6 @@ int ggd_set_route(ggd_ctx* c, int32_t knob, int32_t value) {
       if (value < 0 || value > 2) break;  // 2 only odd parts do, the rest wait in a barrier
       c->sim_unresident = value;
       return GGD_OK;
-    case GGD_ROUTE_MEGA_ROWS:       // 1: the row-block clip-group loop (bf16)
-      c->mega_rows = value != 0;
-      return GGD_OK;
     default:
       break;
   }
@@ -1794,7 +1800,7 @@ int ggd_route_info(ggd_ctx* c, int32_t what, double* out) {
   }
   switch (what) {
     case GGD_INFO_PER_CLIP_AVAILABLE: *out = c->persist ? 1.0 : 0.0; return GGD_OK;
-    case GGD_INFO_LOOP_CAPACITY: *out = c->fused ? (double)mega_capacity(c->desc.dtype, c->desc.seq_len) : 0.0; return GGD_OK;
+    case GGD_INFO_LOOP_CAPACITY: *out = (double)group_capacity(c, false); return GGD_OK;
     case GGD_INFO_PAIR_LAUNCHES: *out = c->pair_launches; return GGD_OK;
     case GGD_INFO_XL_LAUNCHES: *out = c->mega_xl_launches; return GGD_OK;
     case GGD_INFO_WT_RERUNS: *out = c->mega_fallbacks; return GGD_OK;
@@ -1885,7 +1891,7 @@ int ggd_diag(ggd_ctx* c, int32_t what, const int32_t* p, int32_t np, int32_t ite
   }
   if (what == 9 && np >= 1) {  // p[0] != 0: sample through the per-phase launches, not the persistent loop
     c->no_mega = p[0] != 0;
-    *avg_us = c->fused ? (double)mega_capacity(c->desc.dtype, c->desc.seq_len) : 0.0;
+    *avg_us = (double)group_capacity(c, false);
     return GGD_OK;
   }
   if (what == 7 && np >= 1) {  // p[0] != 0: route ggd_sample through the per-step launches
@@ -2156,10 +2162,6 @@ int long_tables(ggd_ctx* c) {
     use(1, c->layers[0].qkv);
     for (int li = 0; li < NL; ++li) {
       const int b0 = 2 + LONG_STAGES_PER_LAYER * li;
-      if (long_mx_out_proj()) {
-        use(b0 + 0, c->layers[li].o_sa);
-        use(b0 + 2, c->layers[li].o_ca);
-      }
       use(b0 + 1, c->layers[li].q_ca);
       use(b0 + 3, c->layers[li].ff1);
       use(b0 + 4, c->layers[li].ff2);
@@ -2372,7 +2374,7 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
     if (r) return r;
   }
   // batches above the loop's capacity run as consecutive launches of up to `cap` clips each
-  const int cap = mega_capacity(D.dtype, D.seq_len);
+  const int cap = group_capacity(c, true);
   const int chunks = (a.n + cap - 1) / cap;
   if (chunks > MEGA_MAX_CHUNKS) return fail(c, GGD_ERR_ARG, "batch too large for the persistent loop");
   HIP_TRY(c, hipMemsetAsync(c->mega_status, 0, sizeof(int) * 2 * MEGA_MAX_CHUNKS, s));
@@ -2389,8 +2391,8 @@ int run_mega(ggd_ctx* c, const ggd_sample_args& a, int nsteps, bool sync) {
     int r = prof_mark(c, s);
     if (r) return r;
   }
-  // GGD_ROUTE_MEGA_ROWS = 1: bf16 shapes on the row-block decomposition (ggd_rows.hip)
-  const bool rows = c->mega_rows && c->kvc && rows_supported(D.dtype, D.seq_len, D.speech_len);
+  // bf16 on the row-block decomposition (ggd_rows.hip), f32 (the parity mode) on the head / chunk one
+  const bool rows = D.dtype != 0;
   c->mega_rows_last = rows;
   auto launch = [&](const MegaArgs& m, int n, bool x) {
     return rows ? launch_rows(D.dtype, D.seq_len, D.speech_len, m, n, x, s) : launch_mega(D.dtype, D.seq_len, m, n, x, s);
@@ -2473,7 +2475,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   HIP_TRY(c, launch_init_state(c->x, a->x_T, a->seed, a->clip_offset, a->n, D.d_pose, D.seq_len, s));
   bool use_persist = c->persist && c->persist_mode != 1;
   if (use_persist && c->persist_mode == 0) {
-    const int cap = c->no_mega ? 0 : mega_capacity(D.dtype, D.seq_len);
+    const int cap = group_capacity(c, true);
     use_persist = cap <= 0 || (a->n + cap - 1) / cap >= 3;
   }
   if (use_persist) {
@@ -2548,7 +2550,7 @@ int ggd_sample(ggd_ctx* c, const ggd_sample_args* a, void* stream) {
   HIP_TRY(c, launch_set_int(c->d_counter, -1, s));
 
   // the persistent loops run every iteration, the last one writing the extras itself
-  if (c->fused && !c->no_mega && nsteps > 0 && mega_capacity(D.dtype, D.seq_len) > 0) {
+  if (nsteps > 0 && group_capacity(c, true) > 0) {
     int r = run_mega(c, *a, nsteps, sync);
     if (r < 0) return r;
     if (r == 0) {

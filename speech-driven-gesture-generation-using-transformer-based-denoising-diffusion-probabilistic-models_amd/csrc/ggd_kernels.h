@@ -302,12 +302,9 @@ constexpr int LONG_STAMPS = 64;
 bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C, int out_npad);
 int long_loop_capacity();   // clips per launch
 // w8: 0 bf16 weights, 1 e4m3 weights widened into bf16 MFMAs, 2 e4m3 weights AND activations on
-// block-scaled fp8 MFMA in the FFN / LayerNorm-projection stages (a.stages' F1 / F2 / P / P2 weights,
-// and R's when long_mx_out_proj(), then hold launch_chain_pack(2, ...) copies)
+// block-scaled fp8 MFMA in the FFN / LayerNorm-projection stages (a.stages' F1 / F2 / P / P2 weights
+// then hold launch_chain_pack(2, ...) copies)
 hipError_t launch_long_loop(int w8, const LongArgs& a, int G, hipStream_t s);
-// w8 = 2: the attention out-projections (stage R) are block-scaled too (their stage weights then
-// hold MX copies as well)
-bool long_mx_out_proj();
 // step-invariant convolved memory K / V^T of one layer for the long loop (keys 0, 1 and >= 1 + Ts zero)
 hipError_t launch_long_kv_cache(const float* kv_mem, const float* kw, const float* kb, const float* vw, const float* vb,
                                 int n, int Ts, int heads, bf16_t* out, hipStream_t s);

@@ -33,10 +33,7 @@ using namespace chainlib;
 // r05y6_c4w_depth_ab.txt): 2 -> 156.1-157.0 ms per C4 launch, 3 -> 159.0-159.5, 4 -> 163.0 (fp8 MFMA
 // route; widened route 163.5-164.4 vs 164.7-165.7 at 3): the loop sits at the 256-VGPR limit, and
 // the 32 registers of the third group cost more than its prefetch distance buys (4 spills).
-#ifndef GGD_LK_DEPTH
-#define GGD_LK_DEPTH 2
-#endif
-constexpr int LK_DEPTH = GGD_LK_DEPTH;
+constexpr int LK_DEPTH = 2;
 constexpr int LK_ARRIVE = 128, LK_FLAGS = 256;  // ctl: tickets [x * 16], arrivals, group flag lines [g * 32]
 
 __device__ __forceinline__ unsigned lk_add(unsigned* p, unsigned v) {
@@ -300,11 +297,8 @@ constexpr size_t LK_XSC = LK_HSC + (size_t)CH_MT * (CH_FF / 32);  //            
 static_assert(LK_XSC + CH_MT * (CH_D / 32) <= sizeof(bf16_t) * CH_MT * HH_STR, "MX images fit the hh region");
 static_assert(CH_MT * XS8_STR <= sizeof(bf16_t) * CH_MT * XS_STR, "fp8 A rows fit the xs region");
 static_assert(LK_XSC >= sizeof(float) * CH_MT * EPS_STR, "eps rows (out_layers) stay clear of the LN scales");
-// GGD_LK_MX_R (A/B switch): the attention out-projections (stage R, A = the hand-off rows,
-// quantised as they are staged) on block-scaled fp8 MFMA too
-#ifndef GGD_LK_MX_R
-#define GGD_LK_MX_R 0
-#endif
+// (the attention out-projections -- stage R, A = the hand-off rows quantised as they are staged -- on
+// block-scaled fp8 MFMA too measured slower: 164 vs 158 ms per C4 launch, round 4)
 // The FFN-up stage's epilogue on the MX route: ReLU^2 of the transposed accumulators into the
 // block-scaled fp8 hidden image.  Lane (c16, g4) holds row 16 i + c16, columns 16 (nt0 + j) + 4 g4
 // .. + 3; a 32-column block is the lane's two tiles x the 4 lane rows of its row (permlane swaps,
@@ -339,7 +333,7 @@ __device__ __forceinline__ void lk_relu2_mx(const f32x4 (&acc)[2][2], const floa
 template <int KIND, int si, bool MX>
 constexpr bool lk_mx() {
   constexpr int k = LkPlan<KIND>::s[si].kind;
-  return MX && (k == SK_F1 || k == SK_F2 || k == SK_P || k == SK_P2 || (GGD_LK_MX_R && k == SK_R));
+  return MX && (k == SK_F1 || k == SK_F2 || k == SK_P || k == SK_P2);
 }
 
 template <bool W8, int KIND, int IT, bool MX, class X>
@@ -839,8 +833,6 @@ bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C
   return dtype != 0 && d_model == CH_D && heads == 8 && L % CH_MT == 0 && L / CH_MT <= 8 && L >= 96 &&
          L <= ATT_LMAX && lkp >= 96 && lkp <= ATT_LMAX && C <= 128 && out_npad == 128 && lds <= 160 * 1024 - 256;
 }
-
-bool long_mx_out_proj() { return GGD_LK_MX_R != 0; }
 
 size_t long_kv_cache_bytes(int n, int Ts, int heads) {
   const int Lkp = (1 + Ts + 31) / 32 * 32;

@@ -1,4 +1,6 @@
-// ggd_mega.hip -- the reverse loop as ONE persistent launch.
+// ggd_mega.hip -- the reverse loop as ONE persistent launch: the head / chunk clip-group loop, f32
+// (the parity mode) only since round 6 -- bf16 contexts run the row-block decomposition of the same
+// loop (ggd_rows.hip: 69.2 vs 75.1 ms per C2 pass on one box, profiles/r06d_c2_rows_ab.txt).
 //
 // The per-phase launches of ggd_fused.hip pay a kernel boundary (grid fill / drain, and loads
 // that start cold behind the boundary's cache maintenance) 17 times per denoise step.  Here
@@ -24,9 +26,7 @@
 // letting the scheduler move the next k step's LDS reads gives 73.5-73.7 ms per C2 launch against
 // 73.9-74.0 (one box, three alternations: profiles/r05w10_c2_fence_qkv_ab.txt); dropping it at the
 // cross-attention query costs 1 ms, at the out-projections / FFN 0.1-0.3 ms (r05w9_c2_fence_sites_ab.txt)
-#ifndef GGD_MK_FENCE_QKV
 #define GGD_MK_FENCE_QKV 0
-#endif
 #include "ggd_megasync.h"
 
 namespace ggd {
@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
       kb_phase<T, RT, CPV>(f[1], part, b, it, smem, pb, [&] { pc.load_tile(1, lane); }, [&] { pc.load_tile(0, lane); });
       if (!mk_sync<CPV, KCPre<T, RT>::TILE_LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
       kc_phase<T, RT, CPV>(f[2], part, b, smem, pc);
-      if (li + 1 < NL || !GGD_MK_FUSE_KD) {
+      if (li + 1 < NL) {
         KDPre<T, RT> pd(f[3], part, wave);
         if (!mk_sync<CPV>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [&] { pd.load(lane); }, ar)) return;
         kd_phase<T, RT, CPV>(f[3], part, b, smem, pd);
@@ -100,60 +100,50 @@ __global__ void __launch_bounds__(FT) mk_kernel(MegaArgs m, int G) {
 // LDS: the phases' private regions sit behind the resident residual rows (Res<T>); the kernel's
 // static words (role, barrier verdict) need room beside the dynamic allocation
 constexpr size_t MK_LDS_STATIC = 256;
-template <typename T, int RT>
-static size_t mk_lds() {
-  return 160 * 1024 - MK_LDS_STATIC;
-}
+constexpr size_t MK_LDS = 160 * 1024 - MK_LDS_STATIC;
 
-template <typename T, int RT>
-static int mk_capacity_t() {
+// clips one launch of either clip-group loop holds (this one, f32; ggd_rows.hip, bf16): one
+// 512-thread workgroup per CU (160 KiB LDS; 186+ VGPRs allow only one too), 8 per clip
+int mega_capacity(int dtype, int L) {
+  (void)dtype;
+  (void)L;
   static int cap = -1;
   if (cap < 0) {
-    (void)hipFuncSetAttribute((const void*)mk_kernel<T, RT, CP_COH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    // residency from the LDS budget (the occupancy query rejects > 64 KiB of dynamic LDS):
-    // one 512-thread workgroup per CU
     int dev = 0, cus = 0, lds_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
     (void)hipGetLastError();  // nothing above may leave a sticky error for the next launch
-    const int per = lds_cu >= (int)mk_lds<T, RT>() ? 1 : 0;  // registers: 186+ VGPRs also allow only one
+    const int per = lds_cu >= (int)MK_LDS ? 1 : 0;
     cap = std::min(32, per * cus / 8);  // control words hold 32 groups
   }
   return cap;
 }
 
-static inline bool mk_rt3(int L) { return L <= 48; }
-
-int mega_capacity(int dtype, int L) {
-  if (dtype == 0) return mk_rt3(L) ? mk_capacity_t<float, 3>() : mk_capacity_t<float, 4>();
-  return mk_rt3(L) ? mk_capacity_t<bf16_t, 3>() : mk_capacity_t<bf16_t, 4>();
-}
-
-template <typename T, int RT>
+template <int RT>
 static hipError_t launch_mega_t(const MegaArgs& a, int n, bool xl, hipStream_t s) {
   const int G = n, nwg = xl ? 64 * ((G + 7) / 8) : 8 * G;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)mk_kernel<T, RT, CP_XL>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)mk_kernel<T, RT, CP_COH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)mk_kernel<float, RT, CP_XL>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)mk_kernel<float, RT, CP_COH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();
     attr = true;
   }
   if (xl)
-    hipLaunchKernelGGL((mk_kernel<T, RT, CP_XL>), dim3(nwg), dim3(FT), (mk_lds<T, RT>()), s, a, G);
+    hipLaunchKernelGGL((mk_kernel<float, RT, CP_XL>), dim3(nwg), dim3(FT), MK_LDS, s, a, G);
   else
-    hipLaunchKernelGGL((mk_kernel<T, RT, CP_COH>), dim3(nwg), dim3(FT), (mk_lds<T, RT>()), s, a, G);
+    hipLaunchKernelGGL((mk_kernel<float, RT, CP_COH>), dim3(nwg), dim3(FT), MK_LDS, s, a, G);
   return hipGetLastError();
 }
 
+// f32 only: bf16 contexts run the row-block loop (launch_rows)
 hipError_t launch_mega(int dtype, int L, const MegaArgs& a, int n, bool xl, hipStream_t s) {
-  if (n < 1 || n > mega_capacity(dtype, L)) return hipErrorInvalidValue;
+  if (dtype != 0 || L > 64 || n < 1 || n > mega_capacity(dtype, L)) return hipErrorInvalidValue;
   if (xl && (a.placement != 0 || 64 * ((n + 7) / 8) > 8 * mega_capacity(dtype, L))) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(a.ctl, 0, sizeof(unsigned) * MEGA_CTL_WORDS, s);
   if (e != hipSuccess) return e;
-  if (dtype == 0) return mk_rt3(L) ? launch_mega_t<float, 3>(a, n, xl, s) : launch_mega_t<float, 4>(a, n, xl, s);
-  return mk_rt3(L) ? launch_mega_t<bf16_t, 3>(a, n, xl, s) : launch_mega_t<bf16_t, 4>(a, n, xl, s);
+  return L <= 48 ? launch_mega_t<3>(a, n, xl, s) : launch_mega_t<4>(a, n, xl, s);
 }
 
 }  // namespace ggd

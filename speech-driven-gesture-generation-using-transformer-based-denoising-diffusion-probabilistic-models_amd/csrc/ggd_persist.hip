@@ -187,50 +187,10 @@ __device__ __forceinline__ void fattn_lds(unsigned char* att, int Lq, int Lk, fl
       a.stamps[i] = __builtin_amdgcn_s_memtime();                                               \
   } while (0)
 
-// A/B switch: the self-attention QKV of a head pair computed transposed with the 3-tap conv in
-// registers (1) or through a pre-conv bf16 image and a conv pass (0)
-#ifndef GGD_PSK_QKV_CONV
-#define GGD_PSK_QKV_CONV 1
-#endif
-// A/B switch: the out-projections, the FFN-up chunk and the FFN-down residual computed transposed
-// (a lane holds 4 consecutive columns of one row: float4 / 8-byte LDS epilogues instead of scalar ones)
-#ifndef GGD_PSK_TR
-#define GGD_PSK_TR 1
-#endif
-// A/B switch (clip pairs, transposed route): each part runs the attention out-projections on its
-// OWN four heads only (K = 128 of 256: half the MFMAs and half the 128 KiB weight stream) and the
-// partners exchange bf16 partial sums, as after the FFN (1), instead of swapping their heads'
-// attention outputs and both running the full out-projection (0)
-#ifndef GGD_PSK_SPLITO
-#define GGD_PSK_SPLITO 1
-#endif
-// per-GEMM k-step fence of the transposed pair / clip route (pmma FENCE; -1: the unit's
-// GGD_SCHED_FENCE): emb_x, QKV, SA out-projection, CA query, CA out-projection, FFN-up, FFN-down,
-// output projection
-#ifndef GGD_PSK_FENCE_EMB
-#define GGD_PSK_FENCE_EMB -1
-#endif
-#ifndef GGD_PSK_FENCE_QKV
-#define GGD_PSK_FENCE_QKV -1
-#endif
-#ifndef GGD_PSK_FENCE_OSA
-#define GGD_PSK_FENCE_OSA -1
-#endif
-#ifndef GGD_PSK_FENCE_Q
-#define GGD_PSK_FENCE_Q -1
-#endif
-#ifndef GGD_PSK_FENCE_OCA
-#define GGD_PSK_FENCE_OCA -1
-#endif
-#ifndef GGD_PSK_FENCE_FF1
-#define GGD_PSK_FENCE_FF1 -1
-#endif
-#ifndef GGD_PSK_FENCE_FF2
-#define GGD_PSK_FENCE_FF2 -1
-#endif
-#ifndef GGD_PSK_FENCE_OUT  // fenced: 7.14 vs 7.20 ms per C5 launch, mean of five alternations on two
-#define GGD_PSK_FENCE_OUT 1  // boxes (profiles/r05w14_c5_fence_sites_ab.txt, r05w15_c5_fence_out_ab.txt)
-#endif
+// Per-GEMM k-step fences of the transposed pair / clip route (pmma FENCE; -1: the unit's
+// GGD_SCHED_FENCE): only the output projection keeps the fence -- 7.14 vs 7.20 ms per C5 launch, mean
+// of five alternations on two boxes (profiles/r05w14_c5_fence_sites_ab.txt, r05w15_c5_fence_out_ab.txt)
+constexpr int PSK_FENCE_OUT = 1;
 
 constexpr int PK_THREADS = 512;  // 8 waves: two per SIMD, so one wave's LDS / L2 waits overlap the other's MFMAs
 
@@ -238,13 +198,14 @@ constexpr int PK_THREADS = 512;  // 8 waves: two per SIMD, so one wave's LDS / L
 // Clip pairs.  With fewer clips than CUs (C5: 128 clips per GPU on 256 CUs) one workgroup per
 // clip leaves half the chip idle, so a clip can be split over TWO workgroups: part p runs the
 // attention of heads 4p .. 4p + 3 and FFN chunks 4p .. 4p + 3 (1024 / 128 = 8 chunks).  The
-// partners meet three times per layer: after self-attention and after cross-attention each
-// hands its four heads' outputs (bf16, L x 128) to the other, which then runs the full
-// out-projection itself (a redundant 256 x 256 GEMM is cheaper than a second hand-off and keeps
-// the residual bit-identical to the one-workgroup loop); after the FFN each hands its FFN-down
-// partial (L x 256, rounded to bf16) and both add part 0's + part 1's.  Every other step-loop value
-// (embedding, LayerNorms, out-projection, posterior update with its counter noise) is computed
-// identically by both, so both hold the same pose state and part 0 alone writes it.
+// partners meet three times per layer: after the self- and the cross-attention each runs the
+// out-projection on its OWN four heads' columns (K = 128 of 256) and after the FFN its FFN-down on its
+// own four chunks; each hands that partial sum (L x 256, rounded to bf16) to the other and both add
+// part 0's + part 1's (round 5: half the out-projection MFMAs and weight stream; swapping the heads'
+// attention outputs and running the whole out-projection in both was 7.53 vs 7.43 ms per C5 launch).
+// Every other step-loop value (embedding, LayerNorms, output projection, posterior update with its
+// counter noise) is computed identically by both, so both hold the same pose state and part 0 alone
+// writes it.
 //
 // Placement: a workgroup takes a ticket on its XCD; when every XCD holds its pairs' slots, the
 // partners share an L2 and hand-offs are plain stores + sc1 loads (as ggd_mega.hip's CP_XL);
@@ -325,50 +286,7 @@ __device__ __forceinline__ void pp_put16(const __amdgpu_buffer_rsrc_t& r, int of
     __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, CP_COH);
 }
 
-// this part's four heads of the attention output (Ob columns 128 part ..) -> its hand-off slot
-template <int R, int SX>
-__device__ __forceinline__ void pp_put_heads(const bf16_t* Ob, int part, unsigned char* slot, int L, bool xl, int tid) {
-  constexpr int NI = (R * 16 + PK_THREADS - 1) / PK_THREADS;
-  const __amdgpu_buffer_rsrc_t r = uni_rsrc(slot, (uint32_t)PAIR_SLOT_BYTES);
-#pragma unroll
-  for (int k = 0; k < NI; ++k) {
-    const int i = tid + k * PK_THREADS, row = i >> 4, c = i & 15;
-    if (row < L) pp_put16(r, i * 16, *(const pp_u32x4*)(Ob + row * SX + 128 * part + c * 8), xl);
-  }
-}
-// the partner's four heads from its slot -> Ob columns 128 (part ^ 1) ..
-template <int R, int SX>
-__device__ __forceinline__ void pp_get_heads(bf16_t* Ob, int part, const unsigned char* slot, int L, int tid) {
-  constexpr int NI = (R * 16 + PK_THREADS - 1) / PK_THREADS;
-  const __amdgpu_buffer_rsrc_t r = uni_rsrc(slot, (uint32_t)PAIR_SLOT_BYTES);
-  pp_u32x4 v[NI];
-#pragma unroll
-  for (int k = 0; k < NI; ++k) {
-    const int i = tid + k * PK_THREADS;
-    if ((i >> 4) < L) v[k] = __builtin_amdgcn_raw_buffer_load_b128(r, i * 16, 0, CP_COH);
-  }
-#pragma unroll
-  for (int k = 0; k < NI; ++k) {
-    const int i = tid + k * PK_THREADS, row = i >> 4, c = i & 15;
-    if (row < L) *(pp_u32x4*)(Ob + row * SX + 128 * (part ^ 1) + c * 8) = v[k];
-  }
-}
-
-// the two partners swap their heads' attention outputs (Ob columns 128 part .. <-> 128 (part ^ 1) ..)
-template <int R, int SX>
-__device__ __forceinline__ bool pp_swap_heads(bf16_t* Ob, int part, unsigned char* xb, unsigned& ep, unsigned* flags,
-                                              bool xl, int* status, int* s_ok, int L, int tid) {
-  ++ep;
-  const size_t sl = (size_t)(ep & 1) * PAIR_SLOT_BYTES;
-  pp_put_heads<R, SX>(Ob, part, xb + (size_t)part * 2 * PAIR_SLOT_BYTES + sl, L, xl, tid);
-  if (!pp_sync(flags, part, ep, xl, status, s_ok)) return false;
-  pp_get_heads<R, SX>(Ob, part, xb + (size_t)(part ^ 1) * 2 * PAIR_SLOT_BYTES + sl, L, tid);
-  bar_lds();
-  return true;
-}
-
-// partial sums of the two halves of a K split (FFN-down; with GGD_PSK_SPLITO the attention
-// out-projections): wave w's accumulators of column tiles 2w, 2w + 1, rounded to bf16 and handed
+// partial sums of the two halves of a K split (FFN-down and the attention out-projections): wave w's accumulators of column tiles 2w, 2w + 1, rounded to bf16 and handed
 // over in lane order; both parts add part 0's + part 1's -- each rounds its OWN partial too, so both
 // add the same two bf16 values and hold the same bits
 template <int RT>
@@ -420,7 +338,7 @@ __device__ __forceinline__ bool pp_sum_partials(f32x4 (&acc)[RT][2], int part, u
 template <int RT, bool PAIR>
 __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
   // the split out-projections: pairs on the transposed route
-  constexpr bool SPLITO = PAIR && GGD_PSK_SPLITO && GGD_PSK_TR;
+  constexpr bool SPLITO = PAIR;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int s_role, s_ok;
   if (a.gate && !gate_open(a.gate, a.gate_xl)) return;  // the loop this launch stands in for ran
@@ -543,7 +461,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
       bar_lds();
       f32x4 acc[RT][2];
       zero_acc(acc);
-      pmma<RT, 2, 4, 8, false, GGD_PSK_FENCE_EMB>(acc, Xb, SHD, 0, fb, lane);
+      pmma<RT, 2, 4, 8, false, -1>(acc, Xb, SHD, 0, fb, lane);
       {  // fb <- layer 0's first FFN-down chunk
         const int td[2] = {2 * wave, 2 * wave + 1};
         pload<2, 4>(fb, a.layers[0].ff2, 32, td, 4 * c0f, lane);
@@ -572,7 +490,6 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
       for (int hi = 0; hi < HP; ++hi) {
         LANE_IDS();
         const int hp = hp0 + hi;
-#if GGD_PSK_QKV_CONV
         // the head pair's QKV computed transposed, the 3-tap conv over tokens in registers (DPP
         // lane rotations, conv_tokens: the clip-group loop's KA epilogue) and the convolved rows
         // written straight into the two attention images -- no pre-conv image, no conv pass, one
@@ -581,7 +498,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         {
           f32x4 acc[RT][2];
           zero_acc(acc);
-          pmma_n<RT, 2, 8, 16, true, GGD_PSK_FENCE_QKV>(acc, Xn, SX, 0, fa, nq, lane);
+          pmma_n<RT, 2, 8, 16, true, -1>(acc, Xn, SX, 0, fa, nq, lane);
           if (hi < HP - 1) {  // refill: the next head pair, or the SA out-projection
             const int tq[2] = {12 * (hp + 1) + tq0, 12 * (hp + 1) + tq1};
             if (nq == 2) pload<2, 8>(fa, w.qkv, 8, tq, 0, lane);
@@ -628,59 +545,14 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           fattn_lds<R>(att_sa + hh * PL::ATT_B, L, L, a.scale, Ob + (2 * hp + hh) * FDK, SX, t2);
           bar_lds();
         }
-#else
-        const float bq0 = w.qkv_b[hp * 192 + tq0 * 16 + c16], bq1 = w.qkv_b[hp * 192 + tq1 * 16 + c16];
-        const ConvW cq = conv_w(w.sa_qw, w.sa_qb, tid & 31), ck = conv_w(w.sa_kw, w.sa_kb, tid & 31),
-                    cv = conv_w(w.sa_vw, w.sa_vb, tid & 31);
-        {
-          f32x4 acc[RT][2];
-          zero_acc(acc);
-          pmma_n<RT, 2, 8>(acc, Xn, SX, 0, fa, nq, lane);
-          if (hi < HP - 1) {  // refill: the next head pair, or the SA out-projection
-            const int tq[2] = {12 * (hp + 1) + tq0, 12 * (hp + 1) + tq1};
-            if (nq == 2) pload<2, 8>(fa, w.qkv, 8, tq, 0, lane);
-            else pload<1, 8>(fa, w.qkv, 8, tq, 0, lane);
-          } else {
-            const int to[2] = {2 * wave, 2 * wave + 1};
-            if constexpr (SPLITO) pload<2, 4>(fa, w.o_sa, 8, to, 4 * part, lane);  // K rows of its own heads
-            else pload<2, 8>(fa, w.o_sa, 8, to, 0, lane);
-          }
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            if (j >= nq) break;
-            const int col = (j == 0 ? tq0 : tq1) * 16 + c16;
-            const float bias = j == 0 ? bq0 : bq1;
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) Yb[(rt * 16 + 4 * g4 + r) * PL::SYB + col] = from_f32<T>(acc[rt][j][r] + bias);
-          }
-        }
-        bar_lds();
-        {  // both heads of the pair at once: threads 0-255 head 2hp, 256-511 head 2hp + 1
-          LANE_IDS();
-          const int hh = tid >> 8, t2 = tid & 255;
-          unsigned char* at = att_sa + hh * PL::ATT_B;
-          const T* Yh = Yb + hh * 96;
-          conv_rows<T, false, R, NT / 2, T>((T*)(at + AT::OQ), AT::SQ, Yh, PL::SYB, L, cq, t2);
-          conv_rows<T, false, FLK, NT / 2, T>((T*)(at + AT::OK), AT::SQ, Yh + 32, PL::SYB, L, ck, t2);
-          conv_rows<T, true, FLK, NT / 2, T>((T*)(at + AT::OV), AT::SV, Yh + 64, PL::SYB, L, cv, t2);
-          bar_lds();
-          fattn_lds<R>(at, L, L, a.scale, Ob + (2 * hp + hh) * FDK, SX, t2);
-          bar_lds();
-        }
-#endif
       }
       PSTAMP(2);
-      if constexpr (PAIR && !SPLITO)
-        if (!pp_swap_heads<R, SX>(Ob, part, xb, ep, flags, xl, a.status, &s_ok, L, tid)) return;
       // SA out-projection + residual
       {
-        #if GGD_PSK_TR
         const float4 bo4[2] = {ld_f4(w.o_sa_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.o_sa_b + (2 * wave + 1) * 16 + 4 * g4)};
         f32x4 acc[RT][2];
         zero_acc(acc);
-        if constexpr (SPLITO) pmma<RT, 2, 4, 16, true, GGD_PSK_FENCE_OSA>(acc, Ob, SX, 4 * part, fa, lane);  // its own heads' columns
+        if constexpr (SPLITO) pmma<RT, 2, 4, 16, true, -1>(acc, Ob, SX, 4 * part, fa, lane);  // its own heads' columns
         else pmma<RT, 2, 8, 16, true>(acc, Ob, SX, 0, fa, lane);
         if constexpr (PAIR) {  // fa <- cross-attn Q of this part's heads: wave w owns column tile 8 part + w
           const int tq[1] = {8 * part + wave};
@@ -694,31 +566,6 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           if (!pp_sum_partials<RT>(acc, part, xb, ep, flags, xl, a.status, &s_ok, wave, lane)) return;
         LSTAMP(8);
         p_resid_tr<RT>(Hs, acc, bo4, wave, c16, g4);
-#else
-        const float bo0 = w.o_sa_b[(2 * wave) * 16 + c16], bo1 = w.o_sa_b[(2 * wave + 1) * 16 + c16];
-        f32x4 acc[RT][2];
-        zero_acc(acc);
-        pmma<RT, 2, 8>(acc, Ob, SX, 0, fa, lane);
-        if constexpr (PAIR) {  // fa <- cross-attn Q of this part's heads: wave w owns column tile 8 part + w
-          const int tq[1] = {8 * part + wave};
-          pload<1, 8>(fa, w.q_ca, 8, tq, 0, lane);
-        } else {  // fa <- cross-attn Q of every head: wave w owns head w's two column tiles
-          const int tq[2] = {2 * wave, 2 * wave + 1};
-          pload<2, 8>(fa, w.q_ca, 8, tq, 0, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int col = (2 * wave + j) * 16 + c16;
-          const float bo = j == 0 ? bo0 : bo1;
-#pragma unroll
-          for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float* p = Hs + (rt * 16 + 4 * g4 + r) * SH + col;
-              *p = *p + (acc[rt][j][r] + bo);
-            }
-        }
-#endif
         bar_lds();
       }
       // ---------------- cross-attention block (nn.py:163-167) ----------------
@@ -745,12 +592,11 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         // PAIR: the part's 4 heads, wave w one column tile (8 part + w)
         constexpr int NQJ = PAIR ? 1 : 2;
         const int qt0 = PAIR ? 8 * part + wave : 2 * wave;
-#if GGD_PSK_TR
         // transposed, the 3-tap conv over tokens in registers: Yqb holds the CONVOLVED queries,
         // which the attention reads in place (no conv pass per head pair)
         f32x4 acc[RT][NQJ];
         zero_acc(acc);
-        pmma<RT, NQJ, 8, 16, true, GGD_PSK_FENCE_Q>(acc, Xn, SX, 0, fa, lane);
+        pmma<RT, NQJ, 8, 16, true, -1>(acc, Xn, SX, 0, fa, lane);
         {  // fa <- the CA out-projection
           const int to[2] = {2 * wave, 2 * wave + 1};
           if constexpr (SPLITO) pload<2, 4>(fa, w.o_ca, 8, to, 4 * part, lane);
@@ -772,28 +618,6 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           for (int rt = 0; rt < RT; ++rt) put_tok4<T, false>(Yqb, SX, rt * 16 + c16, (qt0 + j) * 16 + 4 * g4, v[rt]);
         }
       }
-#else
-        const float bq0 = w.q_ca_b[qt0 * 16 + c16], bq1 = w.q_ca_b[(qt0 + 1) * 16 + c16];
-        f32x4 acc[RT][NQJ];
-        zero_acc(acc);
-        pmma<RT, NQJ, 8>(acc, Xn, SX, 0, fa, lane);
-        {  // fa <- the CA out-projection
-          const int to[2] = {2 * wave, 2 * wave + 1};
-          if constexpr (SPLITO) pload<2, 4>(fa, w.o_ca, 8, to, 4 * part, lane);
-          else pload<2, 8>(fa, w.o_ca, 8, to, 0, lane);
-        }
-        bar_lds();
-#pragma unroll
-        for (int j = 0; j < NQJ; ++j) {
-          const int col = (qt0 + j) * 16 + c16;
-          const float bias = j == 0 ? bq0 : bq1;
-#pragma unroll
-          for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) Yqb[(rt * 16 + 4 * g4 + r) * SX + col] = from_f32<T>(acc[rt][j][r] + bias);
-        }
-      }
-#endif
       LSTAMP(10);
       // head pairs: both heads' conv and attention at once (threads 0-255 head 2hp, 256-511 head
       // 2hp + 1); the next pair's memory K|V loads fly under this pair's work
@@ -807,31 +631,21 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         kvs.store(at, t2);
         if (hi < HP - 1) kvs.load(kvc_b + (size_t)(hd + 2) * KVC_ELEMS, t2);
         bar_lds();
-#if !GGD_PSK_TR
-        conv_rows<T, false, R, NT / 2, T>((T*)(at + AT::OQ), AT::SQ, Yqb + hd * FDK, SX, L, dq, t2);
-#endif
         if (fixer) {
           fx.store<T, R>(at, dk, dv, Lk, lane);
           if (hi < HP - 1) fx.load(kvs_t, kvm_b, a.Ts, hd + 2, lane);
         }
         bar_lds();
-#if GGD_PSK_TR
         fattn_lds<R>(at, L, Lk, a.scale, Ob + hd * FDK, SX, t2, Yqb + hd * FDK, SX);
-#else
-        fattn_lds<R>(at, L, Lk, a.scale, Ob + hd * FDK, SX, t2);
-#endif
         bar_lds();
       }
       PSTAMP(3);
-      if constexpr (PAIR && !SPLITO)
-        if (!pp_swap_heads<R, SX>(Ob, part, xb, ep, flags, xl, a.status, &s_ok, L, tid)) return;
       // CA out-projection + residual
       {
-        #if GGD_PSK_TR
         const float4 bo4[2] = {ld_f4(w.o_ca_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.o_ca_b + (2 * wave + 1) * 16 + 4 * g4)};
         f32x4 acc[RT][2];
         zero_acc(acc);
-        if constexpr (SPLITO) pmma<RT, 2, 4, 16, true, GGD_PSK_FENCE_OCA>(acc, Ob, SX, 4 * part, fa, lane);
+        if constexpr (SPLITO) pmma<RT, 2, 4, 16, true, -1>(acc, Ob, SX, 4 * part, fa, lane);
         else pmma<RT, 2, 8, 16, true>(acc, Ob, SX, 0, fa, lane);
         {  // fa <- FFN-up chunk c0f (fb already holds FFN-down chunk c0f)
           const int tf[1] = {8 * c0f + wave};
@@ -842,28 +656,6 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           if (!pp_sum_partials<RT>(acc, part, xb, ep, flags, xl, a.status, &s_ok, wave, lane)) return;
         LSTAMP(16);
         p_resid_tr<RT>(Hs, acc, bo4, wave, c16, g4);
-#else
-        const float bo0 = w.o_ca_b[(2 * wave) * 16 + c16], bo1 = w.o_ca_b[(2 * wave + 1) * 16 + c16];
-        f32x4 acc[RT][2];
-        zero_acc(acc);
-        pmma<RT, 2, 8>(acc, Ob, SX, 0, fa, lane);
-        {  // fa <- FFN-up chunk c0f (fb already holds FFN-down chunk c0f)
-          const int tf[1] = {8 * c0f + wave};
-          pload<1, 8>(fa, w.ff1, 8, tf, 0, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int col = (2 * wave + j) * 16 + c16;
-          const float bo = j == 0 ? bo0 : bo1;
-#pragma unroll
-          for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float* p = Hs + (rt * 16 + 4 * g4 + r) * SH + col;
-              *p = *p + (acc[rt][j][r] + bo);
-            }
-        }
-#endif
         bar_lds();
       }
       // ---------------- feed-forward block (nn.py:170-172) ----------------
@@ -881,17 +673,10 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         for (int ci = 0; ci < NC; ++ci) {
           LANE_IDS();
           const int c = c0f + ci;
-#if GGD_PSK_TR
           const float4 bf4 = ld_f4(w.ff1_b + (8 * c + wave) * 16 + 4 * g4);
           f32x4 acc[RT][1];
           zero_acc(acc);
-          pmma<RT, 1, 8, 16, true, GGD_PSK_FENCE_FF1>(acc, Xn, SX, 0, fa, lane);
-#else
-          const float bf = w.ff1_b[(8 * c + wave) * 16 + c16];
-          f32x4 acc[RT][1];
-          zero_acc(acc);
-          pmma<RT, 1, 8>(acc, Xn, SX, 0, fa, lane);
-#endif
+          pmma<RT, 1, 8, 16, true, -1>(acc, Xn, SX, 0, fa, lane);
           if (ci < NC - 1) {
             const int tf[1] = {8 * (c + 1) + wave};
             pload<1, 8>(fa, w.ff1, 8, tf, 0, lane);
@@ -906,7 +691,6 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
           // the chunk image is double-buffered: chunk c + 1 writes the other buffer, so no barrier
           // is needed behind the FFN-down MFMAs (the next chunk's barrier orders the reuse)
           T* Hc = Hd + (c & 1) * (PL::HID / sizeof(T));
-#if GGD_PSK_TR
           {  // row 16 rt + c16, chunk columns 16 w + 4 g4 .. + 3: one 8-byte store per row tile
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt) {
@@ -916,21 +700,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
             }
           }
           bar_lds();
-          pmma<RT, 2, 4, 8, true, GGD_PSK_FENCE_FF2>(accd, Hc, SHD, 0, fb, lane);
-#else
-          {
-            const int col = (8 * c + wave) * 16 + c16 - 128 * c;  // column inside the chunk
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float v = fmaxf(acc[rt][0][r] + bf, 0.f);
-                Hc[(rt * 16 + 4 * g4 + r) * SHD + col] = from_f32<T>(v * v);
-              }
-          }
-          bar_lds();
-          pmma<RT, 2, 4>(accd, Hc, SHD, 0, fb, lane);
-#endif
+          pmma<RT, 2, 4, 8, true, -1>(accd, Hc, SHD, 0, fb, lane);
           {
             const int td[2] = {2 * wave, 2 * wave + 1};
             if (ci < NC - 1)
@@ -946,24 +716,8 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
         if constexpr (PAIR)  // FFN-down partials of the two halves of K
           if (!pp_sum_partials<RT>(accd, part, xb, ep, flags, xl, a.status, &s_ok, wave, lane)) return;
         LSTAMP(14);
-#if GGD_PSK_TR
         const float4 b24[2] = {ld_f4(w.ff2_b + (2 * wave) * 16 + 4 * g4), ld_f4(w.ff2_b + (2 * wave + 1) * 16 + 4 * g4)};
         p_resid_tr<RT>(Hs, accd, b24, wave, c16, g4);
-#else
-        const float b20 = w.ff2_b[(2 * wave) * 16 + c16], b21 = w.ff2_b[(2 * wave + 1) * 16 + c16];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int col = (2 * wave + j) * 16 + c16;
-          const float b2 = j == 0 ? b20 : b21;
-#pragma unroll
-          for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float* p = Hs + (rt * 16 + 4 * g4 + r) * SH + col;
-              *p = *p + (accd[rt][j][r] + b2);
-            }
-        }
-#endif
         bar_lds();
       }
     }
@@ -977,7 +731,7 @@ __global__ void __launch_bounds__(PK_THREADS) psk_kernel(PersistArgs a, int P) {
       const float bo = a.b_out[wave * 16 + c16];
       f32x4 acc[RT][1];
       zero_acc(acc);
-      pmma<RT, 1, 8, 16, false, GGD_PSK_FENCE_OUT>(acc, Xn, SX, 0, fa, lane);
+      pmma<RT, 1, 8, 16, false, PSK_FENCE_OUT>(acc, Xn, SX, 0, fa, lane);
       {  // fa <- layer 0's first QKV pair (next step)
         const int tq[2] = {qoff + tq0, qoff + tq1};
         if (nq == 2) pload<2, 8>(fa, a.layers[0].qkv, 8, tq, 0, lane);

@@ -32,40 +32,13 @@
 #pragma once
 #include "ggd_fusedlib.h"
 
-// Round-4 switches of the persistent loop's KE rows phase (A/B builds: -DGGD_MK_...=0/1; both
-// bit-identical, both on: scripts/ab.sh on one box, profiles/r04m_c2_ab.txt, C2 mk_kernel 75.07 ->
-// 74.21 ms (FUSE_KD) and 74.85 ms (CMAP))
-//   GGD_MK_FUSE_KD  the last layer's FFN-down reduction runs inside KE, for each block's rows (one
-//                   clip-group barrier and the KD phase fewer per step: 16 instead of 17)
-//   GGD_MK_CMAP     KE update threads take channel t % 128 (coalesced x access) instead of t / 3
-#ifndef GGD_MK_FUSE_KD
-#define GGD_MK_FUSE_KD 1
-#endif
-#ifndef GGD_MK_CMAP
-#define GGD_MK_CMAP 1
-#endif
-// per-GEMM k-step fence (WGemm::run FENCE; -1: the unit's GGD_SCHED_FENCE): out-projections,
-// QKV, cross-attention query, FFN-up, FFN-down, output projection, emb_x of the updated rows
-#ifndef GGD_MK_FENCE_OUT
-#define GGD_MK_FENCE_OUT -1
-#endif
+// KE rows phase (round 4, both measured on one box, profiles/r04m_c2_ab.txt): the last layer's
+// FFN-down reduction runs inside KE for each block's rows (one clip-group barrier and the KD phase
+// fewer per step: 75.07 -> 74.21 ms per C2 launch), and the update threads take channel t % 128
+// (coalesced x access; 74.85 ms).  The per-GEMM k-step fences (WGemm::run FENCE) follow the unit's
+// GGD_SCHED_FENCE except KA's QKV tile, whose fence is per unit (ggd_mega.hip: none, r05w10)
 #ifndef GGD_MK_FENCE_QKV
 #define GGD_MK_FENCE_QKV -1
-#endif
-#ifndef GGD_MK_FENCE_Q
-#define GGD_MK_FENCE_Q -1
-#endif
-#ifndef GGD_MK_FENCE_FF1
-#define GGD_MK_FENCE_FF1 -1
-#endif
-#ifndef GGD_MK_FENCE_FF2
-#define GGD_MK_FENCE_FF2 -1
-#endif
-#ifndef GGD_MK_FENCE_EPS
-#define GGD_MK_FENCE_EPS -1
-#endif
-#ifndef GGD_MK_FENCE_EMB
-#define GGD_MK_FENCE_EMB -1
 #endif
 
 namespace ggd {
@@ -121,7 +94,7 @@ __device__ __forceinline__ void residual_gemm_then(float* Hs, const T* A, int SA
       acc[rt][j] = f32x4{h.x + bias[j].x, h.y + bias[j].y, h.z + bias[j].z, h.w + bias[j].w};
     }
   }
-  g.template run_then<true, GGD_MK_FENCE_OUT>(acc, A, SA, lane, after, NJ, false);
+  g.template run_then<true, -1>(acc, A, SA, lane, after, NJ, false);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int col = (NJ * wave + j) * 16 + 4 * g4;
@@ -384,7 +357,7 @@ __device__ __forceinline__ void kb_phase(const FA& a, int h, int b, int it, unsi
   if constexpr (!R::ON) kvs.store(att, tid);
   if (wave < 2) {  // the head's query, convolved over tokens in registers, into the Q image
     f32x4 acc[RT][1];
-    gq.template run<true, GGD_MK_FENCE_Q>(acc, Ax, Frag<T>::SX, lane);
+    gq.template run<true, -1>(acc, Ax, Frag<T>::SX, lane);
     f32x4 v[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
@@ -460,7 +433,7 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   T* Hc = (T*)(pv + PL::IMG + PL::ST);
   {
     f32x4 acc[RT][1];
-    gf.template run<true, GGD_MK_FENCE_FF1>(acc, Ax, Frag<T>::SX, lane);
+    gf.template run<true, -1>(acc, Ax, Frag<T>::SX, lane);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const float v0 = fmaxf(acc[rt][0][0] + bf.x, 0.f), v1 = fmaxf(acc[rt][0][1] + bf.y, 0.f);
@@ -472,7 +445,7 @@ __device__ __forceinline__ void kc_phase(const FA& a, int c, int b, unsigned cha
   STAMP(4);
   {
     f32x4 acc[RT][2];
-    gd.template run<true, GGD_MK_FENCE_FF2>(acc, Hc, SHC, lane);
+    gd.template run<true, -1>(acc, Hc, SHC, lane);
     const OutRowsP<CP> out((T*)a.ffp + ((size_t)b * 8 + c) * L * FD, (uint32_t)(sizeof(T) * L * FD));
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -682,7 +655,7 @@ __device__ __forceinline__ void emb_rows_store(const FA& a, int b, int r0, int R
   f32x4 acc[1][2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) acc[0][j] = f32x4{pe[j].x, pe[j].y, pe[j].z, pe[j].w};
-  ge.template run<true, GGD_MK_FENCE_EMB>(acc, Xb, KerPlan<T>::SB, lane, 2, false);
+  ge.template run<true, -1>(acc, Xb, KerPlan<T>::SB, lane, 2, false);
   const OutRowsP<CP> ho(a.h + ((size_t)b * a.L + r0) * FD, (uint32_t)(sizeof(float) * R * FD));  // rows >= R dropped
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -775,12 +748,10 @@ __device__ __forceinline__ void ker_phase(const FA& a, int p, int b, int k, unsi
   STAMP(0);
   // the last layer's KD for the block's rows only: h = h_KC + (sum of the 8 FFN-down partials in
   // chunk order + b2), kd_phase's arithmetic; thread (row i = tid / 64, columns 4 (tid % 64) ..)
-  // (without GGD_MK_FUSE_KD: the KD phase ran, the rows are staged from h)
   const int si = tid >> 6, sc = 4 * (tid & 63), srow = min(r0 + max(min(si, R - 1), 0), L - 1);  // R = 0 when L < 8
-  if constexpr (!GGD_MK_FUSE_KD) glds_rows<FT, CP>(Hs, sizeof(float) * SH, a.h + (row0 + r0) * FD, sizeof(float) * FD, R, 1);
   float4 part[8];
 #pragma unroll
-  for (int c = 0; c < (GGD_MK_FUSE_KD ? 8 : 0); ++c) {
+  for (int c = 0; c < 8; ++c) {
     const uint32_t off = (uint32_t)(sizeof(T) * ((((size_t)b * 8 + c) * L + srow) * FD + sc));
     if constexpr (sizeof(T) == 2) {
       const uint2 u = ld_8B<CP>(a.ffp, off);
@@ -792,14 +763,13 @@ __device__ __forceinline__ void ker_phase(const FA& a, int p, int b, int k, unsi
     }
   }
   float4 sres = make_float4(0.f, 0.f, 0.f, 0.f);
-  if constexpr (!GGD_MK_FUSE_KD) {
-  } else if constexpr (RS::ON) {
+  if constexpr (RS::ON) {
     sres = *(const float4*)((const float*)smem + srow * SH + sc);
   } else {
     const uint4 u = ld_16B<CP>(a.h, (uint32_t)(sizeof(float) * ((row0 + srow) * FD + sc)));
     sres = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
   }
-  const float4 sb2 = GGD_MK_FUSE_KD ? ld_f4(a.ff2_b + sc) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 sb2 = ld_f4(a.ff2_b + sc);
   WGemm<T, 1, KT, 1> go(a.w_out, KT, 0);  // wave w: channel tile w (prefetched at the barrier)
   go.tiles[0] = wave;
 #pragma unroll
@@ -809,13 +779,8 @@ __device__ __forceinline__ void ker_phase(const FA& a, int p, int b, int k, unsi
   // takes channel t % 128 and the (t / 128)-th quad of it: with L % 4 == 0 every lane of a wave
   // then holds the same frames, so each x store / load of the wave covers one frame row's
   // consecutive channels (a few cache lines) instead of 64 scattered rows (C <= 128, E's rows)
-#if GGD_MK_CMAP
   const int uc = tid & 127, qi = ((uc * L + r0) >> 2) + (tid >> 7);
   const bool qon = uc < C && tid < 3 * 128;
-#else
-  const int uc = tid / 3, qi = ((uc * L + r0) >> 2) + (tid - 3 * uc);
-  const bool qon = uc < C;
-#endif
   StepRec rec = ld_rec(a.steps + k);
   float xq[4] = {0.f, 0.f, 0.f, 0.f}, zq[4] = {0.f, 0.f, 0.f, 0.f};
   float mq[4] = {0.f, 0.f, 0.f, 0.f}, pq[4] = {0.f, 0.f, 0.f, 0.f}, tq[4] = {0.f, 0.f, 0.f, 0.f};
@@ -846,7 +811,7 @@ __device__ __forceinline__ void ker_phase(const FA& a, int p, int b, int k, unsi
     if (l >= R || c >= C) Xb[l * SB + c] = from_f32<T>(0.f);
   }
   __syncthreads();  // every operand above has landed
-  if (GGD_MK_FUSE_KD && si < R) {
+  if (si < R) {
     float4 y = part[0];
 #pragma unroll
     for (int c = 1; c < 8; ++c) {
@@ -858,7 +823,7 @@ __device__ __forceinline__ void ker_phase(const FA& a, int p, int b, int k, unsi
     *(float4*)(Hs + si * SH + sc) =
         make_float4(sres.x + (y.x + sb2.x), sres.y + (y.y + sb2.y), sres.z + (y.z + sb2.z), sres.w + (y.w + sb2.w));
   }
-  if constexpr (GGD_MK_FUSE_KD) bar_lds();
+  bar_lds();
   // the emb operands, in flight across LN_out, eps and the update (issued after the wait above, so
   // that it does not hold for them)
   WGemm<T, 2, KTE, 1> ge(a.w_emb, KTE, 0);
@@ -872,7 +837,7 @@ __device__ __forceinline__ void ker_phase(const FA& a, int p, int b, int k, unsi
   STAMP(1);
   if (16 * wave < C) {
     f32x4 acc[1][1];
-    go.template run<true, GGD_MK_FENCE_EPS>(acc, Xn, Frag<T>::SX, lane);
+    go.template run<true, -1>(acc, Xn, Frag<T>::SX, lane);
     *(float4*)(E + c16 * SE + 16 * wave + 4 * g4) =
         make_float4(acc[0][0][0] + bo.x, acc[0][0][1] + bo.y, acc[0][0][2] + bo.z, acc[0][0][3] + bo.w);
   }

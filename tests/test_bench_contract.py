@@ -44,7 +44,7 @@ def test_clip_step_flops_hand_count():
     assert abs((tw - conv2) / 1e6 - 11839.6) < 0.1
 
 
-@pytest.mark.parametrize("workload,prefix", [("c2", "mk_kernel"), ("c5", "psk_kernel")])
+@pytest.mark.parametrize("workload,prefix", [("c2", "mr_kernel"), ("c5", "psk_kernel")])
 def test_pmc_traffic_reads_committed_summary(workload, prefix):
     tr = bench.pmc_traffic(prefix, workload)
     assert tr is not None and os.path.exists(os.path.join(ROOT, tr["source"]))
@@ -109,7 +109,7 @@ def test_rehearsal_at_the_c5_eight_gpu_shape():
 def test_headline_pmc_summary_matches_the_kernel_sources():
     """The default (driver-run) C2 line prices its roofline traffic from a PMC summary taken on THIS
     csrc/ tree: a kernel change has to come with a fresh summary (scripts/pmc_all.sh)."""
-    tr = bench.pmc_traffic("mk_kernel", "c2")
+    tr = bench.pmc_traffic("mr_kernel", "c2")
     assert tr is not None and not tr.get("stale"), tr
     assert tr["bytes_per_launch"] > 0
 

@@ -11,8 +11,8 @@ Unlike a short trajectory's final sample (x_T and the shared noise dominate it n
 has no such floor: the bf16 bound of SURVEY.md 8d, eps rel-RMS <= 1e-2, applies directly.
 
 Routes (include/ggd.h GGD_ROUTE_*): the clip-group persistent loop (C2 / C3): bf16 on the row-block
-decomposition mr_kernel (ggd_rows.hip, GGD_ROUTE_MEGA_ROWS = 1) and on the head / chunk one mk_kernel
-(the default), f32 on mk_kernel; the one-workgroup-per-clip loop and the clip-pair loop psk_kernel (C5), the long-clip loop
+decomposition mr_kernel (ggd_rows.hip), f32 on the head / chunk one mk_kernel (ggd_mega.hip); the
+one-workgroup-per-clip loop and the clip-pair loop psk_kernel (C5), the long-clip loop
 lk_kernel (C4: fp8 step weights on block-scaled fp8 MFMA -- the default, e4m3 activations too, bound
 SURVEY.md 8d fp8 eps rel-RMS <= 1e-1 -- or widened into bf16 MFMAs, and bf16).  Weights: reference init with perturbed LN / BN
 (perturb=True), as models/modules/transformer.py:88-118 and models/model.py:94-112 run them.
@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 
 D_POSE = 123
 T_SPREAD = (999, 731, 402, 118, 0)
-ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_LONG_LOOP, ROUTE_FP8_MFMA, ROUTE_MEGA_ROWS = 0, 1, 7, 9, 10
+ROUTE_PER_CLIP, ROUTE_PAIR, ROUTE_LONG_LOOP, ROUTE_FP8_MFMA = 0, 1, 7, 9
 INFO_PAIR_LAUNCHES, INFO_LONG_LAUNCHES, INFO_ROWS_LOOP = 2, 6, 9
 PERTURBED = "pose_decoder.layers.0.cross_attn.output.weight"
 
@@ -46,9 +46,8 @@ def _info(ctx, what):
 
 # route name -> (dtype, clips, L, wav samples, per-clip mode, pair mode, bound on eps / pred_x_start)
 ROUTES = {
-    "mk_bf16": ("bf16", 4, 40, 32000, 1, 0, 1e-2),     # head / chunk clip-group loop (mk_kernel, default)
-    "mkr_bf16": ("bf16", 4, 40, 32000, 1, 0, 1e-2),    # row-block clip-group loop (mr_kernel, GGD_ROUTE_MEGA_ROWS 1)
-    "mk_f32": ("f32", 3, 40, 32000, 1, 0, 1e-5),
+    "mr_bf16": ("bf16", 4, 40, 32000, 1, 0, 1e-2),     # row-block clip-group loop (mr_kernel)
+    "mk_f32": ("f32", 3, 40, 32000, 1, 0, 1e-5),       # head / chunk clip-group loop (mk_kernel)
     "psk_bf16": ("bf16", 4, 40, 32000, 2, 1, 1e-2),
     "pair_bf16": ("bf16", 4, 40, 32000, 2, 2, 1e-2),
     "lk_fp8": ("fp8", 2, 160, 128000, 0, 0, 1e-1),     # block-scaled fp8 MFMA (GGD_ROUTE_FP8_MFMA 0)
@@ -98,7 +97,6 @@ def run_route(pkg, beat_cfg, sd, route, ts, seed=5):
         assert ctx.lib.ggd_set_route(ctx.h, ROUTE_PER_CLIP, {0: 0, 1: 1, 2: 2}[per_clip]) == 0
         assert ctx.lib.ggd_set_route(ctx.h, ROUTE_PAIR, pair) == 0
         assert ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 1 if route == "lk_fp8w" else 0) == 0
-        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_MEGA_ROWS, 1 if route == "mkr_bf16" else 0) == 0
         for t in ts:
             x = th.randn(n, D_POSE, L, generator=g)
             z = th.randn(1, n, D_POSE, L, generator=g)
@@ -107,10 +105,9 @@ def run_route(pkg, beat_cfg, sd, route, ts, seed=5):
                 assert int(_info(ctx, INFO_PAIR_LAUNCHES)) == 1
             if route.startswith("lk"):
                 assert int(_info(ctx, INFO_LONG_LAUNCHES)) == 1
-            if route.startswith("mk"):
-                assert int(_info(ctx, INFO_ROWS_LOOP)) == (1 if route == "mkr_bf16" else 0)
+            if route.startswith("m"):
+                assert int(_info(ctx, INFO_ROWS_LOOP)) == (1 if route == "mr_bf16" else 0)
     finally:
-        ctx.lib.ggd_set_route(ctx.h, ROUTE_MEGA_ROWS, 0)
         ctx.lib.ggd_set_route(ctx.h, ROUTE_PER_CLIP, 0)
         ctx.lib.ggd_set_route(ctx.h, ROUTE_PAIR, 0)
         ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0)

@@ -417,7 +417,7 @@ def test_inpaint_model_generate_sample_f32(pkg, setup_inp):
 
 # ------------------------------------------------------------------------------------------
 # Route selection of ggd_sample (bf16): the one-workgroup-per-clip loop (psk_kernel) is chosen
-# automatically when the clip-group loop (mk_kernel) would need >= 3 chunks (the C5 shape,
+# automatically when the clip-group loop (bf16: mr_kernel) would need >= 3 chunks (the C5 shape,
 # 128 clips per GPU); both must agree with the oracle and with each other.
 # ------------------------------------------------------------------------------------------
 
@@ -573,7 +573,7 @@ def test_unresident_loops_fall_back_on_device_bf16(pkg, beat_cfg, setup, sync, s
         model.sync()
         timeouts0 = _info(ctx, INFO_BARRIER_TIMEOUTS)
         assert ctx.lib.ggd_set_route(ctx.h, ROUTE_SIM_UNRESIDENT, sim) == 0
-        _route(ctx, 1)                                        # clip-group loop (mk_kernel), never resident
+        _route(ctx, 1)                                        # clip-group loop (mr_kernel), never resident
         outs["mk_sim"] = run()
         model.sync()                                          # no error: the fallback ran the clips
         assert _info(ctx, INFO_GATED_FALLBACKS) == 1
