@@ -77,14 +77,15 @@ __device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_dst) {
                : "memory");
 }
 template <int NK>
-__device__ __forceinline__ void w2_dma(const void* w, unsigned char* dst, int wave, int lane) {
+__device__ __forceinline__ void w2_dma_range(const void* w, unsigned char* dst, int wave, int lane, int p0, int p1) {
   typedef __attribute__((address_space(3))) unsigned char lds_u8;
   const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_u8*)(dst + wave * 2 * NK * 1024));
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int k = 0; k < NK; ++k)
-      glds16_asm((const char*)w + ((size_t)((2 * wave + j) * KT + k) * 64 + lane) * 16, base + (j * NK + k) * 1024);
+  for (int q = 0; q < 2 * NK; ++q) {
+    if (q < p0 || q >= p1) continue;
+    const int j = q / NK, k = q % NK;
+    glds16_asm((const char*)w + ((size_t)((2 * wave + j) * KT + k) * 64 + lane) * 16, base + (j * NK + k) * 1024);
+  }
 }
 // this wave's two tiles' k step k from such a copy
 template <int NK, int J>
@@ -158,9 +159,13 @@ __device__ __forceinline__ void ln_publish_row(const float* Hr, int R, T* img_ro
 // ------------------------------------------------------------------------------------------
 // KA: LN1 image -> QKV of head h + conv + self-attention (ka_phase without the residual rows)
 // ------------------------------------------------------------------------------------------
-template <int RT, int CP, typename FA, typename H, typename H0>
+// step(k): issued after the QKV GEMM's k step k (the next phases' weight streams, spread over the GEMM
+// instead of issued in one batch in front of the GEMM / the attention: 67.78 -> 67.52 ms per C2
+// launch with KE's emb loads behind LN_out, one box, profiles/r06l_c2_rows_issue_ab.txt); hook: after
+// the attention
+template <int RT, int CP, typename FA, typename H, typename HS>
 __device__ __forceinline__ void ka_rows(const FA& a, int h, int b, unsigned char* smem, Pre1<T, RT>& pre, H&& hook,
-                                        H0&& hook0) {
+                                        HS&& step) {
   using RP = RowPlan<RT>;
   const int tid = ltid(), lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int L = a.L, c16 = lane & 15, g4 = lane >> 4;
@@ -180,13 +185,12 @@ __device__ __forceinline__ void ka_rows(const FA& a, int h, int b, unsigned char
   so.store(Xn);
   bar_lds();
   STAMP(1);
-  // half of KB's CA out-projection weights into LDS while the QKV GEMM runs (KB's operand intake is
-  // its bound: round 6)
-  w2_dma<RowPlan<RT>::GCK>(a.w.o_ca, smem + RowPlan<RT>::GC, wave, lane);
+  // (the QKV GEMM's step hook issues KB's SA out-projection tile 0 and the LDS-DMA of most of KB's CA
+  // out-projection weights: KB's operand intake is its bound, round 6)
   using AT = FAtt<T, RT * 16>;
   {
     f32x4 acc[RT][1];
-    gm.template run<true>(acc, Xn, SX, lane, nq);
+    gm.template run_then<true>(acc, Xn, SX, lane, [&](int k) { step(k); }, nq);
     if (nq) {
       f32x4 v[RT];
 #pragma unroll
@@ -207,7 +211,6 @@ __device__ __forceinline__ void ka_rows(const FA& a, int h, int b, unsigned char
   }
   bar_lds();
   STAMP(2);
-  hook0();
   if (L <= 32)
     fattn<T, 2, RT * 16, false, CP>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
   else
@@ -217,7 +220,7 @@ __device__ __forceinline__ void ka_rows(const FA& a, int h, int b, unsigned char
   STAMP_END(3);
 }
 
-// KB's SA out-projection tiles 2w, 2w + 1, issued by KA's hooks around its attention.  (The query
+// KB's SA out-projection tiles 2w, 2w + 1: tile 0 issued inside KA's QKV GEMM, tile 1 after its attention.  (The query
 // tiles are issued in KB behind its staging loads: vector loads complete in issue order, so a
 // stream issued in KA in front of them delays the staging -- measured: 256 KiB of KA-issued weights
 // made KB's staging 2.15 us instead of ~0.7, profiles/r05b_stamps_rows.txt.)
@@ -229,6 +232,11 @@ struct KBRPre {
     go.tiles[1] = 2 * wave + 1;
   }
   __device__ __forceinline__ void load_tile(int j, int lane) { go.load_tile(j, lane); }
+  __device__ __forceinline__ void load_tile_step(int j, int k, int lane) {
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+    const u32x4 v = ggd::G((const u32x4*)go.W)[((size_t)go.tiles[j] * KT + k) * 64 + lane];
+    go.wb[j][k] = make_uint4(v.x, v.y, v.z, v.w);
+  }
   static constexpr int TILE_LOADS = decltype(go)::G;
 };
 
@@ -654,10 +662,10 @@ __device__ __forceinline__ void ke_rows(const FA& a, T* xn, int p, int b, int k,
   WGemm<T, 2, KTE, 1> ge(a.w_emb, KTE, 0);
   ge.tiles[0] = 2 * wave;
   ge.tiles[1] = 2 * wave + 1;
-  ge.load(0, lane);
   float4 pe[2];
   emb_init(a, r0, lane, wave, pe);
   ln_rows_wave<T>(Hs, R, Xn, lane, wave);
+  ge.load(0, lane);
   bar_lds();
   STAMP(1);
   if (16 * wave < C) {
@@ -739,7 +747,13 @@ __global__ void __launch_bounds__(FT) mr_kernel(MegaArgs m, int G) {
       cfa_t f = fa0 + 4 * li;
       asm volatile("" : "+s"(f));  // per-layer arguments are re-read, not held across the loop
       KBRPre pb(f[0], wave);
-      ka_rows<RT, CPV>(f[0], part, b, smem, pn, [&] { pb.load_tile(1, lane); }, [&] { pb.load_tile(0, lane); });
+      ka_rows<RT, CPV>(f[0], part, b, smem, pn, [&] { pb.load_tile(1, lane); },
+                       [&](int k) {  // QKV k step k: the LDS-DMA pieces of it and tile 0's k step k
+                         constexpr int NP = 2 * RowPlan<RT>::GCK;
+                         w2_dma_range<RowPlan<RT>::GCK>(f[0].w.o_ca, smem + RowPlan<RT>::GC, wave, lane, k * NP / 8,
+                                                        (k + 1) * NP / 8);
+                         pb.load_tile_step(0, k, lane);
+                       });
       if (!mk_sync<CPV, KBRPre::TILE_LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
       // (the four per-layer argument blocks differ only in h / h_out, which these phases read as f[1] /
       // f[3] hold them: h; and in the phase-stamp pointer of the diagnostics)
