@@ -123,7 +123,7 @@ WORKLOADS = {
 # this same command (scripts/pmc_all.sh -> scripts/pmc.sh + pmc_summary.py: 2 x FETCH_SIZE +
 # WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), one summary per workload; PMC cannot
 # run inside the timed region, so the figure is the profile's, keyed by kernel symbol and workload
-PMC_SUMMARY = {"c2": "r05zf", "c4": "r05zf", "c5": "r05zf"}   # profile tag per workload (its dominant kernel's code)
+PMC_SUMMARY = {"c2": "r06m", "c4": "r06m", "c5": "r06m"}   # profile tag per workload (its dominant kernel's code)
 
 
 def csrc_hash():
@@ -154,13 +154,15 @@ def pmc_traffic(kernel_prefix, workload):
     if d.get("_csrc") != csrc_hash():   # the kernels changed since the counters were taken: no traffic figure
         return {"stale": True, "source": os.path.relpath(path, ROOT), "summary_csrc": d.get("_csrc"),
                 "current_csrc": csrc_hash()}
+    best = None   # the busiest instantiation: a gated stand-in launch (e.g. the write-through re-run) exits at once
     for k, e in d.items():
         name = k.replace("(anonymous namespace)::", "")
         if name.startswith("void ggd::" + kernel_prefix) and "hbm_read_bytes" in e and "hbm_write_bytes" in e:
-            return {"bytes_per_launch": e["hbm_read_bytes"] + e["hbm_write_bytes"],
-                    "read": e["hbm_read_bytes"], "write": e["hbm_write_bytes"],
-                    "source": os.path.relpath(path, ROOT)}
-    return None
+            tot = e["hbm_read_bytes"] + e["hbm_write_bytes"]
+            if best is None or tot > best["bytes_per_launch"]:
+                best = {"bytes_per_launch": tot, "read": e["hbm_read_bytes"], "write": e["hbm_write_bytes"],
+                        "kernel": name, "source": os.path.relpath(path, ROOT)}
+    return best
 
 
 def parse():
