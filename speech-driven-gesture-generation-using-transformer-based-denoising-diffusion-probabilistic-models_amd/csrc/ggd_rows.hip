@@ -163,9 +163,9 @@ __device__ __forceinline__ void ln_publish_row(const float* Hr, int R, T* img_ro
 // instead of issued in one batch in front of the GEMM / the attention: 67.78 -> 67.52 ms per C2
 // launch with KE's emb loads behind LN_out, one box, profiles/r06l_c2_rows_issue_ab.txt); hook: after
 // the attention
-template <int RT, int CP, typename FA, typename H, typename HS>
+template <int RT, int CP, typename FA, typename H, typename HS, typename H0>
 __device__ __forceinline__ void ka_rows(const FA& a, int h, int b, unsigned char* smem, Pre1<T, RT>& pre, H&& hook,
-                                        HS&& step) {
+                                        HS&& step, H0&& hook0) {
   using RP = RowPlan<RT>;
   const int tid = ltid(), lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int L = a.L, c16 = lane & 15, g4 = lane >> 4;
@@ -211,6 +211,7 @@ __device__ __forceinline__ void ka_rows(const FA& a, int h, int b, unsigned char
   }
   bar_lds();
   STAMP(2);
+  hook0();
   if (L <= 32)
     fattn<T, 2, RT * 16, false, CP>(att, L, L, a.scale, (T*)a.o_sa + (size_t)b * L * FD + h * FDK, FD);
   else
@@ -220,17 +221,22 @@ __device__ __forceinline__ void ka_rows(const FA& a, int h, int b, unsigned char
   STAMP_END(3);
 }
 
-// KB's SA out-projection tiles 2w, 2w + 1: tile 0 issued inside KA's QKV GEMM, tile 1 after its attention.  (The query
-// tiles are issued in KB behind its staging loads: vector loads complete in issue order, so a
-// stream issued in KA in front of them delays the staging -- measured: 256 KiB of KA-issued weights
-// made KB's staging 2.15 us instead of ~0.7, profiles/r05b_stamps_rows.txt.)
+// KB's SA out-projection tiles 2w, 2w + 1 (tile 0 issued inside KA's QKV GEMM, tile 1 after its
+// attention) and its query tiles of head w (issued in KA before the attention, where the registers are
+// free: C2 mr_kernel 67.87 -> 67.58 ms against streaming them into the registers KB's SA out-projection
+// frees; 2 / 4 / 6 of the 8 k steps early: 68.6-68.9 / 68.5 / 68.0-68.2 ms, one box,
+// profiles/r06n_c2_rows_qhead_ab.txt).  All of it lands before KB's staging does (vector loads
+// complete in issue order), so it must be in flight early: KA's QKV GEMM and attention cover it.
 struct KBRPre {
-  WGemm<T, 2, KT, 1> go;
+  WGemm<T, 2, KT, 1> go, gq;
   template <typename FA>
-  __device__ __forceinline__ KBRPre(const FA& a, int wave) : go(a.w.o_sa, KT, 0) {
+  __device__ __forceinline__ KBRPre(const FA& a, int wave) : go(a.w.o_sa, KT, 0), gq(a.w.q_ca, KT, 0) {
     go.tiles[0] = 2 * wave;
     go.tiles[1] = 2 * wave + 1;
+    gq.tiles[0] = 2 * wave;
+    gq.tiles[1] = 2 * wave + 1;
   }
+  __device__ __forceinline__ void load_q(int lane) { gq.load(0, lane); }
   __device__ __forceinline__ void load_tile(int j, int lane) { go.load_tile(j, lane); }
   __device__ __forceinline__ void load_tile_step(int j, int k, int lane) {
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
@@ -263,9 +269,9 @@ __device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int t_orig, u
   STAMP(0);
   // ---- loads, in the order they are needed (vector loads retire in issue order, so a load issued
   // behind a weight stream is not usable before the whole stream has landed): the staging, then the
-  // small operands of LN2 / the step-token fix / the query epilogue, then the query weights, the
-  // memory K / V fragments and last the CA out-projection weights (round 6: issued behind the
-  // query stream, the conv taps made the SA out-projection segment wait for it, 3.3 us)
+  // small operands of LN2 / the step-token fix / the query epilogue, the memory K / V fragments and
+  // last the CA out-projection weights not in LDS (round 5 issued the conv taps behind the query
+  // weight stream: the SA out-projection segment waited for it, 3.3 us)
   RowsStage<16, CP> so;
   so.load((const T*)a.o_sa + row0 * FD, r0 - 1, L);
   const int hs = (tid >> 6) & 1, hc = 4 * (tid & 63);  // halo residual rows: tokens r0 - 1 / r1 (tid < 128)
@@ -287,13 +293,10 @@ __device__ __forceinline__ void kb_rows(const FA& a, int p, int b, int t_orig, u
   if (tid < 128) *(uint4*)(Hr + (hs ? R + 1 : 0) * SH + hc) = hv;
   bar_lds();
   STAMP(1);
-  // ---- SA out-projection + residual (rows 0 .. 15).  The query tiles of head w (q_ca tiles 2w,
-  // 2w + 1) stream into the registers the SA tiles held, k step by k step as the out-projection
-  // frees them, in flight across LN2
-  WGemm<T, 2, KT, 1> gq(w.q_ca, KT, 0);
-  gq.tiles[0] = 2 * wave;
-  gq.tiles[1] = 2 * wave + 1;
-  residual_gemm_then<T, KT, 2, 1>(Hr, Oi, SX, pre.go, bo, lane, wave, [&](int k) { gq.load_step(k, lane); });
+  // ---- SA out-projection + residual (rows 0 .. 15); the query tiles of head w (q_ca tiles 2w, 2w + 1)
+  // were issued in KA
+  auto& gq = pre.gq;
+  residual_gemm<T, KT, 2, 1>(Hr, Oi, SX, pre.go, bo, lane, wave);
   // memory K / V^T fragments of head w (kvc block: K [64][32] | V^T [32][64], keys 0 / 1 zero): the
   // lane's query dims are {4 g4 .. + 3} u {16 + 4 g4 .. + 3} (the transposed query GEMM's lane map),
   // so its K fragment holds those dims of key 16 t + c16 -- the contraction runs in that order
@@ -753,7 +756,8 @@ __global__ void __launch_bounds__(FT) mr_kernel(MegaArgs m, int G) {
                          w2_dma_range<RowPlan<RT>::GCK>(f[0].w.o_ca, smem + RowPlan<RT>::GC, wave, lane, k * NP / 8,
                                                         (k + 1) * NP / 8);
                          pb.load_tile_step(0, k, lane);
-                       });
+                       },
+                       [&] { pb.load_q(lane); });
       if (!mk_sync<CPV, KBRPre::TILE_LOADS>(ctr, flags, part, ++epoch, m.status, &s_ok, st, [] {}, ar)) return;
       // (the four per-layer argument blocks differ only in h / h_out, which these phases read as f[1] /
       // f[3] hold them: h; and in the phase-stamp pointer of the diagnostics)
