@@ -4,6 +4,13 @@
 #pragma once
 #include "ggd_phases.h"
 
+#ifndef GGD_POLLER_LATE
+#define GGD_POLLER_LATE 0
+#endif
+#ifndef GGD_POLL2
+#define GGD_POLL2 0
+#endif
+
 namespace ggd {
 
 // every wait is bounded by elapsed time (wait_expired, ggd_common.h)
@@ -126,9 +133,18 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
       const int off = (threadIdx.x & 7) * 4;
       int ok = 1;
       const unsigned t0 = wait_t0();
+#if GGD_POLL2
+      unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
+      for (int spin = 0;; ++spin) {
+        const unsigned vn = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);  // in flight while v is checked
+        __builtin_amdgcn_sched_barrier(0);
+        if (__ballot(v < epoch) == 0) break;
+        v = vn;
+#else
       for (int spin = 0;; ++spin) {
         const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
         if (__ballot(v < epoch) == 0) break;
+#endif
         if ((spin & 255) == 255) {
           const bool expired = wait_expired(t0);
           if (expired || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -160,8 +176,13 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
       *s_ok = ok;
     }
   }
+#if !GGD_POLLER_LATE
   if (poller) prefetch();
+#endif
   bar_lds();
+#if GGD_POLLER_LATE
+  if (poller) prefetch();
+#endif
   if (st && threadIdx.x == 0) st[2 * (epoch - 2) + 1] = __builtin_amdgcn_s_memtime();
   if (arr && threadIdx.x == 0) arr[2 * (8 * (epoch - 2) + part) + 1] = __builtin_amdgcn_s_memrealtime();
   return *s_ok != 0;
