@@ -4,12 +4,6 @@
 #pragma once
 #include "ggd_phases.h"
 
-#ifndef GGD_POLLER_LATE
-#define GGD_POLLER_LATE 0
-#endif
-#ifndef GGD_POLL2
-#define GGD_POLL2 0
-#endif
 
 namespace ggd {
 
@@ -126,25 +120,18 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
     if (threadIdx.x == 0) mk_add(ctr, 1u);
   }
   const bool poller = threadIdx.x < 64;
-  if (!poller) prefetch();
+  if (!poller) prefetch();  // (the poller issues its share before the exit barrier, not after: round 6
+                            // measured 69.7 vs 67.6 ms per C2 launch; two polls in flight: 68.0,
+                            // profiles/r06q_c2_barrier_poll_ab.txt)
   if constexpr (CPV == CP_XL) {  // vector poll (a poll load retires behind the wave's earlier loads:
     if (threadIdx.x < 64) {      // the poller issues its prefetch after it)
       const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
       const int off = (threadIdx.x & 7) * 4;
       int ok = 1;
       const unsigned t0 = wait_t0();
-#if GGD_POLL2
-      unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
-      for (int spin = 0;; ++spin) {
-        const unsigned vn = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);  // in flight while v is checked
-        __builtin_amdgcn_sched_barrier(0);
-        if (__ballot(v < epoch) == 0) break;
-        v = vn;
-#else
       for (int spin = 0;; ++spin) {
         const unsigned v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, CP_COH);
         if (__ballot(v < epoch) == 0) break;
-#endif
         if ((spin & 255) == 255) {
           const bool expired = wait_expired(t0);
           if (expired || __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -176,13 +163,8 @@ __device__ __forceinline__ bool mk_sync(unsigned* ctr, unsigned* flags, int part
       *s_ok = ok;
     }
   }
-#if !GGD_POLLER_LATE
   if (poller) prefetch();
-#endif
   bar_lds();
-#if GGD_POLLER_LATE
-  if (poller) prefetch();
-#endif
   if (st && threadIdx.x == 0) st[2 * (epoch - 2) + 1] = __builtin_amdgcn_s_memtime();
   if (arr && threadIdx.x == 0) arr[2 * (8 * (epoch - 2) + part) + 1] = __builtin_amdgcn_s_memrealtime();
   return *s_ok != 0;
