@@ -69,7 +69,7 @@ t = diag(11, [2], 80)
 labels = {0: "KA ln|qkv+conv|-|attn", 1: "KB load|oproj|ln2|q+conv|fix|attn", 2: "KC load|oproj|ln3|ffn1|ffn2",
           3: "KD sum|-|store", 4: "KE ln+out|stage|upd"} if HEADS else \
     {0: "KA stage|qkv+conv|attn", 1: "KB stage|sa-oproj|ln2+fix|q+conv+ca|ca-oproj+ln3", 2: "KC stage|ffn1|ffn2",
-     3: "KD sum+ln1", 4: "KE kd+ln|eps|upd|emb+ln1"}
+     3: "KD sum+ln1", 4: "KE loads|sum|ln|eps|upd|emb+ln1"}
 for j in range(5):
     v = [round(x, 2) for x in t[16 * j + 1:16 * j + 8] if x >= 0]
     print(f"{labels[j]:40s} {v}", flush=True)

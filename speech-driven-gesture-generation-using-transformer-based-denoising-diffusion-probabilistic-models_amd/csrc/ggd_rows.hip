@@ -649,6 +649,7 @@ __device__ __forceinline__ void ke_rows(const FA& a, T* xn, int p, int b, int k,
     if (l >= R || c >= C) Xb[l * SB + c] = from_f32<T>(0.f);
   }
   __syncthreads();
+  STAMP(1);
   if (si < R) {
     float4 y = part[0];
 #pragma unroll
@@ -662,6 +663,7 @@ __device__ __forceinline__ void ke_rows(const FA& a, T* xn, int p, int b, int k,
         make_float4(sres.x + (y.x + sb2.x), sres.y + (y.y + sb2.y), sres.z + (y.z + sb2.z), sres.w + (y.w + sb2.w));
   }
   bar_lds();
+  STAMP(2);
   WGemm<T, 2, KTE, 1> ge(a.w_emb, KTE, 0);
   ge.tiles[0] = 2 * wave;
   ge.tiles[1] = 2 * wave + 1;
@@ -670,7 +672,7 @@ __device__ __forceinline__ void ke_rows(const FA& a, T* xn, int p, int b, int k,
   ln_rows_wave<T>(Hs, R, Xn, lane, wave);
   ge.load(0, lane);
   bar_lds();
-  STAMP(1);
+  STAMP(3);
   if (16 * wave < C) {
     f32x4 acc[1][1];
     go.template run<true>(acc, Xn, SX, lane);
@@ -681,7 +683,7 @@ __device__ __forceinline__ void ke_rows(const FA& a, T* xn, int p, int b, int k,
     philox_normal4(((uint64_t)rec.seed_hi << 32) | rec.seed_lo, rec.clip_offset + (uint32_t)b, (uint32_t)rec.i,
                    TAG_STEP, (uint32_t)qi, zq);
   bar_lds();
-  STAMP(2);
+  STAMP(4);
   {
     const OutRowsP<CP> xo(a.x, (uint32_t)(sizeof(float) * plane));
 #pragma unroll
@@ -704,9 +706,9 @@ __device__ __forceinline__ void ke_rows(const FA& a, T* xn, int p, int b, int k,
     }
   }
   bar_lds();
-  STAMP(3);
+  STAMP(5);
   emb_rows_publish<CP>(a, xn, b, r0, R, Xb, ge, pe, Hr, lane, wave);
-  STAMP_END(4);
+  STAMP_END(6);
 }
 
 template <int RT, int LKT, int CPV>
