@@ -1,8 +1,8 @@
 #!/bin/bash
 # A/B variant of libggd.so: one translation unit rebuilt with extra defines (or from its current
 # source), every other object the in-tree build's:
-#   bash scripts/build_variant.sh NAME "-DGGD_MK_FUSE_KD=1" [UNIT]   -> ab/libggd_NAME.so
-# UNIT defaults to ggd_mega (the persistent loop); run the normal build first.
+#   bash scripts/build_variant.sh NAME "-DSOME_SWITCH=1" [UNIT]   -> ab/libggd_NAME.so
+# UNIT defaults to ggd_mega (the f32 clip-group loop; ggd_rows is the bf16 one); run the normal build first.
 cd "$(dirname "$0")/.." || exit 1
 P=speech-driven-gesture-generation-using-transformer-based-denoising-diffusion-probabilistic-models_amd
 U=${3:-ggd_mega}
