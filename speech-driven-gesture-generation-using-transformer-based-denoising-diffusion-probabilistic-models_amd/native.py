@@ -204,7 +204,7 @@ def load():
         "ggd_tr_head_flatten": (ctypes.c_int, [I32, I32, I32, I32, VP, VP, I32, VP]),
         "ggd_enc_frontend": (ctypes.c_int, [CTX, VP, I32, VP, VP]),
     }
-    if LIB_PATH == DIAG_LIB:
+    if LIB_PATH == DIAG_LIB or hasattr(lib, "ggd_diag"):  # (also a GGD_LIB diag variant, scripts/build_variant.sh)
         sig["ggd_diag"] = (ctypes.c_int, [CTX, I32, VP, I32, I32, VP])
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
