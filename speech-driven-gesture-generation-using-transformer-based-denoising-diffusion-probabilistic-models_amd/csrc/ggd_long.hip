@@ -221,6 +221,7 @@ typedef const __attribute__((address_space(4))) ChainStage* cst_t;
 typedef const __attribute__((address_space(4))) LongArgs cla_T;  // the kernel's argument block, in place
 typedef const __attribute__((address_space(4))) LongLayer* cll_t;
 
+constexpr int LK_UPD_NW = (128 * (CH_MT / 4) + CH_NT - 1) / CH_NT;  // update items per thread (C <= 128)
 template <bool W8, int TGB>
 struct LkCtx {
   cla_T& a;
@@ -233,6 +234,7 @@ struct LkCtx {
   unsigned lane16;
   BBuf<W8, TGB> bb[LK_DEPTH];
   f32x4 acc[2][TGB];
+  float uxo[LK_UPD_NW][4], uz[LK_UPD_NW][4];  // the update's x (and injected noise), loaded at PO (lk_update_load)
 };
 
 template <bool W8, int KIND, int IT, class X>
@@ -244,31 +246,59 @@ __device__ __forceinline__ void lk_issue(X& x) {
   ch_load<W8, GE::TGB>(x.bb[IT % LK_DEPTH], wb, x.lane16, (l / nch) * CH_WAVES * tg, l % nch, upt, tg);
 }
 
+// The update's loads: a thread's <= 2 items' x (and injected noise), issued at the start of the PO
+// stage so that they land during LN_out and out_layers (round 6: loaded inside the update they cost a
+// memory round trip after the eps rows were ready)
+template <class X>
+__device__ __forceinline__ void lk_update_load(X& x) {
+  cla_T& a = x.a;
+  const int C = a.C, L = a.L, l0 = x.part * CH_MT, NWI = C * (CH_MT / 4);
+  const float* xg = a.x + ((size_t)x.b * L + l0) * C;
+#pragma unroll
+  for (int k = 0; k < LK_UPD_NW; ++k) {
+    const int w = min(ltid() + k * CH_NT, NWI - 1);  // clamped: a thread past the items loads a valid one
+    const int c = w / (CH_MT / 4), q4 = (w % (CH_MT / 4)) * 4, l = l0 + q4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x.uxo[k][i] = ld_f32<CP_COH>(xg, (uint32_t)((q4 + i) * C + c));
+    if (a.noise) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x.uz[k][i] = a.noise[(size_t)x.it * a.n * C * L + ((size_t)x.b * C + c) * L + l + i];
+    }
+  }
+}
+
+// one work item = channel c x 4 consecutive frames: one Philox call gives their 4 normals
+// (counter quad (c L + l) / 4, update_kernel's element -> quad map; L and l0 are multiples of 32);
+// x / injected noise from lk_update_load
 template <class X>
 __device__ __forceinline__ void lk_update(X& x, bool to_xs) {
-  // one work item = channel c x 4 consecutive frames: one Philox call gives their 4 normals
-  // (counter quad (c L + l) / 4, update_kernel's element -> quad map; L and l0 are multiples of 32)
   cla_T& a = x.a;
-  const int C = a.C, L = a.L, l0 = x.part * CH_MT;
+  const int C = a.C, L = a.L, l0 = x.part * CH_MT, NWI = C * (CH_MT / 4);
+  constexpr int NW = LK_UPD_NW;
   const StepRec r = a.steps[x.it];
   const float* eps = (const float*)x.hh;
   float* xg = a.x + ((size_t)x.b * L + l0) * C;
   const uint64_t seed = ((uint64_t)r.seed_hi << 32) | r.seed_lo;
-  for (int w = ltid(); w < C * (CH_MT / 4); w += CH_NT) {
-    const int c = w / (CH_MT / 4), q4 = (w % (CH_MT / 4)) * 4, l = l0 + q4;
-    float z[4];
-    if (a.noise) {
+  auto& xo = x.uxo;
+  auto& z = x.uz;
+  if (!a.noise) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) z[i] = a.noise[(size_t)x.it * a.n * C * L + ((size_t)x.b * C + c) * L + l + i];
-    } else {
-      philox_normal4(seed, r.clip_offset + (uint32_t)x.b, (uint32_t)r.i, TAG_STEP, (uint32_t)(c * L + l) >> 2, z);
+    for (int k = 0; k < NW; ++k) {
+      const int w = min(ltid() + k * CH_NT, NWI - 1);
+      const int c = w / (CH_MT / 4), l = l0 + (w % (CH_MT / 4)) * 4;
+      philox_normal4(seed, r.clip_offset + (uint32_t)x.b, (uint32_t)r.i, TAG_STEP, (uint32_t)(c * L + l) >> 2, z[k]);
     }
+  }
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const int w = ltid() + k * CH_NT;
+    if (w >= NWI) continue;
+    const int c = w / (CH_MT / 4), q4 = (w % (CH_MT / 4)) * 4, l = l0 + q4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rr = q4 + i;
-      const float xo = ld_f32<CP_COH>(xg, (uint32_t)(rr * C + c));
       const float ev = eps[rr * EPS_STR + c];
-      const UpdOut o = upd_math(r, a.alg, xo, ev, false, 0.f, false, 0.f, 0.f, 0.f, z[i]);
+      const UpdOut o = upd_math(r, a.alg, xo[k][i], ev, false, 0.f, false, 0.f, 0.f, 0.f, z[k][i]);
       xg[rr * C + c] = o.xn;
       if (a.extras && x.it == a.k0 + a.n_steps - 1) {  // the last iteration's p_sample dict entries
         const size_t plane = (size_t)a.n * C * L, ncl = ((size_t)x.b * C + c) * L + l + i;
@@ -348,6 +378,7 @@ __device__ __forceinline__ void lk_iter(X& x) {
   unsigned char* const xs8 = (unsigned char*)x.xs;
   unsigned char* const hh8 = (unsigned char*)x.hh;
   if constexpr (IT + D1 < GE::TOTAL) lk_issue<W8, KIND, IT + D1>(x);
+  if constexpr (kind == SK_PO && l == 0) lk_update_load(x);
   if constexpr (l == 0 && si > 0) {  // stage hand-offs (LDS); the prefetched weights stay in flight
     ch_bar();
     if constexpr (kind == SK_F1 || kind == SK_P || kind == SK_PO || kind == SK_P2) {
@@ -368,6 +399,17 @@ __device__ __forceinline__ void lk_iter(X& x) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < TGB; ++j) x.acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  [[maybe_unused]] float pev[2][TGB][4];
+  if constexpr (kind == SK_E) {  // the PE rows of the epilogue, in flight across the MFMAs
+    const int L = x.a.L, l0 = x.part * CH_MT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < tg; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          pev[i][j][r] = x.a.pe[(size_t)((l0 + i * 16 + x.g4 + r) % L) * CH_D + (nt0 + j) * 16 + x.c16];
   }
   if constexpr (mx) {
     if constexpr (kind == SK_F2)
@@ -404,7 +446,7 @@ __device__ __forceinline__ void lk_iter(X& x) {
             const float y = fmaxf(v, 0.f);
             x.hh[row * HH_STR + n] = f2bf(y * y);
           } else if constexpr (kind == SK_E) {                    // EPI_PE: h = emb_x(x) + PE[frame]
-            x.hs[row * HS_STR + n] = v + x.a.pe[(size_t)((l0 + row) % L) * CH_D + n];
+            x.hs[row * HS_STR + n] = v + pev[i][j][r];
           } else if constexpr (kind == SK_PO) {                   // eps rows -> LDS (the update reads them)
             ((float*)x.hh)[row * EPS_STR + n] = v;
           } else {                                                 // EPI_T: hand-off rows
@@ -436,36 +478,66 @@ __device__ __forceinline__ void lk_chain(cla_T& a, cst_t sa, int b, int part, in
   x.b = b;
   x.part = part;
   x.it = it;
-  lk_issue<W8, KIND, 0>(x);
-  if constexpr (LK_DEPTH > 2 && GE::TOTAL > 1) lk_issue<W8, KIND, 1>(x);
-  if constexpr (LK_DEPTH > 3 && GE::TOTAL > 2) lk_issue<W8, KIND, 2>(x);
-  static_assert(LK_DEPTH >= 2 && LK_DEPTH <= 4, "the prologue issues LK_DEPTH - 1 iterations");
-  // parameters (bias | scale per stage, LayerNorm vectors), the first stage's A rows
+  // Parameters (bias | scale per stage, LayerNorm vectors) and the first stage's A rows (the attention
+  // output rows of the block, written by the head parts): every load is issued before the first LDS
+  // store -- one memory round trip, not one per stage and pass (round 6: the prologue took 3.4 us of
+  // chain B at 4 stages and 5.9 us at 6, profiles/r06aa_long_chain_stamps.txt) -- then the first
+  // iteration's weights, which arrive while the rows are stored.
+  constexpr int NPJ = 2;  // passes of CH_NT columns per stage (ncols <= 1024)
+  float pv[PL::NS][2][NPJ], lv[PL::NS][2];
 #pragma unroll
   for (int si = 0; si < PL::NS; ++si) {
     const float* wb = sa[si].w.b;
     const float* ws = sa[si].w.scale;
     const int np = PL::s[si].ncols;
-    for (int e = tid; e < np; e += CH_NT) {
-      x.prm[GE::prm(si) + e] = wb[e];
-      x.prm[GE::prm(si) + np + e] = W8 ? ws[e] : 1.0f;
+#pragma unroll
+    for (int j = 0; j < NPJ; ++j) {
+      const int e = min(tid + j * CH_NT, np - 1);  // clamped: a thread past the stage loads a valid element
+      pv[si][0][j] = wb[e];
+      pv[si][1][j] = W8 ? ws[e] : 1.0f;
     }
-    if (sa[si].ln_g && tid < CH_D) {
-      x.prm[GE::ln(si) + tid] = sa[si].ln_g[tid];
-      x.prm[GE::ln(si) + CH_D + tid] = sa[si].ln_b[tid];
+    const float* lg = sa[si].ln_g;
+    if (lg) {
+      const int t = min(tid, CH_D - 1);
+      lv[si][0] = lg[t];
+      lv[si][1] = sa[si].ln_b[t];
     }
   }
   static_assert(PL::s[0].kind == SK_R, "every chain phase opens with the attention output projection");
-  {  // attention output rows of the block (written by the head parts)
+  constexpr int NV = CH_MT * CH_D / 8 / CH_NT;
+  uint4 v[NV];
+  {
     const bf16_t* src = (const bf16_t*)a.att + ((size_t)b * a.L + part * CH_MT) * CH_D;
-    uint4 v[CH_MT * CH_D / 8 / CH_NT];
 #pragma unroll
-    for (int i = 0; i < CH_MT * CH_D / 8 / CH_NT; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int e = tid + i * CH_NT, r = e / (CH_D / 8), cv = e % (CH_D / 8);
       v[i] = ld_16B<CP_XL>(src, (uint32_t)((r * CH_D + 8 * cv) * 2));
     }
+  }
+  lk_issue<W8, KIND, 0>(x);
+  if constexpr (LK_DEPTH > 2 && GE::TOTAL > 1) lk_issue<W8, KIND, 1>(x);
+  if constexpr (LK_DEPTH > 3 && GE::TOTAL > 2) lk_issue<W8, KIND, 2>(x);
+  static_assert(LK_DEPTH >= 2 && LK_DEPTH <= 4, "the prologue issues LK_DEPTH - 1 iterations");
+  static_assert(NPJ * CH_NT >= CH_FF && CH_NT >= CH_D, "prologue passes");
 #pragma unroll
-    for (int i = 0; i < CH_MT * CH_D / 8 / CH_NT; ++i) {
+  for (int si = 0; si < PL::NS; ++si) {
+    const int np = PL::s[si].ncols;
+#pragma unroll
+    for (int j = 0; j < NPJ; ++j) {
+      const int e = tid + j * CH_NT;
+      if (e < np) {
+        x.prm[GE::prm(si) + e] = pv[si][0][j];
+        x.prm[GE::prm(si) + np + e] = pv[si][1][j];
+      }
+    }
+    if (sa[si].ln_g && tid < CH_D) {
+      x.prm[GE::ln(si) + tid] = lv[si][0];
+      x.prm[GE::ln(si) + CH_D + tid] = lv[si][1];
+    }
+  }
+  {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
       const int e = tid + i * CH_NT, r = e / (CH_D / 8), cv = e % (CH_D / 8);
       if constexpr (lk_mx<KIND, 0, MX>()) {  // e4m3 rows + the block scales: a block is 4 lanes' pieces
         // max |v| on the bf16 bits (non-negative bf16 order as integers: v_pk_max_u16), then two
@@ -508,30 +580,34 @@ constexpr int LA_SQ = 40;                    // Q / K operand row stride (bf16, 
 
 // Raw conv inputs: NM bf16 hand-off images of `rows` rows x 32 channels into LDS [NM][rows + 2][32]
 // (rows 0 and rows + 1 are the conv's zero padding), each 16-byte unit loaded once (no halo
-// re-reads), every load issued before the first LDS write.  src[m] = base + col[m] (row stride ld).
+// re-reads); load() issues them, store() writes them after the phase's other loads are issued
+// (lk_attn).  src[m] = base + col[m] (row stride ld).
 constexpr int LA_RAW_UNITS = (3 * ATT_LMAX * 4 + CH_NT - 1) / CH_NT;  // units per thread (max)
-template <int NM>
-__device__ __forceinline__ void la_stage_raw(const void* base, size_t row0, int ld, const int (&col)[3], int rows,
-                                             bf16_t* raw) {
-  const int tid = ltid(), per = rows * 4, total = NM * per;
+template <int NM> struct LaRaw {
   uint4 v[LA_RAW_UNITS];
+  __device__ __forceinline__ void load(const void* base, size_t row0, int ld, const int (&col)[3], int rows) {
+    const int tid = ltid(), per = rows * 4, total = NM * per;
 #pragma unroll
-  for (int i = 0; i < LA_RAW_UNITS; ++i) {
-    const int u = min(tid + i * CH_NT, total - 1), m = u / per, r = (u % per) / 4, cv = u % 4;
-    v[i] = ld_16B<CP_XL>(base, (uint32_t)(((row0 + r) * (size_t)ld + col[m] + cv * 8) * 2));
+    for (int i = 0; i < LA_RAW_UNITS; ++i) {
+      const int u = min(tid + i * CH_NT, total - 1), m = u / per, r = (u % per) / 4, cv = u % 4;
+      v[i] = ld_16B<CP_XL>(base, (uint32_t)(((row0 + r) * (size_t)ld + col[m] + cv * 8) * 2));
+    }
   }
+  __device__ __forceinline__ void store(int rows, bf16_t* raw) const {
+    const int tid = ltid(), per = rows * 4, total = NM * per;
 #pragma unroll
-  for (int i = 0; i < LA_RAW_UNITS; ++i) {
-    const int u = tid + i * CH_NT;
-    if (u >= total) continue;
-    const int m = u / per, r = (u % per) / 4, cv = u % 4;
-    *(uint4*)(raw + ((size_t)m * (rows + 2) + r + 1) * 32 + cv * 8) = v[i];
+    for (int i = 0; i < LA_RAW_UNITS; ++i) {
+      const int u = tid + i * CH_NT;
+      if (u >= total) continue;
+      const int m = u / per, r = (u % per) / 4, cv = u % 4;
+      *(uint4*)(raw + ((size_t)m * (rows + 2) + r + 1) * 32 + cv * 8) = v[i];
+    }
+    for (int u = tid; u < NM * 2 * 4; u += CH_NT) {  // halo rows
+      const int m = u / 8, h = (u / 4) % 2, cv = u % 4;
+      *(uint4*)(raw + ((size_t)m * (rows + 2) + h * (rows + 1)) * 32 + cv * 8) = make_uint4(0, 0, 0, 0);
+    }
   }
-  for (int u = tid; u < NM * 2 * 4; u += CH_NT) {  // halo rows
-    const int m = u / 8, h = (u / 4) % 2, cv = u % 4;
-    *(uint4*)(raw + ((size_t)m * (rows + 2) + h * (rows + 1)) * 32 + cv * 8) = make_uint4(0, 0, 0, 0);
-  }
-}
+};
 
 // conv of raw image m into its operand image: out[i] = b + w0 in[i-1] + w1 in[i] + w2 in[i+1]
 // (LaStrip::conv's expression); TRANS writes V^T.  wl = [w0|w1|w2|b][32] of this matrix.
@@ -584,53 +660,82 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
   float* wl = (float*)(Pall + CH_WAVES * 16 * SP);
   bf16_t* raw = (bf16_t*)(wl + 12 * 32);
   const size_t row0 = (size_t)b * Lq;
+  // Staging: every global load of the phase is issued before the first LDS store (one memory round
+  // trip; round 6 -- the separate load / store passes cost 2.3 us self, 2.7 us cross before the convs)
+  // conv taps and biases [m][w0 | w1 | w2 | b][32] (threads < 384)
+  float wv = 0.f;
+  if (tid < 12 * 32) {
+    const int m = tid / 128, k = (tid / 32) % 4, c = tid % 32;
+    const float* w = CROSS ? (m == 0 ? Ly.ca_qw : m == 1 ? Ly.ca_kw : Ly.ca_vw) : (m == 0 ? Ly.sa_qw : m == 1 ? Ly.sa_kw : Ly.sa_vw);
+    const float* bb = CROSS ? (m == 0 ? Ly.ca_qb : m == 1 ? Ly.ca_kb : Ly.ca_vb) : (m == 0 ? Ly.sa_qb : m == 1 ? Ly.sa_kb : Ly.sa_vb);
+    wv = k < 3 ? w[c * 3 + k] : bb[c];
+  }
+  static_assert(12 * 32 <= CH_NT, "one tap per thread");
+  float k0 = 0.f, k1 = 0.f;  // CROSS: the step-dependent keys 0, 1 of thread t < 96's K / V channel
   if constexpr (CROSS) {
     // keys >= 2 from the step-invariant convolved cache (ggd_set_memory); keys 0 and 1 depend on the
     // step token (memory row 0) and are convolved here, in the cache kernel's expression
     const int colq[3] = {head * 32, 0, 0};
-    la_stage_raw<1>(a.q, row0, CH_D, colq, Lq, raw);
+    LaRaw<1> rq;
+    rq.load(a.q, row0, CH_D, colq, Lq);
     const bf16_t* kc = Ly.kvc + ((size_t)b * CH_WAVES + head) * 2 * Lkp * 32;
     const bf16_t* vc = kc + Lkp * 32;
     const int kpr = Lkp / 8;  // 16-byte units per V^T row
-    for (int u = tid; u < (Lkp - 2) * 4; u += CH_NT) {  // K rows 2 .. Lk_pad - 1
-      const int r = 2 + u / 4, cv = u % 4;
-      *(uint4*)(Km + r * LA_SQ + cv * 8) = *(const uint4*)(kc + r * 32 + cv * 8);
+    constexpr int KU = (ATT_LMAX * 4 + CH_NT - 1) / CH_NT;  // K units (rows 2 .. Lk_pad - 1) per thread
+    constexpr int VU = (32 * ATT_LMAX / 8 + CH_NT - 1) / CH_NT;  // V^T units per thread
+    uint4 kv[KU], vv[VU];
+#pragma unroll
+    for (int i = 0; i < KU; ++i) {
+      const int u = min(tid + i * CH_NT, (Lkp - 2) * 4 - 1), r = 2 + u / 4, cv = u % 4;
+      kv[i] = *(const uint4*)(kc + r * 32 + cv * 8);
     }
+#pragma unroll
+    for (int i = 0; i < VU; ++i) {
+      const int u = min(tid + i * CH_NT, 32 * kpr - 1), c = u / kpr, kb = u % kpr;
+      vv[i] = *(const uint4*)(vc + c * Lkp + kb * 8);
+    }
+    // the step-dependent keys 0, 1: thread t < 64 computes K[t / 32][t % 32], thread 64 + c the V^T
+    // pair of channel c (the memory-row inputs loaded here with the rest)
     const float* r0 = Ly.kv_step + (size_t)t_orig * 2 * CH_D;
     const float* m0 = Ly.kv_mem + (size_t)b * (Lk - 1) * 2 * CH_D;
-    for (int u = tid; u < 32 * kpr; u += CH_NT) {  // V^T rows; keys 0, 1 patched in
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, wb0 = 0.f;
+    if (tid < 96) {
+      const bool isv = tid >= 64;
+      const int c = isv ? tid - 64 : tid % 32, col = (isv ? CH_D : 0) + head * 32 + c;
+      x0 = r0[col];
+      x1 = m0[col];
+      x2 = Lk > 2 ? m0[2 * CH_D + col] : 0.f;
+      const float* w = isv ? Ly.ca_vw : Ly.ca_kw;
+      w0 = w[c * 3];
+      w1 = w[c * 3 + 1];
+      w2 = w[c * 3 + 2];
+      wb0 = isv ? Ly.ca_vb[c] : Ly.ca_kb[c];
+    }
+    rq.store(Lq, raw);
+#pragma unroll
+    for (int i = 0; i < KU; ++i) {
+      const int u = tid + i * CH_NT;
+      if (u >= (Lkp - 2) * 4) continue;
+      const int r = 2 + u / 4, cv = u % 4;
+      *(uint4*)(Km + r * LA_SQ + cv * 8) = kv[i];
+    }
+    k0 = wb0 + w0 * 0.f + w1 * x0 + w2 * x1;  // key 0 (LaStrip::conv's expression)
+    k1 = wb0 + w0 * x0 + w1 * x1 + w2 * x2;   // key 1
+#pragma unroll
+    for (int i = 0; i < VU; ++i) {
+      const int u = tid + i * CH_NT;
+      if (u >= 32 * kpr) continue;
       const int c = u / kpr, kb = u % kpr;
-      uint4 v = *(const uint4*)(vc + c * Lkp + kb * 8);
-      if (kb == 0) {
-        const int col = CH_D + head * 32 + c;
-        const float x0 = r0[col], x1 = m0[col], x2 = Lk > 2 ? m0[2 * CH_D + col] : 0.f;
-        const float* w = Ly.ca_vw;
-        const float bb = Ly.ca_vb[c];
-        const float k0 = bb + w[c * 3] * 0.f + w[c * 3 + 1] * x0 + w[c * 3 + 2] * x1;
-        const float k1 = bb + w[c * 3] * x0 + w[c * 3 + 1] * x1 + w[c * 3 + 2] * x2;
-        v.x = pk_bf16(k0, k1);
-      }
-      *(uint4*)(Vt + c * SV + kb * 8) = v;
+      *(uint4*)(Vt + c * SV + kb * 8) = vv[i];
     }
-    if (tid < 64) {  // K keys 0, 1
-      const int r = tid / 32, c = tid % 32, col = head * 32 + c;
-      const float x0 = r0[col], x1 = m0[col], x2 = Lk > 2 ? m0[2 * CH_D + col] : 0.f;
-      const float* w = Ly.ca_kw;
-      const float bb = Ly.ca_kb[c];
-      const float v = r == 0 ? bb + w[c * 3] * 0.f + w[c * 3 + 1] * x0 + w[c * 3 + 2] * x1
-                             : bb + w[c * 3] * x0 + w[c * 3 + 1] * x1 + w[c * 3 + 2] * x2;
-      Km[r * LA_SQ + c] = f2bf(v);
-    }
+    if (tid < 64) Km[(tid / 32) * LA_SQ + tid % 32] = f2bf(tid < 32 ? k0 : k1);  // (V^T's pair: after the barrier)
   } else {
     const int cols[3] = {head * 32, CH_D + head * 32, 2 * CH_D + head * 32};
-    la_stage_raw<3>(a.qkv, row0, 3 * CH_D, cols, Lq, raw);  // self: Lk = Lq
+    LaRaw<3> rr;
+    rr.load(a.qkv, row0, 3 * CH_D, cols, Lq);  // self: Lk = Lq
+    rr.store(Lq, raw);
   }
-  for (int i = tid; i < 12 * 32; i += CH_NT) {
-    const int m = i / 128, k = (i / 32) % 4, c = i % 32;
-    const float* w = CROSS ? (m == 0 ? Ly.ca_qw : m == 1 ? Ly.ca_kw : Ly.ca_vw) : (m == 0 ? Ly.sa_qw : m == 1 ? Ly.sa_kw : Ly.sa_vw);
-    const float* bb = CROSS ? (m == 0 ? Ly.ca_qb : m == 1 ? Ly.ca_kb : Ly.ca_vb) : (m == 0 ? Ly.sa_qb : m == 1 ? Ly.sa_kb : Ly.sa_vb);
-    wl[i] = k < 3 ? w[c * 3 + k] : bb[c];
-  }
+  if (tid < 12 * 32) wl[tid] = wv;
   if constexpr (!CROSS) {
     for (int i = tid; i < (Lkp - Lk) * 32; i += CH_NT) {
       const int r = Lk + i / 32, c = i % 32;
@@ -640,6 +745,9 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
   }
   bar_lds();
   if (sub && tid == 0) sub[0] = __builtin_amdgcn_s_memrealtime();
+  // V^T keys 0, 1 of channel tid - 64, over the cached row's first pair, once that copy (another
+  // thread's) has landed; the tiles read them after the conv barrier below
+  if (CROSS && tid >= 64 && tid < 96) *(unsigned*)(Vt + (tid - 64) * SV) = pk_bf16(k0, k1);
   la_conv_raw<false>(raw, Lq, wl, Qm, LA_SQ);
   if constexpr (!CROSS) {
     la_conv_raw<false>(raw + (size_t)(Lq + 2) * 32, Lk, wl + 128, Km, LA_SQ);
