@@ -583,6 +583,9 @@ constexpr int LA_SQ = 40;                    // Q / K operand row stride (bf16, 
 // re-reads); load() issues them, store() writes them after the phase's other loads are issued
 // (lk_attn).  src[m] = base + col[m] (row stride ld).
 constexpr int LA_RAW_UNITS = (3 * ATT_LMAX * 4 + CH_NT - 1) / CH_NT;  // units per thread (max)
+// raw row stride (bf16): 32 channels + 8 pad, so that the 16 lanes (4 runs of 4 rows x 4 channel
+// groups) of one LDS pass of la_conv_runs hit 16 distinct 16-byte bank slots
+constexpr int LA_RS = 40;
 template <int NM> struct LaRaw {
   uint4 v[LA_RAW_UNITS];
   __device__ __forceinline__ void load(const void* base, size_t row0, int ld, const int (&col)[3], int rows) {
@@ -600,40 +603,65 @@ template <int NM> struct LaRaw {
       const int u = tid + i * CH_NT;
       if (u >= total) continue;
       const int m = u / per, r = (u % per) / 4, cv = u % 4;
-      *(uint4*)(raw + ((size_t)m * (rows + 2) + r + 1) * 32 + cv * 8) = v[i];
+      *(uint4*)(raw + ((size_t)m * (rows + 2) + r + 1) * LA_RS + cv * 8) = v[i];
     }
     for (int u = tid; u < NM * 2 * 4; u += CH_NT) {  // halo rows
       const int m = u / 8, h = (u / 4) % 2, cv = u % 4;
-      *(uint4*)(raw + ((size_t)m * (rows + 2) + h * (rows + 1)) * 32 + cv * 8) = make_uint4(0, 0, 0, 0);
+      *(uint4*)(raw + ((size_t)m * (rows + 2) + h * (rows + 1)) * LA_RS + cv * 8) = make_uint4(0, 0, 0, 0);
     }
   }
 };
 
-// conv of raw image m into its operand image: out[i] = b + w0 in[i-1] + w1 in[i] + w2 in[i+1]
-// (LaStrip::conv's expression); TRANS writes V^T.  wl = [w0|w1|w2|b][32] of this matrix.
-template <bool TRANS>
-__device__ __forceinline__ void la_conv_raw(const bf16_t* raw, int rows, const float* wl, bf16_t* dst, int S) {
-  for (int u = ltid(); u < rows * 4; u += CH_NT) {
-    const int i = u / 4, cv = u % 4;
-    float x[3][8];
+// The NM convs of an attention phase (raw image m -> operand image m: out[i] = b + w0 in[i-1] + w1 in[i]
+// + w2 in[i+1], LaStrip::conv's expression; matrix 2 of 3 written as V^T): thread (matrix m, run of 4
+// rows, 8-channel group cv) reads the 6 raw rows its 4 outputs need and its 32 taps once, and writes
+// a row's 8 channels as one 16-byte store (a V^T channel's 4 rows as one 8-byte store).  16
+// consecutive lanes are 4 runs x 4 channel groups: with the 80-byte raw rows (LA_RS) each LDS pass
+// touches 16 distinct bank slots.  Round 6: one element per (row, channel group) re-read the taps for
+// every row and took 2.0 us per self-attention phase (profiles/r06ae_c4_barrier_prefetch_ab.txt).
+// rows % 4 == 0 (whole row blocks).  wl = [m][w0 | w1 | w2 | b][32]
+template <int NM>
+__device__ __forceinline__ void la_conv_runs(const bf16_t* raw, int rows, const float* wl, bf16_t* const (&dst)[3],
+                                             const int (&S)[3]) {
+  for (int u = ltid(); u < NM * rows; u += CH_NT) {
+    const int m = u / rows, r = u % rows, cv = r % 4, i0 = (r / 4) * 4;
+    const float* w = wl + m * 128 + cv * 8;
+    const float4 w0a = *(const float4*)(w), w0b = *(const float4*)(w + 4);
+    const float4 w1a = *(const float4*)(w + 32), w1b = *(const float4*)(w + 36);
+    const float4 w2a = *(const float4*)(w + 64), w2b = *(const float4*)(w + 68);
+    const float4 bba = *(const float4*)(w + 96), bbb = *(const float4*)(w + 100);
+    const float w0[8] = {w0a.x, w0a.y, w0a.z, w0a.w, w0b.x, w0b.y, w0b.z, w0b.w};
+    const float w1[8] = {w1a.x, w1a.y, w1a.z, w1a.w, w1b.x, w1b.y, w1b.z, w1b.w};
+    const float w2[8] = {w2a.x, w2a.y, w2a.z, w2a.w, w2b.x, w2b.y, w2b.z, w2b.w};
+    const float bb[8] = {bba.x, bba.y, bba.z, bba.w, bbb.x, bbb.y, bbb.z, bbb.w};
+    const bf16_t* src = raw + ((size_t)m * (rows + 2) + i0) * LA_RS + cv * 8;
+    float x[6][8];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const uint4 q = *(const uint4*)(raw + (size_t)(i + k) * 32 + cv * 8);
-      const unsigned w[4] = {q.x, q.y, q.z, q.w};
+    for (int k = 0; k < 6; ++k) {
+      const uint4 q = *(const uint4*)(src + (size_t)k * LA_RS);
+      const unsigned e4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        x[k][2 * e] = __uint_as_float(w[e] << 16);
-        x[k][2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+        x[k][2 * e] = __uint_as_float(e4[e] << 16);
+        x[k][2 * e + 1] = __uint_as_float(e4[e] & 0xffff0000u);
       }
     }
+    float y[4][8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = cv * 8 + e;
-      const float v = wl[96 + c] + wl[c] * x[0][e] + wl[32 + c] * x[1][e] + wl[64 + c] * x[2][e];
-      if (TRANS)
-        dst[c * S + i] = f2bf(v);
-      else
-        dst[i * S + c] = f2bf(v);
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[q][e] = bb[e] + w0[e] * x[q][e] + w1[e] * x[q + 1][e] + w2[e] * x[q + 2][e];
+    bf16_t* out = dst[m];
+    if (NM == 3 && m == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        *(uint2*)(out + (size_t)(cv * 8 + e) * S[2] + i0) = make_uint2(pk_bf16(y[0][e], y[1][e]), pk_bf16(y[2][e], y[3][e]));
+    } else {
+      const int so = m == 0 ? S[0] : S[1];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *(uint4*)(out + (size_t)(i0 + q) * so + cv * 8) = make_uint4(pk_bf16(y[q][0], y[q][1]), pk_bf16(y[q][2], y[q][3]),
+                                                                    pk_bf16(y[q][4], y[q][5]), pk_bf16(y[q][6], y[q][7]));
     }
   }
 }
@@ -658,7 +686,7 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
   bf16_t* Vt = Km + Lkp * LA_SQ;
   bf16_t* Pall = Vt + 32 * SV;
   float* wl = (float*)(Pall + CH_WAVES * 16 * SP);
-  bf16_t* raw = (bf16_t*)(wl + 12 * 32);
+  bf16_t* raw = Pall;  // the raw conv inputs share the P tiles' region (dead until the tiles)
   const size_t row0 = (size_t)b * Lq;
   // Staging: every global load of the phase is issued before the first LDS store (one memory round
   // trip; round 6 -- the separate load / store passes cost 2.3 us self, 2.7 us cross before the convs)
@@ -748,10 +776,10 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
   // V^T keys 0, 1 of channel tid - 64, over the cached row's first pair, once that copy (another
   // thread's) has landed; the tiles read them after the conv barrier below
   if (CROSS && tid >= 64 && tid < 96) *(unsigned*)(Vt + (tid - 64) * SV) = pk_bf16(k0, k1);
-  la_conv_raw<false>(raw, Lq, wl, Qm, LA_SQ);
-  if constexpr (!CROSS) {
-    la_conv_raw<false>(raw + (size_t)(Lq + 2) * 32, Lk, wl + 128, Km, LA_SQ);
-    la_conv_raw<true>(raw + (size_t)2 * (Lq + 2) * 32, Lk, wl + 256, Vt, SV);
+  {
+    bf16_t* const cd[3] = {Qm, Km, Vt};
+    const int cs[3] = {LA_SQ, LA_SQ, SV};
+    la_conv_runs<CROSS ? 1 : 3>(raw, Lq, wl, cd, cs);  // self: Lk = Lq
   }
   bar_lds();
   if (sub && tid == 0) sub[1] = __builtin_amdgcn_s_memrealtime();
@@ -793,10 +821,17 @@ __global__ void lk_kv_cache_kernel(const float* __restrict__ kv_mem, const float
   }
 }
 
-size_t lk_attn_lds(int L, int Lk) {
+// One attention phase (Lk keys, nm raw conv inputs: 3 self, 1 cross): Q | K | V^T | P tiles (the raw
+// inputs, nm x (L + 2) rows of LA_RS, in the P region: lk_attn places them there) | taps
+size_t lk_attn_lds(int L, int Lk, int nm) {
   const int Lkp = (Lk + 31) / 32 * 32, Lqp = (L + 15) / 16 * 16;
-  return 2 * ((size_t)Lqp * LA_SQ + (size_t)Lkp * LA_SQ + 32 * (size_t)(Lkp + 8) + CH_WAVES * 16 * (size_t)(Lkp + 8)) +
-         sizeof(float) * 12 * 32 + 2 * (size_t)3 * (L + 2) * 32;  // + the raw conv inputs
+  const size_t p = std::max((size_t)CH_WAVES * 16 * (Lkp + 8), (size_t)nm * (L + 2) * LA_RS);
+  return 2 * ((size_t)Lqp * LA_SQ + (size_t)Lkp * LA_SQ + 32 * (size_t)(Lkp + 8) + p) + sizeof(float) * 12 * 32;
+}
+// the raw conv inputs fit the P region (lk_attn's layout)
+static bool lk_raw_fits(int L, int Lk, int nm) {
+  const int Lkp = (Lk + 31) / 32 * 32;
+  return (size_t)nm * (L + 2) * LA_RS <= (size_t)CH_WAVES * 16 * (Lkp + 8);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -864,7 +899,8 @@ template <bool W8>
 size_t lk_lds(int L, int Lk) {
   size_t m = LkGeo<W8, K_BL>::LDS;
   m = std::max(m, LkGeo<W8, K_B>::LDS);
-  return std::max(m, LK_HS + lk_attn_lds(L, Lk));
+  m = std::max(m, LK_HS + lk_attn_lds(L, L, 3));  // self-attention
+  return std::max(m, LK_HS + lk_attn_lds(L, Lk, 1));  // cross-attention
 }
 
 // Verification kernel (ggd_mx_layernorm): lk_layernorm_mx -- the long loop's LayerNorm into the
@@ -939,6 +975,7 @@ bool long_loop_supported(int dtype, int d_model, int heads, int L, int Ts, int C
   const size_t lds = std::max(lk_lds<true>(L, 1 + Ts), lk_lds<false>(L, 1 + Ts));
   const int lkp = (1 + Ts + 31) / 32 * 32;  // memory keys, padded (whole-clip tiles: 96 .. 192)
   return dtype != 0 && d_model == CH_D && heads == 8 && L % CH_MT == 0 && L / CH_MT <= 8 && L >= 96 &&
+         lk_raw_fits(L, L, 3) && lk_raw_fits(L, 1 + Ts, 1) &&
          L <= ATT_LMAX && lkp >= 96 && lkp <= ATT_LMAX && C <= 128 && out_npad == 128 && lds <= 160 * 1024 - 256;
 }
 
