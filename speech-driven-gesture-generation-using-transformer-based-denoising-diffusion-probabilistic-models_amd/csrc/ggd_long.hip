@@ -69,14 +69,21 @@ __device__ int lk_role(unsigned* ctl, int* status, int nwg, int G) {
 }
 
 // barrier of the clip group's 8 workgroups (one L2): each publishes its epoch in its word of the
-// group's flag line after its stores have drained; wave 0 polls the 8 words with sc1 loads
-__device__ __forceinline__ bool lk_sync(unsigned* flags, int part, unsigned epoch, int* status, int* s_ok) {
+// group's flag line after its stores have drained; wave 0 polls the 8 words with sc1 loads.
+// prefetch: the next phase's loads that do not depend on the other workgroups' stores (weights,
+// parameters, cached keys), issued after the drain so that they are in flight across the wait;
+// the polling wave issues its share after its poll (a poll load would retire behind them)
+__device__ __forceinline__ void lk_nop() {}
+template <typename F = void (*)()>
+__device__ __forceinline__ bool lk_sync(unsigned* flags, int part, unsigned epoch, int* status, int* s_ok,
+                                        F&& prefetch = lk_nop) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
     __builtin_amdgcn_raw_buffer_store_b32(epoch, r, part * 4, 0, 0);
   }
+  if (threadIdx.x >= 64) prefetch();
   if (threadIdx.x < 64) {
     const __amdgpu_buffer_rsrc_t r = uni_rsrc(flags, 32u);
     const int off = (threadIdx.x & 7) * 4;
@@ -96,6 +103,7 @@ __device__ __forceinline__ bool lk_sync(unsigned* flags, int part, unsigned epoc
       __builtin_amdgcn_s_sleep(1);
     }
     if (threadIdx.x == 0) *s_ok = ok;
+    prefetch();
   }
   bar_lds();
   return *s_ok != 0;
@@ -674,8 +682,63 @@ __device__ __forceinline__ void lk_attn_tiles(const bf16_t* Qm, const bf16_t* Km
   clip_attn_tiles<LKT, CH_WAVES, LA_SQ>(Qm, Km, Vt, P, SV, SP, Lq, Lk, sl2, out, CH_D, wave, lane);
 }
 
+// An attention phase's loads that need nothing from the phase before it, issued by lk_sync's
+// prefetch hook (round 6): the conv taps and biases [m][w0 | w1 | w2 | b][32] (threads < 384), and for
+// the cross-attention the layer's cached convolved memory keys 2 .. (K rows, V^T rows: step-invariant,
+// ggd_set_memory) and the inputs of the step-dependent keys 0, 1 (thread t < 64: K[t / 32][t % 32],
+// thread 64 + c: the V^T pair of channel c)
+constexpr int LA_KU = (ATT_LMAX * 4 + CH_NT - 1) / CH_NT;      // K units (rows 2 .. Lk_pad - 1) per thread
+constexpr int LA_VU = (32 * ATT_LMAX / 8 + CH_NT - 1) / CH_NT;  // V^T units per thread
+template <bool CROSS> struct LaPre {
+  float wv;
+  uint4 kv[CROSS ? LA_KU : 1], vv[CROSS ? LA_VU : 1];
+  float x0, x1, x2, w0, w1, w2, wb0;
+  __device__ __forceinline__ void load(cla_T& a, cll_t lyp, int b, int head, int t_orig) {
+    const __attribute__((address_space(4))) LongLayer& Ly = *lyp;
+    const int tid = ltid();
+    static_assert(12 * 32 <= CH_NT, "one tap per thread");
+    wv = 0.f;
+    if (tid < 12 * 32) {
+      const int m = tid / 128, k = (tid / 32) % 4, c = tid % 32;
+      const float* w = CROSS ? (m == 0 ? Ly.ca_qw : m == 1 ? Ly.ca_kw : Ly.ca_vw) : (m == 0 ? Ly.sa_qw : m == 1 ? Ly.sa_kw : Ly.sa_vw);
+      const float* bb = CROSS ? (m == 0 ? Ly.ca_qb : m == 1 ? Ly.ca_kb : Ly.ca_vb) : (m == 0 ? Ly.sa_qb : m == 1 ? Ly.sa_kb : Ly.sa_vb);
+      wv = k < 3 ? w[c * 3 + k] : bb[c];
+    }
+    if constexpr (CROSS) {
+      const int Lk = 1 + a.Ts, Lkp = (Lk + 31) / 32 * 32, kpr = Lkp / 8;
+      const bf16_t* kc = Ly.kvc + ((size_t)b * CH_WAVES + head) * 2 * Lkp * 32;
+      const bf16_t* vc = kc + Lkp * 32;
+#pragma unroll
+      for (int i = 0; i < LA_KU; ++i) {
+        const int u = min(tid + i * CH_NT, (Lkp - 2) * 4 - 1), r = 2 + u / 4, cv = u % 4;
+        kv[i] = *(const uint4*)(kc + r * 32 + cv * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < LA_VU; ++i) {
+        const int u = min(tid + i * CH_NT, 32 * kpr - 1), c = u / kpr, kb = u % kpr;
+        vv[i] = *(const uint4*)(vc + c * Lkp + kb * 8);
+      }
+      const float* r0 = Ly.kv_step + (size_t)t_orig * 2 * CH_D;
+      const float* m0 = Ly.kv_mem + (size_t)b * (Lk - 1) * 2 * CH_D;
+      x0 = x1 = x2 = w0 = w1 = w2 = wb0 = 0.f;
+      if (tid < 96) {
+        const bool isv = tid >= 64;
+        const int c = isv ? tid - 64 : tid % 32, col = (isv ? CH_D : 0) + head * 32 + c;
+        x0 = r0[col];
+        x1 = m0[col];
+        x2 = Lk > 2 ? m0[2 * CH_D + col] : 0.f;
+        const float* w = isv ? Ly.ca_vw : Ly.ca_kw;
+        w0 = w[c * 3];
+        w1 = w[c * 3 + 1];
+        w2 = w[c * 3 + 2];
+        wb0 = isv ? Ly.ca_vb[c] : Ly.ca_kb[c];
+      }
+    }
+  }
+};
+
 template <bool CROSS>
-__device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, int t_orig,
+__device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, const LaPre<CROSS>* pre,
                                                   unsigned char* scratch, unsigned long long* sub = nullptr) {
   // sub (diagnostics): realtime stamps after staging, after the convs, after the query tiles
   const __attribute__((address_space(4))) LongLayer& Ly = *lyp;
@@ -689,16 +752,17 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
   bf16_t* raw = Pall;  // the raw conv inputs share the P tiles' region (dead until the tiles)
   const size_t row0 = (size_t)b * Lq;
   // Staging: every global load of the phase is issued before the first LDS store (one memory round
-  // trip; round 6 -- the separate load / store passes cost 2.3 us self, 2.7 us cross before the convs)
-  // conv taps and biases [m][w0 | w1 | w2 | b][32] (threads < 384)
+  // trip; round 6 -- the separate load / store passes cost 2.3 us self, 2.7 us cross before the convs).
+  // The cross-attention's taps, cached keys and memory rows are in flight since the barrier (pre).
   float wv = 0.f;
-  if (tid < 12 * 32) {
+  if constexpr (CROSS) {
+    wv = pre->wv;
+  } else if (tid < 12 * 32) {  // conv taps and biases [m][w0 | w1 | w2 | b][32]
     const int m = tid / 128, k = (tid / 32) % 4, c = tid % 32;
-    const float* w = CROSS ? (m == 0 ? Ly.ca_qw : m == 1 ? Ly.ca_kw : Ly.ca_vw) : (m == 0 ? Ly.sa_qw : m == 1 ? Ly.sa_kw : Ly.sa_vw);
-    const float* bb = CROSS ? (m == 0 ? Ly.ca_qb : m == 1 ? Ly.ca_kb : Ly.ca_vb) : (m == 0 ? Ly.sa_qb : m == 1 ? Ly.sa_kb : Ly.sa_vb);
+    const float* w = m == 0 ? Ly.sa_qw : m == 1 ? Ly.sa_kw : Ly.sa_vw;
+    const float* bb = m == 0 ? Ly.sa_qb : m == 1 ? Ly.sa_kb : Ly.sa_vb;
     wv = k < 3 ? w[c * 3 + k] : bb[c];
   }
-  static_assert(12 * 32 <= CH_NT, "one tap per thread");
   float k0 = 0.f, k1 = 0.f;  // CROSS: the step-dependent keys 0, 1 of thread t < 96's K / V channel
   if constexpr (CROSS) {
     // keys >= 2 from the step-invariant convolved cache (ggd_set_memory); keys 0 and 1 depend on the
@@ -706,55 +770,23 @@ __device__ __forceinline__ void lk_attn(cla_T& a, cll_t lyp, int b, int head, in
     const int colq[3] = {head * 32, 0, 0};
     LaRaw<1> rq;
     rq.load(a.q, row0, CH_D, colq, Lq);
-    const bf16_t* kc = Ly.kvc + ((size_t)b * CH_WAVES + head) * 2 * Lkp * 32;
-    const bf16_t* vc = kc + Lkp * 32;
     const int kpr = Lkp / 8;  // 16-byte units per V^T row
-    constexpr int KU = (ATT_LMAX * 4 + CH_NT - 1) / CH_NT;  // K units (rows 2 .. Lk_pad - 1) per thread
-    constexpr int VU = (32 * ATT_LMAX / 8 + CH_NT - 1) / CH_NT;  // V^T units per thread
-    uint4 kv[KU], vv[VU];
-#pragma unroll
-    for (int i = 0; i < KU; ++i) {
-      const int u = min(tid + i * CH_NT, (Lkp - 2) * 4 - 1), r = 2 + u / 4, cv = u % 4;
-      kv[i] = *(const uint4*)(kc + r * 32 + cv * 8);
-    }
-#pragma unroll
-    for (int i = 0; i < VU; ++i) {
-      const int u = min(tid + i * CH_NT, 32 * kpr - 1), c = u / kpr, kb = u % kpr;
-      vv[i] = *(const uint4*)(vc + c * Lkp + kb * 8);
-    }
-    // the step-dependent keys 0, 1: thread t < 64 computes K[t / 32][t % 32], thread 64 + c the V^T
-    // pair of channel c (the memory-row inputs loaded here with the rest)
-    const float* r0 = Ly.kv_step + (size_t)t_orig * 2 * CH_D;
-    const float* m0 = Ly.kv_mem + (size_t)b * (Lk - 1) * 2 * CH_D;
-    float x0 = 0.f, x1 = 0.f, x2 = 0.f, w0 = 0.f, w1 = 0.f, w2 = 0.f, wb0 = 0.f;
-    if (tid < 96) {
-      const bool isv = tid >= 64;
-      const int c = isv ? tid - 64 : tid % 32, col = (isv ? CH_D : 0) + head * 32 + c;
-      x0 = r0[col];
-      x1 = m0[col];
-      x2 = Lk > 2 ? m0[2 * CH_D + col] : 0.f;
-      const float* w = isv ? Ly.ca_vw : Ly.ca_kw;
-      w0 = w[c * 3];
-      w1 = w[c * 3 + 1];
-      w2 = w[c * 3 + 2];
-      wb0 = isv ? Ly.ca_vb[c] : Ly.ca_kb[c];
-    }
     rq.store(Lq, raw);
 #pragma unroll
-    for (int i = 0; i < KU; ++i) {
+    for (int i = 0; i < LA_KU; ++i) {
       const int u = tid + i * CH_NT;
       if (u >= (Lkp - 2) * 4) continue;
       const int r = 2 + u / 4, cv = u % 4;
-      *(uint4*)(Km + r * LA_SQ + cv * 8) = kv[i];
+      *(uint4*)(Km + r * LA_SQ + cv * 8) = pre->kv[i];
     }
-    k0 = wb0 + w0 * 0.f + w1 * x0 + w2 * x1;  // key 0 (LaStrip::conv's expression)
-    k1 = wb0 + w0 * x0 + w1 * x1 + w2 * x2;   // key 1
+    k0 = pre->wb0 + pre->w0 * 0.f + pre->w1 * pre->x0 + pre->w2 * pre->x1;  // key 0 (LaStrip::conv's expression)
+    k1 = pre->wb0 + pre->w0 * pre->x0 + pre->w1 * pre->x1 + pre->w2 * pre->x2;  // key 1
 #pragma unroll
-    for (int i = 0; i < VU; ++i) {
+    for (int i = 0; i < LA_VU; ++i) {
       const int u = tid + i * CH_NT;
       if (u >= 32 * kpr) continue;
       const int c = u / kpr, kb = u % kpr;
-      *(uint4*)(Vt + c * SV + kb * 8) = vv[i];
+      *(uint4*)(Vt + c * SV + kb * 8) = pre->vv[i];
     }
     if (tid < 64) Km[(tid / 32) * LA_SQ + tid % 32] = f2bf(tid < 32 ? k0 : k1);  // (V^T's pair: after the barrier)
   } else {
@@ -871,13 +903,16 @@ __global__ void __launch_bounds__(CH_NT) lk_kernel(LongArgs args, int G) {
     const int t_orig = a.steps[it].t_orig;
     for (int li = 0; li < NL; ++li) {
       const cst_t sl = st + 2 + LONG_STAGES_PER_LAYER * li;
-      lk_attn<false>(a, lay + li, b, part, t_orig, smem + LK_HS, stamps && k == 1 && li == 0 ? stamps + 56 : nullptr);
+      lk_attn<false>(a, lay + li, b, part, nullptr, smem + LK_HS, stamps && k == 1 && li == 0 ? stamps + 56 : nullptr);
       if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
       stamp();
       if (rows) lk_chain<W8, K_A, MX>(a, sl, b, part, it, smem);         // R(o_sa) + P(LN2, q_ca)
-      if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
-      stamp();
-      lk_attn<true>(a, lay + li, b, part, t_orig, smem + LK_HS, stamps && k == 1 && li == 0 ? stamps + 60 : nullptr);
+      {  // (the cross-attention's step-invariant keys and taps: loaded at the barrier)
+        LaPre<true> pc;
+        if (!lk_sync(flags, part, ++epoch, a.status, &s_ok, [&] { pc.load(a, lay + li, b, part, t_orig); })) return;
+        stamp();
+        lk_attn<true>(a, lay + li, b, part, &pc, smem + LK_HS, stamps && k == 1 && li == 0 ? stamps + 60 : nullptr);
+      }
       if (!lk_sync(flags, part, ++epoch, a.status, &s_ok)) return;
       stamp();
       if (rows) {
