@@ -123,7 +123,7 @@ WORKLOADS = {
 # this same command (scripts/pmc_all.sh -> scripts/pmc.sh + pmc_summary.py: 2 x FETCH_SIZE +
 # WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md), one summary per workload; PMC cannot
 # run inside the timed region, so the figure is the profile's, keyed by kernel symbol and workload
-PMC_SUMMARY = {"c2": "r06u", "c4": "r06u", "c5": "r06u"}   # profile tag per workload (its dominant kernel's code)
+PMC_SUMMARY = {"c2": "r06ai", "c4": "r06ai", "c5": "r06ai"}   # profile tag per workload (its dominant kernel's code)
 
 
 def csrc_hash():
