@@ -739,6 +739,38 @@ def test_long_loop_equals_launch_route(pkg, beat_cfg, setup, setup_fp8, dtype, n
         assert rel_rms(out_l["sample"].cpu(), want["sample"]) <= 5e-2
 
 
+# The long-clip loop at its other row-block counts (L = 96 / 128: 3 / 4 row blocks, fewer query tiles
+# and keys than C4's 160) -- the attention's LDS plan (raw conv rows in the P tiles' region, sized per
+# phase since round 6), the conv runs over L rows and the chain prologue -- bit for bit against the
+# launch route (fp8 weights widened, as above), and the loop must have run.
+@pytest.mark.parametrize("Lc", [96, 128])
+def test_long_loop_other_lengths_equal_launch_route(pkg, beat_cfg, setup, Lc):
+    _, sd, _ = setup
+    model, diffusion = make_model(pkg, beat_cfg, sd, "fp8")
+    n, steps = 2, 3
+    wav, x, _ = inputs(n, seed=95, wav_len=800 * Lc, L_=Lc)
+    zs = th.randn(steps, n, D_POSE, Lc, generator=th.Generator().manual_seed(96))
+    ctx, _ = model.prepare(wav.cuda(), Lc)
+
+    def run():
+        return diffusion.p_sample_loop(model, (n, D_POSE, Lc), model_kwargs={"wav": wav.cuda()}, noise=x.cuda(),
+                                       step_noise=zs.cuda(), n_steps=steps)
+
+    try:
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 1) == 0
+        out_l = run()
+        launches = int(_info(ctx, INFO_LONG_LAUNCHES))
+        assert ctx.lib.ggd_set_route(ctx.h, ROUTE_LONG_LOOP, 1) == 0
+        out_r = run()
+        assert int(_info(ctx, INFO_LONG_LAUNCHES)) == 0
+    finally:
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_LONG_LOOP, 0)
+        ctx.lib.ggd_set_route(ctx.h, ROUTE_FP8_MFMA, 0)
+    assert launches == 1, "the long-clip loop did not run at this length"
+    for k in ("sample", "eps"):
+        assert th.equal(out_l[k].cpu(), out_r[k].cpu()), k
+
+
 def test_c1_tedexp_b1_full_50_step_loop_f32(pkg, tedexp_cfg, setup_c1):
     """Config C1 as BASELINE.md states it: tedexp (two-way CrossAttention, d 512, 10 layers), B = 1,
     timestep_respacing "50", ALL 50 DDPM steps on injected noise vs the oracle loop, f32 (nn.py:381-447)."""
